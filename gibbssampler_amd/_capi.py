@@ -1,0 +1,120 @@
+"""ctypes binding of libgibbs_hip.so (include/gibbs_capi.h).
+
+This is the reference-side binding a maintainer would add to
+Gabriel-Ducrocq/GibbsSampler: plain ctypes over the C-ABI,
+device pointers from torch tensors, the HIP stream from
+``torch.cuda.current_stream().cuda_stream``.  There is no CPU fallback: if the
+library is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GIBBS_HIP_LIB", os.path.join(_HERE, "libgibbs_hip.so"))
+
+GS_MODE_CENTERED = 0
+GS_MODE_NONCENTERED = 1
+GS_QUIRK_ASIS_RECENTRE_CENTERED = 1
+GS_NPARAM = 10
+NSTAT = {1: 2, 2: 4, 3: 8}
+
+c_int_p = ctypes.POINTER(ctypes.c_int)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+
+
+class GsModelDesc(ctypes.Structure):
+    _fields_ = [
+        ("lmax", ctypes.c_int),
+        ("nside", ctypes.c_int),
+        ("nfields", ctypes.c_int),
+        ("nchains", ctypes.c_int),
+        ("chain0", ctypes.c_int),
+        ("quirks", ctypes.c_int),
+        ("n_iter_metropolis", ctypes.c_int),
+        ("bl", c_double_p),
+        ("noise_var", c_double_p),
+        ("bins", c_int_p * 4),
+        ("nbin_edges", ctypes.c_int * 4),
+        ("blocks", c_int_p * 4),
+        ("nblock_edges", ctypes.c_int * 4),
+        ("prop_var", c_double_p * 4),
+    ]
+
+
+class GibbsHipError(RuntimeError):
+    pass
+
+
+_lib = None
+
+# (name, restype, argtypes)
+_VP = ctypes.c_void_p
+_SIGS = [
+    ("gs_abi_version", ctypes.c_int, []),
+    ("gs_last_error", ctypes.c_char_p, []),
+    ("gs_plan_create", ctypes.c_int, [ctypes.POINTER(GsModelDesc), ctypes.POINTER(_VP)]),
+    ("gs_plan_destroy", ctypes.c_int, [_VP]),
+    ("gs_plan_info", ctypes.c_int, [_VP, c_int_p, c_int_p, c_int_p, c_int_p]),
+    ("gs_var_expand", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
+    ("gs_real_to_complex", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
+    ("gs_complex_to_real", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
+    ("gs_remove_monopole_dipole", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP]),
+    ("gs_alm2cl", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP]),
+    ("gs_unfold_bins", ctypes.c_int, [ctypes.c_int, _VP, _VP, ctypes.c_int, _VP, _VP]),
+    ("gs_block_params", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP]),
+    ("gs_cr_sweep", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                   _VP, _VP, _VP]),
+    ("gs_cls_draw", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
+    ("gs_nc_mh", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
+    ("gs_stats_to_noncentered", ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    ("gs_recentre", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("gs_step_centered", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP]),
+    ("gs_step_noncentered", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
+                                           _VP, _VP]),
+    ("gs_step_asis", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
+                                    _VP, _VP, ctypes.c_int, _VP]),
+    ("gs_sweep_timing", ctypes.c_int, [_VP, ctypes.c_int, c_double_p, c_int_p]),
+]
+
+EXPORTED = [n for n, _, _ in _SIGS]
+
+
+def load(path=None):
+    """Load the HIP library (raises GibbsHipError when absent)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise GibbsHipError(f"libgibbs_hip.so not found at {p}: run __graft_entry__.build() "
+                            "(there is no CPU fallback)")
+    lib = ctypes.CDLL(p)
+    for name, res, args in _SIGS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gs_abi_version() != 1:
+        raise GibbsHipError("ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc, what="gibbs_hip"):
+    if rc != 0:
+        msg = _lib.gs_last_error().decode() if _lib is not None else "?"
+        raise GibbsHipError(f"{what} failed: {msg}")
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise GibbsHipError("tensor must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

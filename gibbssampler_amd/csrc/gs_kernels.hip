@@ -1,0 +1,1159 @@
+// gs_kernels.hip -- MI355X (gfx950) kernels and C-ABI of the Gibbs hot path.
+//
+// Data layout in HBM (DESIGN.md "Layout"):
+//   d_alm   [F][NR]                 NR = (L+1)^2, real m-major (utils.py:49-76)
+//   s       [nchains][F][NR]
+//   params  [nchains][L+1][GS_NPARAM]   per-l CR operator (M, Lchol)
+//   stats   [nchains][nstat][L+1]       per-l sufficient statistics
+//   dl      [nchains][nspec][maxbins]   binned D_l
+//
+// The CR sweep is tiled over the (l, m) triangle: one wave owns 64
+// consecutive l (lanes) and a range of m rows, so each lane keeps its l's
+// operator in registers and accumulates its l's statistics without atomics;
+// per-(task, l) partial sums are reduced in a fixed order by k_stats_finish
+// (bitwise reproducible).  Row m of a tile is one contiguous 16-B-per-lane
+// segment of every field, so every load/store wave-instruction is coalesced.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <string>
+#include <vector>
+#include <cstring>
+#include <algorithm>
+
+#include "gibbs_capi.h"
+#include "gs_rng.h"
+
+using namespace gs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(const std::string& msg) {
+    g_last_error = msg;
+    return -1;
+}
+
+#define GS_CHECK(expr)                                                                  \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return set_error(std::string(#expr) + ": " + hipGetErrorString(_e));       \
+    } while (0)
+
+#define GS_LAUNCH_CHECK(name)                                                           \
+    do {                                                                                \
+        hipError_t _e = hipGetLastError();                                              \
+        if (_e != hipSuccess)                                                           \
+            return set_error(std::string("launch ") + name + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+constexpr int WAVE = 64;
+constexpr int NP = GS_NPARAM;
+constexpr double PI = 3.14159265358979323846;
+
+inline int nstat_of(int F) { return F == 1 ? GS_NSTAT_1 : (F == 2 ? GS_NSTAT_2 : GS_NSTAT_3); }
+inline int nspec_of(int F) { return F == 1 ? 1 : (F == 2 ? 2 : 4); }
+
+}  // namespace
+
+struct gs_plan {
+    int device = 0;
+    int L = 0, nside = 0, Npix = 0, F = 0, nchains = 0, chain0 = 0, quirks = 0, n_iter_mh = 1;
+    int nspec = 0, nstat = 0, maxbins = 0;
+    double kappa[3] = {0, 0, 0};
+    int nbins[4] = {0, 0, 0, 0};
+    int nblocks[4] = {0, 0, 0, 0};
+    int acc_off[4] = {0, 0, 0, 0};   // offset of each spectrum's accept flags
+    int nacc = 0;                    // accept flags per chain
+    int mh_order[4] = {0, 1, 2, 3};
+    bool has_mh = false;
+    // device constants
+    double* bl = nullptr;            // [L+1]
+    int* ell2bin = nullptr;          // [nspec][L+1]
+    int* bins = nullptr;             // [nspec][maxbins+1]
+    int* blocks = nullptr;           // [nspec][maxbins+1] (clipped edges)
+    double* prop_sd = nullptr;       // [nspec][maxbins]
+    int* meta = nullptr;             // [16]: nbins[4], nblocks[4], acc_off[4], mh_order[4]
+    int4* tasks = nullptr;           // [ntask] (tile, m0, m1, 0)
+    int* tile_task0 = nullptr;       // [ntile+1]
+    int ntask = 0, ntile = 0, rows_per_task = 64;
+    // workspace
+    double* partials = nullptr;      // [nchains][ntask][nstat][64]
+    double* params = nullptr;        // [nchains][L+1][NP]
+    double* stats = nullptr;         // [nchains][nstat][L+1]
+    double* prop = nullptr;          // [nchains][nspec][maxbins]
+    double* logr = nullptr;          // [nchains][nspec][maxbins]
+    double* dl_tmp = nullptr;        // [nchains][nspec][maxbins]
+    // dominant-kernel timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+};
+
+// ============================================================================
+// device helpers
+// ============================================================================
+__device__ __forceinline__ double var_from_dl(double D, int ell) {
+    // generate_var_cl (utils.py:126-129): D*2*pi/(l(l+1)), l=0 keeps D_0
+    return ell == 0 ? D : D * 2.0 * PI / (double)(ell * (ell + 1));
+}
+
+__device__ __forceinline__ double dl_at(const double* __restrict__ dl_chain, const int* __restrict__ ell2bin,
+                                        int maxbins, int Lp1, int sp, int ell) {
+    const int b = ell2bin[sp * Lp1 + ell];
+    return b < 0 ? 0.0 : dl_chain[sp * maxbins + b];
+}
+
+// lower Cholesky of the TE block of C and the B entry, zero-variance rule
+struct CovChol { double a00, a10, a11, aB; };
+
+__device__ __forceinline__ CovChol cov_chol_teb(double tt, double ee, double te, double bb) {
+    CovChol c;
+    if (tt != 0.0) {
+        c.a00 = sqrt(tt);
+        c.a10 = te / c.a00;
+        c.a11 = sqrt(fmax(ee - c.a10 * c.a10, 0.0));
+    } else {
+        c.a00 = 0.0; c.a10 = 0.0; c.a11 = sqrt(ee);
+    }
+    c.aB = sqrt(bb);
+    return c;
+}
+
+// ============================================================================
+// stand-alone layout kernels
+// ============================================================================
+__device__ __forceinline__ void complex_index_to_lm(int L, long long i, int& ell, int& m) {
+    // row m starts at S(m) = m(2L+3-m)/2 (ell = m)
+    const double b = 2.0 * L + 3.0;
+    int mm = (int)floor((b - sqrt(fmax(b * b - 8.0 * (double)i, 0.0))) * 0.5);
+    mm = max(0, min(mm, L));
+    while (mm < L && (long long)(mm + 1) * (2 * L + 2 - mm) / 2 <= i) ++mm;
+    while (mm > 0 && (long long)mm * (2 * L + 3 - mm) / 2 > i) --mm;
+    m = mm;
+    ell = (int)(i - (long long)mm * (2 * L + 3 - mm) / 2) + mm;
+}
+
+__global__ void k_var_expand(int L, int n, const double* __restrict__ dl, double* __restrict__ var) {
+    const long long nc = (long long)(L + 1) * (L + 2) / 2;
+    const long long nr = (long long)(L + 1) * (L + 1);
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < nc * n; g += (long long)gridDim.x * blockDim.x) {
+        const int k = (int)(g / nc);
+        const long long i = g % nc;
+        int ell, m;
+        complex_index_to_lm(L, i, ell, m);
+        const double v = var_from_dl(dl[(long long)k * (L + 1) + ell], ell);
+        double* o = var + k * nr;
+        if (m == 0) o[ell] = v;
+        else { const long long r = 2 * i - (L + 1); o[r] = v; o[r + 1] = v; }
+    }
+}
+
+__global__ void k_real_to_complex(int L, int n, const double* __restrict__ re, double* __restrict__ cx) {
+    const long long nc = (long long)(L + 1) * (L + 2) / 2;
+    const long long nr = (long long)(L + 1) * (L + 1);
+    const double isq2 = 1.0 / sqrt(2.0);
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < nc * n; g += (long long)gridDim.x * blockDim.x) {
+        const int k = (int)(g / nc);
+        const long long i = g % nc;
+        const double* a = re + k * nr;
+        double* o = cx + 2 * (k * nc + i);
+        if (i <= L) { o[0] = a[i]; o[1] = 0.0; }
+        else { const long long r = 2 * i - (L + 1); o[0] = a[r] / sqrt(2.0); o[1] = a[r + 1] / sqrt(2.0); }
+        (void)isq2;
+    }
+}
+
+__global__ void k_complex_to_real(int L, int n, const double* __restrict__ cx, double* __restrict__ re) {
+    const long long nc = (long long)(L + 1) * (L + 2) / 2;
+    const long long nr = (long long)(L + 1) * (L + 1);
+    const double sq2 = sqrt(2.0);
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < nc * n; g += (long long)gridDim.x * blockDim.x) {
+        const int k = (int)(g / nc);
+        const long long i = g % nc;
+        const double* c = cx + 2 * (k * nc + i);
+        double* o = re + k * nr;
+        if (i <= L) o[i] = c[0];
+        else { const long long r = 2 * i - (L + 1); o[r] = c[0] * sq2; o[r + 1] = c[1] * sq2; }
+    }
+}
+
+__global__ void k_remove_md(int L, int n, double* __restrict__ alm) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    double* a = alm + (long long)k * (L + 1) * (L + 1);
+    a[0] = 0.0; a[1] = 0.0; a[L + 1] = 0.0; a[L + 2] = 0.0;
+}
+
+// generic alm2cl: one wave per (array, 64-l tile), lanes = l, loop over m
+__global__ void k_alm2cl(int L, int n, const double* __restrict__ x, const double* __restrict__ y, double* __restrict__ cl) {
+    const int ntile = (L + WAVE) / WAVE;
+    const int w = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    const int lane = threadIdx.x & (WAVE - 1);
+    if (w >= n * ntile) return;
+    const int k = w / ntile, t = w % ntile;
+    const int ell = t * WAVE + lane;
+    if (ell > L) return;
+    const long long nr = (long long)(L + 1) * (L + 1);
+    const double* a = x + k * nr;
+    const double* b = y + k * nr;
+    double s = a[ell] * b[ell];
+    for (int m = 1; m <= ell; ++m) {
+        const long long i = (long long)m * (2 * L + 1 - m) / 2 + ell;
+        const long long r = 2 * i - (L + 1);
+        s += a[r] * b[r] + a[r + 1] * b[r + 1];
+    }
+    cl[(long long)k * (L + 1) + ell] = s / (2.0 * ell + 1.0);
+}
+
+__global__ void k_unfold(int n, const double* __restrict__ binned, const int* __restrict__ bins, int nbins,
+                         double* __restrict__ out) {
+    const int Lp1 = 0;
+    (void)Lp1;
+    const int k = blockIdx.y;
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
+        const double v = binned[(long long)k * nbins + b];
+        const int lo = bins[b], hi = bins[b + 1];
+        const int base = bins[0];
+        for (int l = lo; l < hi; ++l) out[(long long)k * (bins[nbins] - base) + (l - base)] = v;
+    }
+}
+
+// ============================================================================
+// per-(chain, l) CR operator
+// ============================================================================
+// MODE 0 centered (CenteredGibbs.py:324-351):   Sigma = (C^+ + diag(b^2 k))^-1, M = Sigma diag(b k)
+// MODE 1 non-centered (NonCenteredGibbs.py:141-174): Sigma = (I + A^T diag(b^2 k) A)^-1,
+//                                                   M = Sigma A^T diag(b k), A = chol(C)
+template <int F, int MODE>
+__global__ __launch_bounds__(256) void k_block_params(int L, int nchains, int maxbins, const double* __restrict__ dl,
+                                                      const int* __restrict__ ell2bin, const double* __restrict__ bl,
+                                                      double k0, double k1, double k2, double* __restrict__ params) {
+    const int Lp1 = L + 1;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nchains * Lp1) return;
+    const int chain = g / Lp1, ell = g % Lp1;
+    constexpr int NS = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    const double* dlc = dl + (long long)chain * NS * maxbins;
+    const double b = bl[ell];
+    double* p = params + (long long)g * NP;
+    const double kap[3] = {k0, k1, k2};
+    if constexpr (F != 3) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const double v = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, f, ell), ell);
+            double sig, M;
+            if constexpr (MODE == 0) {
+                const double iv = v != 0.0 ? 1.0 / v : 0.0;
+                sig = 1.0 / (kap[f] * b * b + iv);
+                M = sig * (kap[f] * b);
+            } else {
+                sig = 1.0 / (1.0 + kap[f] * b * b * v);
+                M = sig * (sqrt(v) * b * kap[f]);
+            }
+            p[f] = M;
+            p[F + f] = sqrt(sig);
+        }
+    } else {
+        const double tt = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 0, ell), ell);
+        const double ee = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 1, ell), ell);
+        const double bb = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 2, ell), ell);
+        const double te = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 3, ell), ell);
+        const double p0 = b * b * k0, p1 = b * b * k1, p2 = b * b * k2;
+        double s00, s11, s01, s22, M00, M01, M10, M11, M22;
+        if constexpr (MODE == 0) {
+            double it, ie, ite;
+            if (tt != 0.0 && ee != 0.0) {
+                const double det = tt * ee - te * te;
+                it = ee / det; ie = tt / det; ite = -te / det;
+            } else {
+                it = tt != 0.0 ? 1.0 / tt : 0.0;
+                ie = ee != 0.0 ? 1.0 / ee : 0.0;
+                ite = 0.0;
+            }
+            const double q00 = it + p0, q11 = ie + p1, q01 = ite;
+            const double det = q00 * q11 - q01 * q01;
+            s00 = q11 / det; s11 = q00 / det; s01 = -q01 / det;
+            const double ib = bb != 0.0 ? 1.0 / bb : 0.0;
+            s22 = 1.0 / (ib + p2);
+            M00 = s00 * (b * k0); M01 = s01 * (b * k1);
+            M10 = s01 * (b * k0); M11 = s11 * (b * k1);
+            M22 = s22 * (b * k2);
+        } else {
+            const CovChol A = cov_chol_teb(tt, ee, te, bb);
+            // Q = I + A^T P A, A = [[a00, 0], [a10, a11]]
+            const double q00 = 1.0 + A.a00 * A.a00 * p0 + A.a10 * A.a10 * p1;
+            const double q01 = A.a10 * A.a11 * p1;
+            const double q11 = 1.0 + A.a11 * A.a11 * p1;
+            const double det = q00 * q11 - q01 * q01;
+            s00 = q11 / det; s11 = q00 / det; s01 = -q01 / det;
+            s22 = 1.0 / (1.0 + A.aB * A.aB * p2);
+            // M = S A^T diag(b k): A^T = [[a00, a10], [0, a11]]
+            const double bt = b * k0, be = b * k1;
+            const double c00 = A.a00 * bt, c01 = A.a10 * be, c11 = A.a11 * be;   // A^T diag(bk)
+            M00 = s00 * c00; M01 = s00 * c01 + s01 * c11;
+            M10 = s01 * c00; M11 = s01 * c01 + s11 * c11;
+            M22 = s22 * (A.aB * b * k2);
+        }
+        const double l00 = sqrt(s00);
+        const double l10 = s01 / l00;
+        const double l11 = sqrt(fmax(s11 - l10 * l10, 0.0));
+        p[0] = M00; p[1] = M01; p[2] = M10; p[3] = M11; p[4] = M22;
+        p[5] = l00; p[6] = l10; p[7] = l11; p[8] = sqrt(s22); p[9] = 0.0;
+    }
+}
+
+// ============================================================================
+// fused CR draw + per-l statistics (the dominant, HBM-bound kernel)
+// ============================================================================
+template <int F>
+struct SweepAcc {
+    static constexpr int NS = F == 1 ? GS_NSTAT_1 : (F == 2 ? GS_NSTAT_2 : GS_NSTAT_3);
+    double v[NS];
+};
+
+template <int F, bool REPLAY, bool STORE>
+__global__ __launch_bounds__(256) void k_cr_sweep(int L, int nchains, int ntask, const int4* __restrict__ tasks,
+                                                  const double* __restrict__ d, const double* __restrict__ params,
+                                                  const double* __restrict__ z, double* __restrict__ s,
+                                                  double* __restrict__ partials, uint32_t seed_lo, uint32_t seed_hi,
+                                                  uint32_t iter, uint32_t substep, int chain0) {
+    constexpr int NS = SweepAcc<F>::NS;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (wave >= nchains * ntask) return;
+    // task-major order: the waves of one workgroup work on the same (l, m)
+    // tile of different chains and share the d_alm reads in L1/L2
+    const int task = wave / nchains;
+    const int chain = wave % nchains;
+    const int4 tk = tasks[task];
+    const int ell = L - WAVE * tk.x - 63 + lane;
+    const bool lane_ok = ell >= 0;
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    const uint32_t tag = TAG_CR | (substep << 8);
+
+    double pm[NP];
+    if (lane_ok) {
+        const double* pp = params + ((long long)chain * (L + 1) + ell) * NP;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) pm[q] = pp[q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) pm[q] = 0.0;
+    }
+    double acc[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) acc[q] = 0.0;
+
+    const double* zc = REPLAY ? z + (long long)chain * F * NR : nullptr;
+    double* sc = s + (long long)chain * F * NR;
+
+    for (int m = tk.y; m < tk.z; ++m) {
+        if (!(lane_ok && ell >= m)) continue;
+        const long long i = (long long)m * (2 * L + 1 - m) / 2 + ell;
+        const long long r = m == 0 ? (long long)ell : 2 * i - (L + 1);
+        const int nv = m == 0 ? 1 : 2;
+        double dv[F][2], zv[F][2], sv[F][2];
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            dv[f][0] = d[f * NR + r];
+            dv[f][1] = nv == 2 ? d[f * NR + r + 1] : 0.0;
+            if constexpr (REPLAY) {
+                zv[f][0] = zc[f * NR + r];
+                zv[f][1] = nv == 2 ? zc[f * NR + r + 1] : 0.0;
+            } else {
+                box_muller(philox((uint32_t)i, (uint32_t)f, tag, iter, key), zv[f][0], zv[f][1]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if constexpr (F == 3) {
+                sv[0][c] = pm[0] * dv[0][c] + pm[1] * dv[1][c] + pm[5] * zv[0][c];
+                sv[1][c] = pm[2] * dv[0][c] + pm[3] * dv[1][c] + pm[6] * zv[0][c] + pm[7] * zv[1][c];
+                sv[2][c] = pm[4] * dv[2][c] + pm[8] * zv[2][c];
+            } else {
+#pragma unroll
+                for (int f = 0; f < F; ++f) sv[f][c] = pm[f] * dv[f][c] + zv[f][c] * pm[F + f];
+            }
+        }
+        if (nv == 1) {
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[f][1] = 0.0;
+        }
+        if constexpr (STORE) {
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+                sc[f * NR + r] = sv[f][0];
+                if (nv == 2) sc[f * NR + r + 1] = sv[f][1];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if constexpr (F == 3) {
+                acc[0] += sv[0][c] * sv[0][c];
+                acc[1] += sv[1][c] * sv[1][c];
+                acc[2] += sv[2][c] * sv[2][c];
+                acc[3] += sv[0][c] * sv[1][c];
+                acc[4] += dv[0][c] * sv[0][c];
+                acc[5] += dv[1][c] * sv[0][c];
+                acc[6] += dv[1][c] * sv[1][c];
+                acc[7] += dv[2][c] * sv[2][c];
+            } else {
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    acc[f] += sv[f][c] * sv[f][c];
+                    acc[F + f] += dv[f][c] * sv[f][c];
+                }
+            }
+        }
+    }
+    double* po = partials + ((long long)chain * ntask + task) * NS * WAVE;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
+}
+
+// fixed-order reduction of the sweep partials: stats[chain][q][l]
+__global__ void k_stats_finish(int L, int nchains, int ntask, int nstat, const int* __restrict__ tile_task0,
+                               const double* __restrict__ partials, double* __restrict__ stats) {
+    const int Lp1 = L + 1;
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= (long long)nchains * nstat * Lp1) return;
+    const int ell = (int)(g % Lp1);
+    const int q = (int)((g / Lp1) % nstat);
+    const int chain = (int)(g / ((long long)Lp1 * nstat));
+    const int t = (L - ell) / WAVE;
+    const int lane = ell - (L - WAVE * t - 63);
+    double acc = 0.0;
+    for (int task = tile_task0[t]; task < tile_task0[t + 1]; ++task)
+        acc += partials[(((long long)chain * ntask + task) * nstat + q) * WAVE + lane];
+    stats[g] = acc;
+}
+
+// ============================================================================
+// centered C_l draw (CenteredGibbs.py:54-93) + TEB inverse-Wishart
+// ============================================================================
+// grid: (nchains, nspec); IG spectra one bin per thread
+template <int F>
+__global__ __launch_bounds__(256) void k_cls_draw(int L, int nchains, int maxbins, const int* __restrict__ bins,
+                                                  const int* __restrict__ nbins_arr, const double* __restrict__ stats,
+                                                  const double* __restrict__ variates, uint32_t seed_lo,
+                                                  uint32_t seed_hi, uint32_t iter, int chain0,
+                                                  double* __restrict__ dl_out) {
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    constexpr int NS = SweepAcc<F>::NS;
+    const int chain = blockIdx.x;
+    const int sp = blockIdx.y;
+    const int Lp1 = L + 1;
+    const int nb = nbins_arr[sp];
+    const int* be = bins + sp * (maxbins + 1);
+    const double* st = stats + (long long)chain * NS * Lp1;
+    double* out = dl_out + ((long long)chain * NSP + sp) * maxbins;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    // which stat row holds ss of this spectrum
+    int ssrow = sp;                 // F=1: ssTT=0; F=2: ssEE=0, ssBB=1; F=3: ssTT, ssEE, ssBB, ssTE = 0..3
+    const bool iw = (F == 3) && (sp != 2);
+    if (iw) {
+        if (sp != 0) return;        // the TT block draws TT, EE and TE together
+        for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+            double nu = 0.0, a = 0.0, dd = 0.0, c = 0.0;
+            for (int l = be[b]; l < be[b + 1]; ++l) {
+                const double w = (double)l * (l + 1) / (2.0 * PI);
+                nu += 2.0 * l + 1.0;
+                a += w * st[0 * Lp1 + l];
+                dd += w * st[1 * Lp1 + l];
+                c += w * st[3 * Lp1 + l];
+            }
+            nu -= 3.0;
+            double tt = 0.0, ee = 0.0, te = 0.0;
+            if (b >= 2) {
+                const double det = a * dd - c * c;
+                const double s00 = dd / det, s11 = a / det, s01 = -c / det;
+                const double l00 = sqrt(s00);
+                const double l10 = s01 / l00;
+                const double l11 = sqrt(s11 - l10 * l10);
+                const double c1 = sqrt(2.0 * gamma_mt(0.5 * nu, key, b, 16, iter, 0));
+                const double c2 = sqrt(2.0 * gamma_mt(0.5 * (nu - 1.0), key, b, 17, iter, 0));
+                const double n = normal1(key, b, 0, TAG_IW_N, iter);
+                const double b00 = l00 * c1;
+                const double b10 = l10 * c1 + l11 * n;
+                const double b11 = l11 * c2;
+                const double w00 = b00 * b00, w01 = b00 * b10, w11 = b10 * b10 + b11 * b11;
+                const double wd = w00 * w11 - w01 * w01;
+                tt = w11 / wd; ee = w00 / wd; te = -w01 / wd;
+            }
+            dl_out[((long long)chain * NSP + 0) * maxbins + b] = tt;
+            dl_out[((long long)chain * NSP + 1) * maxbins + b] = ee;
+            dl_out[((long long)chain * NSP + 3) * maxbins + b] = te;
+        }
+        return;
+    }
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        double beta = 0.0, expo = 0.0;
+        for (int l = be[b]; l < be[b + 1]; ++l) {
+            const double chat = st[ssrow * Lp1 + l] / (2.0 * l + 1.0);
+            beta += (2.0 * l + 1.0) * l * (l + 1.0) * (chat / (4.0 * PI));
+            expo += (2.0 * l + 1.0) / 2.0;
+        }
+        const double alpha = b == 0 ? 1.0 : expo - 1.0;
+        double X;
+        if (variates) X = variates[((long long)chain * NSP + sp) * maxbins + b];
+        else X = b < 2 ? 0.0 : 1.0 / gamma_mt(alpha, key, b, sp, iter, 0);
+        out[b] = b < 2 ? 0.0 : beta * X;
+    }
+}
+
+// ============================================================================
+// non-centered Metropolis-within-Gibbs (NonCenteredGibbs.py:292-445)
+// ============================================================================
+// standard normal truncated to [a, inf), a <= 0 (scipy truncnorm._ppf case_left)
+__device__ __forceinline__ double tn_ppf(double q, double a) {
+    const double pa = normcdf(a), pma = normcdf(-a);
+    const double plo = pa + q * pma;
+    const double phi = (1.0 - q) * pma;
+    return plo < 0.5 ? normcdfinv(plo) : -normcdfinv(phi);
+}
+
+__device__ __forceinline__ double log_ndtr(double x) {
+    if (x > -5.0) return log1p(-0.5 * erfc(x / sqrt(2.0)));
+    const double t = -x / sqrt(2.0);
+    return log(0.5 * erfcx(t)) - t * t;
+}
+
+// per-l log-likelihood term without the constant S_dd (NonCenteredGibbs.py:357-377)
+template <int F>
+__device__ __forceinline__ double f_ell(const double* __restrict__ st, int Lp1, int l, double b, double k0, double k1,
+                                        double k2, double v0, double v1, double v2, double v3) {
+    if constexpr (F == 1) {
+        const double a = sqrt(v0);
+        return -0.5 * k0 * (-2.0 * b * (a * st[1 * Lp1 + l]) + b * b * (a * a * st[0 * Lp1 + l]));
+    } else if constexpr (F == 2) {
+        const double aE = sqrt(v0), aB = sqrt(v1);
+        const double fE = -0.5 * k0 * (-2.0 * b * (aE * st[2 * Lp1 + l]) + b * b * (aE * aE * st[0 * Lp1 + l]));
+        const double fB = -0.5 * k1 * (-2.0 * b * (aB * st[3 * Lp1 + l]) + b * b * (aB * aB * st[1 * Lp1 + l]));
+        return fE + fB;
+    } else {
+        // v0..v3 = TT, EE, BB, TE
+        const CovChol A = cov_chol_teb(v0, v1, v3, v2);
+        const double ssTT = st[0 * Lp1 + l], ssEE = st[1 * Lp1 + l], ssBB = st[2 * Lp1 + l], ssTE = st[3 * Lp1 + l];
+        const double dTsT = st[4 * Lp1 + l], dEsT = st[5 * Lp1 + l], dEsE = st[6 * Lp1 + l], dBsB = st[7 * Lp1 + l];
+        const double fT = -0.5 * k0 * (-2.0 * b * (A.a00 * dTsT) + b * b * (A.a00 * A.a00 * ssTT));
+        const double linE = A.a10 * dEsT + A.a11 * dEsE;
+        const double quadE = A.a10 * A.a10 * ssTT + A.a10 * A.a11 * ssTE + A.a11 * A.a10 * ssTE + A.a11 * A.a11 * ssEE;
+        const double fE = -0.5 * k1 * (-2.0 * b * linE + b * b * quadE);
+        const double fB = -0.5 * k2 * (-2.0 * b * (A.aB * dBsB) + b * b * (A.aB * A.aB * ssBB));
+        return fT + fE + fB;
+    }
+}
+
+__device__ __forceinline__ bool psd_ok(double tt, double ee, double te) {
+    if (tt == 0.0 && te == 0.0) return ee >= 0.0;
+    return tt > 0.0 && ee > 0.0 && tt * ee - te * te > 0.0;
+}
+
+// fixed-order wave reduction; the lane-0 total is broadcast so every lane
+// takes the same accept decision
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return __shfl(v, 0, 64);
+}
+
+// one workgroup per chain; spectra sequential (MH order), blocks of a
+// spectrum in parallel (disjoint l ranges => independent), one wave per block
+template <int F>
+__global__ __launch_bounds__(256) void k_nc_mh(int L, int nchains, int maxbins, const int* __restrict__ bins,
+                                               const int* __restrict__ nbins_arr, const int* __restrict__ blocks,
+                                               const int* __restrict__ nblocks_arr, const int* __restrict__ acc_off,
+                                               const int* __restrict__ mh_order, int nacc, int n_iter_mh,
+                                               const int* __restrict__ ell2bin, const double* __restrict__ bl,
+                                               double k0, double k1, double k2, const double* __restrict__ prop_sd,
+                                               const double* __restrict__ stats, double* __restrict__ dl,
+                                               double* __restrict__ prop, double* __restrict__ logr,
+                                               const double* __restrict__ u_prop, const double* __restrict__ u_acc,
+                                               uint32_t seed_lo, uint32_t seed_hi, uint32_t iter, int chain0,
+                                               int32_t* __restrict__ accept_out) {
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    constexpr int NS = SweepAcc<F>::NS;
+    const int chain = blockIdx.x;
+    const int Lp1 = L + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    double* D = dl + (long long)chain * NSP * maxbins;
+    double* P = prop + (long long)chain * NSP * maxbins;
+    double* R = logr + (long long)chain * NSP * maxbins;
+    const double* st = stats + (long long)chain * NS * Lp1;
+
+    // proposals for every spectrum (NonCenteredGibbs.py:292-309) and the
+    // per-bin log proposal ratios (313-330, 410-413)
+    for (int sp = 0; sp < NSP; ++sp) {
+        const int nb = nbins_arr[sp];
+        const bool te = (F == 3 && sp == 3);
+        for (int b = 2 + tid; b < nb; b += blockDim.x) {
+            const double sd = prop_sd[sp * maxbins + b];
+            const double old = D[sp * maxbins + b];
+            double p, lr;
+            if (te) {
+                const double y = u_prop ? normcdfinv(u_prop[((long long)chain * NSP + sp) * maxbins + b])
+                                        : normal1(key, b, sp, TAG_TN, iter);
+                p = old + sd * y;
+                lr = 0.0;
+            } else {
+                const double a = -old / sd;
+                const double q = u_prop ? u_prop[((long long)chain * NSP + sp) * maxbins + b]
+                                        : uniform1(key, b, sp, TAG_TN, iter);
+                p = old + sd * tn_ppf(q, a);
+                lr = log_ndtr(old / sd) - log_ndtr(p / sd);
+            }
+            P[sp * maxbins + b] = p;
+            R[sp * maxbins + b] = lr;
+        }
+    }
+    __syncthreads();
+
+    for (int oi = 0; oi < NSP; ++oi) {
+        const int sp = mh_order[oi];
+        const int nbk = nblocks_arr[sp];
+        const int* be = bins + sp * (maxbins + 1);
+        const int* bk = blocks + sp * (maxbins + 1);
+        for (int att = 0; att < n_iter_mh; ++att) {
+            for (int blk = wv; blk < nbk; blk += 4) {
+                const int lo = bk[blk], hi = bk[blk + 1];
+                double diff = 0.0;
+                int bad = 0;
+                if (hi > lo) {
+                    for (int l = be[lo] + lane; l < be[hi]; l += 64) {
+                        double vo[4], vn[4];
+#pragma unroll
+                        for (int q = 0; q < NSP; ++q) {
+                            const double Dv = dl_at(D, ell2bin, maxbins, Lp1, q, l);
+                            vo[q] = var_from_dl(Dv, l);
+                            vn[q] = vo[q];
+                        }
+                        vn[sp] = var_from_dl(P[sp * maxbins + ell2bin[sp * Lp1 + l]], l);
+                        if constexpr (F == 3) {
+                            if (!psd_ok(vn[0], vn[1], vn[3])) { bad = 1; continue; }
+                        }
+                        const double b = bl[l];
+                        const double fn = f_ell<F>(st, Lp1, l, b, k0, k1, k2, vn[0], vn[1], NSP > 2 ? vn[2] : 0.0,
+                                                   NSP > 3 ? vn[3] : 0.0);
+                        const double fo = f_ell<F>(st, Lp1, l, b, k0, k1, k2, vo[0], vo[1], NSP > 2 ? vo[2] : 0.0,
+                                                   NSP > 3 ? vo[3] : 0.0);
+                        diff += fn - fo;
+                    }
+                }
+                double lrs = 0.0;
+                for (int q = lo + lane; q < hi; q += 64) lrs += R[sp * maxbins + q];
+                diff = wave_sum(diff);
+                lrs = wave_sum(lrs);
+                const int anybad = __any(bad);
+                const int flat = acc_off[sp] + blk * n_iter_mh + att;
+                const double u = u_acc ? u_acc[(long long)chain * nacc + flat]
+                                       : uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
+                const double log_r = anybad ? -INFINITY : diff + lrs;
+                const bool acc = log(u) < log_r;
+                if (acc)
+                    for (int q = lo + lane; q < hi; q += 64) D[sp * maxbins + q] = P[sp * maxbins + q];
+                if (lane == 0 && accept_out) accept_out[(long long)chain * nacc + flat] = acc ? 1 : 0;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// stats of s_nc = A^+ s, A = chol(C(dl)) (ASIS.py:185-189)
+template <int F>
+__global__ void k_stats_to_nc(int L, int nchains, int maxbins, const double* __restrict__ dl,
+                              const int* __restrict__ ell2bin, double* __restrict__ stats) {
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    constexpr int NS = SweepAcc<F>::NS;
+    const int Lp1 = L + 1;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nchains * Lp1) return;
+    const int chain = g / Lp1, l = g % Lp1;
+    const double* D = dl + (long long)chain * NSP * maxbins;
+    double* st = stats + (long long)chain * NS * Lp1;
+    if constexpr (F != 3) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const double v = var_from_dl(dl_at(D, ell2bin, maxbins, Lp1, f, l), l);
+            const double T = v != 0.0 ? sqrt(1.0 / v) : 0.0;
+            st[f * Lp1 + l] *= T * T;
+            st[(F + f) * Lp1 + l] *= T;
+        }
+    } else {
+        const double tt = var_from_dl(dl_at(D, ell2bin, maxbins, Lp1, 0, l), l);
+        const double ee = var_from_dl(dl_at(D, ell2bin, maxbins, Lp1, 1, l), l);
+        const double bb = var_from_dl(dl_at(D, ell2bin, maxbins, Lp1, 2, l), l);
+        const double te = var_from_dl(dl_at(D, ell2bin, maxbins, Lp1, 3, l), l);
+        const CovChol A = cov_chol_teb(tt, ee, te, bb);
+        const double i00 = A.a00 != 0.0 ? 1.0 / A.a00 : 0.0;
+        const double i11 = A.a11 != 0.0 ? 1.0 / A.a11 : 0.0;
+        const double t10 = -A.a10 * i00 * i11;
+        const double iB = A.aB != 0.0 ? 1.0 / A.aB : 0.0;
+        const double ssTT = st[0 * Lp1 + l], ssEE = st[1 * Lp1 + l], ssBB = st[2 * Lp1 + l], ssTE = st[3 * Lp1 + l];
+        const double dTsT = st[4 * Lp1 + l], dEsT = st[5 * Lp1 + l], dEsE = st[6 * Lp1 + l], dBsB = st[7 * Lp1 + l];
+        st[0 * Lp1 + l] = i00 * i00 * ssTT;
+        st[1 * Lp1 + l] = t10 * t10 * ssTT + 2.0 * t10 * i11 * ssTE + i11 * i11 * ssEE;
+        st[2 * Lp1 + l] = iB * iB * ssBB;
+        st[3 * Lp1 + l] = i00 * t10 * ssTT + i00 * i11 * ssTE;
+        st[4 * Lp1 + l] = dTsT * i00;
+        st[5 * Lp1 + l] = dEsT * i00;
+        st[6 * Lp1 + l] = dEsT * t10 + dEsE * i11;
+        st[7 * Lp1 + l] = dBsB * iB;
+    }
+}
+
+// s <- R_l s, R = A(C_new) [A(C_old)^+]
+template <int F>
+__global__ void k_recentre(int L, int nchains, int maxbins, const double* __restrict__ dl_new,
+                           const double* __restrict__ dl_old, const int* __restrict__ ell2bin, double* __restrict__ s) {
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    const int Lp1 = L + 1;
+    const long long nc = (long long)(L + 1) * (L + 2) / 2;
+    const long long NR = (long long)(L + 1) * (L + 1);
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < nc * nchains;
+         g += (long long)gridDim.x * blockDim.x) {
+        const int chain = (int)(g / nc);
+        const long long i = g % nc;
+        int l, m;
+        complex_index_to_lm(L, i, l, m);
+        const long long r = m == 0 ? (long long)l : 2 * i - (L + 1);
+        const int nv = m == 0 ? 1 : 2;
+        const double* Dn = dl_new + (long long)chain * NSP * maxbins;
+        const double* Do = dl_old ? dl_old + (long long)chain * NSP * maxbins : nullptr;
+        double* sc = s + (long long)chain * F * NR;
+        if constexpr (F != 3) {
+            for (int f = 0; f < F; ++f) {
+                double R = sqrt(var_from_dl(dl_at(Dn, ell2bin, maxbins, Lp1, f, l), l));
+                if (Do) {
+                    const double v = var_from_dl(dl_at(Do, ell2bin, maxbins, Lp1, f, l), l);
+                    R *= v != 0.0 ? sqrt(1.0 / v) : 0.0;
+                }
+                for (int c = 0; c < nv; ++c) sc[f * NR + r + c] *= R;
+            }
+        } else {
+            const CovChol An = cov_chol_teb(var_from_dl(dl_at(Dn, ell2bin, maxbins, Lp1, 0, l), l),
+                                            var_from_dl(dl_at(Dn, ell2bin, maxbins, Lp1, 1, l), l),
+                                            var_from_dl(dl_at(Dn, ell2bin, maxbins, Lp1, 3, l), l),
+                                            var_from_dl(dl_at(Dn, ell2bin, maxbins, Lp1, 2, l), l));
+            double t00 = 1.0, t10 = 0.0, t11 = 1.0, tB = 1.0;
+            if (Do) {
+                const CovChol Ao = cov_chol_teb(var_from_dl(dl_at(Do, ell2bin, maxbins, Lp1, 0, l), l),
+                                                var_from_dl(dl_at(Do, ell2bin, maxbins, Lp1, 1, l), l),
+                                                var_from_dl(dl_at(Do, ell2bin, maxbins, Lp1, 3, l), l),
+                                                var_from_dl(dl_at(Do, ell2bin, maxbins, Lp1, 2, l), l));
+                t00 = Ao.a00 != 0.0 ? 1.0 / Ao.a00 : 0.0;
+                t11 = Ao.a11 != 0.0 ? 1.0 / Ao.a11 : 0.0;
+                t10 = -Ao.a10 * t00 * t11;
+                tB = Ao.aB != 0.0 ? 1.0 / Ao.aB : 0.0;
+            }
+            const double r00 = An.a00 * t00;
+            const double r10 = An.a10 * t00 + An.a11 * t10;
+            const double r11 = An.a11 * t11;
+            const double rB = An.aB * tB;
+            for (int c = 0; c < nv; ++c) {
+                const double sT = sc[0 * NR + r + c], sE = sc[1 * NR + r + c];
+                sc[0 * NR + r + c] = r00 * sT;
+                sc[1 * NR + r + c] = r10 * sT + r11 * sE;
+                sc[2 * NR + r + c] *= rB;
+            }
+        }
+    }
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+namespace {
+
+template <typename T>
+int dev_upload(T** dst, const std::vector<T>& src) {
+    if (src.empty()) { *dst = nullptr; return 0; }
+    GS_CHECK(hipMalloc((void**)dst, src.size() * sizeof(T)));
+    GS_CHECK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+}
+
+template <typename T>
+int dev_alloc(T** dst, size_t n) {
+    GS_CHECK(hipMalloc((void**)dst, std::max<size_t>(n, 1) * sizeof(T)));
+    GS_CHECK(hipMemset(*dst, 0, std::max<size_t>(n, 1) * sizeof(T)));
+    return 0;
+}
+
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+inline unsigned nblk(long long n, int bs) { return (unsigned)std::max<long long>(1, std::min<long long>((n + bs - 1) / bs, 1 << 20)); }
+
+void build_tasks(gs_plan* p) {
+    const int L = p->L;
+    p->ntile = (L + 1 + WAVE - 1) / WAVE;
+    // rows per task: aim for >= 4096 waves so every SIMD has several to hide latency
+    int tm = 64;
+    auto count = [&](int rows_per) {
+        long long n = 0;
+        for (int t = 0; t < p->ntile; ++t) {
+            const int R = L - WAVE * t + 1;
+            n += (R + rows_per - 1) / rows_per;
+        }
+        return n;
+    };
+    while (tm > 4 && count(tm) * p->nchains < 4096) tm /= 2;
+    p->rows_per_task = tm;
+    std::vector<int4> tasks;
+    std::vector<int> t0;
+    for (int t = 0; t < p->ntile; ++t) {
+        t0.push_back((int)tasks.size());
+        const int R = L - WAVE * t + 1;
+        const int nch = (R + tm - 1) / tm;
+        for (int c = 0; c < nch; ++c) {
+            const int m0 = (int)((long long)c * R / nch), m1 = (int)((long long)(c + 1) * R / nch);
+            tasks.push_back(make_int4(t, m0, m1, 0));
+        }
+    }
+    t0.push_back((int)tasks.size());
+    p->ntask = (int)tasks.size();
+    dev_upload(&p->tasks, tasks);
+    dev_upload(&p->tile_task0, t0);
+}
+
+int check_plan(const gs_plan* p) {
+    if (!p) return set_error("null plan");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_abi_version(void) { return GS_ABI_VERSION; }
+const char* gs_last_error(void) { return g_last_error.c_str(); }
+
+int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
+    if (!desc || !out) return set_error("gs_plan_create: null argument");
+    const int L = desc->lmax, F = desc->nfields;
+    if (L < 2 || L > 16384) return set_error("gs_plan_create: lmax out of range");
+    if (F < 1 || F > 3) return set_error("gs_plan_create: nfields must be 1, 2 or 3");
+    if (desc->nchains < 1) return set_error("gs_plan_create: nchains < 1");
+    if (!desc->bl || !desc->noise_var) return set_error("gs_plan_create: bl / noise_var required");
+    gs_plan* p = new gs_plan();
+    GS_CHECK(hipGetDevice(&p->device));
+    p->L = L; p->F = F; p->nside = desc->nside; p->Npix = 12 * desc->nside * desc->nside;
+    p->nchains = desc->nchains; p->chain0 = desc->chain0; p->quirks = desc->quirks;
+    p->n_iter_mh = std::max(1, desc->n_iter_metropolis);
+    p->nspec = nspec_of(F); p->nstat = nstat_of(F);
+    for (int f = 0; f < F; ++f) {
+        if (!(desc->noise_var[f] > 0)) { delete p; return set_error("noise_var must be > 0"); }
+        p->kappa[f] = (double)p->Npix / (4.0 * PI * desc->noise_var[f]);
+    }
+    int maxbins = 0;
+    for (int sp = 0; sp < p->nspec; ++sp) {
+        if (!desc->bins[sp] || desc->nbin_edges[sp] < 2) { delete p; return set_error("bins required for every spectrum"); }
+        p->nbins[sp] = desc->nbin_edges[sp] - 1;
+        maxbins = std::max(maxbins, p->nbins[sp]);
+        const int* e = desc->bins[sp];
+        for (int i = 0; i + 1 < desc->nbin_edges[sp]; ++i)
+            if (e[i] < 0 || e[i + 1] < e[i] || e[i + 1] > L + 1) { delete p; return set_error("invalid bin edges"); }
+    }
+    p->maxbins = maxbins;
+    if (F == 3) {
+        for (int sp : {1, 3}) {
+            if (p->nbins[sp] != p->nbins[0] ||
+                !std::equal(desc->bins[sp], desc->bins[sp] + desc->nbin_edges[sp], desc->bins[0])) {
+                delete p;
+                return set_error("TEB: TT, EE and TE must share bins (inverse-Wishart draw)");
+            }
+        }
+    }
+    std::vector<double> bl(desc->bl, desc->bl + L + 1);
+    std::vector<int> ell2bin((size_t)p->nspec * (L + 1), -1), bins((size_t)p->nspec * (maxbins + 1), 0),
+        blocks((size_t)p->nspec * (maxbins + 1), 0);
+    std::vector<double> psd((size_t)p->nspec * maxbins, 0.0);
+    p->has_mh = true;
+    int off = 0;
+    if (F == 3) { p->mh_order[0] = 1; p->mh_order[1] = 2; p->mh_order[2] = 0; p->mh_order[3] = 3; }
+    for (int sp = 0; sp < p->nspec; ++sp) {
+        const int* e = desc->bins[sp];
+        for (int i = 0; i <= p->nbins[sp]; ++i) bins[sp * (maxbins + 1) + i] = e[i];
+        for (int i = 0; i < p->nbins[sp]; ++i)
+            for (int l = e[i]; l < e[i + 1]; ++l) ell2bin[sp * (L + 1) + l] = i;
+        if (desc->blocks[sp] && desc->nblock_edges[sp] >= 2) {
+            p->nblocks[sp] = desc->nblock_edges[sp] - 1;
+            for (int i = 0; i <= p->nblocks[sp]; ++i)
+                blocks[sp * (maxbins + 1) + i] = std::min(std::max(desc->blocks[sp][i], 0), p->nbins[sp]);
+        } else {
+            p->has_mh = false;
+        }
+        if (desc->prop_var[sp]) {
+            for (int b = 2; b < p->nbins[sp]; ++b) psd[sp * maxbins + b] = std::sqrt(desc->prop_var[sp][b - 2]);
+        } else {
+            p->has_mh = false;
+        }
+    }
+    for (int oi = 0; oi < p->nspec; ++oi) {
+        const int sp = p->mh_order[oi];
+        p->acc_off[sp] = off;
+        off += p->nblocks[sp] * p->n_iter_mh;
+    }
+    p->nacc = off;
+    int rc = 0;
+    rc |= dev_upload(&p->bl, bl);
+    rc |= dev_upload(&p->ell2bin, ell2bin);
+    rc |= dev_upload(&p->bins, bins);
+    rc |= dev_upload(&p->blocks, blocks);
+    rc |= dev_upload(&p->prop_sd, psd);
+    std::vector<int> meta(16, 0);
+    for (int k = 0; k < 4; ++k) {
+        meta[k] = p->nbins[k]; meta[4 + k] = p->nblocks[k]; meta[8 + k] = p->acc_off[k]; meta[12 + k] = p->mh_order[k];
+    }
+    rc |= dev_upload(&p->meta, meta);
+    build_tasks(p);
+    const size_t nc = (size_t)p->nchains;
+    rc |= dev_alloc(&p->partials, nc * p->ntask * p->nstat * WAVE);
+    rc |= dev_alloc(&p->params, nc * (L + 1) * NP);
+    rc |= dev_alloc(&p->stats, nc * p->nstat * (L + 1));
+    rc |= dev_alloc(&p->prop, nc * p->nspec * maxbins);
+    rc |= dev_alloc(&p->logr, nc * p->nspec * maxbins);
+    rc |= dev_alloc(&p->dl_tmp, nc * p->nspec * maxbins);
+    if (rc) { gs_plan_destroy(p); return -1; }
+    *out = p;
+    return 0;
+}
+
+int gs_plan_destroy(gs_plan* p) {
+    if (!p) return 0;
+    void* bufs[] = {p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->tile_task0, p->partials,
+                    p->params, p->stats, p->prop, p->logr, p->dl_tmp};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+    delete p;
+    return 0;
+}
+
+int gs_plan_info(const gs_plan* p, int* maxbins, int* nstat, int* nblocks_total, int* nspec) {
+    if (check_plan(p)) return -1;
+    if (maxbins) *maxbins = p->maxbins;
+    if (nstat) *nstat = p->nstat;
+    if (nblocks_total) *nblocks_total = p->nacc;
+    if (nspec) *nspec = p->nspec;
+    return 0;
+}
+
+// ---- stand-alone helpers ----------------------------------------------------
+int gs_var_expand(int lmax, int n, const double* dl, double* var, void* stream) {
+    const long long nc = (long long)(lmax + 1) * (lmax + 2) / 2 * n;
+    hipLaunchKernelGGL(k_var_expand, dim3(nblk(nc, 256)), dim3(256), 0, S(stream), lmax, n, dl, var);
+    GS_LAUNCH_CHECK("k_var_expand");
+    return 0;
+}
+
+int gs_real_to_complex(int lmax, int n, const double* re, double* cx, void* stream) {
+    const long long nc = (long long)(lmax + 1) * (lmax + 2) / 2 * n;
+    hipLaunchKernelGGL(k_real_to_complex, dim3(nblk(nc, 256)), dim3(256), 0, S(stream), lmax, n, re, cx);
+    GS_LAUNCH_CHECK("k_real_to_complex");
+    return 0;
+}
+
+int gs_complex_to_real(int lmax, int n, const double* cx, double* re, void* stream) {
+    const long long nc = (long long)(lmax + 1) * (lmax + 2) / 2 * n;
+    hipLaunchKernelGGL(k_complex_to_real, dim3(nblk(nc, 256)), dim3(256), 0, S(stream), lmax, n, cx, re);
+    GS_LAUNCH_CHECK("k_complex_to_real");
+    return 0;
+}
+
+int gs_remove_monopole_dipole(int lmax, int n, double* alm, void* stream) {
+    hipLaunchKernelGGL(k_remove_md, dim3(nblk(n, 64)), dim3(64), 0, S(stream), lmax, n, alm);
+    GS_LAUNCH_CHECK("k_remove_md");
+    return 0;
+}
+
+int gs_alm2cl(int lmax, int n, const double* x, const double* y, double* cl, void* stream) {
+    const int ntile = (lmax + WAVE) / WAVE;
+    const long long waves = (long long)n * ntile;
+    hipLaunchKernelGGL(k_alm2cl, dim3(nblk(waves, 4)), dim3(256), 0, S(stream), lmax, n, x, y ? y : x, cl);
+    GS_LAUNCH_CHECK("k_alm2cl");
+    return 0;
+}
+
+int gs_unfold_bins(int n, const double* binned, const int* bins, int nbins, double* out, void* stream) {
+    hipLaunchKernelGGL(k_unfold, dim3(nblk(nbins, 256), n), dim3(256), 0, S(stream), n, binned, bins, nbins, out);
+    GS_LAUNCH_CHECK("k_unfold");
+    return 0;
+}
+
+// ---- plan stages -----------------------------------------------------------------
+int gs_block_params(gs_plan* p, int mode, const double* dl, double* params, void* stream) {
+    if (check_plan(p)) return -1;
+    const long long n = (long long)p->nchains * (p->L + 1);
+    const dim3 g(nblk(n, 256)), b(256);
+#define GS_BP(FF, MM) hipLaunchKernelGGL((k_block_params<FF, MM>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, dl, \
+                                         p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], params)
+    if (mode == GS_MODE_CENTERED) {
+        if (p->F == 1) GS_BP(1, 0); else if (p->F == 2) GS_BP(2, 0); else GS_BP(3, 0);
+    } else if (mode == GS_MODE_NONCENTERED) {
+        if (p->F == 1) GS_BP(1, 1); else if (p->F == 2) GS_BP(2, 1); else GS_BP(3, 1);
+    } else {
+        return set_error("gs_block_params: bad mode");
+    }
+#undef GS_BP
+    GS_LAUNCH_CHECK("k_block_params");
+    return 0;
+}
+
+static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1) {
+    if (!p->timing) return 0;
+    if (p->ev_used + 2 > p->ev.size()) {
+        for (int k = 0; k < 64; ++k) {
+            hipEvent_t e;
+            GS_CHECK(hipEventCreate(&e));
+            p->ev.push_back(e);
+        }
+    }
+    *e0 = p->ev[p->ev_used];
+    *e1 = p->ev[p->ev_used + 1];
+    p->ev_used += 2;
+    GS_CHECK(hipEventRecord(*e0, s));
+    return 0;
+}
+
+int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
+                uint32_t iteration, uint32_t substep, double* s_out, double* stats, void* stream) {
+    if (check_plan(p)) return -1;
+    if (!d_alm || !params || !stats) return set_error("gs_cr_sweep: null argument");
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    const long long waves = (long long)p->nchains * p->ntask;
+    const dim3 g(nblk(waves, 4)), b(256);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing_begin(p, S(stream), &e0, &e1)) return -1;
+    const bool rep = z != nullptr, st = s_out != nullptr;
+#define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntask, \
+                                             p->tasks, d_alm, params, z, s_out, p->partials, slo, shi, iteration,  \
+                                             substep, p->chain0)
+#define GS_SWF(FF) do { if (rep && st) GS_SW(FF, true, true); else if (rep) GS_SW(FF, true, false); \
+                        else if (st) GS_SW(FF, false, true); else GS_SW(FF, false, false); } while (0)
+    if (p->F == 1) GS_SWF(1); else if (p->F == 2) GS_SWF(2); else GS_SWF(3);
+#undef GS_SWF
+#undef GS_SW
+    GS_LAUNCH_CHECK("k_cr_sweep");
+    if (p->timing) GS_CHECK(hipEventRecord(e1, S(stream)));
+    const long long n = (long long)p->nchains * p->nstat * (p->L + 1);
+    hipLaunchKernelGGL(k_stats_finish, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, p->ntask,
+                       p->nstat, p->tile_task0, p->partials, stats);
+    GS_LAUNCH_CHECK("k_stats_finish");
+    return 0;
+}
+
+int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_t seed, uint32_t iteration,
+                double* dl_out, void* stream) {
+    if (check_plan(p)) return -1;
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    const dim3 g(p->nchains, p->nspec), b(256);
+#define GS_CD(FF) hipLaunchKernelGGL((k_cls_draw<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
+                                     stats, variates, slo, shi, iteration, p->chain0, dl_out)
+    if (p->F == 1) GS_CD(1); else if (p->F == 2) GS_CD(2); else GS_CD(3);
+#undef GS_CD
+    GS_LAUNCH_CHECK("k_cls_draw");
+    return 0;
+}
+
+int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, const double* u_acc, uint64_t seed,
+             uint32_t iteration, int32_t* accept_out, void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->has_mh) return set_error("gs_nc_mh: plan has no MH blocks / proposal variances");
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    const dim3 g(p->nchains), b(256);
+#define GS_MH(FF) hipLaunchKernelGGL((k_nc_mh<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
+                                     p->blocks, p->meta + 4, p->meta + 8, p->meta + 12, p->nacc, p->n_iter_mh,     \
+                                     p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], p->prop_sd, stats, dl, \
+                                     p->prop, p->logr, u_prop, u_acc, slo, shi, iteration, p->chain0, accept_out)
+    if (p->F == 1) GS_MH(1); else if (p->F == 2) GS_MH(2); else GS_MH(3);
+#undef GS_MH
+    GS_LAUNCH_CHECK("k_nc_mh");
+    return 0;
+}
+
+int gs_stats_to_noncentered(gs_plan* p, const double* dl, double* stats, void* stream) {
+    if (check_plan(p)) return -1;
+    const long long n = (long long)p->nchains * (p->L + 1);
+#define GS_TN(FF) hipLaunchKernelGGL((k_stats_to_nc<FF>), dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, \
+                                     p->maxbins, dl, p->ell2bin, stats)
+    if (p->F == 1) GS_TN(1); else if (p->F == 2) GS_TN(2); else GS_TN(3);
+#undef GS_TN
+    GS_LAUNCH_CHECK("k_stats_to_nc");
+    return 0;
+}
+
+int gs_recentre(gs_plan* p, const double* dl_new, const double* dl_old, double* s, void* stream) {
+    if (check_plan(p)) return -1;
+    const long long n = (long long)p->nchains * (p->L + 1) * (p->L + 2) / 2;
+#define GS_RC(FF) hipLaunchKernelGGL((k_recentre<FF>), dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, \
+                                     p->maxbins, dl_new, dl_old, p->ell2bin, s)
+    if (p->F == 1) GS_RC(1); else if (p->F == 2) GS_RC(2); else GS_RC(3);
+#undef GS_RC
+    GS_LAUNCH_CHECK("k_recentre");
+    return 0;
+}
+
+// ---- fused iterations ------------------------------------------------------
+int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
+                     const double* igvar, uint64_t seed, uint32_t it, void* stream) {
+    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
+    if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
+    return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
+}
+
+int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
+                        const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
+                        void* stream) {
+    if (gs_block_params(p, GS_MODE_NONCENTERED, dl, p->params, stream)) return -1;
+    if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
+    return gs_nc_mh(p, p->stats, dl, u_prop, u_acc, seed, it, accept_out, stream);
+}
+
+int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z, const double* igvar,
+                 const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
+                 double* dl_tmp_out, int recentre, void* stream) {
+    double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
+    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
+    if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
+    if (gs_cls_draw(p, p->stats, igvar, seed, it, tmp, stream)) return -1;
+    if (gs_stats_to_noncentered(p, tmp, p->stats, stream)) return -1;
+    const size_t bytes = (size_t)p->nchains * p->nspec * p->maxbins * sizeof(double);
+    GS_CHECK(hipMemcpyAsync(dl, tmp, bytes, hipMemcpyDeviceToDevice, S(stream)));
+    if (gs_nc_mh(p, p->stats, dl, u_prop, u_acc, seed, it, accept_out, stream)) return -1;
+    if (recentre && s_out) {
+        // ASIS.py:203 (quirk) re-centres the centered map: s <- A(C_new) s;
+        // the corrected form is s <- A(C_new) A(C_tmp)^+ s
+        const bool quirk = (p->quirks & GS_QUIRK_ASIS_RECENTRE_CENTERED) != 0;
+        if (gs_recentre(p, dl, quirk ? nullptr : tmp, s_out, stream)) return -1;
+    }
+    return 0;
+}
+
+int gs_sweep_timing(gs_plan* p, int enable, double* total_ms, int* count) {
+    if (check_plan(p)) return -1;
+    if (enable) {
+        p->timing = true;
+        p->ev_used = 0;
+        return 0;
+    }
+    double tot = 0.0;
+    int n = 0;
+    for (size_t k = 0; k + 1 < p->ev_used; k += 2) {
+        GS_CHECK(hipEventSynchronize(p->ev[k + 1]));
+        float ms = 0.f;
+        GS_CHECK(hipEventElapsedTime(&ms, p->ev[k], p->ev[k + 1]));
+        tot += ms;
+        ++n;
+    }
+    p->timing = false;
+    p->ev_used = 0;
+    if (total_ms) *total_ms = tot;
+    if (count) *count = n;
+    return 0;
+}
+
+}  // extern "C"

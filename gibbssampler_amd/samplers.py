@@ -1,0 +1,130 @@
+"""Batched full-sky Gibbs drivers on the device (the loops of the reference drivers).
+
+``BatchedRunner`` runs ``nchains`` chains of one of the three samplers in
+lock-step on one GPU:
+
+  * ``centered``    GibbsSampler.run_polarization (GibbsSampler.py:118-180): an
+                    initial CR (ula=True, GibbsSampler.py:41,136-138), then per
+                    iteration CR (closed form, CenteredGibbs.py:317-353 -- the
+                    exact full-sky limit of the PCG branch) + inverse-Gamma /
+                    inverse-Wishart C_l draw.  History includes the start.
+  * ``noncentered`` NonCenteredGibbs.run_polarization (NonCenteredGibbs.py:529-571),
+                    all_sph: non-centered CR + MH blocks.  History includes the start.
+  * ``asis``        ASIS.run_polarization (ASIS.py:134-226): centered CR, centered
+                    C_l draw, non-centering, NC MH, re-centring.  History
+                    excludes the start (ASIS.py:150-206).
+
+Everything stays in HBM; only the returned histories are copied back.
+"""
+import time
+
+import numpy as np
+import torch
+
+from .engine import GibbsPlan, MH_ORDER
+
+INIT_ITER = 0xFFFFFFFF
+
+
+class BatchedRunner:
+    def __init__(self, kind, lmax, nside, nfields, nchains, bl, noise_var, bins, d_alm, blocks=None,
+                 proposal_variances=None, rng="native", seed=0, chain0=0, quirks=1, n_iter_metropolis=1,
+                 materialize_recentre=False, store_skymap=True):
+        if kind not in ("centered", "noncentered", "asis"):
+            raise ValueError(kind)
+        if rng not in ("native", "replay"):
+            raise ValueError(rng)
+        self.kind, self.rng, self.seed = kind, rng, int(seed)
+        self.plan = GibbsPlan(lmax, nside, nfields, nchains, bl, noise_var, bins, blocks=blocks,
+                              proposal_variances=proposal_variances, chain0=chain0, quirks=quirks,
+                              n_iter_metropolis=n_iter_metropolis)
+        p = self.plan
+        self.d = p.data_tensor(d_alm)
+        self.s = p.zeros(p.nchains, p.F, p.NR) if store_skymap else None
+        self.dl = None
+        self.dl_tmp = p.zeros(p.nchains, p.nspec, p.maxbins)
+        self.accept = p.zeros(p.nchains, max(p.nacc, 1), dtype=torch.int32)
+        self.materialize_recentre = materialize_recentre
+        self.iteration = 0
+
+    # -- one iteration ---------------------------------------------------------------
+    def _replay(self):
+        p = self.plan
+        z = p.replay_cr_normals()
+        ig = up = ua = None
+        if self.kind in ("centered", "asis"):
+            ig = p.replay_invgamma()
+        if self.kind in ("noncentered", "asis"):
+            up, ua = p.replay_mh_uniforms()
+        return z, ig, up, ua
+
+    def init(self, dls_init):
+        p = self.plan
+        self.dl = p.dl_tensor(dls_init)
+        self.iteration = 0
+        if self.kind == "centered":
+            # the reference's initial CR (GibbsSampler.py:136-138) -- consumes its draws
+            z = p.replay_cr_normals() if self.rng == "replay" else None
+            params = p.block_params(0, self.dl)
+            p.cr_sweep(self.d, params, z=z, seed=self.seed, iteration=INIT_ITER, s_out=self.s,
+                       store=self.s is not None)
+
+    def step(self):
+        p = self.plan
+        it = self.iteration + 1
+        z = ig = up = ua = None
+        if self.rng == "replay":
+            z, ig, up, ua = self._replay()
+        if self.kind == "centered":
+            p.step_centered(self.d, self.dl, self.s, z=z, igvar=ig, seed=self.seed, iteration=it)
+        elif self.kind == "noncentered":
+            p.step_noncentered(self.d, self.dl, self.s, z=z, u_prop=up, u_acc=ua, seed=self.seed, iteration=it,
+                               accept=self.accept)
+        else:
+            p.step_asis(self.d, self.dl, self.s, z=z, igvar=ig, u_prop=up, u_acc=ua, seed=self.seed, iteration=it,
+                        accept=self.accept, dl_tmp=self.dl_tmp, recentre=self.materialize_recentre)
+        self.iteration = it
+
+    # -- a whole run --------------------------------------------------------------------
+    def run(self, dls_init, n_iter, timings=False):
+        p = self.plan
+        self.init(dls_init)
+        with_start = self.kind != "asis"
+        H = p.zeros(n_iter + (1 if with_start else 0), p.nchains, p.nspec, p.maxbins)
+        A = p.zeros(n_iter, p.nchains, max(p.nacc, 1), dtype=torch.int32)
+        if with_start:
+            H[0].copy_(self.dl)
+        t_steps = []
+        for i in range(n_iter):
+            t0 = time.perf_counter() if timings else 0.0
+            self.step()
+            H[i + (1 if with_start else 0)].copy_(self.dl)
+            if self.kind != "centered":
+                A[i].copy_(self.accept)
+            if timings:
+                torch.cuda.synchronize()
+                t_steps.append(time.perf_counter() - t0)
+        Hn = H.cpu().numpy()
+        hist = {s: Hn[:, :, k, :len(p.bins[s]) - 1] for k, s in enumerate(p.spectra)}
+        acc = None
+        if self.kind != "centered":
+            An = A.cpu().numpy()
+            acc, off = {}, 0
+            for s in MH_ORDER[p.F]:
+                n = (len(p.blocks[s]) - 1) * p.n_iter_metropolis
+                acc[s] = An[:, :, off:off + n]
+                off += n
+        if timings:
+            return hist, acc, np.array(t_steps)
+        return hist, acc
+
+    def skymap(self):
+        """Current sky map [nchains, F, (L+1)^2] as the reference would hold it
+        (for ASIS with lazy re-centring the re-centred map is materialised here)."""
+        if self.s is None:
+            return None
+        s = self.s.clone()
+        if self.kind == "asis" and not self.materialize_recentre and self.iteration > 0:
+            quirk = True
+            self.plan.recentre(self.dl, s, None if quirk else self.dl_tmp)
+        return s

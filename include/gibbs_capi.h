@@ -1,0 +1,148 @@
+/*
+ * gibbs_capi.h -- C-ABI of libgibbs_hip.so, the MI355X-native Gibbs hot path.
+ *
+ * Plain pointers and sizes only.  All array pointers passed to gs_* compute
+ * calls are DEVICE pointers (caller-owned, e.g. torch tensor.data_ptr());
+ * gs_model_desc carries HOST pointers that are copied once at plan creation.
+ * Every compute call is asynchronous on the given hipStream_t (passed as
+ * void*, NULL = default stream) and returns 0 on success, <0 on error with a
+ * message in gs_last_error().  A plan is bound to the device that was current
+ * when it was created; it is not thread-safe.  No call allocates, copies
+ * host<->device or synchronises, so every step is capturable in a hipGraph.
+ *
+ * Reference interfaces replaced (Gabriel-Ducrocq/GibbsSampler, file:line):
+ *   gs_var_expand            utils.generate_var_cl             utils.py:114-147,
+ *                            variance_expension.generate_var_cl_cython  variance_expension.pyx:8-33
+ *   gs_real_to_complex       utils.real_to_complex             utils.py:49-60, variance_expension.pyx:84-100
+ *   gs_complex_to_real       utils.complex_to_real             utils.py:63-76, variance_expension.pyx:65-81
+ *   gs_remove_monopole_dipole  remove_monopole_dipole_contributions  variance_expension.pyx:103-111
+ *   gs_alm2cl                hp.alm2cl on real-layout a_lm     CenteredGibbs.py:30,61
+ *   gs_unfold_bins           utils.unfold_bins                 utils.py:150-162
+ *   gs_block_params          per-l Sigma/Cholesky of the CR    CenteredGibbs.py:324-337 (centered),
+ *                            NonCenteredGibbs.py:141-151 (non-centered); TEB 3x3 semantics of the
+ *                            cp38 helpers compute_inverse_and_cholesky / compute_sigma_and_chol
+ *   gs_cr_sweep              the Gaussian CR draw + alm2cl/sufficient-statistic reduction
+ *                            CenteredGibbs.py:340-353, NonCenteredGibbs.py:160-176
+ *   gs_cls_draw              PolarizedCenteredClsSampler.sample CenteredGibbs.py:54-93 (+ TEB inverse-Wishart)
+ *   gs_nc_mh                 PolarizationNonCenteredClsSampler.sample NonCenteredGibbs.py:292-445 (all_sph)
+ *   gs_stats_to_noncentered  ASIS non-centering s_nc = C^-1/2 s  ASIS.py:185-189
+ *   gs_step_centered / gs_step_noncentered / gs_step_asis
+ *                            one iteration of GibbsSampler.run_polarization GibbsSampler.py:142-173,
+ *                            NonCenteredGibbs.run_polarization NonCenteredGibbs.py:546-560,
+ *                            ASIS.run_polarization ASIS.py:158-206
+ *
+ * Layouts (fp64):
+ *   real a_lm layout, NR = (L+1)^2 per field (utils.py:49-76); alm arrays are
+ *   [nchains][nfields][NR]; data d_alm is [nfields][NR] (shared by chains).
+ *   binned spectra: [nchains][nspec][maxbins] (maxbins = max over spectra).
+ *   statistics: [nchains][nstat][L+1], see GS_NSTAT_* below.
+ *   fields: nfields=1 (T), 2 (E,B), 3 (T,E,B); spectra: [TT] / [EE,BB] /
+ *   [TT,EE,BB,TE].
+ *
+ * RNG: replay mode when the variate pointer is non-NULL (host-drawn numpy
+ * variates in the reference's draw order); native mode otherwise
+ * (Philox4x32-10 keyed by (seed, global chain id), counter = (element,
+ * field, tag|substep, iteration); independent of launch geometry).
+ */
+#ifndef GIBBS_CAPI_H
+#define GIBBS_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+#define GS_MODE_CENTERED 0
+#define GS_MODE_NONCENTERED 1
+
+#define GS_QUIRK_ASIS_RECENTRE_CENTERED 1   /* ASIS.py:203 re-centres the centered map */
+
+/* number of per-l statistics per chain, by nfields:
+ *  1: [ssTT, dTsT]
+ *  2: [ssEE, ssBB, dEsE, dBsB]
+ *  3: [ssTT, ssEE, ssBB, ssTE, dTsT, dEsT, dEsE, dBsB]
+ * ss = sum over the slots of l of s_X s_Y ; dXsY = sum of d_X s_Y. */
+#define GS_NSTAT_1 2
+#define GS_NSTAT_2 4
+#define GS_NSTAT_3 8
+#define GS_NPARAM 10   /* doubles per (chain, l) in a block-parameter table */
+
+typedef struct gs_plan gs_plan;
+
+typedef struct gs_model_desc {
+    int lmax;                 /* L                                           */
+    int nside;                /* HEALPix N_side (Npix = 12 N_side^2)          */
+    int nfields;              /* 1, 2 or 3                                    */
+    int nchains;              /* chains batched in this plan                  */
+    int chain0;               /* global id of the plan's first chain (RNG key) */
+    int quirks;               /* GS_QUIRK_* bit set                           */
+    int n_iter_metropolis;    /* MH attempts per block (NonCenteredGibbs.py:427) */
+    const double* bl;         /* host [L+1] beam b_l                          */
+    const double* noise_var;  /* host [nfields] per-pixel noise variance      */
+    const int* bins[4];       /* host bin edges per spectrum                  */
+    int nbin_edges[4];        /* number of edges (= nbins + 1)                */
+    const int* blocks[4];     /* host MH block edges per spectrum (nullable)  */
+    int nblock_edges[4];
+    const double* prop_var[4];/* host [nbins-2] MH proposal variances (nullable) */
+} gs_model_desc;
+
+int gs_abi_version(void);
+const char* gs_last_error(void);
+
+int gs_plan_create(const gs_model_desc* desc, gs_plan** out);
+int gs_plan_destroy(gs_plan* plan);
+/* query sizes of the plan's layouts */
+int gs_plan_info(const gs_plan* plan, int* maxbins, int* nstat, int* nblocks_total, int* nspec);
+
+/* ---- stand-alone layout / expansion helpers (no plan needed) ---------------- */
+int gs_var_expand(int lmax, int n, const double* dl, double* var, void* stream);
+int gs_real_to_complex(int lmax, int n, const double* re, double* cplx_interleaved, void* stream);
+int gs_complex_to_real(int lmax, int n, const double* cplx_interleaved, double* re, void* stream);
+int gs_remove_monopole_dipole(int lmax, int n, double* alm, void* stream);
+int gs_alm2cl(int lmax, int n, const double* x, const double* y, double* cl, void* stream);
+int gs_unfold_bins(int n, const double* binned, const int* bins, int nbins, double* out, void* stream);
+
+/* ---- plan-level hot-path stages ------------------------------------------- */
+/* per-(chain, l) (M, Cholesky) table of the CR: s = M d + Lchol z */
+int gs_block_params(gs_plan* plan, int mode, const double* dl_binned, double* params, void* stream);
+/* fused CR draw + statistics: writes s (nullable => not stored) and stats */
+int gs_cr_sweep(gs_plan* plan, const double* d_alm, const double* params, const double* z_replay,
+                uint64_t seed, uint32_t iteration, uint32_t substep,
+                double* s_out, double* stats, void* stream);
+/* centered C_l draw (inverse-Gamma; TEB: inverse-Wishart TT/EE/TE) */
+int gs_cls_draw(gs_plan* plan, const double* stats, const double* invgamma_replay,
+                uint64_t seed, uint32_t iteration, double* dl_binned_out, void* stream);
+/* non-centered Metropolis-within-Gibbs over blocks (in/out dl_binned) */
+int gs_nc_mh(gs_plan* plan, const double* stats, double* dl_binned,
+             const double* u_prop_replay, const double* u_accept_replay,
+             uint64_t seed, uint32_t iteration, int32_t* accept_out, void* stream);
+/* stats of s_nc = A(C)^+ s with A = chol(C(dl_binned)) (ASIS non-centering) */
+int gs_stats_to_noncentered(gs_plan* plan, const double* dl_binned, double* stats, void* stream);
+/* s <- T_l s for T_l = A(C(dl_new)) [A(C(dl_old))^+ unless dl_old NULL] */
+int gs_recentre(gs_plan* plan, const double* dl_new, const double* dl_old, double* s, void* stream);
+
+/* ---- fused iterations ------------------------------------------------------ */
+int gs_step_centered(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
+                     const double* z_replay, const double* invgamma_replay,
+                     uint64_t seed, uint32_t iteration, void* stream);
+int gs_step_noncentered(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
+                        const double* z_replay, const double* u_prop_replay, const double* u_accept_replay,
+                        uint64_t seed, uint32_t iteration, int32_t* accept_out, void* stream);
+/* dl_tmp_out: nullable, receives the centered draw; recentre: 0 lazy (s_out keeps the
+ * centered CR draw), 1 materialise the re-centred map in s_out */
+int gs_step_asis(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
+                 const double* z_replay, const double* invgamma_replay,
+                 const double* u_prop_replay, const double* u_accept_replay,
+                 uint64_t seed, uint32_t iteration, int32_t* accept_out, double* dl_tmp_out,
+                 int recentre, void* stream);
+
+/* device-side timing of the dominant kernel (hipEvents on the plan's stream) */
+int gs_sweep_timing(gs_plan* plan, int enable, double* total_ms, int* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GIBBS_CAPI_H */
