@@ -55,6 +55,7 @@ _SIGS = [
     ("gs_plan_create", ctypes.c_int, [ctypes.POINTER(GsModelDesc), ctypes.POINTER(_VP)]),
     ("gs_plan_destroy", ctypes.c_int, [_VP]),
     ("gs_plan_info", ctypes.c_int, [_VP, c_int_p, c_int_p, c_int_p, c_int_p]),
+    ("gs_plan_sweep_info", ctypes.c_int, [_VP, c_int_p, c_int_p]),
     ("gs_var_expand", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_real_to_complex", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_complex_to_real", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),

@@ -20,6 +20,7 @@
 #include <vector>
 #include <cstring>
 #include <algorithm>
+#include <cstdlib>
 
 #include "gibbs_capi.h"
 #include "gs_rng.h"
@@ -69,6 +70,14 @@ struct gs_plan {
     int nacc = 0;                    // accept flags per chain
     int mh_order[4] = {0, 1, 2, 3};
     bool has_mh = false;
+    // MH phases: spectra whose blocks are mutually independent run in one launch
+    int nphase = 0;
+    int phase_n[4] = {0, 0, 0, 0};
+    int phase_off[4] = {0, 0, 0, 0};
+    int2* phase_tab = nullptr;       // (spectrum, block) pairs, phase-major
+    int phase_sp[4][2] = {{-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}};
+    int* ell2blk = nullptr;          // [nspec][L+1] MH block of each l (-1: none)
+    double* gbuf = nullptr;          // [nchains][2][L+1] per-l likelihood differences
     // device constants
     double* bl = nullptr;            // [L+1]
     int* ell2bin = nullptr;          // [nspec][L+1]
@@ -76,11 +85,11 @@ struct gs_plan {
     int* blocks = nullptr;           // [nspec][maxbins+1] (clipped edges)
     double* prop_sd = nullptr;       // [nspec][maxbins]
     int* meta = nullptr;             // [16]: nbins[4], nblocks[4], acc_off[4], mh_order[4]
-    int4* tasks = nullptr;           // [ntask] (tile, m0, m1, 0)
-    int* tile_task0 = nullptr;       // [ntile+1]
-    int ntask = 0, ntile = 0, rows_per_task = 64;
+    int2* tasks = nullptr;           // [npair] (tile group, row chunk) of the CR sweep
+    int npair = 0, ntile = 0, nchunk = 0, rows_per_task = 64;
+    int ntask = 0;                   // valid (tile, chunk) waves per chain
     // workspace
-    double* partials = nullptr;      // [nchains][ntask][nstat][64]
+    double* partials = nullptr;      // [nchains][ntile][nchunk][nstat][64]
     double* params = nullptr;        // [nchains][L+1][NP]
     double* stats = nullptr;         // [nchains][nstat][L+1]
     double* prop = nullptr;          // [nchains][nspec][maxbins]
@@ -314,22 +323,135 @@ struct SweepAcc {
     double v[NS];
 };
 
+// two consecutive doubles of the real layout, 8-byte aligned: the pair
+// (sqrt2 Re, sqrt2 Im) of one (l, m) starts at slot 2i-(L+1), which is odd
+// whenever L+1 is odd; gfx950 global accesses need only dword alignment
+typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
+
+// one (l, m) entry of every field: NV = 1 (m = 0, one real slot) or 2 (re, im)
+template <int F, int NV>
+__device__ __forceinline__ void load_d(const double* __restrict__ d, long long NR, long long r, double (&dv)[F][2]) {
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+        for (int c = 0; c < NV; ++c) dv[f][c] = d[f * NR + r + c];
+}
+
+template <int F, bool REPLAY, bool STORE, int NV>
+__device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const double* __restrict__ zc,
+                                            double* __restrict__ sc, long long NR, long long r, uint32_t i,
+                                            uint32_t tag, uint32_t iter, Key key, const double (&pm)[NP],
+                                            double (&acc)[SweepAcc<F>::NS], const double* __restrict__ tab) {
+    double zv[F][2], sv[F][NV];
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+        if constexpr (REPLAY) {
+#pragma unroll
+            for (int c = 0; c < NV; ++c) zv[f][c] = zc[f * NR + r + c];
+        } else {
+#if defined(GS_EXPERIMENT_NO_BM)
+            // timing experiment only: Philox without the Box-Muller transform
+            const uint4 w = philox(i, (uint32_t)f, tag, iter, key);
+            zv[f][0] = (double)w.x - (double)w.y; zv[f][1] = (double)w.z - (double)w.w;
+#elif defined(GS_EXPERIMENT_NO_RNG)
+            zv[f][0] = (double)(i ^ f); zv[f][1] = (double)(i + iter);
+#elif defined(GS_OCML_BM)
+            box_muller(philox(i, (uint32_t)f, tag, iter, key), zv[f][0], zv[f][1]);
+#else
+            box_muller_tab(philox(i, (uint32_t)f, tag, iter, key), tab, zv[f][0], zv[f][1]);
+#endif
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+        if constexpr (F == 3) {
+            sv[0][c] = pm[0] * dv[0][c] + pm[1] * dv[1][c] + pm[5] * zv[0][c];
+            sv[1][c] = pm[2] * dv[0][c] + pm[3] * dv[1][c] + pm[6] * zv[0][c] + pm[7] * zv[1][c];
+            sv[2][c] = pm[4] * dv[2][c] + pm[8] * zv[2][c];
+        } else {
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[f][c] = pm[f] * dv[f][c] + zv[f][c] * pm[F + f];
+        }
+    }
+    if constexpr (STORE) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+#if defined(GS_VEC16)
+            if constexpr (NV == 2) {
+                dbl2u v; v.x = sv[f][0]; v.y = sv[f][1];
+#if defined(GS_NO_NT)
+                *reinterpret_cast<dbl2u*>(sc + f * NR + r) = v;
+#else
+                __builtin_nontemporal_store(v, reinterpret_cast<dbl2u*>(sc + f * NR + r));
+#endif
+                continue;
+            }
+#endif
+#pragma unroll
+            for (int c = 0; c < NV; ++c) {
+#if defined(GS_NO_NT)
+                sc[f * NR + r + c] = sv[f][c];
+#else
+                __builtin_nontemporal_store(sv[f][c], &sc[f * NR + r + c]);
+#endif
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+        if constexpr (F == 3) {
+            acc[0] += sv[0][c] * sv[0][c];
+            acc[1] += sv[1][c] * sv[1][c];
+            acc[2] += sv[2][c] * sv[2][c];
+            acc[3] += sv[0][c] * sv[1][c];
+            acc[4] += dv[0][c] * sv[0][c];
+            acc[5] += dv[1][c] * sv[0][c];
+            acc[6] += dv[1][c] * sv[1][c];
+            acc[7] += dv[2][c] * sv[2][c];
+        } else {
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+                acc[f] += sv[f][c] * sv[f][c];
+                acc[F + f] += dv[f][c] * sv[f][c];
+            }
+        }
+    }
+}
+
+// Tiling of the (l, m) triangle: 64-wide l tiles, descending from l = L
+// (tile t holds l in [L-64t-63, L-64t]); a workgroup = 4 waves = 4 adjacent
+// tiles (256 consecutive l) x one chunk of TM rows m, so every row of the
+// workgroup is one contiguous 4 KiB run per field and chain; consecutive
+// workgroups are consecutive chains of the same (tiles, rows) block and
+// share the data reads in L2.
+#ifndef GS_SWEEP_WAVES_PER_SIMD
+#define GS_SWEEP_WAVES_PER_SIMD 1
+#endif
 template <int F, bool REPLAY, bool STORE>
-__global__ __launch_bounds__(256) void k_cr_sweep(int L, int nchains, int ntask, const int4* __restrict__ tasks,
-                                                  const double* __restrict__ d, const double* __restrict__ params,
-                                                  const double* __restrict__ z, double* __restrict__ s,
-                                                  double* __restrict__ partials, uint32_t seed_lo, uint32_t seed_hi,
-                                                  uint32_t iter, uint32_t substep, int chain0) {
+__global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L, int nchains, int ntile, int nchunk, int tm,
+                                                  const int2* __restrict__ tasks, const double* __restrict__ d,
+                                                  const double* __restrict__ params, const double* __restrict__ z,
+                                                  double* __restrict__ s, double* __restrict__ partials,
+                                                  uint32_t seed_lo, uint32_t seed_hi, uint32_t iter, uint32_t substep,
+                                                  int chain0) {
     constexpr int NS = SweepAcc<F>::NS;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    __shared__ double tab[REPLAY ? 1 : BM_TAB_DOUBLES];
+    if constexpr (!REPLAY) {
+        bm_stage_tables(tab);
+        __syncthreads();
+    }
+    const int pair = blockIdx.x / nchains;
+    const int chain = blockIdx.x % nchains;
     const int lane = threadIdx.x & 63;
-    if (wave >= nchains * ntask) return;
-    // task-major order: the waves of one workgroup work on the same (l, m)
-    // tile of different chains and share the d_alm reads in L1/L2
-    const int task = wave / nchains;
-    const int chain = wave % nchains;
-    const int4 tk = tasks[task];
-    const int ell = L - WAVE * tk.x - 63 + lane;
+    const int2 gc = tasks[pair];
+    const int t = 4 * gc.x + (threadIdx.x >> 6);
+    if (t >= ntile) return;
+    const int lhi = L - WAVE * t;
+    const int m0 = gc.y * tm;
+    const int m1 = min(m0 + tm, lhi + 1);
+    if (m0 >= m1) return;
+    const int ell_lo = lhi - 63;
+    const int ell = ell_lo + lane;
     const bool lane_ok = ell >= 0;
     const long long NR = (long long)(L + 1) * (L + 1);
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
@@ -351,72 +473,55 @@ __global__ __launch_bounds__(256) void k_cr_sweep(int L, int nchains, int ntask,
     const double* zc = REPLAY ? z + (long long)chain * F * NR : nullptr;
     double* sc = s + (long long)chain * F * NR;
 
-    for (int m = tk.y; m < tk.z; ++m) {
-        if (!(lane_ok && ell >= m)) continue;
-        const long long i = (long long)m * (2 * L + 1 - m) / 2 + ell;
-        const long long r = m == 0 ? (long long)ell : 2 * i - (L + 1);
-        const int nv = m == 0 ? 1 : 2;
-        double dv[F][2], zv[F][2], sv[F][2];
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            dv[f][0] = d[f * NR + r];
-            dv[f][1] = nv == 2 ? d[f * NR + r + 1] : 0.0;
-            if constexpr (REPLAY) {
-                zv[f][0] = zc[f * NR + r];
-                zv[f][1] = nv == 2 ? zc[f * NR + r + 1] : 0.0;
-            } else {
-                box_muller(philox((uint32_t)i, (uint32_t)f, tag, iter, key), zv[f][0], zv[f][1]);
-            }
+    int m = m0;
+    double dv[F][2];
+    if (m == 0) {
+        if (lane_ok) {
+            load_d<F, 1>(d, NR, ell, dv);
+            sweep_entry<F, REPLAY, STORE, 1>(dv, zc, sc, NR, ell, (uint32_t)ell, tag, iter, key, pm, acc, tab);
         }
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if constexpr (F == 3) {
-                sv[0][c] = pm[0] * dv[0][c] + pm[1] * dv[1][c] + pm[5] * zv[0][c];
-                sv[1][c] = pm[2] * dv[0][c] + pm[3] * dv[1][c] + pm[6] * zv[0][c] + pm[7] * zv[1][c];
-                sv[2][c] = pm[4] * dv[2][c] + pm[8] * zv[2][c];
-            } else {
-#pragma unroll
-                for (int f = 0; f < F; ++f) sv[f][c] = pm[f] * dv[f][c] + zv[f][c] * pm[F + f];
-            }
+        m = 1;
+    }
+    // row m starts at complex index S(m) = m(2L+3-m)/2 (l = m); slot r = 2i-(L+1)
+    long long i = (long long)m * (2 * L + 1 - m) / 2 + ell;
+    if (m1 - 1 <= ell_lo && ell_lo >= 0) {
+        // off-diagonal block: every lane active on every row; the next row's
+        // data is loaded before this row's draw (register double buffer)
+#if !defined(GS_PREFETCH)
+        for (; m < m1; ++m) {
+            load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
+            sweep_entry<F, REPLAY, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
+            i += L - m;
         }
-        if (nv == 1) {
+#else
+        if (m < m1) load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
+        for (; m < m1; ++m) {
+            const long long inext = i + (L - m);
+            double dn[F][2];
+            if (m + 1 < m1) load_d<F, 2>(d, NR, 2 * inext - (L + 1), dn);
+            sweep_entry<F, REPLAY, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
 #pragma unroll
-            for (int f = 0; f < F; ++f) sv[f][1] = 0.0;
+            for (int f = 0; f < F; ++f) { dv[f][0] = dn[f][0]; dv[f][1] = dn[f][1]; }
+            i = inext;
         }
-        if constexpr (STORE) {
-#pragma unroll
-            for (int f = 0; f < F; ++f) {
-                sc[f * NR + r] = sv[f][0];
-                if (nv == 2) sc[f * NR + r + 1] = sv[f][1];
+#endif
+    } else {
+        for (; m < m1; ++m) {
+            if (lane_ok && ell >= m) {
+                load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
+                sweep_entry<F, REPLAY, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm,
+                                                 acc, tab);
             }
-        }
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if constexpr (F == 3) {
-                acc[0] += sv[0][c] * sv[0][c];
-                acc[1] += sv[1][c] * sv[1][c];
-                acc[2] += sv[2][c] * sv[2][c];
-                acc[3] += sv[0][c] * sv[1][c];
-                acc[4] += dv[0][c] * sv[0][c];
-                acc[5] += dv[1][c] * sv[0][c];
-                acc[6] += dv[1][c] * sv[1][c];
-                acc[7] += dv[2][c] * sv[2][c];
-            } else {
-#pragma unroll
-                for (int f = 0; f < F; ++f) {
-                    acc[f] += sv[f][c] * sv[f][c];
-                    acc[F + f] += dv[f][c] * sv[f][c];
-                }
-            }
+            i += L - m;
         }
     }
-    double* po = partials + ((long long)chain * ntask + task) * NS * WAVE;
+    double* po = partials + (((long long)chain * ntile + t) * nchunk + gc.y) * NS * WAVE;
 #pragma unroll
     for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
 }
 
 // fixed-order reduction of the sweep partials: stats[chain][q][l]
-__global__ void k_stats_finish(int L, int nchains, int ntask, int nstat, const int* __restrict__ tile_task0,
+__global__ void k_stats_finish(int L, int nchains, int ntile, int nchunk, int tm, int nstat,
                                const double* __restrict__ partials, double* __restrict__ stats) {
     const int Lp1 = L + 1;
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -426,9 +531,10 @@ __global__ void k_stats_finish(int L, int nchains, int ntask, int nstat, const i
     const int chain = (int)(g / ((long long)Lp1 * nstat));
     const int t = (L - ell) / WAVE;
     const int lane = ell - (L - WAVE * t - 63);
+    const int cmax = (L - WAVE * t) / tm;
+    const double* pp = partials + ((long long)chain * ntile + t) * nchunk * nstat * WAVE + q * WAVE + lane;
     double acc = 0.0;
-    for (int task = tile_task0[t]; task < tile_task0[t + 1]; ++task)
-        acc += partials[(((long long)chain * ntask + task) * nstat + q) * WAVE + lane];
+    for (int c = 0; c <= cmax; ++c) acc += pp[(long long)c * nstat * WAVE];
     stats[g] = acc;
 }
 
@@ -561,105 +667,129 @@ __device__ __forceinline__ double wave_sum(double v) {
     return __shfl(v, 0, 64);
 }
 
-// one workgroup per chain; spectra sequential (MH order), blocks of a
-// spectrum in parallel (disjoint l ranges => independent), one wave per block
+// proposals (NonCenteredGibbs.py:292-309) and per-bin log proposal ratios
+// (313-330, 410-413): one thread per (chain, spectrum, bin)
 template <int F>
-__global__ __launch_bounds__(256) void k_nc_mh(int L, int nchains, int maxbins, const int* __restrict__ bins,
-                                               const int* __restrict__ nbins_arr, const int* __restrict__ blocks,
-                                               const int* __restrict__ nblocks_arr, const int* __restrict__ acc_off,
-                                               const int* __restrict__ mh_order, int nacc, int n_iter_mh,
-                                               const int* __restrict__ ell2bin, const double* __restrict__ bl,
-                                               double k0, double k1, double k2, const double* __restrict__ prop_sd,
-                                               const double* __restrict__ stats, double* __restrict__ dl,
-                                               double* __restrict__ prop, double* __restrict__ logr,
-                                               const double* __restrict__ u_prop, const double* __restrict__ u_acc,
-                                               uint32_t seed_lo, uint32_t seed_hi, uint32_t iter, int chain0,
-                                               int32_t* __restrict__ accept_out) {
+__global__ __launch_bounds__(256) void k_mh_propose(int nchains, int maxbins, const int* __restrict__ nbins_arr,
+                                                    const double* __restrict__ prop_sd, const double* __restrict__ dl,
+                                                    double* __restrict__ prop, double* __restrict__ logr,
+                                                    const double* __restrict__ u_prop, uint32_t seed_lo,
+                                                    uint32_t seed_hi, uint32_t iter, int chain0) {
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= (long long)nchains * NSP * maxbins) return;
+    const int b = (int)(g % maxbins);
+    const int sp = (int)((g / maxbins) % NSP);
+    const int chain = (int)(g / ((long long)maxbins * NSP));
+    if (b < 2 || b >= nbins_arr[sp]) return;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    const double sd = prop_sd[sp * maxbins + b];
+    const double old = dl[g];
+    double p, lr;
+    if (F == 3 && sp == 3) {
+        // TE: symmetric normal proposal (build spec; no positivity constraint)
+        const double y = u_prop ? normcdfinv(u_prop[g]) : normal1(key, b, sp, TAG_TN, iter);
+        p = old + sd * y;
+        lr = 0.0;
+    } else {
+        const double a = -old / sd;
+        const double q = u_prop ? u_prop[g] : uniform1(key, b, sp, TAG_TN, iter);
+        p = old + sd * tn_ppf(q, a);
+        lr = log_ndtr(old / sd) - log_ndtr(p / sd);
+    }
+    prop[g] = p;
+    logr[g] = lr;
+}
+
+// MH phase, step 1: per-(chain, l) likelihood difference of the phase's
+// spectra, g = f_l(proposed) - f_l(current) (-inf when the proposed TE block
+// is not positive definite).  One thread per (chain, l): the per-l
+// decomposition of the all_sph likelihood makes this fully parallel.
+template <int F>
+__global__ __launch_bounds__(256) void k_mh_terms(int L, int nchains, int maxbins, int sp0, int sp1,
+                                                  const int* __restrict__ ell2blk, const int* __restrict__ ell2bin,
+                                                  const double* __restrict__ bl, double k0, double k1, double k2,
+                                                  const double* __restrict__ stats, const double* __restrict__ dl,
+                                                  const double* __restrict__ prop, double* __restrict__ gbuf) {
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
-    const int chain = blockIdx.x;
     const int Lp1 = L + 1;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= (long long)nchains * Lp1) return;
+    const int chain = (int)(g / Lp1), l = (int)(g % Lp1);
+    const double* D = dl + (long long)chain * NSP * maxbins;
+    const double* P = prop + (long long)chain * NSP * maxbins;
+    const double* st = stats + (long long)chain * NS * Lp1;
+    double vo[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NSP; ++q) vo[q] = var_from_dl(dl_at(D, ell2bin, maxbins, Lp1, q, l), l);
+    const double b = bl[l];
+    const double fo = f_ell<F>(st, Lp1, l, b, k0, k1, k2, vo[0], vo[1], vo[2], vo[3]);
+    const int sps[2] = {sp0, sp1};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int sp = sps[k];
+        if (sp < 0) continue;
+        double out = 0.0;
+        if (ell2blk[sp * Lp1 + l] >= 0) {
+            double vn[4] = {vo[0], vo[1], vo[2], vo[3]};
+            vn[sp] = var_from_dl(P[sp * maxbins + ell2bin[sp * Lp1 + l]], l);
+            bool ok = true;
+            if constexpr (F == 3) ok = psd_ok(vn[0], vn[1], vn[3]);
+            out = ok ? f_ell<F>(st, Lp1, l, b, k0, k1, k2, vn[0], vn[1], vn[2], vn[3]) - fo : -INFINITY;
+        }
+        gbuf[((long long)chain * 2 + k) * Lp1 + l] = out;
+    }
+}
+
+// MH phase, step 2: one wave per (chain, block): fixed-order sum of the
+// block's g_l and proposal log ratios, accept with log u < delta + log r,
+// n_iter_metropolis attempts (NonCenteredGibbs.py:427-442).
+template <int F>
+__global__ __launch_bounds__(256) void k_mh_accept(int L, int nchains, int maxbins, int sp0,
+                                                   const int* __restrict__ bins, const int* __restrict__ blocks,
+                                                   const int2* __restrict__ phase_blk, int nphase_blk,
+                                                   const int* __restrict__ acc_off, int nacc, int n_iter_mh,
+                                                   const double* __restrict__ gbuf, double* __restrict__ dl,
+                                                   const double* __restrict__ prop, const double* __restrict__ logr,
+                                                   const double* __restrict__ u_acc, uint32_t seed_lo,
+                                                   uint32_t seed_hi, uint32_t iter, int chain0,
+                                                   int32_t* __restrict__ accept_out) {
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    const long long w = blockIdx.x * 4LL + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= (long long)nchains * nphase_blk) return;
+    const int chain = (int)(w / nphase_blk);
+    const int2 sb = phase_blk[w % nphase_blk];
+    const int sp = sb.x, blk = sb.y;
+    const int k = sp == sp0 ? 0 : 1;
+    const int Lp1 = L + 1;
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
     double* D = dl + (long long)chain * NSP * maxbins;
-    double* P = prop + (long long)chain * NSP * maxbins;
-    double* R = logr + (long long)chain * NSP * maxbins;
-    const double* st = stats + (long long)chain * NS * Lp1;
-
-    // proposals for every spectrum (NonCenteredGibbs.py:292-309) and the
-    // per-bin log proposal ratios (313-330, 410-413)
-    for (int sp = 0; sp < NSP; ++sp) {
-        const int nb = nbins_arr[sp];
-        const bool te = (F == 3 && sp == 3);
-        for (int b = 2 + tid; b < nb; b += blockDim.x) {
-            const double sd = prop_sd[sp * maxbins + b];
-            const double old = D[sp * maxbins + b];
-            double p, lr;
-            if (te) {
-                const double y = u_prop ? normcdfinv(u_prop[((long long)chain * NSP + sp) * maxbins + b])
-                                        : normal1(key, b, sp, TAG_TN, iter);
-                p = old + sd * y;
-                lr = 0.0;
-            } else {
-                const double a = -old / sd;
-                const double q = u_prop ? u_prop[((long long)chain * NSP + sp) * maxbins + b]
-                                        : uniform1(key, b, sp, TAG_TN, iter);
-                p = old + sd * tn_ppf(q, a);
-                lr = log_ndtr(old / sd) - log_ndtr(p / sd);
-            }
-            P[sp * maxbins + b] = p;
-            R[sp * maxbins + b] = lr;
-        }
-    }
-    __syncthreads();
-
-    for (int oi = 0; oi < NSP; ++oi) {
-        const int sp = mh_order[oi];
-        const int nbk = nblocks_arr[sp];
-        const int* be = bins + sp * (maxbins + 1);
-        const int* bk = blocks + sp * (maxbins + 1);
-        for (int att = 0; att < n_iter_mh; ++att) {
-            for (int blk = wv; blk < nbk; blk += 4) {
-                const int lo = bk[blk], hi = bk[blk + 1];
-                double diff = 0.0;
-                int bad = 0;
-                if (hi > lo) {
-                    for (int l = be[lo] + lane; l < be[hi]; l += 64) {
-                        double vo[4], vn[4];
-#pragma unroll
-                        for (int q = 0; q < NSP; ++q) {
-                            const double Dv = dl_at(D, ell2bin, maxbins, Lp1, q, l);
-                            vo[q] = var_from_dl(Dv, l);
-                            vn[q] = vo[q];
-                        }
-                        vn[sp] = var_from_dl(P[sp * maxbins + ell2bin[sp * Lp1 + l]], l);
-                        if constexpr (F == 3) {
-                            if (!psd_ok(vn[0], vn[1], vn[3])) { bad = 1; continue; }
-                        }
-                        const double b = bl[l];
-                        const double fn = f_ell<F>(st, Lp1, l, b, k0, k1, k2, vn[0], vn[1], NSP > 2 ? vn[2] : 0.0,
-                                                   NSP > 3 ? vn[3] : 0.0);
-                        const double fo = f_ell<F>(st, Lp1, l, b, k0, k1, k2, vo[0], vo[1], NSP > 2 ? vo[2] : 0.0,
-                                                   NSP > 3 ? vo[3] : 0.0);
-                        diff += fn - fo;
-                    }
-                }
-                double lrs = 0.0;
-                for (int q = lo + lane; q < hi; q += 64) lrs += R[sp * maxbins + q];
-                diff = wave_sum(diff);
-                lrs = wave_sum(lrs);
-                const int anybad = __any(bad);
-                const int flat = acc_off[sp] + blk * n_iter_mh + att;
-                const double u = u_acc ? u_acc[(long long)chain * nacc + flat]
-                                       : uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
-                const double log_r = anybad ? -INFINITY : diff + lrs;
-                const bool acc = log(u) < log_r;
-                if (acc)
-                    for (int q = lo + lane; q < hi; q += 64) D[sp * maxbins + q] = P[sp * maxbins + q];
-                if (lane == 0 && accept_out) accept_out[(long long)chain * nacc + flat] = acc ? 1 : 0;
-            }
-            __syncthreads();
-        }
+    const double* P = prop + (long long)chain * NSP * maxbins;
+    const double* R = logr + (long long)chain * NSP * maxbins;
+    const double* G = gbuf + ((long long)chain * 2 + k) * Lp1;
+    const int* be = bins + sp * (maxbins + 1);
+    const int* bk = blocks + sp * (maxbins + 1);
+    const int lo = bk[blk], hi = bk[blk + 1];
+    double lrs = 0.0, diff = 0.0;
+    for (int q = lo + lane; q < hi; q += 64) lrs += R[sp * maxbins + q];
+    if (hi > lo)
+        for (int l = be[lo] + lane; l < be[hi]; l += 64) diff += G[l];
+    lrs = wave_sum(lrs);
+    diff = wave_sum(diff);
+    bool taken = false;
+    for (int att = 0; att < n_iter_mh; ++att) {
+        const int flat = acc_off[sp] + blk * n_iter_mh + att;
+        const double u = u_acc ? u_acc[(long long)chain * nacc + flat]
+                               : uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
+        // after an acceptance the proposal IS the current state: delta = 0
+        const double log_r = (taken ? 0.0 : diff) + lrs;
+        const bool acc = log(u) < log_r;
+        if (acc && !taken)
+            for (int q = lo + lane; q < hi; q += 64) D[sp * maxbins + q] = P[sp * maxbins + q];
+        taken = taken || acc;
+        if (lane == 0 && accept_out) accept_out[(long long)chain * nacc + flat] = acc ? 1 : 0;
     }
 }
 
@@ -790,33 +920,26 @@ inline unsigned nblk(long long n, int bs) { return (unsigned)std::max<long long>
 void build_tasks(gs_plan* p) {
     const int L = p->L;
     p->ntile = (L + 1 + WAVE - 1) / WAVE;
-    // rows per task: aim for >= 4096 waves so every SIMD has several to hide latency
-    int tm = 64;
-    auto count = [&](int rows_per) {
+    auto waves = [&](int tm) {
         long long n = 0;
-        for (int t = 0; t < p->ntile; ++t) {
-            const int R = L - WAVE * t + 1;
-            n += (R + rows_per - 1) / rows_per;
-        }
+        for (int t = 0; t < p->ntile; ++t) n += (L - WAVE * t) / tm + 1;
         return n;
     };
-    while (tm > 4 && count(tm) * p->nchains < 4096) tm /= 2;
-    p->rows_per_task = tm;
-    std::vector<int4> tasks;
-    std::vector<int> t0;
-    for (int t = 0; t < p->ntile; ++t) {
-        t0.push_back((int)tasks.size());
-        const int R = L - WAVE * t + 1;
-        const int nch = (R + tm - 1) / tm;
-        for (int c = 0; c < nch; ++c) {
-            const int m0 = (int)((long long)c * R / nch), m1 = (int)((long long)(c + 1) * R / nch);
-            tasks.push_back(make_int4(t, m0, m1, 0));
-        }
+    // rows per chunk: aim for >= 8192 waves so every SIMD has several to hide latency
+    int tm = 64;
+    while (tm > 4 && waves(tm) * p->nchains < 8192) tm /= 2;
+    if (const char* env = getenv("GS_SWEEP_ROWS")) {
+        const int v = atoi(env);
+        if (v >= 1 && v <= 1024) tm = v;
     }
-    t0.push_back((int)tasks.size());
-    p->ntask = (int)tasks.size();
+    p->rows_per_task = tm;
+    p->nchunk = L / tm + 1;
+    p->ntask = (int)waves(tm);
+    std::vector<int2> tasks;
+    for (int g = 0; 4 * g < p->ntile; ++g)
+        for (int c = 0; c * tm <= L - WAVE * 4 * g; ++c) tasks.push_back(make_int2(g, c));
+    p->npair = (int)tasks.size();
     dev_upload(&p->tasks, tasks);
-    dev_upload(&p->tile_task0, t0);
 }
 
 int check_plan(const gs_plan* p) {
@@ -898,6 +1021,21 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
         off += p->nblocks[sp] * p->n_iter_mh;
     }
     p->nacc = off;
+    // phases: F=1 [TT]; F=2 [EE, BB]; F=3 [EE, BB], [TT], [TE] (BB shares no
+    // likelihood term with T/E; EE, TT, TE all enter the TE block)
+    std::vector<std::vector<int>> phases;
+    if (F == 1) phases = {{0}};
+    else if (F == 2) phases = {{0, 1}};
+    else phases = {{1, 2}, {0}, {3}};
+    std::vector<int2> ptab;
+    p->nphase = (int)phases.size();
+    for (int ph = 0; ph < p->nphase; ++ph) {
+        p->phase_off[ph] = (int)ptab.size();
+        for (size_t q = 0; q < phases[ph].size(); ++q) p->phase_sp[ph][q] = phases[ph][q];
+        for (int sp : phases[ph])
+            for (int b = 0; b < p->nblocks[sp]; ++b) ptab.push_back(make_int2(sp, b));
+        p->phase_n[ph] = (int)ptab.size() - p->phase_off[ph];
+    }
     int rc = 0;
     rc |= dev_upload(&p->bl, bl);
     rc |= dev_upload(&p->ell2bin, ell2bin);
@@ -909,9 +1047,19 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
         meta[k] = p->nbins[k]; meta[4 + k] = p->nblocks[k]; meta[8 + k] = p->acc_off[k]; meta[12 + k] = p->mh_order[k];
     }
     rc |= dev_upload(&p->meta, meta);
+    rc |= dev_upload(&p->phase_tab, ptab);
+    std::vector<int> e2k((size_t)p->nspec * (L + 1), -1);
+    for (int sp = 0; sp < p->nspec; ++sp)
+        for (int b = 0; b < p->nblocks[sp]; ++b) {
+            const int lo = blocks[sp * (maxbins + 1) + b], hi = blocks[sp * (maxbins + 1) + b + 1];
+            if (hi <= lo) continue;
+            for (int l = desc->bins[sp][lo]; l < desc->bins[sp][hi]; ++l) e2k[sp * (L + 1) + l] = b;
+        }
+    rc |= dev_upload(&p->ell2blk, e2k);
+    rc |= dev_alloc(&p->gbuf, (size_t)p->nchains * 2 * (L + 1));
     build_tasks(p);
     const size_t nc = (size_t)p->nchains;
-    rc |= dev_alloc(&p->partials, nc * p->ntask * p->nstat * WAVE);
+    rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunk * p->nstat * WAVE);
     rc |= dev_alloc(&p->params, nc * (L + 1) * NP);
     rc |= dev_alloc(&p->stats, nc * p->nstat * (L + 1));
     rc |= dev_alloc(&p->prop, nc * p->nspec * maxbins);
@@ -924,7 +1072,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
-    void* bufs[] = {p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->tile_task0, p->partials,
+    void* bufs[] = {p->ell2blk, p->gbuf, p->phase_tab, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials,
                     p->params, p->stats, p->prop, p->logr, p->dl_tmp};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -939,6 +1087,13 @@ int gs_plan_info(const gs_plan* p, int* maxbins, int* nstat, int* nblocks_total,
     if (nstat) *nstat = p->nstat;
     if (nblocks_total) *nblocks_total = p->nacc;
     if (nspec) *nspec = p->nspec;
+    return 0;
+}
+
+int gs_plan_sweep_info(const gs_plan* p, int* ntask, int* rows_per_task) {
+    if (check_plan(p)) return -1;
+    if (ntask) *ntask = p->ntask;
+    if (rows_per_task) *rows_per_task = p->rows_per_task;
     return 0;
 }
 
@@ -1024,14 +1179,13 @@ int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const dou
     if (check_plan(p)) return -1;
     if (!d_alm || !params || !stats) return set_error("gs_cr_sweep: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    const long long waves = (long long)p->nchains * p->ntask;
-    const dim3 g(nblk(waves, 4)), b(256);
+    const dim3 g((unsigned)((long long)p->nchains * p->npair)), b(256);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing_begin(p, S(stream), &e0, &e1)) return -1;
     const bool rep = z != nullptr, st = s_out != nullptr;
-#define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntask, \
-                                             p->tasks, d_alm, params, z, s_out, p->partials, slo, shi, iteration,  \
-                                             substep, p->chain0)
+#define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
+                                             p->nchunk, p->rows_per_task, p->tasks, d_alm, params, z, s_out,         \
+                                             p->partials, slo, shi, iteration, substep, p->chain0)
 #define GS_SWF(FF) do { if (rep && st) GS_SW(FF, true, true); else if (rep) GS_SW(FF, true, false); \
                         else if (st) GS_SW(FF, false, true); else GS_SW(FF, false, false); } while (0)
     if (p->F == 1) GS_SWF(1); else if (p->F == 2) GS_SWF(2); else GS_SWF(3);
@@ -1040,8 +1194,8 @@ int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const dou
     GS_LAUNCH_CHECK("k_cr_sweep");
     if (p->timing) GS_CHECK(hipEventRecord(e1, S(stream)));
     const long long n = (long long)p->nchains * p->nstat * (p->L + 1);
-    hipLaunchKernelGGL(k_stats_finish, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, p->ntask,
-                       p->nstat, p->tile_task0, p->partials, stats);
+    hipLaunchKernelGGL(k_stats_finish, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
+                       p->nchunk, p->rows_per_task, p->nstat, p->partials, stats);
     GS_LAUNCH_CHECK("k_stats_finish");
     return 0;
 }
@@ -1064,14 +1218,33 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
     if (check_plan(p)) return -1;
     if (!p->has_mh) return set_error("gs_nc_mh: plan has no MH blocks / proposal variances");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    const dim3 g(p->nchains), b(256);
-#define GS_MH(FF) hipLaunchKernelGGL((k_nc_mh<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
-                                     p->blocks, p->meta + 4, p->meta + 8, p->meta + 12, p->nacc, p->n_iter_mh,     \
-                                     p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], p->prop_sd, stats, dl, \
-                                     p->prop, p->logr, u_prop, u_acc, slo, shi, iteration, p->chain0, accept_out)
-    if (p->F == 1) GS_MH(1); else if (p->F == 2) GS_MH(2); else GS_MH(3);
-#undef GS_MH
-    GS_LAUNCH_CHECK("k_nc_mh");
+    const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
+#define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
+                                     p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi, iteration, \
+                                     p->chain0)
+    if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
+#undef GS_MP
+    GS_LAUNCH_CHECK("k_mh_propose");
+    const long long nl = (long long)p->nchains * (p->L + 1);
+    for (int ph = 0; ph < p->nphase; ++ph) {
+        const int nb = p->phase_n[ph];
+        if (nb == 0) continue;
+        const int sp0 = p->phase_sp[ph][0], sp1 = p->phase_sp[ph][1];
+#define GS_MT(FF) hipLaunchKernelGGL((k_mh_terms<FF>), dim3(nblk(nl, 256)), dim3(256), 0, S(stream), p->L, p->nchains, \
+                                     p->maxbins, sp0, sp1, p->ell2blk, p->ell2bin, p->bl, p->kappa[0], p->kappa[1],  \
+                                     p->kappa[2], stats, dl, p->prop, p->gbuf)
+        if (p->F == 1) GS_MT(1); else if (p->F == 2) GS_MT(2); else GS_MT(3);
+#undef GS_MT
+        GS_LAUNCH_CHECK("k_mh_terms");
+        const long long waves = (long long)p->nchains * nb;
+        const int2* tab = p->phase_tab + p->phase_off[ph];
+#define GS_MA(FF) hipLaunchKernelGGL((k_mh_accept<FF>), dim3(nblk(waves, 4)), dim3(256), 0, S(stream), p->L, p->nchains, \
+                                     p->maxbins, sp0, p->bins, p->blocks, tab, nb, p->meta + 8, p->nacc, p->n_iter_mh, \
+                                     p->gbuf, dl, p->prop, p->logr, u_acc, slo, shi, iteration, p->chain0, accept_out)
+        if (p->F == 1) GS_MA(1); else if (p->F == 2) GS_MA(2); else GS_MA(3);
+#undef GS_MA
+        GS_LAUNCH_CHECK("k_mh_accept");
+    }
     return 0;
 }
 

@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "gs_bm_tables.h"
 
 namespace gs {
 
@@ -26,8 +27,11 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
     uint32_t k0 = k.k0, k1 = k.k1;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        // one v_mad_u64_u32 per product (hi:lo in a register pair)
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         const uint32_t n0 = hi1 ^ c1 ^ k0;
         const uint32_t n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
@@ -41,12 +45,78 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
+// ln(x) for normal finite x > 0 (the Box-Muller radius): x = m 2^e with
+// m in [sqrt(1/2), sqrt(2)); ln m = 2 atanh(s), s = (m-1)/(m+1), |s| < 0.172;
+// the atanh series through s^21 is below 2.5e-17 relative; m - 1 is exact.
+__device__ __forceinline__ double bm_log(double x) {
+    int e;
+    double m = frexp(x, &e);
+    if (m < 0.70710678118654752440) { m *= 2.0; e -= 1; }
+    const double f = m - 1.0;
+    const double sv = f / (2.0 + f);
+    const double s2 = sv * sv;
+    double p = 0.047619047619047616;
+    p = fma(p, s2, 0.05263157894736842);
+    p = fma(p, s2, 0.058823529411764705);
+    p = fma(p, s2, 0.06666666666666667);
+    p = fma(p, s2, 0.07692307692307693);
+    p = fma(p, s2, 0.09090909090909091);
+    p = fma(p, s2, 0.1111111111111111);
+    p = fma(p, s2, 0.14285714285714285);
+    p = fma(p, s2, 0.2);
+    p = fma(p, s2, 0.3333333333333333);
+    const double ts = 2.0 * sv;
+    const double lnm = fma(ts * s2, p, ts);
+    const double de = (double)e;
+    return fma(de, 0.6931471805599453, fma(de, 2.3190468138462996e-17, lnm));
+}
+
+// sin and cos of 2 pi u for u in (0, 1): u = q/4 + y exactly (|y| <= 1/8),
+// Taylor polynomials of sin(2 pi y) / cos(2 pi y) (|2 pi y| <= pi/4,
+// truncation < 5e-17), then the quadrant rotation.
+__device__ __forceinline__ void bm_sincos2pi(double u, double& sn, double& cs) {
+    const double q = rint(4.0 * u);
+    const double y = fma(q, -0.25, u);
+    const double y2 = y * y;
+    double ps = 0.10422916220813984;
+    ps = fma(ps, y2, -0.7181223017785006);
+    ps = fma(ps, y2, 3.819952584848282);
+    ps = fma(ps, y2, -15.09464257682299);
+    ps = fma(ps, y2, 42.058693944897655);
+    ps = fma(ps, y2, -76.70585975306139);
+    ps = fma(ps, y2, 81.60524927607506);
+    ps = fma(ps, y2, -41.34170224039976);
+    ps = fma(ps, y2, 6.283185307179586);
+    const double sy = ps * y;
+    double pc = -0.03638284114254567;
+    pc = fma(pc, y2, 0.28200596845579123);
+    pc = fma(pc, y2, -1.714390711088672);
+    pc = fma(pc, y2, 7.903536371318469);
+    pc = fma(pc, y2, -26.4262567833744);
+    pc = fma(pc, y2, 60.24464137187666);
+    pc = fma(pc, y2, -85.45681720669373);
+    pc = fma(pc, y2, 64.9393940226683);
+    pc = fma(pc, y2, -19.739208802178716);
+    const double cy = fma(pc, y2, 1.0);
+    const int k = (int)q & 3;
+    const double a = (k & 1) ? cy : sy;
+    const double b = (k & 1) ? sy : cy;
+    sn = (k & 2) ? -a : a;
+    cs = ((k + 1) & 2) ? -b : b;
+}
+
 __device__ __forceinline__ void box_muller(uint4 w, double& z0, double& z1) {
     const double u1 = u53(w.x, w.y);
     const double u2 = u53(w.z, w.w);
+#if defined(GS_OCML_BM)
     const double r = sqrt(-2.0 * log(u1));
     double sn, cs;
-    sincos(2.0 * M_PI * u2, &sn, &cs);
+    sincospi(2.0 * u2, &sn, &cs);
+#else
+    const double r = sqrt(-2.0 * bm_log(u1));
+    double sn, cs;
+    bm_sincos2pi(u2, sn, cs);
+#endif
     z0 = r * cs;
     z1 = r * sn;
 }
@@ -87,6 +157,67 @@ __device__ inline double gamma_mt(double alpha, Key k, uint32_t b, uint32_t spec
         g = g * exp(log(ub) / alpha);
     }
     return g;
+}
+
+// ---- table-driven fp64 Box-Muller for the CR sweep ------------------------
+// The tables (gs_bm_tables.h, correctly rounded) are staged in LDS once per
+// workgroup: tab[0..255] = {c_k, -ln c_k} (128 cells of [sqrt(1/2), sqrt(2))),
+// tab[256..767] = {sin, cos}(2 pi k / 256).  Accuracy ~1-2 ulp: every
+// operation is fp64; only the polynomial degree drops (|r| < 0.0055 for the
+// log1p, |phi| < 2 pi / 256 for the trigonometric remainder).
+constexpr int BM_TAB_DOUBLES = 768;
+
+__device__ __forceinline__ void bm_stage_tables(double* tab) {
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) tab[k] = BM_LOG_TAB[k];
+    for (int k = threadIdx.x; k < 512; k += blockDim.x) tab[256 + k] = BM_TRIG_TAB[k];
+}
+
+__device__ __forceinline__ double bm_log_tab(double x, const double* __restrict__ tab) {
+    int e;
+    double m = frexp(x, &e);
+    if (m < 0.70710678118654752440) { m *= 2.0; e -= 1; }
+    int k = (int)((m - BM_LOG_LO) * BM_LOG_INVW);
+    k = min(max(k, 0), 127);
+    const double c = tab[2 * k], nlc = tab[2 * k + 1];
+    const double r = fma(m, c, -1.0);
+    double p = 0.14285714285714285;
+    p = fma(p, r, -0.16666666666666666);
+    p = fma(p, r, 0.2);
+    p = fma(p, r, -0.25);
+    p = fma(p, r, 0.3333333333333333);
+    p = fma(p, r, -0.5);
+    const double l1p = fma(p * r, r, r);
+    const double de = (double)e;
+    return fma(de, 0.6931471805599453, fma(de, 2.3190468138462996e-17, nlc + l1p));
+}
+
+// sin, cos of 2 pi u for u = (K + 0.5) 2^-53, K = (wz >> 5) 2^26 + (ww >> 6)
+__device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const double* __restrict__ tab,
+                                              double& sn, double& cs) {
+    const uint32_t k = wz >> 24;
+    const double y = ((double)((wz >> 5) & 0x7FFFFu) * 67108864.0 + (double)(ww >> 6) + 0.5) *
+                     (1.0 / 9007199254740992.0);
+    const double ph = y * 6.283185307179586;
+    const double p2 = ph * ph;
+    double ps = fma(p2, -1.984126984126984e-4, 8.333333333333333e-3);
+    ps = fma(ps, p2, -0.16666666666666666);
+    const double sph = fma(ph * p2, ps, ph);
+    double pc = fma(p2, 2.48015873015873e-5, -1.388888888888889e-3);
+    pc = fma(pc, p2, 4.1666666666666664e-2);
+    pc = fma(pc, p2, -0.5);
+    const double cph = fma(pc, p2, 1.0);
+    const double sk = tab[256 + 2 * k], ck = tab[256 + 2 * k + 1];
+    sn = fma(sk, cph, ck * sph);
+    cs = fma(ck, cph, -(sk * sph));
+}
+
+__device__ __forceinline__ void box_muller_tab(uint4 w, const double* __restrict__ tab, double& z0, double& z1) {
+    const double u1 = u53(w.x, w.y);
+    const double r = sqrt(-2.0 * bm_log_tab(u1, tab));
+    double sn, cs;
+    bm_sincos_tab(w.z, w.w, tab, sn, cs);
+    z0 = r * cs;
+    z1 = r * sn;
 }
 
 }  // namespace gs

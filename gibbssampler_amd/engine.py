@@ -87,6 +87,9 @@ class GibbsPlan:
         C.check(self.lib.gs_plan_info(h, ctypes.byref(mb), ctypes.byref(ns), ctypes.byref(nacc), ctypes.byref(nsp)))
         self.maxbins, self.nstat, self.nacc, self.nspec = mb.value, ns.value, nacc.value, nsp.value
         self.NR = (self.L + 1) ** 2
+        nt, rpt = ctypes.c_int(), ctypes.c_int()
+        C.check(self.lib.gs_plan_sweep_info(h, ctypes.byref(nt), ctypes.byref(rpt)))
+        self.ntask, self.rows_per_task = nt.value, rpt.value
         # host-side replay helpers (data independent)
         ell = np.arange(self.L + 1, dtype=np.float64)
         expo = (2 * ell + 1) / 2

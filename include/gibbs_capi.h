@@ -96,6 +96,8 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out);
 int gs_plan_destroy(gs_plan* plan);
 /* query sizes of the plan's layouts */
 int gs_plan_info(const gs_plan* plan, int* maxbins, int* nstat, int* nblocks_total, int* nspec);
+/* tiling of the CR sweep: tasks per chain, m-rows per task */
+int gs_plan_sweep_info(const gs_plan* plan, int* ntask, int* rows_per_task);
 
 /* ---- stand-alone layout / expansion helpers (no plan needed) ---------------- */
 int gs_var_expand(int lmax, int n, const double* dl, double* var, void* stream);

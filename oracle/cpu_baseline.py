@@ -1,0 +1,100 @@
+"""CPU baseline for bench.py (TEST/MEASUREMENT INFRASTRUCTURE, single core numpy).
+
+A vectorised numpy port of the reference's non-centered all_sph Gibbs
+iteration with the reference's per-call work structure
+(NonCenteredGibbs.py:134-176 CR; 292-445 MH), generalised to TEB exactly as
+the build specifies it:
+
+  * CR: per-slot operator from the per-l block algebra, z ~ np.random.normal;
+  * MH: truncated-normal proposals for every bin, then for every block a full
+    re-expansion of the per-slot variances (generate_var_cl, utils.py:139) and
+    a full-sky log-likelihood sum over all (L+1)^2 slots of every field
+    (compute_log_likelihood_all_sph, NonCenteredGibbs.py:357-377), one uniform
+    per block -- the reference evaluates the likelihood in full per block.
+
+Pure-Python loops of the reference (generate_var_cl_cython, utils.py:114-135)
+are replaced by numpy indexing, so this baseline is FASTER than the reference
+itself (SURVEY.md 6 measured 374.7 ms per generate_var_cl call at L=1024).
+"""
+import time
+
+import numpy as np
+
+from . import harmonic as H
+
+
+def _loglik_full(model, un, s_nc, sl):
+    """-1/2 sum_slots sum_X kappa_X (d_X - b (A s)_X)^2 over the whole sky."""
+    F = model.nfields
+    d = model.d_alm
+    b = model.bl[sl]
+    var = H.var_from_dl(un)
+    if F != 3:
+        out = 0.0
+        for f in range(F):
+            r = d[f] - b * np.sqrt(var[f])[sl] * s_nc[f]
+            out += np.sum(r * r) * model.kappa[f]
+        return -0.5 * out
+    tt, ee, bb, te = var[0], var[1], var[2], var[3]
+    a00 = np.sqrt(tt)
+    a10 = np.where(a00 > 0, te / np.where(a00 > 0, a00, 1.0), 0.0)
+    a11 = np.sqrt(np.maximum(ee - a10 * a10, 0.0))
+    rT = d[0] - b * a00[sl] * s_nc[0]
+    rE = d[1] - b * (a10[sl] * s_nc[0] + a11[sl] * s_nc[1])
+    rB = d[2] - b * np.sqrt(bb)[sl] * s_nc[2]
+    return -0.5 * (model.kappa[0] * np.sum(rT * rT) + model.kappa[1] * np.sum(rE * rE)
+                   + model.kappa[2] * np.sum(rB * rB))
+
+
+def nc_iteration(model, dl_binned, sl=None):
+    """One NonCenteredGibbs iteration (all_sph) on the host."""
+    sl = H.slot_ell(model.L) if sl is None else sl
+    un = model.unfold(dl_binned)
+    M, Lc = H.noncentered_params(model, un)
+    z = np.stack([np.random.normal(size=H.nreal(model.L)) for _ in range(model.nfields)])
+    s_nc = H.cr_apply(model, M, Lc, model.d_alm, z)
+    cur = {s: np.array(v, dtype=np.float64) for s, v in dl_binned.items()}
+    order = list(model.spectra) if model.nfields != 3 else ["EE", "BB", "TT", "TE"]
+    prop, logr = {}, {}
+    for s in order:
+        sd = np.sqrt(model.proposal_variances[s])
+        old = cur[s][2:]
+        u = np.random.uniform(size=len(old))
+        if s == "TE":
+            from scipy.special import ndtri
+            p = old + sd * ndtri(u)
+            lr = np.zeros(len(old))
+        else:
+            p = old + sd * H.truncnorm_ppf_std(u, -old / sd)
+            lr = H.truncnorm_log_ratio(old, p, sd)
+        prop[s] = np.concatenate([np.zeros(2), p])
+        logr[s] = np.concatenate([np.zeros(2), lr])
+    old_lik = _loglik_full(model, model.unfold(cur), s_nc, sl)
+    for s in order:
+        bl = model.blocks[s]
+        nb = len(cur[s])
+        for i in range(len(bl) - 1):
+            lo, hi = int(bl[i]), min(int(bl[i + 1]), nb)
+            new = {k: v.copy() for k, v in cur.items()}
+            new[s][lo:hi] = prop[s][lo:hi]
+            new_lik = _loglik_full(model, model.unfold(new), s_nc, sl)
+            log_r = new_lik - old_lik + np.sum(logr[s][lo:hi])
+            if np.log(np.random.uniform()) < log_r:
+                cur, old_lik = new, new_lik
+    return cur
+
+
+def time_noncentered(model, dl_init, budget_s=20.0, max_iter=5, seed=0):
+    """Run NC iterations until the time budget is spent; returns (iters/s, n)."""
+    np.random.seed(seed)
+    sl = H.slot_ell(model.L)
+    cur = dl_init
+    t0 = time.perf_counter()
+    n = 0
+    while n < max_iter:
+        cur = nc_iteration(model, cur, sl)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return n / dt, n, dt

@@ -188,17 +188,19 @@ def test_native_cls_draw_matches_oracle(F):
 
 
 @pytest.mark.parametrize("F", [1, 2, 3])
-def test_native_nc_mh_matches_oracle(F):
+@pytest.mark.parametrize("n_iter", [1, 2])
+def test_native_nc_mh_matches_oracle(F, n_iter):
     L, nside = 40, 16
     m, init = make_problem(L, nside, F, seed=6)
-    p = _plan(m, nchains=2, chain0=1)
+    p = _plan(m, nchains=2, chain0=1, n_iter_metropolis=n_iter)
     dl = p.dl_tensor(init)
     _, st = p.cr_sweep(p.data_tensor(m.d_alm), p.block_params(1, dl), seed=SEED, iteration=4)
     acc = p.split_accept(p.nc_mh(st, dl, seed=SEED, iteration=4))
     out = p.dl_dicts(dl)
     stn = st.cpu().numpy()
     for c in range(2):
-        ref, racc = H.nc_mh(m, init, rows_to_stats(F, stn[c]), seed=SEED, chain=1 + c, iteration=4)
+        ref, racc = H.nc_mh(m, init, rows_to_stats(F, stn[c]), seed=SEED, chain=1 + c, iteration=4,
+                            n_iter=n_iter)
         for sp in m.spectra:
             np.testing.assert_array_equal(acc[sp][c], np.array(racc[sp]), err_msg=sp)
             np.testing.assert_allclose(out[c][sp], ref[sp], rtol=1e-10, err_msg=sp)
