@@ -65,6 +65,7 @@ _SIGS = [
     ("gs_block_params", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_cr_sweep", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                    _VP, _VP, _VP]),
+    ("gs_sweep_stats", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     ("gs_cls_draw", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
     ("gs_nc_mh", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
     ("gs_stats_to_noncentered", ctypes.c_int, [_VP, _VP, _VP, _VP]),

@@ -323,11 +323,6 @@ struct SweepAcc {
     double v[NS];
 };
 
-// two consecutive doubles of the real layout, 8-byte aligned: the pair
-// (sqrt2 Re, sqrt2 Im) of one (l, m) starts at slot 2i-(L+1), which is odd
-// whenever L+1 is odd; gfx950 global accesses need only dword alignment
-typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
-
 // one (l, m) entry of every field: NV = 1 (m = 0, one real slot) or 2 (re, im)
 template <int F, int NV>
 __device__ __forceinline__ void load_d(const double* __restrict__ d, long long NR, long long r, double (&dv)[F][2]) {
@@ -337,15 +332,22 @@ __device__ __forceinline__ void load_d(const double* __restrict__ d, long long N
         for (int c = 0; c < NV; ++c) dv[f][c] = d[f * NR + r + c];
 }
 
-template <int F, bool REPLAY, bool STORE, int NV>
+// ZM: 0 native RNG draw, 1 replay (z from memory), 2 statistics of a given s
+template <int F, int ZM, bool STORE, int NV>
 __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const double* __restrict__ zc,
                                             double* __restrict__ sc, long long NR, long long r, uint32_t i,
                                             uint32_t tag, uint32_t iter, Key key, const double (&pm)[NP],
                                             double (&acc)[SweepAcc<F>::NS], const double* __restrict__ tab) {
     double zv[F][2], sv[F][NV];
+    if constexpr (ZM == 2) {
+#pragma unroll
+        for (int f = 0; f < F; ++f)
+#pragma unroll
+            for (int c = 0; c < NV; ++c) sv[f][c] = sc[f * NR + r + c];
+    } else {
 #pragma unroll
     for (int f = 0; f < F; ++f) {
-        if constexpr (REPLAY) {
+        if constexpr (ZM == 1) {
 #pragma unroll
             for (int c = 0; c < NV; ++c) zv[f][c] = zc[f * NR + r + c];
         } else {
@@ -373,29 +375,13 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
             for (int f = 0; f < F; ++f) sv[f][c] = pm[f] * dv[f][c] + zv[f][c] * pm[F + f];
         }
     }
+    }
     if constexpr (STORE) {
+        // streaming output: non-temporal stores keep the data tiles in L2
 #pragma unroll
-        for (int f = 0; f < F; ++f) {
-#if defined(GS_VEC16)
-            if constexpr (NV == 2) {
-                dbl2u v; v.x = sv[f][0]; v.y = sv[f][1];
-#if defined(GS_NO_NT)
-                *reinterpret_cast<dbl2u*>(sc + f * NR + r) = v;
-#else
-                __builtin_nontemporal_store(v, reinterpret_cast<dbl2u*>(sc + f * NR + r));
-#endif
-                continue;
-            }
-#endif
+        for (int f = 0; f < F; ++f)
 #pragma unroll
-            for (int c = 0; c < NV; ++c) {
-#if defined(GS_NO_NT)
-                sc[f * NR + r + c] = sv[f][c];
-#else
-                __builtin_nontemporal_store(sv[f][c], &sc[f * NR + r + c]);
-#endif
-            }
-        }
+            for (int c = 0; c < NV; ++c) __builtin_nontemporal_store(sv[f][c], &sc[f * NR + r + c]);
     }
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
@@ -427,7 +413,7 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
 #ifndef GS_SWEEP_WAVES_PER_SIMD
 #define GS_SWEEP_WAVES_PER_SIMD 1
 #endif
-template <int F, bool REPLAY, bool STORE>
+template <int F, int ZM, bool STORE>
 __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L, int nchains, int ntile, int nchunk, int tm,
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
                                                   const double* __restrict__ params, const double* __restrict__ z,
@@ -435,8 +421,8 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
                                                   uint32_t seed_lo, uint32_t seed_hi, uint32_t iter, uint32_t substep,
                                                   int chain0) {
     constexpr int NS = SweepAcc<F>::NS;
-    __shared__ double tab[REPLAY ? 1 : BM_TAB_DOUBLES];
-    if constexpr (!REPLAY) {
+    __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
+    if constexpr (ZM == 0) {
         bm_stage_tables(tab);
         __syncthreads();
     }
@@ -458,7 +444,7 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
     const uint32_t tag = TAG_CR | (substep << 8);
 
     double pm[NP];
-    if (lane_ok) {
+    if (ZM != 2 && lane_ok) {
         const double* pp = params + ((long long)chain * (L + 1) + ell) * NP;
 #pragma unroll
         for (int q = 0; q < NP; ++q) pm[q] = pp[q];
@@ -470,7 +456,7 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
 #pragma unroll
     for (int q = 0; q < NS; ++q) acc[q] = 0.0;
 
-    const double* zc = REPLAY ? z + (long long)chain * F * NR : nullptr;
+    const double* zc = ZM == 1 ? z + (long long)chain * F * NR : nullptr;
     double* sc = s + (long long)chain * F * NR;
 
     int m = m0;
@@ -478,7 +464,7 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
     if (m == 0) {
         if (lane_ok) {
             load_d<F, 1>(d, NR, ell, dv);
-            sweep_entry<F, REPLAY, STORE, 1>(dv, zc, sc, NR, ell, (uint32_t)ell, tag, iter, key, pm, acc, tab);
+            sweep_entry<F, ZM, STORE, 1>(dv, zc, sc, NR, ell, (uint32_t)ell, tag, iter, key, pm, acc, tab);
         }
         m = 1;
     }
@@ -490,7 +476,7 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
 #if !defined(GS_PREFETCH)
         for (; m < m1; ++m) {
             load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
-            sweep_entry<F, REPLAY, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
+            sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
             i += L - m;
         }
 #else
@@ -499,7 +485,7 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
             const long long inext = i + (L - m);
             double dn[F][2];
             if (m + 1 < m1) load_d<F, 2>(d, NR, 2 * inext - (L + 1), dn);
-            sweep_entry<F, REPLAY, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
+            sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
 #pragma unroll
             for (int f = 0; f < F; ++f) { dv[f][0] = dn[f][0]; dv[f][1] = dn[f][1]; }
             i = inext;
@@ -509,7 +495,7 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
         for (; m < m1; ++m) {
             if (lane_ok && ell >= m) {
                 load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
-                sweep_entry<F, REPLAY, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm,
+                sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm,
                                                  acc, tab);
             }
             i += L - m;
@@ -925,9 +911,11 @@ void build_tasks(gs_plan* p) {
         for (int t = 0; t < p->ntile; ++t) n += (L - WAVE * t) / tm + 1;
         return n;
     };
-    // rows per chunk: aim for >= 8192 waves so every SIMD has several to hide latency
-    int tm = 64;
-    while (tm > 4 && waves(tm) * p->nchains < 8192) tm /= 2;
+    // rows per chunk: fixed (independent of the chain count), so the fixed-order
+    // statistic sums -- and therefore every chain's trajectory -- are bit-identical
+    // whatever the batch size or GPU count; 32 rows measured best at the
+    // BASELINE size (tools/sweep_rows.sh)
+    int tm = 32;
     if (const char* env = getenv("GS_SWEEP_ROWS")) {
         const int v = atoi(env);
         if (v >= 1 && v <= 1024) tm = v;
@@ -1174,10 +1162,11 @@ static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e
     return 0;
 }
 
-int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
-                uint32_t iteration, uint32_t substep, double* s_out, double* stats, void* stream) {
+static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
+                        uint32_t iteration, uint32_t substep, double* s_out, double* stats, bool given,
+                        void* stream) {
     if (check_plan(p)) return -1;
-    if (!d_alm || !params || !stats) return set_error("gs_cr_sweep: null argument");
+    if (!d_alm || !stats || (!given && !params) || (given && !s_out)) return set_error("gs_cr_sweep: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const dim3 g((unsigned)((long long)p->nchains * p->npair)), b(256);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1186,8 +1175,9 @@ int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const dou
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunk, p->rows_per_task, p->tasks, d_alm, params, z, s_out,         \
                                              p->partials, slo, shi, iteration, substep, p->chain0)
-#define GS_SWF(FF) do { if (rep && st) GS_SW(FF, true, true); else if (rep) GS_SW(FF, true, false); \
-                        else if (st) GS_SW(FF, false, true); else GS_SW(FF, false, false); } while (0)
+#define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
+                        else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
+                        else GS_SW(FF, 0, false); } while (0)
     if (p->F == 1) GS_SWF(1); else if (p->F == 2) GS_SWF(2); else GS_SWF(3);
 #undef GS_SWF
 #undef GS_SW
@@ -1198,6 +1188,15 @@ int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const dou
                        p->nchunk, p->rows_per_task, p->nstat, p->partials, stats);
     GS_LAUNCH_CHECK("k_stats_finish");
     return 0;
+}
+
+int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
+                uint32_t iteration, uint32_t substep, double* s_out, double* stats, void* stream) {
+    return sweep_launch(p, d_alm, params, z, seed, iteration, substep, s_out, stats, false, stream);
+}
+
+int gs_sweep_stats(gs_plan* p, const double* d_alm, const double* s, double* stats, void* stream) {
+    return sweep_launch(p, d_alm, nullptr, nullptr, 0, 0, 0, const_cast<double*>(s), stats, true, stream);
 }
 
 int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_t seed, uint32_t iteration,

@@ -1,0 +1,395 @@
+"""The reference's class surface (drop-in for main_polarization.py), backed by the HIP path.
+
+Mirrors Gabriel-Ducrocq/GibbsSampler:
+  GibbsSampler        GibbsSampler.py:8-192
+  CenteredGibbs       CenteredGibbs.py:859-876
+  NonCenteredGibbs    NonCenteredGibbs.py:449-582
+  ASIS                ASIS.py:16-233
+and the step samplers the drivers own (``constrained_sampler``,
+``cls_sampler``; ``centered_cls_sampler`` / ``non_centered_cls_sampler``
+for ASIS) with the same ``sample`` signatures and return conventions.
+
+What the build covers (BASELINE.json north_star): the full-sky,
+isotropic-noise harmonic path (``mask_path=None``; ``all_sph`` semantics) for
+T-only, EB (the reference's polarization runs) and TEB.  The reference's
+centered full-sky runs go through its PCG branch (CenteredGibbs.py:845-850,
+qcinv); on the full sky with isotropic noise that system is diagonal and the
+closed form (CenteredGibbs.py:317-353) is its exact solution, which is what
+runs here.  Masked / pixel-domain variants (PCG, auxiliary-variable, MALA,
+over-relaxation, pixel-domain MH likelihood) need the spherical-harmonic
+transform and raise NotImplementedError.
+
+Extra keyword arguments (all optional): ``nchains`` (batched chains on one
+GPU), ``rng`` ("native" Philox or "replay" = numpy's global RNG in the
+reference's draw order), ``seed`` (native streams), ``fields`` ("EB" or
+"TEB" for polarization), ``chain0`` (global id of the first chain),
+``reference_quirks`` (ASIS re-centring of the centered map, ASIS.py:203).
+"""
+import time
+
+import numpy as np
+
+from .problem import gauss_beam
+from . import _capi as C
+
+_SPECTRA = {1: ("TT",), 2: ("EE", "BB"), 3: ("TT", "EE", "BB", "TE")}
+
+
+def _nfields(polarization, fields):
+    if not polarization:
+        return 1
+    if fields is None or fields.upper() == "EB":
+        return 2
+    if fields.upper() == "TEB":
+        return 3
+    raise ValueError("fields must be 'EB' or 'TEB'")
+
+
+def _scalar_noise(noise, what):
+    a = np.atleast_1d(np.asarray(noise, dtype=np.float64))
+    if not np.all(a == a.flat[0]):
+        raise NotImplementedError(f"{what}: anisotropic pixel noise needs the pixel-domain (SHT) path")
+    return float(a.flat[0])
+
+
+def _harmonic_data(pix_map, nfields, lmax):
+    keys = {1: ("TT",), 2: ("EE", "BB"), 3: ("TT", "EE", "BB")}[nfields]
+    if nfields == 1 and not isinstance(pix_map, dict):
+        arr = np.asarray(pix_map, dtype=np.float64)
+        if arr.shape[-1] == (lmax + 1) ** 2:
+            return {"TT": arr}
+        raise NotImplementedError("temperature data given as a pixel map needs the SHT (map2alm) path; "
+                                  "pass the real-layout a_lm (utils.complex_to_real of map2alm) instead")
+    missing = [k for k in keys if k not in pix_map]
+    if missing:
+        raise NotImplementedError(f"pix_map lacks harmonic data {missing}: pixel-domain maps (Q/U) need the "
+                                  "SHT path; pass real-layout a_lm under 'TT'/'EE'/'BB' (all_sph form, "
+                                  "main_polarization.py:43-45)")
+    return {k: np.asarray(pix_map[k], dtype=np.float64) for k in keys}
+
+
+def _default_bins(lmax, nfields):
+    return {s: np.arange(0, lmax + 2) for s in _SPECTRA[nfields]}
+
+
+def _default_blocks(bins):
+    """MHClsSampler default (ClsSampler.py:66-67): one block per bin from bin 2."""
+    return {s: np.arange(2, len(b)) for s, b in bins.items()}
+
+
+class GibbsSampler:
+    """GibbsSampler.py:8-192."""
+
+    _kind = None
+
+    def __init__(self, pix_map, noise, beam_fwhm_deg, nside, lmax, polarization=False, bins=None, n_iter=10000,
+                 gibbs_cr=False, rj_step=False, ula=False, *, nchains=1, rng="native", seed=0, fields=None,
+                 chain0=0, reference_quirks=True, noise_pol=None, proposal_variances=None,
+                 metropolis_blocks=None, n_iter_metropolis=1, mask_path=None):
+        if mask_path is not None:
+            raise NotImplementedError("masked (cut-sky) samplers need the SHT path (SURVEY.md 8f f1/f2)")
+        self.noise = noise
+        self.beam = beam_fwhm_deg
+        self.nside = nside
+        self.lmax = lmax
+        self.polarization = polarization
+        self.Npix = 12 * nside ** 2
+        self.n_iter = n_iter
+        self.gibbs_cr = gibbs_cr
+        self.rj_step = rj_step
+        self.ula = True                      # GibbsSampler.py:41 (hard-coded)
+        self.nfields = _nfields(polarization, fields)
+        self.spectra = _SPECTRA[self.nfields]
+        self.pix_map = pix_map
+        self.bl_gauss = gauss_beam((np.pi / 180) * beam_fwhm_deg, lmax)
+        self.bl_map = self.compute_bl_map(beam_fwhm_deg)
+        if bins is None:
+            self.bins = _default_bins(lmax, self.nfields)
+        elif isinstance(bins, dict):
+            self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
+        else:
+            self.bins = {self.spectra[0]: np.asarray(bins)}
+        self.dls_to_cls_array = np.array([2 * np.pi / (l * (l + 1)) if l != 0 else 0 for l in range(lmax + 1)])
+        nt = _scalar_noise(noise, "noise")
+        if self.nfields == 1:
+            noise_var = [nt]
+        else:
+            npol = _scalar_noise(noise_pol if noise_pol is not None else noise, "noise_pol")
+            noise_var = [npol, npol] if self.nfields == 2 else [nt, npol, npol]
+        self.noise_var = np.array(noise_var)
+        self.nchains = int(nchains)
+        self.rng = rng
+        self.seed = seed
+        self.chain0 = chain0
+        self.reference_quirks = reference_quirks
+        self.proposal_variances = proposal_variances
+        self.metropolis_blocks = metropolis_blocks
+        self.n_iter_metropolis = n_iter_metropolis
+        self._runner = None
+
+    # -- helpers of the reference base class --------------------------------------------
+    def dls_to_cls(self, dls_):
+        """GibbsSampler.py:56-62."""
+        return dls_[:] * self.dls_to_cls_array
+
+    def compute_bl_map(self, beam_fwhm_deg):
+        """GibbsSampler.py:64-74: b_l expanded to the real a_lm layout."""
+        bl = gauss_beam((np.pi / 180) * beam_fwhm_deg, self.lmax)
+        return np.concatenate([bl, np.array([cl for m in range(1, self.lmax + 1) for cl in bl[m:] for _ in range(2)])])
+
+    # -- the device runner ------------------------------------------------------------------
+    def _make_runner(self):
+        from .samplers import BatchedRunner
+        if self._runner is None:
+            d = _harmonic_data(self.pix_map, self.nfields, self.lmax)
+            blocks = None
+            pv = None
+            if self._kind in ("noncentered", "asis"):
+                blocks = self.metropolis_blocks if self.metropolis_blocks is not None else _default_blocks(self.bins)
+                if isinstance(blocks, dict):
+                    blocks = {s: np.asarray(blocks[s]) for s in self.spectra}
+                else:
+                    blocks = {self.spectra[0]: np.asarray(blocks)}
+                pv = self.proposal_variances
+                if not isinstance(pv, dict):
+                    pv = {self.spectra[0]: np.asarray(pv)}
+            self._runner = BatchedRunner(kind=self._kind, lmax=self.lmax, nside=self.nside, nfields=self.nfields,
+                                         nchains=self.nchains, bl=self.bl_gauss, noise_var=self.noise_var,
+                                         bins=self.bins, d_alm=d, blocks=blocks, proposal_variances=pv,
+                                         rng=self.rng, seed=self.seed, chain0=self.chain0,
+                                         quirks=C.GS_QUIRK_ASIS_RECENTRE_CENTERED if self.reference_quirks else 0,
+                                         n_iter_metropolis=self.n_iter_metropolis)
+        return self._runner
+
+    def _squeeze(self, a):
+        return a[:, 0] if self.nchains == 1 else a
+
+    def _run_common(self, dls_init):
+        runner = self._make_runner()
+        init = dls_init if isinstance(dls_init, dict) else {self.spectra[0]: dls_init}
+        h, acc, t = runner.run(init, self.n_iter, timings=True)
+        h = {s: self._squeeze(v) for s, v in h.items()}
+        if acc is not None:
+            acc = {s: self._squeeze(v) for s, v in acc.items()}
+        return h, acc, t
+
+    def run(self, dls_init):
+        """GibbsSampler.py:183-192."""
+        return self.run_polarization(dls_init) if self.polarization else self.run_temperature(dls_init)
+
+    def run_polarization(self, dls_init):
+        raise NotImplementedError
+
+    def run_temperature(self, dls_init):
+        raise NotImplementedError
+
+    @property
+    def skymap(self):
+        """Current batched sky map [nchains, F, (L+1)^2] (device tensor)."""
+        return None if self._runner is None else self._runner.skymap()
+
+
+class CenteredGibbs(GibbsSampler):
+    """CenteredGibbs.py:859-876 (full-sky closed-form CR + inverse-Gamma/Wishart C_l draw)."""
+
+    _kind = "centered"
+
+    def __init__(self, pix_map, noise_temp, noise_pol, beam, nside, lmax, Npix, mask_path=None,
+                 polarization=False, bins=None, n_iter=100000, rj_step=False, all_sph=False, gibbs_cr=False,
+                 overrelaxation=False, ula=False, **kw):
+        if gibbs_cr or overrelaxation or rj_step:
+            if mask_path is not None:
+                raise NotImplementedError("auxiliary-variable / over-relaxation / RJPO CR need the SHT path")
+        super().__init__(pix_map, noise_temp, beam, nside, lmax, polarization=polarization, bins=bins,
+                         n_iter=n_iter, gibbs_cr=gibbs_cr, rj_step=rj_step, mask_path=mask_path,
+                         noise_pol=noise_pol, **kw)
+        self.all_sph = all_sph
+        self.overrelaxation = overrelaxation
+        self.constrained_sampler = CenteredConstrainedRealization(self)
+        self.cls_sampler = CenteredClsSampler(self)
+
+    def run_polarization(self, dls_init):
+        """GibbsSampler.run_polarization (GibbsSampler.py:118-180): returns
+        (h_dls, h_accept_cr, h_duration_cr, h_duration_cls_sampling)."""
+        h, _, t = self._run_common(dls_init)
+        n = len(t)
+        return h, np.ones(n, dtype=int), np.asarray(t), np.zeros(n)
+
+    def run_temperature(self, dls_init):
+        """GibbsSampler.run_temperature (GibbsSampler.py:76-116)."""
+        h, _, t = self._run_common(dls_init)
+        return h["TT"], np.ones(len(t), dtype=int), list(t)
+
+
+class NonCenteredGibbs(GibbsSampler):
+    """NonCenteredGibbs.py:449-582 (all_sph: per-l block MH)."""
+
+    _kind = "noncentered"
+
+    def __init__(self, pix_map, noise_I, noise_Q, beam, nside, lmax, Npix, proposal_variances,
+                 metropolis_blocks=None, polarization=False, bins=None, n_iter=10000, n_iter_metropolis=1,
+                 mask_path=None, all_sph=False, **kw):
+        super().__init__(pix_map, noise_I, beam, nside, lmax, polarization=polarization, bins=bins, n_iter=n_iter,
+                         mask_path=mask_path, noise_pol=noise_Q, proposal_variances=proposal_variances,
+                         metropolis_blocks=metropolis_blocks, n_iter_metropolis=n_iter_metropolis, **kw)
+        self.all_sph = all_sph
+        self.constrained_sampler = NonCenteredConstrainedRealization(self)
+        self.cls_sampler = NonCenteredClsSampler(self)
+
+    def run_polarization(self, dls_init):
+        """NonCenteredGibbs.py:529-571: (h_dls, total_accept, h_duration_cr, h_duration_cls)."""
+        h, acc, t = self._run_common(dls_init)
+        return h, acc, np.array([]), np.array([])
+
+    def run_temperature(self, dls_init):
+        """NonCenteredGibbs.py:488-527: (h_dl, total_accept, h_time_seconds)."""
+        h, acc, t = self._run_common(dls_init)
+        return h["TT"][1:], acc["TT"], np.asarray(t)
+
+
+class ASIS(GibbsSampler):
+    """ASIS.py:16-233 (interweaving: centered CR + C_l draw, non-centering, NC MH, re-centring)."""
+
+    _kind = "asis"
+
+    def __init__(self, pix_map, noise, noise_Q, beam, nside, lmax, Npix, proposal_variances, metropolis_blocks=None,
+                 polarization=False, bins=None, n_iter=10000, n_iter_metropolis=1, mask_path=None, gibbs_cr=False,
+                 rj_step=False, all_sph=False, n_gibbs=20, overrelaxation=False, **kw):
+        super().__init__(pix_map, noise, beam, nside, lmax, polarization=polarization, bins=bins, n_iter=n_iter,
+                         gibbs_cr=gibbs_cr, rj_step=rj_step, mask_path=mask_path, noise_pol=noise_Q,
+                         proposal_variances=proposal_variances, metropolis_blocks=metropolis_blocks,
+                         n_iter_metropolis=n_iter_metropolis, **kw)
+        self.all_sph = all_sph
+        self.n_gibbs = n_gibbs
+        self.overrelaxation = overrelaxation
+        self.constrained_sampler = CenteredConstrainedRealization(self)
+        self.constrained_sampler.n_gibbs = n_gibbs
+        self.centered_cls_sampler = CenteredClsSampler(self)
+        self.non_centered_cls_sampler = NonCenteredClsSampler(self)
+
+    def run_polarization(self, dls_init):
+        """ASIS.py:134-226: (h_dls, total_accept, accept_cr|None, h_iteration_duration,
+        h_duration_cr, h_duration_cls_sampling, h_duration_cls_nc_sampling)."""
+        h, acc, t = self._run_common(dls_init)
+        z = np.zeros(len(t))
+        return h, acc, None, np.asarray(t), z, z, z
+
+    def run_temperature(self, dls_init):
+        """ASIS.py:69-131: (h_dls, h_accept, h_accept_cr, h_time_seconds)."""
+        h, acc, t = self._run_common(dls_init)
+        return h["TT"], acc["TT"], np.ones(len(t), dtype=int), np.asarray(t)
+
+
+# ---------------------------------------------------------------------------------------
+# single-step samplers (the objects the drivers own) -- numpy in / numpy out, one chain
+# ---------------------------------------------------------------------------------------
+class _StepBase:
+    def __init__(self, owner):
+        self.owner = owner
+        self.lmax = owner.lmax
+        self.nside = owner.nside
+        self.Npix = owner.Npix
+        self.bl_map = owner.bl_map
+        self.bl_gauss = owner.bl_gauss
+        self.pix_map = owner.pix_map
+        self.mask_path = None
+        self.pcg_accuracy = 1.0e-5          # CenteredGibbs.py:280 (kept for the result dict)
+        self.gibbs_cr = owner.gibbs_cr
+        self.n_gibbs = 1
+        self._plan = None
+        self._d = None
+
+    def _unbinned_plan(self):
+        """A 1-chain plan with unbinned spectra (the CR steps take unbinned D_l)."""
+        from .engine import GibbsPlan
+        if self._plan is None:
+            o = self.owner
+            bins = {s: np.arange(0, o.lmax + 2) for s in o.spectra}
+            self._plan = GibbsPlan(o.lmax, o.nside, o.nfields, 1, o.bl_gauss, o.noise_var, bins)
+            self._d = self._plan.data_tensor(_harmonic_data(o.pix_map, o.nfields, o.lmax))
+        return self._plan
+
+    def _binned_plan(self):
+        return self.owner._make_runner().plan
+
+    def _as_dict(self, x):
+        return x if isinstance(x, dict) else {self.owner.spectra[0]: x}
+
+    def _fields_dict(self, s):
+        keys = {1: ("TT",), 2: ("EE", "BB"), 3: ("TT", "EE", "BB")}[self.owner.nfields]
+        out = {k: s[i] for i, k in enumerate(keys)}
+        return out if self.owner.nfields != 1 else out["TT"]
+
+    def _draw(self, mode, all_dls):
+        p = self._unbinned_plan()
+        dl = p.dl_tensor(self._as_dict(all_dls))
+        z = p.replay_cr_normals() if self.owner.rng == "replay" else None
+        self._it = getattr(self, "_it", 0) + 1
+        params = p.block_params(mode, dl)
+        s, _ = p.cr_sweep(self._d, params, z=z, seed=self.owner.seed, iteration=0xFFFF0000 + self._it)
+        return self._fields_dict(s.cpu().numpy()[0])
+
+
+class CenteredConstrainedRealization(_StepBase):
+    """PolarizedCenteredConstrainedRealization.sample (CenteredGibbs.py:317-353, 828-850)
+    / CenteredConstrainedRealization (CenteredGibbs.py:103-232), full sky."""
+
+    def sample(self, all_dls, s_old=None, *args, **kw):
+        return self._draw(C.GS_MODE_CENTERED, all_dls), 1
+
+    sample_no_mask = sample
+
+
+class NonCenteredConstrainedRealization(_StepBase):
+    """PolarizedNonCenteredConstrainedRealization.sample_no_mask (NonCenteredGibbs.py:134-176);
+    returns accept 0 like the reference (176)."""
+
+    def sample(self, all_dls, *args, **kw):
+        return self._draw(C.GS_MODE_NONCENTERED, all_dls), 0
+
+    sample_no_mask = sample
+
+
+class _StatsMixin:
+    def _stats_of(self, alms):
+        import torch
+        p = self._binned_plan()
+        o = self.owner
+        keys = {1: ("TT",), 2: ("EE", "BB"), 3: ("TT", "EE", "BB")}[o.nfields]
+        a = alms if isinstance(alms, dict) else {"TT": alms}
+        s = torch.from_numpy(np.stack([np.asarray(a[k], dtype=np.float64) for k in keys])[None].copy()).to(p.device)
+        st = p.zeros(1, p.nstat, p.L + 1)
+        C.check(p.lib.gs_sweep_stats(p._h, C.ptr(self.owner._make_runner().d), C.ptr(s), C.ptr(st),
+                                     C.stream_ptr()), "gs_sweep_stats")
+        return st
+
+
+class CenteredClsSampler(_StepBase, _StatsMixin):
+    """PolarizedCenteredClsSampler.sample (CenteredGibbs.py:54-93) / CenteredClsSampler (24-48)."""
+
+    def sample(self, alms):
+        p = self._binned_plan()
+        st = self._stats_of(alms)
+        var = p.replay_invgamma() if self.owner.rng == "replay" else None
+        self._it = getattr(self, "_it", 0) + 1
+        out = p.dl_dicts(p.cls_draw(st, variates=var, seed=self.owner.seed, iteration=0xFFFE0000 + self._it))[0]
+        return out if self.owner.nfields != 1 else out["TT"]
+
+
+class NonCenteredClsSampler(_StepBase, _StatsMixin):
+    """PolarizationNonCenteredClsSampler.sample (NonCenteredGibbs.py:401-445), all_sph."""
+
+    def sample(self, s_nonCentered, binned_dls_old, *args):
+        p = self._binned_plan()
+        st = self._stats_of(s_nonCentered)
+        dl = p.dl_tensor(self._as_dict(binned_dls_old))
+        up = ua = None
+        if self.owner.rng == "replay":
+            up, ua = p.replay_mh_uniforms()
+        self._it = getattr(self, "_it", 0) + 1
+        acc = p.split_accept(p.nc_mh(st, dl, up, ua, seed=self.owner.seed, iteration=0xFFFD0000 + self._it))
+        out = p.dl_dicts(dl)[0]
+        acc = {s: list(v[0]) for s, v in acc.items()}
+        if self.owner.nfields == 1:
+            return out["TT"], acc["TT"]
+        return out, acc

@@ -114,6 +114,9 @@ int gs_block_params(gs_plan* plan, int mode, const double* dl_binned, double* pa
 int gs_cr_sweep(gs_plan* plan, const double* d_alm, const double* params, const double* z_replay,
                 uint64_t seed, uint32_t iteration, uint32_t substep,
                 double* s_out, double* stats, void* stream);
+/* statistics (alm2cl auto/cross + data correlations) of a given s
+ * [nchains][nfields][NR] -- hp.alm2cl of CenteredGibbs.py:30,61 */
+int gs_sweep_stats(gs_plan* plan, const double* d_alm, const double* s, double* stats, void* stream);
 /* centered C_l draw (inverse-Gamma; TEB: inverse-Wishart TT/EE/TE) */
 int gs_cls_draw(gs_plan* plan, const double* stats, const double* invgamma_replay,
                 uint64_t seed, uint32_t iteration, double* dl_binned_out, void* stream);
