@@ -426,10 +426,17 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
         bm_stage_tables(tab);
         __syncthreads();
     }
-    const int pair = blockIdx.x / nchains;
-    const int chain = blockIdx.x % nchains;
+    // XCD-aware remap (bijective): workgroups are dealt round-robin over the 8
+    // XCDs, so physical id b runs on XCD b % 8; give each XCD a contiguous range
+    // of logical ids so that all chains of one (tiles, rows) block share one
+    // XCD's L2 for the data reads (speed only -- any placement is correct)
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int pair = wg / nchains;
+    const int chain = wg % nchains;
     const int lane = threadIdx.x & 63;
     const int2 gc = tasks[pair];
+    if (gc.x < 0) return;                       // padding pair
     const int t = 4 * gc.x + (threadIdx.x >> 6);
     if (t >= ntile) return;
     const int lhi = L - WAVE * t;
@@ -923,9 +930,36 @@ void build_tasks(gs_plan* p) {
     p->rows_per_task = tm;
     p->nchunk = L / tm + 1;
     p->ntask = (int)waves(tm);
-    std::vector<int2> tasks;
+    // (tile group, row chunk) pairs, with their work in active lane-rows
+    std::vector<std::pair<long long, int2>> work;
     for (int g = 0; 4 * g < p->ntile; ++g)
-        for (int c = 0; c * tm <= L - WAVE * 4 * g; ++c) tasks.push_back(make_int2(g, c));
+        for (int c = 0; c * tm <= L - WAVE * 4 * g; ++c) {
+            long long wl = 0;
+            for (int t = 4 * g; t < std::min(4 * g + 4, p->ntile); ++t) {
+                const int lhi = L - WAVE * t, lo = std::max(lhi - 63, 0);
+                for (int m = c * tm; m < std::min(c * tm + tm, lhi + 1); ++m) wl += lhi - std::max(lo, m) + 1;
+            }
+            work.push_back({wl, make_int2(g, c)});
+        }
+    // the sweep gives XCD x a contiguous range of pairs (all chains of a pair on
+    // one XCD); deal the pairs heaviest-first over 8 buckets so every XCD gets
+    // the same work, padding with empty pairs (g = -1) to a multiple of 8
+    std::stable_sort(work.begin(), work.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    const int per = (int)((work.size() + 7) / 8);
+    std::vector<std::vector<int2>> bucket(8);
+    std::vector<long long> load(8, 0);
+    for (const auto& w : work) {
+        int best = -1;
+        for (int x = 0; x < 8; ++x)
+            if ((int)bucket[x].size() < per && (best < 0 || load[x] < load[best])) best = x;
+        bucket[best].push_back(w.second);
+        load[best] += w.first;
+    }
+    std::vector<int2> tasks;
+    for (int x = 0; x < 8; ++x) {
+        for (const int2& t : bucket[x]) tasks.push_back(t);
+        for (int k = (int)bucket[x].size(); k < per; ++k) tasks.push_back(make_int2(-1, 0));
+    }
     p->npair = (int)tasks.size();
     dev_upload(&p->tasks, tasks);
 }
