@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
+    ap.add_argument("--timing-launches", type=int, default=20,
+                    help="eager steps after the timed loop whose sweep launches are timed with hipEvents")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -84,21 +87,33 @@ def main():
     runner.init(P["dls_init"])
     for _ in range(args.warmup):
         runner.step()
+    trace = plan.zeros(args.steps, plan.nchains, plan.nspec, plan.maxbins)
+    use_graph = not args.no_graph
+    if use_graph:
+        # one hipGraph per Gibbs iteration: the D_l trace is written on the device
+        runner.capture_graph(trace=trace, trace_capacity=args.steps)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    plan.sweep_timing(True)
-    trace = plan.zeros(args.steps, plan.nchains, plan.nspec, plan.maxbins)
     t0 = time.perf_counter()
     for i in range(args.steps):
         runner.step()
-        trace[i].copy_(runner.dl)
+        if not use_graph:
+            trace[i].copy_(runner.dl)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
     elapsed = t1 - t0
+    # dominant-kernel timing: hipEvents around every sweep launch (on its stream) of
+    # eager steps of the same state right after the timed loop
+    runner.graph = None
+    plan.iteration_counter(False)
+    plan.sweep_timing(True)
+    for _ in range(args.timing_launches):
+        runner.step()
+    torch.cuda.synchronize()
     sweep_ms, sweep_n = plan.sweep_timing(False)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -144,6 +159,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (analytic fiducial spectra, d = b s + n in harmonic space, seed 0)",
             "config": {"workload": f"{args.workload} TEB all_sph full-sky" if args.fields == 3 else args.workload,
+                       "launch": "hipGraph per iteration" if use_graph else "eager",
                        "nside": args.nside, "lmax": args.lmax, "nfields": args.fields,
                        "chains_per_gpu": args.nchains, "global_chains": args.nchains * world,
                        "rng": "native philox4x32-10", "parallelism": f"chains sharded over {world} GPU(s)"},

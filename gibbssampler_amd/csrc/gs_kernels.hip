@@ -75,6 +75,9 @@ struct gs_plan {
     int phase_n[4] = {0, 0, 0, 0};
     int phase_off[4] = {0, 0, 0, 0};
     int2* phase_tab = nullptr;       // (spectrum, block) pairs, phase-major
+    int4* phase_rng = nullptr;       // per phase entry: (lo bin, hi bin, l0, l1); wide blocks first
+    int phase_nwide[4] = {0, 0, 0, 0};
+    int mh_lmin = 0;
     int phase_sp[4][2] = {{-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}};
     int* ell2blk = nullptr;          // [nspec][L+1] MH block of each l (-1: none)
     double* gbuf = nullptr;          // [nchains][2][L+1] per-l likelihood differences
@@ -95,6 +98,10 @@ struct gs_plan {
     double* prop = nullptr;          // [nchains][nspec][maxbins]
     double* logr = nullptr;          // [nchains][nspec][maxbins]
     double* dl_tmp = nullptr;        // [nchains][nspec][maxbins]
+    // device iteration counter (hipGraph replay of whole steps)
+    uint32_t* iter_dev = nullptr;
+    bool iter_dev_on = false;
+    const uint32_t* itp() const { return iter_dev_on ? iter_dev : nullptr; }
     // dominant-kernel timing
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -114,6 +121,14 @@ __device__ __forceinline__ double dl_at(const double* __restrict__ dl_chain, con
     const int b = ell2bin[sp * Lp1 + ell];
     return b < 0 ? 0.0 : dl_chain[sp * maxbins + b];
 }
+
+// iteration counter of the counter-based streams: a host value, or (for
+// hipGraph replay) a device word advanced by k_iter_advance once per step
+struct IterArg {
+    uint32_t host;
+    const uint32_t* dev;
+    __device__ __forceinline__ uint32_t get() const { return dev ? *dev : host; }
+};
 
 // lower Cholesky of the TE block of C and the B entry, zero-variance rule
 struct CovChol { double a00, a10, a11, aB; };
@@ -237,11 +252,10 @@ __global__ void k_unfold(int n, const double* __restrict__ binned, const int* __
 // MODE 1 non-centered (NonCenteredGibbs.py:141-174): Sigma = (I + A^T diag(b^2 k) A)^-1,
 //                                                   M = Sigma A^T diag(b k), A = chol(C)
 template <int F, int MODE>
-__global__ __launch_bounds__(256) void k_block_params(int L, int nchains, int maxbins, const double* __restrict__ dl,
-                                                      const int* __restrict__ ell2bin, const double* __restrict__ bl,
-                                                      double k0, double k1, double k2, double* __restrict__ params) {
+__device__ __forceinline__ void block_params_at(int g, int L, int nchains, int maxbins, const double* __restrict__ dl,
+                                                const int* __restrict__ ell2bin, const double* __restrict__ bl,
+                                                double k0, double k1, double k2, double* __restrict__ params) {
     const int Lp1 = L + 1;
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nchains * Lp1) return;
     const int chain = g / Lp1, ell = g % Lp1;
     constexpr int NS = F == 1 ? 1 : (F == 2 ? 2 : 4);
@@ -314,6 +328,14 @@ __global__ __launch_bounds__(256) void k_block_params(int L, int nchains, int ma
     }
 }
 
+template <int F, int MODE>
+__global__ __launch_bounds__(256) void k_block_params(int L, int nchains, int maxbins, const double* __restrict__ dl,
+                                                      const int* __restrict__ ell2bin, const double* __restrict__ bl,
+                                                      double k0, double k1, double k2, double* __restrict__ params) {
+    block_params_at<F, MODE>(blockIdx.x * blockDim.x + threadIdx.x, L, nchains, maxbins, dl, ell2bin, bl, k0, k1, k2,
+                             params);
+}
+
 // ============================================================================
 // fused CR draw + per-l statistics (the dominant, HBM-bound kernel)
 // ============================================================================
@@ -361,6 +383,9 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
             box_muller(philox(i, (uint32_t)f, tag, iter, key), zv[f][0], zv[f][1]);
 #else
             box_muller_tab(philox(i, (uint32_t)f, tag, iter, key), tab, zv[f][0], zv[f][1]);
+#endif
+#if defined(GS_SERIAL_FIELDS)
+            __builtin_amdgcn_sched_barrier(0);
 #endif
         }
     }
@@ -418,8 +443,9 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
                                                   const double* __restrict__ params, const double* __restrict__ z,
                                                   double* __restrict__ s, double* __restrict__ partials,
-                                                  uint32_t seed_lo, uint32_t seed_hi, uint32_t iter, uint32_t substep,
+                                                  uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, uint32_t substep,
                                                   int chain0) {
+    const uint32_t iter = itarg.get();
     constexpr int NS = SweepAcc<F>::NS;
     __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
     if constexpr (ZM == 0) {
@@ -539,8 +565,9 @@ template <int F>
 __global__ __launch_bounds__(256) void k_cls_draw(int L, int nchains, int maxbins, const int* __restrict__ bins,
                                                   const int* __restrict__ nbins_arr, const double* __restrict__ stats,
                                                   const double* __restrict__ variates, uint32_t seed_lo,
-                                                  uint32_t seed_hi, uint32_t iter, int chain0,
+                                                  uint32_t seed_hi, IterArg itarg, int chain0,
                                                   double* __restrict__ dl_out) {
+    const uint32_t iter = itarg.get();
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
     const int chain = blockIdx.x;
@@ -663,13 +690,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 // proposals (NonCenteredGibbs.py:292-309) and per-bin log proposal ratios
 // (313-330, 410-413): one thread per (chain, spectrum, bin)
 template <int F>
-__global__ __launch_bounds__(256) void k_mh_propose(int nchains, int maxbins, const int* __restrict__ nbins_arr,
-                                                    const double* __restrict__ prop_sd, const double* __restrict__ dl,
-                                                    double* __restrict__ prop, double* __restrict__ logr,
-                                                    const double* __restrict__ u_prop, uint32_t seed_lo,
-                                                    uint32_t seed_hi, uint32_t iter, int chain0) {
+__device__ __forceinline__ void mh_propose_at(long long g, int nchains, int maxbins, const int* __restrict__ nbins_arr,
+                                              const double* __restrict__ prop_sd, const double* __restrict__ dl,
+                                              double* __restrict__ prop, double* __restrict__ logr,
+                                              const double* __restrict__ u_prop, uint32_t seed_lo,
+                                              uint32_t seed_hi, IterArg itarg, int chain0) {
+    const uint32_t iter = itarg.get();
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
-    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (g >= (long long)nchains * NSP * maxbins) return;
     const int b = (int)(g % maxbins);
     const int sp = (int)((g / maxbins) % NSP);
@@ -692,6 +719,35 @@ __global__ __launch_bounds__(256) void k_mh_propose(int nchains, int maxbins, co
     }
     prop[g] = p;
     logr[g] = lr;
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void k_mh_propose(int nchains, int maxbins, const int* __restrict__ nbins_arr,
+                                                    const double* __restrict__ prop_sd, const double* __restrict__ dl,
+                                                    double* __restrict__ prop, double* __restrict__ logr,
+                                                    const double* __restrict__ u_prop, uint32_t seed_lo,
+                                                    uint32_t seed_hi, IterArg itarg, int chain0) {
+    mh_propose_at<F>(blockIdx.x * (long long)blockDim.x + threadIdx.x, nchains, maxbins, nbins_arr, prop_sd, dl, prop,
+                     logr, u_prop, seed_lo, seed_hi, itarg, chain0);
+}
+
+// non-centered prologue: the MH proposals depend only on the current D_l, not
+// on the CR draw, so they are made in the same launch as the CR block
+// parameters (proposal workgroups first; both halves are latency-bound).
+template <int F>
+__global__ __launch_bounds__(256) void k_nc_prologue(int nblk_prop, int L, int nchains, int maxbins,
+                                                     const int* __restrict__ ell2bin, const double* __restrict__ bl,
+                                                     double k0, double k1, double k2, double* __restrict__ params,
+                                                     const int* __restrict__ nbins_arr, const double* __restrict__ prop_sd,
+                                                     const double* __restrict__ dl, double* __restrict__ prop,
+                                                     double* __restrict__ logr, const double* __restrict__ u_prop,
+                                                     uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, int chain0) {
+    if ((int)blockIdx.x < nblk_prop)
+        mh_propose_at<F>(blockIdx.x * (long long)blockDim.x + threadIdx.x, nchains, maxbins, nbins_arr, prop_sd, dl,
+                         prop, logr, u_prop, seed_lo, seed_hi, itarg, chain0);
+    else
+        block_params_at<F, 1>(((int)blockIdx.x - nblk_prop) * blockDim.x + threadIdx.x, L, nchains, maxbins, dl,
+                              ell2bin, bl, k0, k1, k2, params);
 }
 
 // MH phase, step 1: per-(chain, l) likelihood difference of the phase's
@@ -746,8 +802,9 @@ __global__ __launch_bounds__(256) void k_mh_accept(int L, int nchains, int maxbi
                                                    const double* __restrict__ gbuf, double* __restrict__ dl,
                                                    const double* __restrict__ prop, const double* __restrict__ logr,
                                                    const double* __restrict__ u_acc, uint32_t seed_lo,
-                                                   uint32_t seed_hi, uint32_t iter, int chain0,
+                                                   uint32_t seed_hi, IterArg itarg, int chain0,
                                                    int32_t* __restrict__ accept_out) {
+    const uint32_t iter = itarg.get();
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     const long long w = blockIdx.x * 4LL + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -783,6 +840,150 @@ __global__ __launch_bounds__(256) void k_mh_accept(int L, int nchains, int maxbi
             for (int q = lo + lane; q < hi; q += 64) D[sp * maxbins + q] = P[sp * maxbins + q];
         taken = taken || acc;
         if (lane == 0 && accept_out) accept_out[(long long)chain * nacc + flat] = acc ? 1 : 0;
+    }
+}
+
+// MH phases fused in one launch: one workgroup per chain walks the phases;
+// per phase the per-l terms go to LDS, the per-(block, attempt) uniforms are
+// drawn in parallel, blocks of <= 16 l are decided by one thread each and
+// wider blocks by one wave each (fixed-order sums), then a barrier publishes
+// the updated D_l to the next phase (same workgroup).
+constexpr int MH_SMALL = 16;   // blocks of <= MH_SMALL multipoles are decided by one thread
+
+struct MhPhases {
+    int nphase;
+    int sp[4][2];
+    int off[4];
+    int n[4];
+    int nwide[4];
+    int lmin;     // smallest multipole any MH block covers (terms below it are never read)
+};
+
+template <int F>
+__global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases ph, const int2* __restrict__ phase_tab,
+                                                  const int4* __restrict__ phase_rng,
+                                                  const int* __restrict__ bins, const int* __restrict__ blocks,
+                                                  const int* __restrict__ acc_off, int nacc, int n_iter_mh,
+                                                  const int* __restrict__ ell2blk, const int* __restrict__ ell2bin,
+                                                  const double* __restrict__ bl, double k0, double k1, double k2,
+                                                  const double* __restrict__ stats, double* __restrict__ dl,
+                                                  const double* __restrict__ prop, const double* __restrict__ logr,
+                                                  const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
+                                                  IterArg itarg, int chain0, int32_t* __restrict__ accept_out) {
+    const uint32_t iter = itarg.get();
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    constexpr int NS = SweepAcc<F>::NS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int Lp1 = L + 1;
+    int maxnb = 0;
+    for (int q = 0; q < ph.nphase; ++q) maxnb = max(maxnb, ph.n[q]);
+    double* g = smem;                               // [2][L+1]
+    double* ub = g + 2 * Lp1;                       // [phase blocks x n_iter]
+    double* Ds = ub + maxnb * n_iter_mh;            // [NSP][maxbins] LDS copy of this chain's D_l
+    int* e2b = reinterpret_cast<int*>(Ds + NSP * maxbins);   // [NSP][L+1]
+    const int chain = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    double* D = dl + (long long)chain * NSP * maxbins;
+    const double* P = prop + (long long)chain * NSP * maxbins;
+    const double* R = logr + (long long)chain * NSP * maxbins;
+    const double* st = stats + (long long)chain * NS * Lp1;
+    for (int k = tid; k < NSP * Lp1; k += blockDim.x) e2b[k] = ell2bin[k];
+    for (int q = 0; q < ph.nphase; ++q) {
+        const int nb = ph.n[q];
+        if (nb == 0) continue;
+        const int sp0 = ph.sp[q][0], sp1 = ph.sp[q][1];
+        const int2* tab = phase_tab + ph.off[q];
+        const int4* rng = phase_rng + ph.off[q];
+        const int nwide = ph.nwide[q];
+        for (int k = tid; k < NSP * maxbins; k += blockDim.x) Ds[k] = D[k];
+        __syncthreads();
+        // per-l likelihood differences of the phase's spectra
+#if defined(GS_ABL_MH_TERMS)
+        for (int l = tid; l < Lp1; l += blockDim.x) { g[l] = 0.0; g[Lp1 + l] = 0.0; }
+        if (false)
+#endif
+        for (int l = ph.lmin + tid; l < Lp1; l += blockDim.x) {
+            double vo[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s = 0; s < NSP; ++s) vo[s] = var_from_dl(dl_at(Ds, e2b, maxbins, Lp1, s, l), l);
+            const double b = bl[l];
+            const double fo = f_ell<F>(st, Lp1, l, b, k0, k1, k2, vo[0], vo[1], vo[2], vo[3]);
+            const int sps[2] = {sp0, sp1};
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int sp = sps[k];
+                if (sp < 0) continue;
+                double out = 0.0;
+                if (ell2blk[sp * Lp1 + l] >= 0) {
+                    double vn[4] = {vo[0], vo[1], vo[2], vo[3]};
+                    vn[sp] = var_from_dl(P[sp * maxbins + e2b[sp * Lp1 + l]], l);
+                    bool ok = true;
+                    if constexpr (F == 3) ok = psd_ok(vn[0], vn[1], vn[3]);
+                    out = ok ? f_ell<F>(st, Lp1, l, b, k0, k1, k2, vn[0], vn[1], vn[2], vn[3]) - fo : -INFINITY;
+                }
+                g[k * Lp1 + l] = out;
+            }
+        }
+        // accept uniforms of every (block, attempt), in parallel
+        for (int j = tid; j < nb * n_iter_mh; j += blockDim.x) {
+            const int2 sb = tab[j / n_iter_mh];
+            const int att = j % n_iter_mh;
+            const int flat = acc_off[sb.x] + sb.y * n_iter_mh + att;
+#if defined(GS_ABL_MH_U)
+            ub[j] = 0.5 + 1e-9 * flat;
+#else
+            ub[j] = u_acc ? u_acc[(long long)chain * nacc + flat]
+                          : uniform1(key, sb.y, (uint32_t)sb.x | ((uint32_t)att << 8), TAG_MH_U, iter);
+#endif
+        }
+        __syncthreads();
+        // narrow blocks: one thread each
+#if defined(GS_ABL_MH_NARROW)
+        if (false)
+#endif
+        for (int j = nwide + tid; j < nb; j += blockDim.x) {
+            const int2 sb = tab[j];
+            const int4 r = rng[j];
+            const int sp = sb.x, blk = sb.y, k = sp == sp0 ? 0 : 1;
+            const int lo = r.x, hi = r.y, l0 = r.z, l1 = r.w;
+            double diff = 0.0, lrs = 0.0;
+            for (int l = l0; l < l1; ++l) diff += g[k * Lp1 + l];
+            for (int b = lo; b < hi; ++b) lrs += R[sp * maxbins + b];
+            bool taken = false;
+            for (int att = 0; att < n_iter_mh; ++att) {
+                const bool acc = log(ub[j * n_iter_mh + att]) < (taken ? 0.0 : diff) + lrs;
+                if (acc && !taken)
+                    for (int b = lo; b < hi; ++b) D[sp * maxbins + b] = P[sp * maxbins + b];
+                taken = taken || acc;
+                if (accept_out) accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
+            }
+        }
+        // wide blocks: one wave each
+#if defined(GS_ABL_MH_WIDE)
+        if (false)
+#endif
+        for (int j = wv; j < nwide; j += nwv) {
+            const int2 sb = tab[j];
+            const int4 r = rng[j];
+            const int sp = sb.x, blk = sb.y, k = sp == sp0 ? 0 : 1;
+            const int lo = r.x, hi = r.y, l0 = r.z, l1 = r.w;
+            double diff = 0.0, lrs = 0.0;
+            for (int l = l0 + lane; l < l1; l += 64) diff += g[k * Lp1 + l];
+            for (int b = lo + lane; b < hi; b += 64) lrs += R[sp * maxbins + b];
+            diff = wave_sum(diff);
+            lrs = wave_sum(lrs);
+            bool taken = false;
+            for (int att = 0; att < n_iter_mh; ++att) {
+                const bool acc = log(ub[j * n_iter_mh + att]) < (taken ? 0.0 : diff) + lrs;
+                if (acc && !taken)
+                    for (int b = lo + lane; b < hi; b += 64) D[sp * maxbins + b] = P[sp * maxbins + b];
+                taken = taken || acc;
+                if (lane == 0 && accept_out)
+                    accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -885,6 +1086,17 @@ __global__ void k_recentre(int L, int nchains, int maxbins, const double* __rest
             }
         }
     }
+}
+
+__global__ void k_iter_advance(uint32_t* it) { *it += 1u; }
+
+// trace[(it - 1) % capacity] <- dl, it from the device counter (or host value)
+__global__ void k_record_trace(long long n, const double* __restrict__ dl, double* __restrict__ trace, int capacity,
+                               IterArg itarg) {
+    const uint32_t it = itarg.get();
+    const long long slot = (long long)((it + capacity - 1u) % (uint32_t)capacity);
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
+        trace[slot * n + k] = dl[k];
 }
 
 // ============================================================================
@@ -1050,14 +1262,28 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     else if (F == 2) phases = {{0, 1}};
     else phases = {{1, 2}, {0}, {3}};
     std::vector<int2> ptab;
+    std::vector<int4> prng;
+    int lmin = L + 1;
     p->nphase = (int)phases.size();
     for (int ph = 0; ph < p->nphase; ++ph) {
         p->phase_off[ph] = (int)ptab.size();
         for (size_t q = 0; q < phases[ph].size(); ++q) p->phase_sp[ph][q] = phases[ph][q];
-        for (int sp : phases[ph])
-            for (int b = 0; b < p->nblocks[sp]; ++b) ptab.push_back(make_int2(sp, b));
+        // wide blocks (> MH_SMALL multipoles, one wave each in k_mh_fused) first
+        for (int pass = 0; pass < 2; ++pass)
+            for (int sp : phases[ph])
+                for (int b = 0; b < p->nblocks[sp]; ++b) {
+                    const int lo = blocks[sp * (maxbins + 1) + b], hi = blocks[sp * (maxbins + 1) + b + 1];
+                    const int l0 = hi > lo ? bins[sp * (maxbins + 1) + lo] : 0;
+                    const int l1 = hi > lo ? bins[sp * (maxbins + 1) + hi] : 0;
+                    if ((l1 - l0 > MH_SMALL) != (pass == 0)) continue;
+                    ptab.push_back(make_int2(sp, b));
+                    prng.push_back(make_int4(lo, hi, l0, l1));
+                    if (pass == 0) p->phase_nwide[ph]++;
+                    if (hi > lo) lmin = std::min(lmin, l0);
+                }
         p->phase_n[ph] = (int)ptab.size() - p->phase_off[ph];
     }
+    p->mh_lmin = std::min(lmin, L);
     int rc = 0;
     rc |= dev_upload(&p->bl, bl);
     rc |= dev_upload(&p->ell2bin, ell2bin);
@@ -1070,6 +1296,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     }
     rc |= dev_upload(&p->meta, meta);
     rc |= dev_upload(&p->phase_tab, ptab);
+    rc |= dev_upload(&p->phase_rng, prng);
     std::vector<int> e2k((size_t)p->nspec * (L + 1), -1);
     for (int sp = 0; sp < p->nspec; ++sp)
         for (int b = 0; b < p->nblocks[sp]; ++b) {
@@ -1087,6 +1314,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->prop, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->logr, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->dl_tmp, nc * p->nspec * maxbins);
+    rc |= dev_alloc(&p->iter_dev, 4);
     if (rc) { gs_plan_destroy(p); return -1; }
     *out = p;
     return 0;
@@ -1094,7 +1322,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
-    void* bufs[] = {p->ell2blk, p->gbuf, p->phase_tab, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials,
+    void* bufs[] = {p->iter_dev, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials,
                     p->params, p->stats, p->prop, p->logr, p->dl_tmp};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1208,7 +1436,7 @@ static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, c
     const bool rep = z != nullptr, st = s_out != nullptr;
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunk, p->rows_per_task, p->tasks, d_alm, params, z, s_out,         \
-                                             p->partials, slo, shi, iteration, substep, p->chain0)
+                                             p->partials, slo, shi, IterArg{iteration, p->itp()}, substep, p->chain0)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
                         else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
                         else GS_SW(FF, 0, false); } while (0)
@@ -1239,12 +1467,15 @@ int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const dim3 g(p->nchains, p->nspec), b(256);
 #define GS_CD(FF) hipLaunchKernelGGL((k_cls_draw<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
-                                     stats, variates, slo, shi, iteration, p->chain0, dl_out)
+                                     stats, variates, slo, shi, IterArg{iteration, p->itp()}, p->chain0, dl_out)
     if (p->F == 1) GS_CD(1); else if (p->F == 2) GS_CD(2); else GS_CD(3);
 #undef GS_CD
     GS_LAUNCH_CHECK("k_cls_draw");
     return 0;
 }
+
+static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
+                     uint32_t iteration, int32_t* accept_out, void* stream);
 
 int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, const double* u_acc, uint64_t seed,
              uint32_t iteration, int32_t* accept_out, void* stream) {
@@ -1252,12 +1483,43 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
     if (!p->has_mh) return set_error("gs_nc_mh: plan has no MH blocks / proposal variances");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
+#if defined(GS_ABL_MH_NOPROPOSE)
+    if (false)
+#endif
 #define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
-                                     p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi, iteration, \
+                                     p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi, IterArg{iteration, p->itp()}, \
                                      p->chain0)
     if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
 #undef GS_MP
     GS_LAUNCH_CHECK("k_mh_propose");
+    return mh_decide(p, stats, dl, u_acc, slo, shi, iteration, accept_out, stream);
+}
+
+// the MH phases proper (proposals already in p->prop / p->logr)
+static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
+                     uint32_t iteration, int32_t* accept_out, void* stream) {
+    int maxnb = 0;
+    MhPhases ph{};
+    ph.nphase = p->nphase;
+    ph.lmin = p->mh_lmin;
+    for (int q = 0; q < 4; ++q) {
+        ph.sp[q][0] = p->phase_sp[q][0]; ph.sp[q][1] = p->phase_sp[q][1];
+        ph.off[q] = p->phase_off[q]; ph.n[q] = p->phase_n[q]; ph.nwide[q] = p->phase_nwide[q];
+        maxnb = std::max(maxnb, p->phase_n[q]);
+    }
+    const size_t lds = (2 * (size_t)(p->L + 1) + (size_t)maxnb * p->n_iter_mh + (size_t)p->nspec * p->maxbins) *
+                           sizeof(double) + (size_t)p->nspec * (p->L + 1) * sizeof(int);
+    if (lds <= 128 * 1024) {
+#define GS_MF(FF) hipLaunchKernelGGL((k_mh_fused<FF>), dim3(p->nchains), dim3(1024), lds, S(stream), p->L, p->maxbins, ph, \
+                                     p->phase_tab, p->phase_rng, p->bins, p->blocks, p->meta + 8, p->nacc, p->n_iter_mh, p->ell2blk,    \
+                                     p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop,       \
+                                     p->logr, u_acc, slo, shi, IterArg{iteration, p->itp()}, p->chain0, accept_out)
+        if (p->F == 1) GS_MF(1); else if (p->F == 2) GS_MF(2); else GS_MF(3);
+#undef GS_MF
+        GS_LAUNCH_CHECK("k_mh_fused");
+        return 0;
+    }
+    // very large l_max: two launches per phase (terms in HBM, one wave per block)
     const long long nl = (long long)p->nchains * (p->L + 1);
     for (int ph = 0; ph < p->nphase; ++ph) {
         const int nb = p->phase_n[ph];
@@ -1273,7 +1535,7 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
         const int2* tab = p->phase_tab + p->phase_off[ph];
 #define GS_MA(FF) hipLaunchKernelGGL((k_mh_accept<FF>), dim3(nblk(waves, 4)), dim3(256), 0, S(stream), p->L, p->nchains, \
                                      p->maxbins, sp0, p->bins, p->blocks, tab, nb, p->meta + 8, p->nacc, p->n_iter_mh, \
-                                     p->gbuf, dl, p->prop, p->logr, u_acc, slo, shi, iteration, p->chain0, accept_out)
+                                     p->gbuf, dl, p->prop, p->logr, u_acc, slo, shi, IterArg{iteration, p->itp()}, p->chain0, accept_out)
         if (p->F == 1) GS_MA(1); else if (p->F == 2) GS_MA(2); else GS_MA(3);
 #undef GS_MA
         GS_LAUNCH_CHECK("k_mh_accept");
@@ -1314,9 +1576,20 @@ int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out,
 int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
                         const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
                         void* stream) {
-    if (gs_block_params(p, GS_MODE_NONCENTERED, dl, p->params, stream)) return -1;
+    if (check_plan(p)) return -1;
+    if (!p->has_mh) return set_error("gs_step_noncentered: plan has no MH blocks / proposal variances");
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    const int nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
+    const int nbq = nblk((long long)p->nchains * (p->L + 1), 256);
+#define GS_PRO(FF) hipLaunchKernelGGL((k_nc_prologue<FF>), dim3(nbp + nbq), dim3(256), 0, S(stream), nbp, p->L,        \
+                                      p->nchains, p->maxbins, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], \
+                                      p->params, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi,            \
+                                      IterArg{it, p->itp()}, p->chain0)
+    if (p->F == 1) GS_PRO(1); else if (p->F == 2) GS_PRO(2); else GS_PRO(3);
+#undef GS_PRO
+    GS_LAUNCH_CHECK("k_nc_prologue");
     if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
-    return gs_nc_mh(p, p->stats, dl, u_prop, u_acc, seed, it, accept_out, stream);
+    return mh_decide(p, p->stats, dl, u_acc, slo, shi, it, accept_out, stream);
 }
 
 int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z, const double* igvar,
@@ -1336,6 +1609,31 @@ int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, con
         const bool quirk = (p->quirks & GS_QUIRK_ASIS_RECENTRE_CENTERED) != 0;
         if (gs_recentre(p, dl, quirk ? nullptr : tmp, s_out, stream)) return -1;
     }
+    return 0;
+}
+
+int gs_iteration_counter(gs_plan* p, int enable, uint32_t start) {
+    if (check_plan(p)) return -1;
+    p->iter_dev_on = enable != 0;
+    if (enable) GS_CHECK(hipMemcpy(p->iter_dev, &start, sizeof(uint32_t), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int gs_advance_iteration(gs_plan* p, void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->iter_dev_on) return set_error("gs_advance_iteration: device counter not enabled");
+    hipLaunchKernelGGL(k_iter_advance, dim3(1), dim3(1), 0, S(stream), p->iter_dev);
+    GS_LAUNCH_CHECK("k_iter_advance");
+    return 0;
+}
+
+int gs_record_trace(gs_plan* p, const double* dl, double* trace, int capacity, uint32_t iteration, void* stream) {
+    if (check_plan(p)) return -1;
+    if (capacity < 1) return set_error("gs_record_trace: capacity < 1");
+    const long long n = (long long)p->nchains * p->nspec * p->maxbins;
+    hipLaunchKernelGGL(k_record_trace, dim3(nblk(n, 256)), dim3(256), 0, S(stream), n, dl, trace, capacity,
+                       IterArg{iteration, p->itp()});
+    GS_LAUNCH_CHECK("k_record_trace");
     return 0;
 }
 

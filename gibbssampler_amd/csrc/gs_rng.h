@@ -32,8 +32,14 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#if defined(GS_XOR3)
+        uint32_t n0, n2;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c1), "s"(k0));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c3), "s"(k1));
+#else
         const uint32_t n0 = hi1 ^ c1 ^ k0;
         const uint32_t n2 = hi0 ^ c3 ^ k1;
+#endif
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
@@ -211,11 +217,37 @@ __device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const do
     cs = fma(ck, cph, -(sk * sph));
 }
 
+// sqrt(t), t >= 0: hardware reciprocal square root (~2^-29 relative) and one
+// Newton step (error ~2^-58), then r = t y; exact 0 at t = 0
+__device__ __forceinline__ double bm_sqrt(double t) {
+#if defined(GS_RSQ_SQRT)
+    double y = __builtin_amdgcn_rsq(t);
+    const double h = 0.5 * t;
+    y = y * fma(-h * y, y, 1.5);
+    return t > 0.0 ? t * y : 0.0;
+#else
+    return sqrt(t);
+#endif
+}
+
 __device__ __forceinline__ void box_muller_tab(uint4 w, const double* __restrict__ tab, double& z0, double& z1) {
     const double u1 = u53(w.x, w.y);
-    const double r = sqrt(-2.0 * bm_log_tab(u1, tab));
+#if defined(GS_ABL_NOLOG)
+    const double lg = u1 - 1.0;           // timing ablation only
+#else
+    const double lg = bm_log_tab(u1, tab);
+#endif
+#if defined(GS_ABL_NOSQRT)
+    const double r = -2.0 * lg;           // timing ablation only
+#else
+    const double r = bm_sqrt(-2.0 * lg);
+#endif
     double sn, cs;
+#if defined(GS_ABL_NOTRIG)
+    sn = (double)w.z * 2.3283064365386963e-10; cs = (double)w.w * 2.3283064365386963e-10;   // ablation
+#else
     bm_sincos_tab(w.z, w.w, tab, sn, cs);
+#endif
     z0 = r * cs;
     z1 = r * sn;
 }

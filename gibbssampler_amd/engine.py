@@ -226,6 +226,17 @@ class GibbsPlan:
                                       C.ptr(u_prop), C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept),
                                       C.ptr(dl_tmp), 1 if recentre else 0, self._s()), "gs_step_asis")
 
+    # ---- hipGraph support ---------------------------------------------------------------
+    def iteration_counter(self, enable, start=1):
+        C.check(self.lib.gs_iteration_counter(self._h, 1 if enable else 0, int(start)), "gs_iteration_counter")
+
+    def advance_iteration(self):
+        C.check(self.lib.gs_advance_iteration(self._h, self._s()), "gs_advance_iteration")
+
+    def record_trace(self, dl, trace, capacity, iteration=0):
+        C.check(self.lib.gs_record_trace(self._h, C.ptr(dl), C.ptr(trace), int(capacity), int(iteration), self._s()),
+                "gs_record_trace")
+
     # ---- timing of the dominant kernel (hipEvents on the launch stream) ---------------
     def sweep_timing(self, enable):
         tot = ctypes.c_double()

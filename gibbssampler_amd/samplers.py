@@ -46,6 +46,7 @@ class BatchedRunner:
         self.accept = p.zeros(p.nchains, max(p.nacc, 1), dtype=torch.int32)
         self.materialize_recentre = materialize_recentre
         self.iteration = 0
+        self.graph = None
 
     # -- one iteration ---------------------------------------------------------------
     def _replay(self):
@@ -69,12 +70,27 @@ class BatchedRunner:
             p.cr_sweep(self.d, params, z=z, seed=self.seed, iteration=INIT_ITER, s_out=self.s,
                        store=self.s is not None)
 
-    def step(self):
+    # -- hipGraph: capture one whole iteration, replay it per step ------------------
+    def capture_graph(self, trace=None, trace_capacity=None):
+        """Capture one iteration (plus an optional device-side trace record) in a
+        hipGraph; subsequent ``step()`` calls replay it.  Native RNG only: the
+        iteration counter lives on the device and advances inside the graph."""
+        if self.rng != "native":
+            raise ValueError("graph capture needs the native (counter-based) RNG")
         p = self.plan
-        it = self.iteration + 1
-        z = ig = up = ua = None
-        if self.rng == "replay":
-            z, ig, up, ua = self._replay()
+        p.iteration_counter(True, self.iteration + 1)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._launch_step(0)
+            if trace is not None:
+                p.record_trace(self.dl, trace, trace_capacity)
+            p.advance_iteration()
+        self.graph = g
+        return g
+
+    def _launch_step(self, it, z=None, ig=None, up=None, ua=None):
+        p = self.plan
         if self.kind == "centered":
             p.step_centered(self.d, self.dl, self.s, z=z, igvar=ig, seed=self.seed, iteration=it)
         elif self.kind == "noncentered":
@@ -83,6 +99,18 @@ class BatchedRunner:
         else:
             p.step_asis(self.d, self.dl, self.s, z=z, igvar=ig, u_prop=up, u_acc=ua, seed=self.seed, iteration=it,
                         accept=self.accept, dl_tmp=self.dl_tmp, recentre=self.materialize_recentre)
+
+    def step(self):
+        if getattr(self, "graph", None) is not None:
+            self.graph.replay()
+            self.iteration += 1
+            return
+        p = self.plan
+        it = self.iteration + 1
+        z = ig = up = ua = None
+        if self.rng == "replay":
+            z, ig, up, ua = self._replay()
+        self._launch_step(it, z, ig, up, ua)
         self.iteration = it
 
     # -- a whole run --------------------------------------------------------------------

@@ -144,6 +144,16 @@ int gs_step_asis(gs_plan* plan, const double* d_alm, double* dl_binned, double* 
                  uint64_t seed, uint32_t iteration, int32_t* accept_out, double* dl_tmp_out,
                  int recentre, void* stream);
 
+/* hipGraph support: with the device counter enabled every RNG-consuming
+ * kernel reads the iteration from a device word (the host value is ignored)
+ * and gs_advance_iteration increments it, so one captured step replays as the
+ * next iteration */
+int gs_iteration_counter(gs_plan* plan, int enable, uint32_t start);
+int gs_advance_iteration(gs_plan* plan, void* stream);
+/* trace[(it-1) % capacity][nchains][nspec][maxbins] <- dl_binned (history of GibbsSampler.py:172-173) */
+int gs_record_trace(gs_plan* plan, const double* dl_binned, double* trace, int capacity, uint32_t iteration,
+                    void* stream);
+
 /* device-side timing of the dominant kernel (hipEvents on the plan's stream) */
 int gs_sweep_timing(gs_plan* plan, int enable, double* total_ms, int* count);
 
