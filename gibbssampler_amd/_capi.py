@@ -16,6 +16,8 @@ GS_MODE_CENTERED = 0
 GS_MODE_NONCENTERED = 1
 GS_QUIRK_ASIS_RECENTRE_CENTERED = 1
 GS_NPARAM = 10
+GS_ALM_REAL = 0
+GS_ALM_COMPLEX = 1
 NSTAT = {1: 2, 2: 4, 3: 8}
 
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -79,6 +81,12 @@ _SIGS = [
     ("gs_advance_iteration", ctypes.c_int, [_VP, _VP]),
     ("gs_record_trace", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_uint32, _VP]),
     ("gs_sweep_timing", ctypes.c_int, [_VP, ctypes.c_int, c_double_p, c_int_p]),
+    ("gs_sht_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_VP)]),
+    ("gs_sht_destroy", ctypes.c_int, [_VP]),
+    ("gs_sht_info", ctypes.c_int, [_VP, c_int_p, c_int_p, ctypes.POINTER(ctypes.c_longlong),
+                                   ctypes.POINTER(ctypes.c_longlong)]),
+    ("gs_sht_alm2map", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
+    ("gs_sht_map2alm", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP]),
 ]
 
 EXPORTED = [n for n, _, _ in _SIGS]

@@ -1,0 +1,30 @@
+// gs_common.h -- error plumbing shared by the translation units of libgibbs_hip.so
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string>
+
+namespace gs_detail {
+
+// one thread-local message for the whole library (gs_last_error)
+inline thread_local std::string g_last_error;
+
+inline int set_error(const std::string& msg) {
+    g_last_error = msg;
+    return -1;
+}
+
+}  // namespace gs_detail
+
+#define GS_CHECK(expr)                                                                        \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return gs_detail::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));   \
+    } while (0)
+
+#define GS_LAUNCH_CHECK(name)                                                                 \
+    do {                                                                                      \
+        hipError_t _e = hipGetLastError();                                                    \
+        if (_e != hipSuccess)                                                                 \
+            return gs_detail::set_error(std::string("launch ") + (name) + ": " + hipGetErrorString(_e)); \
+    } while (0)

@@ -24,31 +24,13 @@
 
 #include "gibbs_capi.h"
 #include "gs_rng.h"
+#include "gs_common.h"
 
 using namespace gs;
 
 namespace {
 
-thread_local std::string g_last_error;
-
-int set_error(const std::string& msg) {
-    g_last_error = msg;
-    return -1;
-}
-
-#define GS_CHECK(expr)                                                                  \
-    do {                                                                                \
-        hipError_t _e = (expr);                                                         \
-        if (_e != hipSuccess)                                                           \
-            return set_error(std::string(#expr) + ": " + hipGetErrorString(_e));       \
-    } while (0)
-
-#define GS_LAUNCH_CHECK(name)                                                           \
-    do {                                                                                \
-        hipError_t _e = hipGetLastError();                                              \
-        if (_e != hipSuccess)                                                           \
-            return set_error(std::string("launch ") + name + ": " + hipGetErrorString(_e)); \
-    } while (0)
+using gs_detail::set_error;
 
 constexpr int WAVE = 64;
 constexpr int NP = GS_NPARAM;
@@ -1186,7 +1168,7 @@ int check_plan(const gs_plan* p) {
 extern "C" {
 
 int gs_abi_version(void) { return GS_ABI_VERSION; }
-const char* gs_last_error(void) { return g_last_error.c_str(); }
+const char* gs_last_error(void) { return gs_detail::g_last_error.c_str(); }
 
 int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     if (!desc || !out) return set_error("gs_plan_create: null argument");

@@ -1,0 +1,1007 @@
+// gs_sht.hip -- HEALPix RING spherical-harmonic transforms on gfx950 (fp64).
+//
+// Replaces the healpy calls of the reference's masked CR variants
+// (hp.alm2map: CenteredGibbs.py:204,505,698,751,791, NonCenteredGibbs.py:350;
+// hp.map2alm: CenteredGibbs.py:298,513,717,773,812, utils.py:89,104,
+// NonCenteredGibbs.py:155).  Conventions: SURVEY.md Appendix A.4 and
+// oracle/sht.py (Condon-Shortley lambda_lm, Zaldarriaga-Seljak F1/F2 spin-2
+// functions, Q + iU = -sum (a_E + i a_B) 2Y_lm, map2alm = (4pi/Npix) x adjoint).
+//
+// Structure (per transform, one chain):
+//   synthesis  k_sht_synth_leg : per (m, ring pair) Legendre sums
+//                  Phi_m(ring) = sum_l a_lm G_lm(theta)      [compute bound, fp64 VALU]
+//              k_sht_synth_ring: per ring pair: alias-fold Phi_m into nphi bins,
+//                  one complex FFT for the north+south rings (Hermitian packing)
+//   analysis   k_sht_anal_ring : per ring pair: one complex FFT of north + i south,
+//                  split, un-alias into Phi_m
+//              k_sht_anal_leg  : per (m, l) sums over rings (4 ring pairs per lane,
+//                  fixed-order LDS reduction per 4-l chunk) -> per-tile partials
+//              k_sht_anal_finish: fixed-order tile sum, weight, output layout
+//
+// Legendre functions run the normalised three-term recurrence in l with a
+// scale exponent (lambda = v * 2^(768 k), k <= 0), so the sin^m theta start
+// values of high m near the poles do not underflow.  A plan-time pass finds,
+// per (m, 64-ring-pair group), the first l where any ring of the group is
+// representable (k = 0) and stores the recurrence state there: the
+// transforms skip the exponentially small part of the (l, ring) plane
+// exactly instead of iterating through it.
+//
+// Ring FFTs: nphi = 4i (caps) or 4 N_side (equator).  Power-of-two lengths
+// use an in-place radix-2 Stockham FFT in LDS; other lengths use Bluestein's
+// chirp-z with a power-of-two length M >= 2 nphi - 1 and a plan-time FFT of
+// the chirp kernel per ring.  Launches are split by M so each uses exactly
+// the LDS it needs (M <= 8192 in LDS; larger M in a global scratch).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "gibbs_capi.h"
+#include "gs_common.h"
+
+using gs_detail::set_error;
+
+namespace {
+
+constexpr double PI = 3.14159265358979323846;
+constexpr int LEG_BLOCK = 256;
+constexpr int RING_BLOCK = 512;
+constexpr int ANA_R = 4;                    // ring pairs per lane (analysis Legendre)
+constexpr int ANA_C = 4;                    // l per reduction chunk
+constexpr int ANA_TILE = ANA_R * LEG_BLOCK; // ring pairs per analysis workgroup
+constexpr int LDS_FFT_MAX = 8192;           // complex points held in LDS
+constexpr double SC_UP = 0x1p768;
+constexpr double SC_DN = 0x1p-768;
+constexpr double SC_HI = 0x1p384;
+constexpr double SC_LO = 0x1p-384;
+
+struct PairGeom {
+    double x;            // cos theta of the north ring
+    double s;            // sin theta
+    double is2;          // 1 / sin^2 theta
+    long long startN;    // first pixel of the north ring
+    long long startS;    // first pixel of the south ring, -1 for the equator
+    int nphi;
+    int phi_half;        // phi0 = phi_half * pi / nphi
+    int M;               // FFT length
+    int logM;
+    long long bs_off;    // Bluestein kernel offset (complex entries), -1 if nphi = M
+};
+
+// per (l, m) recurrence + spin-2 coefficients (64 B, one scalar load)
+struct LegCoef {
+    double a, b;   // lambda_l = a (x lambda_{l-1} - b lambda_{l-2})
+    double P, Q;   // F1 = -(P is2 + Q) lambda_l + R (x is2) lambda_{l-1}
+    double R, T;   // F2 = -T (x is2) lambda_l + Rm is2 lambda_{l-1}
+    double Rm, pad;
+};
+
+struct ShtDev {
+    int L, npair, ngroup, nlm;
+    const PairGeom* geom;
+    const LegCoef* coef;
+    const int* lstart;       // [L+1][ngroup]
+    const double2* st;       // [L+1][npair] (lambda_{ls-1}, lambda_ls), scaled
+    const int* stk;          // [L+1][npair] scale exponent at ls
+};
+
+__device__ __forceinline__ long long cidx(int L, int l, int m) { return (long long)m * (2 * L + 1 - m) / 2 + l; }
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 conj2(double2 a) { return make_double2(a.x, -a.y); }
+
+// e^{i pi t / n} for integer t (reduced mod 2n exactly)
+__device__ __forceinline__ double2 expi_pi_frac(long long t, long long n) {
+    long long r = t % (2 * n);
+    if (r < 0) r += 2 * n;
+    double sn, cs;
+    sincospi((double)r / (double)n, &sn, &cs);
+    return make_double2(cs, sn);
+}
+
+// ---------------------------------------------------------------------------
+// a_lm access in the caller's layout: 0 = real m-major (utils.py:49-76),
+// 1 = healpy complex m-major interleaved
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double2 alm_get(const double* __restrict__ a, int layout, int L, int l, int m) {
+    if (layout == GS_ALM_COMPLEX) {
+        const long long i = cidx(L, l, m);
+        return make_double2(a[2 * i], a[2 * i + 1]);
+    }
+    if (m == 0) return make_double2(a[l], 0.0);
+    const long long r = 2 * cidx(L, l, m) - (L + 1);
+    constexpr double IS2 = 0.70710678118654752440;
+    return make_double2(a[r] * IS2, a[r + 1] * IS2);
+}
+
+__device__ __forceinline__ long long alm_comp_stride(int layout, int L) {
+    return layout == GS_ALM_COMPLEX ? (long long)(L + 1) * (L + 2) : (long long)(L + 1) * (L + 1);
+}
+
+// ---------------------------------------------------------------------------
+// plan-time Legendre start tables
+// ---------------------------------------------------------------------------
+// lambda_mm per (m, pair), scaled: v * 2^(768 k)
+__global__ void k_sht_lmm(int L, int npair, const PairGeom* __restrict__ geom, double* __restrict__ lmm,
+                          int* __restrict__ lmk) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npair) return;
+    const double s = geom[p].s;
+    double v = 0.28209479177387814347;   // 1/sqrt(4 pi)
+    int k = 0;
+    for (int m = 0; m <= L; ++m) {
+        if (m > 0) {
+            v *= -sqrt((2.0 * m + 1.0) / (2.0 * m)) * s;
+            if (fabs(v) < SC_LO) { v *= SC_UP; --k; }
+        }
+        lmm[(long long)m * npair + p] = v;
+        lmk[(long long)m * npair + p] = k;
+    }
+}
+
+// per (m, pair): run the scaled recurrence to find where the group of 64 ring
+// pairs becomes representable, then store the state there
+__global__ __launch_bounds__(256) void k_sht_onset(ShtDev D, const double* __restrict__ lmm, const int* __restrict__ lmk,
+                                                   int* __restrict__ lstart, double2* __restrict__ st,
+                                                   int* __restrict__ stk) {
+    const int L = D.L, npair = D.npair;
+    const int m = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = p < npair;
+    const double x = act ? D.geom[p].x : 0.0;
+    const long long base = cidx(L, m, m);
+    const double v0i = act ? lmm[(long long)m * npair + p] : 0.0;
+    const int k0 = act ? lmk[(long long)m * npair + p] : 0;
+    // pass 1: onset
+    int lon = L + 1;
+    {
+        double v1 = 0.0, v0 = v0i;
+        int k = k0;
+        if (act) {
+            for (int l = m; l <= L; ++l) {
+                if (k == 0) { lon = l; break; }
+                if (l == L) break;
+                const LegCoef c = D.coef[base + (l + 1 - m)];
+                const double vn = c.a * (x * v0 - c.b * v1);
+                v1 = v0; v0 = vn;
+                if (fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
+            }
+        }
+    }
+    // wave minimum (64 consecutive pairs = one group)
+    int ls = lon;
+    for (int o = 32; o > 0; o >>= 1) ls = min(ls, __shfl_xor(ls, o, 64));
+    const int group = p >> 6;
+    if ((threadIdx.x & 63) == 0 && group < D.ngroup) lstart[(long long)m * D.ngroup + group] = ls;
+    // pass 2: state at ls
+    double v1 = 0.0, v0 = v0i;
+    int k = k0;
+    if (act && ls <= L) {
+        for (int l = m; l < ls; ++l) {
+            const LegCoef c = D.coef[base + (l + 1 - m)];
+            const double vn = c.a * (x * v0 - c.b * v1);
+            v1 = v0; v0 = vn;
+            if (k < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
+        }
+    }
+    if (act) {
+        st[(long long)m * npair + p] = make_double2(v1, v0);
+        stk[(long long)m * npair + p] = k;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthesis: Legendre stage
+// ---------------------------------------------------------------------------
+// NC = 1: T (spin 0); 2: E,B -> Q,U; 3: T,E,B -> T,Q,U.
+// phi layout: [comp][ns][m][pair] (double2), ns 0 = north, 1 = south
+template <int NC>
+struct SynAcc {
+    double tp[2], tn[2];        // T: parity + / -
+    double sp[4], sn[4];        // Q re, Q im, U re, U im: parity + / -
+};
+
+template <int NC, bool EVEN>
+__device__ __forceinline__ void syn_accumulate(SynAcc<NC>& A, const LegCoef& c, double v0, double v1, double is2,
+                                               double xis2, double2 aT, double2 aE, double2 aB) {
+    if constexpr (NC != 2) {
+        if (EVEN) { A.tp[0] = fma(aT.x, v0, A.tp[0]); A.tp[1] = fma(aT.y, v0, A.tp[1]); }
+        else      { A.tn[0] = fma(aT.x, v0, A.tn[0]); A.tn[1] = fma(aT.y, v0, A.tn[1]); }
+    }
+    if constexpr (NC != 1) {
+        const double F1 = fma(c.R * xis2, v1, -fma(c.P, is2, c.Q) * v0);
+        const double F2 = fma(c.Rm * is2, v1, -(c.T * xis2) * v0);
+        double* a1 = EVEN ? A.sp : A.sn;   // F1 carries lambda's parity
+        double* a2 = EVEN ? A.sn : A.sp;   // F2 the opposite one
+        a1[0] = fma(aE.x, F1, a1[0]); a2[0] = fma(-aB.y, F2, a2[0]);
+        a1[1] = fma(aE.y, F1, a1[1]); a2[1] = fma(aB.x, F2, a2[1]);
+        a1[2] = fma(aB.x, F1, a1[2]); a2[2] = fma(aE.y, F2, a2[2]);
+        a1[3] = fma(aB.y, F1, a1[3]); a2[3] = fma(-aE.x, F2, a2[3]);
+    }
+}
+
+template <int NC>
+__global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const double* __restrict__ alm, int layout,
+                                                             double2* __restrict__ phi) {
+    const int L = D.L, npair = D.npair;
+    const int q = blockIdx.x;
+    const int p = blockIdx.y * LEG_BLOCK + threadIdx.x;
+    const bool act = p < npair;
+    const int group = p >> 6;
+    double x = 0.0, is2 = 0.0;
+    if (act) { x = D.geom[p].x; is2 = D.geom[p].is2; }
+    const double xis2 = x * is2;
+    const long long cs = alm_comp_stride(layout, L);
+    const double* aT = alm;
+    const double* aE = alm + (NC == 3 ? cs : 0);
+    const double* aB = aE + cs;
+    for (int h = 0; h < 2; ++h) {
+        const int m = h == 0 ? q : L - q;
+        if (h == 1 && m <= q) break;
+        SynAcc<NC> A;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) { A.tp[i] = 0.0; A.tn[i] = 0.0; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { A.sp[i] = 0.0; A.sn[i] = 0.0; }
+        const int ls = group < D.ngroup ? D.lstart[(long long)m * D.ngroup + group] : L + 1;
+        if (ls <= L) {
+            double2 s0 = make_double2(0.0, 0.0);
+            int k = 0;
+            if (act) { s0 = D.st[(long long)m * npair + p]; k = D.stk[(long long)m * npair + p]; }
+            double v1 = s0.x, v0 = s0.y;
+            const LegCoef* cf = D.coef + cidx(L, m, m) - m;   // cf[l] = coefficients of (l, m)
+            int l = ls;
+            const double2 z2 = make_double2(0.0, 0.0);
+            auto ld = [&](const double* a, int ll) { return alm_get(a, layout, L, ll, m); };
+            // phase A: some lane still below the representable range
+            while (l <= L && __any(k < 0)) {
+                const LegCoef c = cf[l];
+                const double2 t = NC != 2 ? ld(aT, l) : z2;
+                const double2 e = NC != 1 ? ld(aE, l) : z2;
+                const double2 b = NC != 1 ? ld(aB, l) : z2;
+                const double w0 = k == 0 ? v0 : 0.0, w1 = k == 0 ? v1 : 0.0;
+                if (((l - m) & 1) == 0) syn_accumulate<NC, true>(A, c, w0, w1, is2, xis2, t, e, b);
+                else syn_accumulate<NC, false>(A, c, w0, w1, is2, xis2, t, e, b);
+                if (l < L) {
+                    const LegCoef cn = cf[l + 1];
+                    const double vn = cn.a * (x * v0 - cn.b * v1);
+                    v1 = v0; v0 = vn;
+                    if (k < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
+                }
+                ++l;
+            }
+            // phase B: plain recurrence, parity unrolled
+            if (l <= L && ((l - m) & 1)) {
+                const LegCoef c = cf[l];
+                syn_accumulate<NC, false>(A, c, v0, v1, is2, xis2, NC != 2 ? ld(aT, l) : z2,
+                                          NC != 1 ? ld(aE, l) : z2, NC != 1 ? ld(aB, l) : z2);
+                if (l < L) {
+                    const LegCoef cn = cf[l + 1];
+                    const double vn = cn.a * (x * v0 - cn.b * v1);
+                    v1 = v0; v0 = vn;
+                }
+                ++l;
+            }
+            for (; l + 1 <= L; l += 2) {
+                const LegCoef c0 = cf[l];
+                const LegCoef c1 = cf[l + 1];
+                syn_accumulate<NC, true>(A, c0, v0, v1, is2, xis2, NC != 2 ? ld(aT, l) : z2,
+                                         NC != 1 ? ld(aE, l) : z2, NC != 1 ? ld(aB, l) : z2);
+                double vn = c1.a * (x * v0 - c1.b * v1);
+                v1 = v0; v0 = vn;
+                syn_accumulate<NC, false>(A, c1, v0, v1, is2, xis2, NC != 2 ? ld(aT, l + 1) : z2,
+                                          NC != 1 ? ld(aE, l + 1) : z2, NC != 1 ? ld(aB, l + 1) : z2);
+                if (l + 2 <= L) {
+                    const LegCoef c2 = cf[l + 2];
+                    vn = c2.a * (x * v0 - c2.b * v1);
+                    v1 = v0; v0 = vn;
+                }
+            }
+            if (l <= L) {
+                const LegCoef c = cf[l];
+                syn_accumulate<NC, true>(A, c, v0, v1, is2, xis2, NC != 2 ? ld(aT, l) : z2,
+                                         NC != 1 ? ld(aE, l) : z2, NC != 1 ? ld(aB, l) : z2);
+            }
+        }
+        if (!act) continue;
+        const long long plane = (long long)(L + 1) * npair;
+        const long long o = (long long)m * npair + p;
+        int comp = 0;
+        if constexpr (NC != 2) {
+            phi[(2 * comp + 0) * plane + o] = make_double2(A.tp[0] + A.tn[0], A.tp[1] + A.tn[1]);
+            phi[(2 * comp + 1) * plane + o] = make_double2(A.tp[0] - A.tn[0], A.tp[1] - A.tn[1]);
+            ++comp;
+        }
+        if constexpr (NC != 1) {
+            // Q = -(...), U = -(...)
+            phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[0] + A.sn[0]), -(A.sp[1] + A.sn[1]));
+            phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[0] - A.sn[0]), -(A.sp[1] - A.sn[1]));
+            ++comp;
+            phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[2] + A.sn[2]), -(A.sp[3] + A.sn[3]));
+            phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[2] - A.sn[2]), -(A.sp[3] - A.sn[3]));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ring FFTs (block-wide, in place, buffer in LDS or global scratch)
+// ---------------------------------------------------------------------------
+// forward (dir = -1): X_k = sum_j x_j e^{-2 pi i jk/M};  dir = +1: conjugate
+// twiddles; tw[k] = e^{-2 pi i k / Mmax}, k < Mmax/2
+__device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
+    constexpr int NBMAX = 16;   // M/2 / blockDim <= 16 (M <= 16384, blockDim 512)
+    const int half = M >> 1;
+    for (int Ns = 1; Ns < M; Ns <<= 1) {
+        double2 o0[NBMAX], o1[NBMAX];
+        int id[NBMAX];
+        const int tstride = Mmax / (2 * Ns);
+#pragma unroll
+        for (int t = 0; t < NBMAX; ++t) {
+            const int j = threadIdx.x + t * blockDim.x;
+            if (j < half) {
+                const double2 a = buf[j];
+                double2 w = tw[(j & (Ns - 1)) * tstride];
+                if (dir > 0) w.y = -w.y;
+                const double2 b = cmul(buf[j + half], w);
+                o0[t] = make_double2(a.x + b.x, a.y + b.y);
+                o1[t] = make_double2(a.x - b.x, a.y - b.y);
+                id[t] = ((j / Ns) * 2 * Ns) + (j & (Ns - 1));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NBMAX; ++t) {
+            const int j = threadIdx.x + t * blockDim.x;
+            if (j < half) { buf[id[t]] = o0[t]; buf[id[t] + Ns] = o1[t]; }
+        }
+        __syncthreads();
+    }
+}
+
+// forward DFT of length n held in buf[0..n) (M = Bluestein length, kern = FFT of
+// the chirp kernel); result in buf[0..n)
+__device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
+                            const double2* __restrict__ bsk) {
+    const int n = g.nphi, M = g.M;
+    if (g.bs_off < 0) { fft_pow2(buf, M, -1, tw, Mmax); return; }
+    const double2* V = bsk + g.bs_off;
+    for (int j = threadIdx.x; j < M; j += blockDim.x) {
+        if (j < n) buf[j] = cmul(buf[j], expi_pi_frac(-(long long)j * j, n));   // c_j = e^{-i pi j^2/n}
+        else buf[j] = make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    fft_pow2(buf, M, -1, tw, Mmax);
+    for (int j = threadIdx.x; j < M; j += blockDim.x) buf[j] = cmul(buf[j], V[j]);
+    __syncthreads();
+    fft_pow2(buf, M, +1, tw, Mmax);
+    const double inv = 1.0 / M;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const double2 c = expi_pi_frac(-(long long)j * j, n);
+        const double2 v = cmul(buf[j], c);
+        buf[j] = make_double2(v.x * inv, v.y * inv);
+    }
+    __syncthreads();
+}
+
+// inverse (unnormalised) DFT: y_j = sum_k Z_k e^{+2 pi i jk/n}
+__device__ void dft_inverse(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
+                            const double2* __restrict__ bsk) {
+    if (g.bs_off < 0) { fft_pow2(buf, g.M, +1, tw, Mmax); return; }
+    for (int j = threadIdx.x; j < g.nphi; j += blockDim.x) buf[j].y = -buf[j].y;
+    __syncthreads();
+    dft_forward(buf, g, tw, Mmax, bsk);
+    for (int j = threadIdx.x; j < g.nphi; j += blockDim.x) buf[j].y = -buf[j].y;
+    __syncthreads();
+}
+
+// plan time: V = FFT_M(w), w_t = e^{+i pi t^2/n} for |t| < n (cyclic)
+__global__ __launch_bounds__(RING_BLOCK) void k_sht_bluestein_setup(const int* __restrict__ pairs,
+                                                                    const PairGeom* __restrict__ geom,
+                                                                    const double2* __restrict__ tw, int Mmax,
+                                                                    double2* __restrict__ bsk) {
+    const PairGeom g = geom[pairs[blockIdx.x]];
+    double2* buf = bsk + g.bs_off;
+    const int n = g.nphi, M = g.M;
+    for (int t = threadIdx.x; t < M; t += blockDim.x) {
+        long long tt = -1;
+        if (t < n) tt = t;
+        else if (t > M - n) tt = M - t;
+        buf[t] = tt >= 0 ? expi_pi_frac(tt * tt, n) : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    fft_pow2(buf, M, -1, tw, Mmax);
+}
+
+__global__ void k_sht_twiddles(int Mmax, double2* __restrict__ tw) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= Mmax / 2) return;
+    double sn, cs;
+    sincospi(-2.0 * (double)k / (double)Mmax, &sn, &cs);
+    tw[k] = make_double2(cs, sn);
+}
+
+// ---------------------------------------------------------------------------
+// synthesis: ring stage.  grid (pairs of this M class, ncomp)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double2 fold_phi(const double2* __restrict__ ph, long long plane_off, int npair, int p, int L,
+                                            int k, int n, int h) {
+    // G_k = sum_{m = k mod n, m <= L} c_m Phi_m e^{i m phi0},  phi0 = h pi / n
+    double2 acc = make_double2(0.0, 0.0);
+    for (int m = k; m <= L; m += n) {
+        const double2 v = ph[plane_off + (long long)m * npair + p];
+        const double cm = m == 0 ? 1.0 : 2.0;
+        const double2 e = h ? expi_pi_frac(m, n) : make_double2(1.0, 0.0);
+        const double2 t = cmul(v, e);
+        acc.x = fma(cm, t.x, acc.x);
+        acc.y = fma(cm, t.y, acc.y);
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(RING_BLOCK) void k_sht_synth_ring(int L, int npair, long long npix,
+                                                               const int* __restrict__ pairs,
+                                                               const PairGeom* __restrict__ geom,
+                                                               const double2* __restrict__ phi,
+                                                               const double2* __restrict__ tw, int Mmax,
+                                                               const double2* __restrict__ bsk,
+                                                               double2* __restrict__ gscratch, double* __restrict__ maps) {
+    extern __shared__ double2 lbuf[];
+    const int p = pairs[blockIdx.x];
+    const int comp = blockIdx.y;
+    const PairGeom g = geom[p];
+    double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
+    const int n = g.nphi;
+    const long long plane = (long long)(L + 1) * npair;
+    const long long offN = (2LL * comp + 0) * plane, offS = (2LL * comp + 1) * plane;
+    const bool eq = g.startS < 0;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int nk = k == 0 ? 0 : n - k;
+        const double2 a = fold_phi(phi, offN, npair, p, L, k, n, g.phi_half);
+        const double2 b = fold_phi(phi, offN, npair, p, L, nk, n, g.phi_half);
+        // Hermitian part of the north spectrum: (G_k + conj G_{-k}) / 2
+        double2 z = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+        if (!eq) {
+            const double2 c = fold_phi(phi, offS, npair, p, L, k, n, g.phi_half);
+            const double2 d = fold_phi(phi, offS, npair, p, L, nk, n, g.phi_half);
+            const double2 s = make_double2(0.5 * (c.x + d.x), 0.5 * (c.y - d.y));
+            z.x -= s.y;   // z += i s
+            z.y += s.x;
+        }
+        buf[k] = z;
+    }
+    __syncthreads();
+    dft_inverse(buf, g, tw, Mmax, bsk);
+    double* mc = maps + (long long)comp * npix;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const double2 y = buf[j];
+        mc[g.startN + j] = y.x;
+        if (!eq) mc[g.startS + j] = y.y;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// analysis: ring stage.  grid (pairs of this M class, ncomp)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(RING_BLOCK) void k_sht_anal_ring(int L, int npair, long long npix,
+                                                              const int* __restrict__ pairs,
+                                                              const PairGeom* __restrict__ geom,
+                                                              const double* __restrict__ maps,
+                                                              const double2* __restrict__ tw, int Mmax,
+                                                              const double2* __restrict__ bsk,
+                                                              double2* __restrict__ gscratch, double2* __restrict__ phi) {
+    extern __shared__ double2 lbuf[];
+    const int p = pairs[blockIdx.x];
+    const int comp = blockIdx.y;
+    const PairGeom g = geom[p];
+    double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
+    const int n = g.nphi;
+    const bool eq = g.startS < 0;
+    const double* mc = maps + (long long)comp * npix;
+    for (int j = threadIdx.x; j < n; j += blockDim.x)
+        buf[j] = make_double2(mc[g.startN + j], eq ? 0.0 : mc[g.startS + j]);
+    __syncthreads();
+    dft_forward(buf, g, tw, Mmax, bsk);
+    const long long plane = (long long)(L + 1) * npair;
+    double2* oN = phi + (2LL * comp + 0) * plane;
+    double2* oS = phi + (2LL * comp + 1) * plane;
+    for (int m = threadIdx.x; m <= L; m += blockDim.x) {
+        const int k = m % n;
+        const int nk = k == 0 ? 0 : n - k;
+        const double2 a = buf[k], b = buf[nk];
+        // north: (Z_k + conj Z_-k)/2 ; south: (Z_k - conj Z_-k)/(2i)
+        double2 xn = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+        double2 xs = make_double2(0.5 * (a.y + b.y), -0.5 * (a.x - b.x));
+        if (g.phi_half) {
+            const double2 e = expi_pi_frac(-(long long)m, n);
+            xn = cmul(xn, e);
+            xs = cmul(xs, e);
+        }
+        if (m == 0) { xn.y = 0.0; xs.y = 0.0; }
+        oN[(long long)m * npair + p] = xn;
+        oS[(long long)m * npair + p] = eq ? make_double2(0.0, 0.0) : xs;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// analysis: Legendre stage.  grid (m pairs, tiles of ANA_TILE ring pairs)
+// out: part[tile][comp][nlm] (double2), unweighted sums
+//   T: sum lambda Phi_T ;  E: sum (Q F1 + i U F2) ;  B: sum (U F1 - i Q F2)
+// ---------------------------------------------------------------------------
+template <int NC>
+__global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const double2* __restrict__ phi,
+                                                            double2* __restrict__ part) {
+    constexpr int NO = NC == 1 ? 2 : (NC == 2 ? 4 : 6);   // real outputs per l
+    constexpr int NV = NO * ANA_C;
+    constexpr int RS = LEG_BLOCK + 1;                      // padded LDS row
+    __shared__ double red[NV * RS];
+    const int L = D.L, npair = D.npair;
+    const int q = blockIdx.x, tile = blockIdx.y;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const long long plane = (long long)(L + 1) * npair;
+    double x[ANA_R], is2[ANA_R];
+    int pr[ANA_R];
+    bool act[ANA_R];
+#pragma unroll
+    for (int r = 0; r < ANA_R; ++r) {
+        pr[r] = tile * ANA_TILE + r * LEG_BLOCK + tid;
+        act[r] = pr[r] < npair;
+        x[r] = act[r] ? D.geom[pr[r]].x : 0.0;
+        is2[r] = act[r] ? D.geom[pr[r]].is2 : 0.0;
+    }
+    for (int h = 0; h < 2; ++h) {
+        const int m = h == 0 ? q : L - q;
+        if (h == 1 && m <= q) break;
+        // per-slot onset l (uniform per wave) and the workgroup's first l
+        int ls[ANA_R];
+        int lmin = L + 1;
+#pragma unroll
+        for (int r = 0; r < ANA_R; ++r) {
+            const int gq = (tile * ANA_TILE + r * LEG_BLOCK) / 64 + wave;
+            ls[r] = gq < D.ngroup ? D.lstart[(long long)m * D.ngroup + gq] : L + 1;
+        }
+        for (int gq = tile * ANA_TILE / 64; gq < min(D.ngroup, (tile + 1) * ANA_TILE / 64); ++gq)
+            lmin = min(lmin, D.lstart[(long long)m * D.ngroup + gq]);
+        // per-slot parity-combined ring phases: [+]: N + S, [-]: N - S
+        double2 fp[ANA_R][NC], fn[ANA_R][NC];
+        double v0[ANA_R], v1[ANA_R];
+        int kk[ANA_R];
+#pragma unroll
+        for (int r = 0; r < ANA_R; ++r) {
+            v0[r] = 0.0; v1[r] = 0.0; kk[r] = -1;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                double2 a = make_double2(0.0, 0.0), b = a;
+                if (act[r] && ls[r] <= L) {
+                    a = phi[(2LL * c + 0) * plane + (long long)m * npair + pr[r]];
+                    b = phi[(2LL * c + 1) * plane + (long long)m * npair + pr[r]];
+                }
+                fp[r][c] = make_double2(a.x + b.x, a.y + b.y);
+                fn[r][c] = make_double2(a.x - b.x, a.y - b.y);
+            }
+        }
+        const LegCoef* cf = D.coef + cidx(L, m, m) - m;
+        const long long obase = cidx(L, m, m) - m;
+        for (int l0 = lmin; l0 <= L; l0 += ANA_C) {
+            double acc[NV];
+#pragma unroll
+            for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+#pragma unroll
+            for (int cc = 0; cc < ANA_C; ++cc) {
+                const int l = l0 + cc;
+                if (l > L) break;
+                const LegCoef c = cf[l];
+                const bool even = ((l - m) & 1) == 0;
+#pragma unroll
+                for (int r = 0; r < ANA_R; ++r) {
+                    if (l < ls[r]) continue;                 // uniform per wave
+                    if (l == ls[r] && act[r]) {
+                        const double2 s0 = D.st[(long long)m * npair + pr[r]];
+                        v1[r] = s0.x; v0[r] = s0.y;
+                        kk[r] = D.stk[(long long)m * npair + pr[r]];
+                    }
+                    const double lam = kk[r] == 0 ? v0[r] : 0.0;
+                    const double lam1 = kk[r] == 0 ? v1[r] : 0.0;
+                    double* a = acc + cc * NO;
+                    int o = 0;
+                    if constexpr (NC != 2) {
+                        const double2 t = even ? fp[r][0] : fn[r][0];
+                        a[0] = fma(lam, t.x, a[0]);
+                        a[1] = fma(lam, t.y, a[1]);
+                        o = 2;
+                    }
+                    if constexpr (NC != 1) {
+                        constexpr int cq = NC == 3 ? 1 : 0;
+                        const double xis2 = x[r] * is2[r];
+                        const double F1 = fma(c.R * xis2, lam1, -fma(c.P, is2[r], c.Q) * lam);
+                        const double F2 = fma(c.Rm * is2[r], lam1, -(c.T * xis2) * lam);
+                        const double2 Q1 = even ? fp[r][cq] : fn[r][cq];       // F1 parity
+                        const double2 U1 = even ? fp[r][cq + 1] : fn[r][cq + 1];
+                        const double2 Q2 = even ? fn[r][cq] : fp[r][cq];       // F2 parity
+                        const double2 U2 = even ? fn[r][cq + 1] : fp[r][cq + 1];
+                        a[o + 0] = fma(F1, Q1.x, fma(-F2, U2.y, a[o + 0]));
+                        a[o + 1] = fma(F1, Q1.y, fma(F2, U2.x, a[o + 1]));
+                        a[o + 2] = fma(F1, U1.x, fma(F2, Q2.y, a[o + 2]));
+                        a[o + 3] = fma(F1, U1.y, fma(-F2, Q2.x, a[o + 3]));
+                    }
+                    if (l < L) {
+                        const LegCoef cn = cf[l + 1];
+                        const double vn = cn.a * (x[r] * v0[r] - cn.b * v1[r]);
+                        v1[r] = v0[r]; v0[r] = vn;
+                        if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
+                    }
+                }
+            }
+            // fixed-order workgroup reduction of the chunk
+#pragma unroll
+            for (int i = 0; i < NV; ++i) red[i * RS + tid] = acc[i];
+            __syncthreads();
+            // thread -> (output v, segment g of 32 partials); 8 segments per output
+            const int v = tid >> 3, g = tid & 7;
+            double sum = 0.0;
+            if (v < NV) {
+                const double* row = red + v * RS + g * 32;
+                for (int i = 0; i < 32; ++i) sum += row[(i + g * 4) & 31];
+            }
+            sum += __shfl_xor(sum, 1, 64);
+            sum += __shfl_xor(sum, 2, 64);
+            sum += __shfl_xor(sum, 4, 64);
+            if (v < NV && g == 0) {
+                const int cc = v / NO, o = v % NO;
+                const int l = l0 + cc;
+                if (l <= L) {
+                    const int comp = o >> 1;
+                    double* dst = reinterpret_cast<double*>(part + ((long long)tile * NC + comp) * D.nlm + obase + l);
+                    dst[o & 1] = sum;
+                }
+            }
+            __syncthreads();
+        }
+        // l below the workgroup's onset: exact zeros
+        for (int l = m + tid; l < min(lmin, L + 1); l += LEG_BLOCK)
+            for (int c = 0; c < NC; ++c) part[((long long)tile * NC + c) * D.nlm + obase + l] = make_double2(0.0, 0.0);
+    }
+    (void)lane;
+}
+
+// sum tiles in fixed order, weight, sign, write the caller's layout (accumulate
+// into it when acc != 0: the Jacobi steps of map2alm(iter > 0))
+template <int NC>
+__global__ void k_sht_anal_finish(int L, int nlm, int ntile, const double2* __restrict__ part, double w, int layout,
+                                  int acc, double* __restrict__ alm) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= (long long)NC * nlm) return;
+    const int comp = (int)(g / nlm);
+    const long long i = g % nlm;
+    double2 s = make_double2(0.0, 0.0);
+    for (int t = 0; t < ntile; ++t) {
+        const double2 v = part[((long long)t * NC + comp) * nlm + i];
+        s.x += v.x; s.y += v.y;
+    }
+    const bool spin0 = NC == 1 || (NC == 3 && comp == 0);
+    const double f = spin0 ? w : -w;
+    s.x *= f; s.y *= f;
+    // (l, m) of complex index i
+    // m = largest with cidx(L, m, m) = m(2L+3-m)/2 <= i
+    const double b = 2.0 * L + 3.0;
+    int m = (int)floor((b - sqrt(fmax(b * b - 8.0 * (double)i, 0.0))) / 2.0);
+    m = max(0, min(m, L));
+    while (m > 0 && (long long)m * (2 * L + 3 - m) / 2 > i) --m;
+    while (m < L && (long long)(m + 1) * (2 * L + 2 - m) / 2 <= i) ++m;
+    const int l = (int)(i - (long long)m * (2 * L + 1 - m) / 2);
+    double* out = alm + comp * alm_comp_stride(layout, L);
+    if (layout == GS_ALM_COMPLEX) {
+        if (acc) { out[2 * i] += s.x; out[2 * i + 1] += s.y; }
+        else { out[2 * i] = s.x; out[2 * i + 1] = s.y; }
+    } else if (m == 0) {
+        if (acc) out[l] += s.x; else out[l] = s.x;
+    } else {
+        constexpr double SQ2 = 1.41421356237309504880;
+        const long long r = 2 * i - (L + 1);
+        if (acc) { out[r] += SQ2 * s.x; out[r + 1] += SQ2 * s.y; }
+        else { out[r] = SQ2 * s.x; out[r + 1] = SQ2 * s.y; }
+    }
+}
+
+__global__ void k_sub_maps(long long n, const double* __restrict__ a, double* __restrict__ b) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g < n) b[g] = a[g] - b[g];
+}
+
+inline unsigned nblocks(long long n, int bs) { return (unsigned)std::max<long long>(1, (n + bs - 1) / bs); }
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+}  // namespace
+
+// ============================================================================
+// plan
+// ============================================================================
+struct gs_sht {
+    int nside = 0, L = 0, npair = 0, ngroup = 0, nlm = 0, ntile = 0, Mmax = 0;
+    long long npix = 0;
+    PairGeom* geom = nullptr;
+    LegCoef* coef = nullptr;
+    int* lstart = nullptr;
+    double2* st = nullptr;
+    int* stk = nullptr;
+    double2* tw = nullptr;
+    double2* bsk = nullptr;
+    double2* phi = nullptr;      // [3][2][L+1][npair]
+    double2* part = nullptr;     // [ntile][3][nlm]
+    double2* gscr = nullptr;     // global FFT scratch for M > LDS_FFT_MAX
+    double* mapw = nullptr;      // [3][npix] Jacobi residual maps
+    // ring classes by FFT length
+    std::vector<int> cls_M;      // M of each class
+    std::vector<int> cls_n;      // pairs in the class
+    std::vector<int*> cls_pairs; // device lists
+    long long bytes = 0;
+    ShtDev dev() const {
+        ShtDev D;
+        D.L = L; D.npair = npair; D.ngroup = ngroup; D.nlm = nlm;
+        D.geom = geom; D.coef = coef; D.lstart = lstart; D.st = st; D.stk = stk;
+        return D;
+    }
+};
+
+namespace {
+
+template <typename T>
+int sht_alloc(gs_sht* p, T** dst, size_t n) {
+    GS_CHECK(hipMalloc((void**)dst, std::max<size_t>(n, 1) * sizeof(T)));
+    p->bytes += (long long)(std::max<size_t>(n, 1) * sizeof(T));
+    return 0;
+}
+
+void sht_free(gs_sht* p) {
+    void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->mapw};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    for (int* b : p->cls_pairs)
+        if (b) (void)hipFree(b);
+    delete p;
+}
+
+int check_sht(const gs_sht* p) { return p ? 0 : set_error("null SHT plan"); }
+
+int ilog2(int v) { int r = 0; while ((1 << r) < v) ++r; return r; }
+
+}  // namespace
+
+extern "C" {
+
+int gs_sht_create(int nside, int lmax, gs_sht** out) {
+    if (!out) return set_error("gs_sht_create: null out");
+    *out = nullptr;
+    if (nside < 1 || nside > 8192 || (nside & (nside - 1))) return set_error("gs_sht_create: nside must be a power of two <= 8192");
+    if (lmax < 0 || lmax > 4 * nside) return set_error("gs_sht_create: lmax out of range (0..4 nside)");
+    gs_sht* p = new gs_sht();
+    const int N = nside, L = lmax;
+    p->nside = N; p->L = L; p->npair = 2 * N; p->ngroup = (p->npair + 63) / 64;
+    p->nlm = (L + 1) * (L + 2) / 2;
+    p->npix = 12LL * N * N;
+    p->ntile = (p->npair + ANA_TILE - 1) / ANA_TILE;
+    // ---- geometry (ring pair r: north ring r+1, south ring 4N-1-r) ----
+    std::vector<PairGeom> geom(p->npair);
+    int Mmax = 2;
+    for (int r = 0; r < p->npair; ++r) {
+        const int i = r + 1;
+        PairGeom g{};
+        if (i < N) {
+            const double omx = (double)i * i / (3.0 * N * N);   // 1 - x, exact-ish
+            g.x = 1.0 - omx;
+            const double s2 = omx * (2.0 - omx);
+            g.s = std::sqrt(s2);
+            g.is2 = 1.0 / s2;
+            g.nphi = 4 * i;
+            g.phi_half = 1;
+            g.startN = 2LL * i * (i - 1);
+            g.startS = p->npix - 2LL * i * (i + 1);
+        } else {
+            g.x = 4.0 / 3.0 - 2.0 * i / (3.0 * N);
+            const double s2 = (1.0 - g.x) * (1.0 + g.x);
+            g.s = std::sqrt(s2);
+            g.is2 = 1.0 / s2;
+            g.nphi = 4 * N;
+            g.phi_half = ((i - N) % 2 == 0) ? 1 : 0;
+            g.startN = 2LL * N * (N - 1) + (long long)(i - N) * 4 * N;
+            const int is = 4 * N - i;   // mirrored ring (same as i at the equator)
+            g.startS = (is == i) ? -1 : 2LL * N * (N - 1) + (long long)(is - N) * 4 * N;
+        }
+        const bool pow2 = (g.nphi & (g.nphi - 1)) == 0;
+        g.M = pow2 ? g.nphi : (1 << ilog2(2 * g.nphi - 1));
+        g.logM = ilog2(g.M);
+        g.bs_off = -1;
+        Mmax = std::max(Mmax, g.M);
+        geom[r] = g;
+    }
+    long long bs_total = 0;
+    std::vector<int> bs_pairs;
+    for (int r = 0; r < p->npair; ++r)
+        if (geom[r].M != geom[r].nphi) { geom[r].bs_off = bs_total; bs_total += geom[r].M; bs_pairs.push_back(r); }
+    p->Mmax = Mmax;
+    // ---- recurrence coefficients ----
+    std::vector<LegCoef> coef(p->nlm);
+    for (int m = 0; m <= L; ++m) {
+        const long long base = (long long)m * (2 * L + 1 - m) / 2;
+        for (int l = m; l <= L; ++l) {
+            LegCoef c{};
+            const double dl = l, dm = m;
+            if (l > m) {
+                c.a = std::sqrt((4.0 * dl * dl - 1.0) / (dl * dl - dm * dm));
+                c.b = std::sqrt(((dl - 1.0) * (dl - 1.0) - dm * dm) / (4.0 * (dl - 1.0) * (dl - 1.0) - 1.0));
+            }
+            if (l >= 2) {
+                const double cl = 2.0 / std::sqrt((dl - 1.0) * dl * (dl + 1.0) * (dl + 2.0));
+                const double f = std::sqrt((2.0 * dl + 1.0) / (2.0 * dl - 1.0) * (dl * dl - dm * dm));
+                c.P = cl * (dl - dm * dm);
+                c.Q = cl * 0.5 * dl * (dl - 1.0);
+                c.R = cl * f;
+                c.T = cl * dm * (dl - 1.0);
+                c.Rm = cl * dm * f;
+            }
+            coef[base + l] = c;
+        }
+    }
+    int rc = 0;
+    rc |= sht_alloc(p, &p->geom, geom.size());
+    rc |= sht_alloc(p, &p->coef, coef.size());
+    rc |= sht_alloc(p, &p->lstart, (size_t)(L + 1) * p->ngroup);
+    rc |= sht_alloc(p, &p->st, (size_t)(L + 1) * p->npair);
+    rc |= sht_alloc(p, &p->stk, (size_t)(L + 1) * p->npair);
+    rc |= sht_alloc(p, &p->tw, (size_t)Mmax / 2);
+    rc |= sht_alloc(p, &p->bsk, (size_t)std::max<long long>(bs_total, 1));
+    rc |= sht_alloc(p, &p->phi, (size_t)3 * 2 * (L + 1) * p->npair);
+    rc |= sht_alloc(p, &p->part, (size_t)p->ntile * 3 * p->nlm);
+    rc |= sht_alloc(p, &p->mapw, (size_t)3 * p->npix);
+    if (rc) { sht_free(p); return -1; }
+    // ring classes by M
+    std::vector<int> Ms;
+    for (auto& g : geom) Ms.push_back(g.M);
+    std::sort(Ms.begin(), Ms.end());
+    Ms.erase(std::unique(Ms.begin(), Ms.end()), Ms.end());
+    long long gscr_need = 0;
+    for (int M : Ms) {
+        std::vector<int> lst;
+        for (int r = 0; r < p->npair; ++r)
+            if (geom[r].M == M) lst.push_back(r);
+        int* d = nullptr;
+        if (hipMalloc((void**)&d, lst.size() * sizeof(int)) != hipSuccess ||
+            hipMemcpy(d, lst.data(), lst.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+            sht_free(p);
+            return set_error("gs_sht_create: ring class upload failed");
+        }
+        p->cls_M.push_back(M);
+        p->cls_n.push_back((int)lst.size());
+        p->cls_pairs.push_back(d);
+        if (M > LDS_FFT_MAX) gscr_need = std::max<long long>(gscr_need, 3LL * (long long)lst.size() * Mmax);
+    }
+    if (gscr_need && sht_alloc(p, &p->gscr, (size_t)gscr_need)) { sht_free(p); return -1; }
+    if (hipMemcpy(p->geom, geom.data(), geom.size() * sizeof(PairGeom), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->coef, coef.data(), coef.size() * sizeof(LegCoef), hipMemcpyHostToDevice) != hipSuccess) {
+        sht_free(p);
+        return set_error("gs_sht_create: table upload failed");
+    }
+    // ---- device-side tables ----
+    double* lmm = nullptr;
+    int* lmk = nullptr;
+    if (hipMalloc((void**)&lmm, (size_t)(L + 1) * p->npair * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&lmk, (size_t)(L + 1) * p->npair * sizeof(int)) != hipSuccess) {
+        if (lmm) (void)hipFree(lmm);
+        sht_free(p);
+        return set_error("gs_sht_create: out of device memory");
+    }
+    if (hipFuncSetAttribute((const void*)k_sht_synth_ring, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            LDS_FFT_MAX * (int)sizeof(double2)) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_sht_anal_ring, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            LDS_FFT_MAX * (int)sizeof(double2)) != hipSuccess) {
+        (void)hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_sht_twiddles, dim3(nblocks(Mmax / 2, 256)), dim3(256), 0, 0, Mmax, p->tw);
+    hipLaunchKernelGGL(k_sht_lmm, dim3(nblocks(p->npair, 64)), dim3(64), 0, 0, L, p->npair, p->geom, lmm, lmk);
+    hipLaunchKernelGGL(k_sht_onset, dim3(nblocks(p->npair, 256), L + 1), dim3(256), 0, 0, p->dev(), lmm, lmk,
+                       p->lstart, p->st, p->stk);
+    if (!bs_pairs.empty()) {
+        int* dp = nullptr;
+        if (hipMalloc((void**)&dp, bs_pairs.size() * sizeof(int)) == hipSuccess &&
+            hipMemcpy(dp, bs_pairs.data(), bs_pairs.size() * sizeof(int), hipMemcpyHostToDevice) == hipSuccess) {
+            hipLaunchKernelGGL(k_sht_bluestein_setup, dim3((unsigned)bs_pairs.size()), dim3(RING_BLOCK), 0, 0, dp,
+                               p->geom, p->tw, Mmax, p->bsk);
+        }
+        (void)hipDeviceSynchronize();
+        if (dp) (void)hipFree(dp);
+    }
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipFree(lmm);
+    (void)hipFree(lmk);
+    if (e != hipSuccess || hipGetLastError() != hipSuccess) {
+        sht_free(p);
+        return set_error(std::string("gs_sht_create: setup kernels failed: ") + hipGetErrorString(e));
+    }
+    *out = p;
+    return 0;
+}
+
+int gs_sht_destroy(gs_sht* p) {
+    if (p) sht_free(p);
+    return 0;
+}
+
+int gs_sht_info(const gs_sht* p, int* nside, int* lmax, long long* npix, long long* device_bytes) {
+    if (check_sht(p)) return -1;
+    if (nside) *nside = p->nside;
+    if (lmax) *lmax = p->L;
+    if (npix) *npix = p->npix;
+    if (device_bytes) *device_bytes = p->bytes;
+    return 0;
+}
+
+static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream) {
+    for (size_t c = 0; c < p->cls_M.size(); ++c) {
+        const int M = p->cls_M[c];
+        const bool glob = M > LDS_FFT_MAX;
+        const size_t lds = glob ? 0 : (size_t)M * sizeof(double2);
+        const dim3 grid(p->cls_n[c], ncomp);
+        double2* scr = glob ? p->gscr : nullptr;
+        if (synth)
+            hipLaunchKernelGGL(k_sht_synth_ring, grid, dim3(RING_BLOCK), lds, S(stream), p->L, p->npair, p->npix,
+                               p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out);
+        else
+            hipLaunchKernelGGL(k_sht_anal_ring, grid, dim3(RING_BLOCK), lds, S(stream), p->L, p->npair, p->npix,
+                               p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi);
+        GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
+    }
+    return 0;
+}
+
+int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* maps, void* stream) {
+    if (check_sht(p)) return -1;
+    if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_alm2map: ncomp must be 1 (T), 2 (E,B) or 3 (T,E,B)");
+    if (layout != GS_ALM_REAL && layout != GS_ALM_COMPLEX) return set_error("gs_sht_alm2map: bad layout");
+    if (!alm || !maps) return set_error("gs_sht_alm2map: null argument");
+    const dim3 grid(p->L / 2 + 1, (p->npair + LEG_BLOCK - 1) / LEG_BLOCK);
+#define GS_SL(NC) hipLaunchKernelGGL((k_sht_synth_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), alm, layout, p->phi)
+    if (ncomp == 1) GS_SL(1); else if (ncomp == 2) GS_SL(2); else GS_SL(3);
+#undef GS_SL
+    GS_LAUNCH_CHECK("k_sht_synth_leg");
+    return sht_rings(p, true, ncomp, nullptr, maps, stream);
+}
+
+static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream) {
+    if (sht_rings(p, false, ncomp, maps, nullptr, stream)) return -1;
+    const dim3 grid(p->L / 2 + 1, p->ntile);
+#define GS_AL(NC) hipLaunchKernelGGL((k_sht_anal_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->phi, p->part)
+    if (ncomp == 1) GS_AL(1); else if (ncomp == 2) GS_AL(2); else GS_AL(3);
+#undef GS_AL
+    GS_LAUNCH_CHECK("k_sht_anal_leg");
+    const double w = 4.0 * PI / (double)p->npix;
+    const long long n = (long long)ncomp * p->nlm;
+#define GS_AF(NC) hipLaunchKernelGGL((k_sht_anal_finish<NC>), dim3(nblocks(n, 256)), dim3(256), 0, S(stream), p->L, p->nlm, \
+                                     p->ntile, p->part, w, layout, acc, alm)
+    if (ncomp == 1) GS_AF(1); else if (ncomp == 2) GS_AF(2); else GS_AF(3);
+#undef GS_AF
+    GS_LAUNCH_CHECK("k_sht_anal_finish");
+    return 0;
+}
+
+int gs_sht_map2alm(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int niter, void* stream) {
+    if (check_sht(p)) return -1;
+    if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_map2alm: ncomp must be 1 (T), 2 (Q,U) or 3 (T,Q,U)");
+    if (layout != GS_ALM_REAL && layout != GS_ALM_COMPLEX) return set_error("gs_sht_map2alm: bad layout");
+    if (!alm || !maps) return set_error("gs_sht_map2alm: null argument");
+    if (niter < 0) return set_error("gs_sht_map2alm: niter < 0");
+    if (sht_analysis(p, ncomp, layout, maps, alm, 0, stream)) return -1;
+    for (int it = 0; it < niter; ++it) {
+        // a += map2alm(m - alm2map(a))   (healpy iter = niter)
+        if (gs_sht_alm2map(p, ncomp, layout, alm, p->mapw, stream)) return -1;
+        const long long n = (long long)ncomp * p->npix;
+        hipLaunchKernelGGL(k_sub_maps, dim3(nblocks(n, 256)), dim3(256), 0, S(stream), n, maps, p->mapw);
+        GS_LAUNCH_CHECK("k_sub_maps");
+        if (sht_analysis(p, ncomp, layout, p->mapw, alm, 1, stream)) return -1;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,114 @@
+"""HEALPix RING spherical-harmonic transforms on the GPU (libgibbs_hip.so).
+
+Device replacement for the healpy calls of the reference's masked paths:
+``hp.alm2map`` (CenteredGibbs.py:204,505,698,751,791; NonCenteredGibbs.py:350),
+``hp.map2alm`` (``iter=0`` at CenteredGibbs.py:298,513,717,773,812; default
+``iter=3`` at utils.py:89,104 and NonCenteredGibbs.py:155) and
+``utils.adjoint_synthesis_hp`` (utils.py:79-111).  Conventions: oracle/sht.py
+(HEALPix / Zaldarriaga-Seljak).
+
+All arrays are torch float64 tensors on the current CUDA (HIP) device.  a_lm
+are in the build's real m-major layout (``layout="real"``, (L+1)^2 per
+component, utils.py:49-76) or healpy's complex order (``layout="complex"``:
+complex128 tensors of (L+1)(L+2)/2 per component).
+"""
+import ctypes
+
+import torch
+
+from . import _capi
+
+_LAYOUT = {"real": _capi.GS_ALM_REAL, "complex": _capi.GS_ALM_COMPLEX}
+
+
+class HealpixSHT:
+    """One device SHT plan for (nside, lmax): ring geometry, recurrence
+    coefficients, Legendre start tables and ring-FFT kernels built once."""
+
+    def __init__(self, nside, lmax):
+        self.lib = _capi.load()
+        self.nside, self.lmax = int(nside), int(lmax)
+        self.npix = 12 * self.nside ** 2
+        h = ctypes.c_void_p()
+        _capi.check(self.lib.gs_sht_create(self.nside, self.lmax, ctypes.byref(h)), "gs_sht_create")
+        self.handle = h
+        nb = ctypes.c_longlong()
+        _capi.check(self.lib.gs_sht_info(h, None, None, None, ctypes.byref(nb)), "gs_sht_info")
+        self.device_bytes = nb.value
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self.lib.gs_sht_destroy(h)
+            self.handle = None
+
+    # -- shapes -----------------------------------------------------------------
+    @property
+    def nreal(self):
+        return (self.lmax + 1) ** 2
+
+    @property
+    def ncomplex(self):
+        return (self.lmax + 1) * (self.lmax + 2) // 2
+
+    def _alm_view(self, alm, layout, ncomp):
+        if layout == "complex":
+            if alm.dtype != torch.complex128:
+                raise TypeError("complex layout needs complex128 a_lm")
+            alm = alm.contiguous()
+            if alm.numel() != ncomp * self.ncomplex:
+                raise ValueError("a_lm size does not match (ncomp, lmax)")
+            return torch.view_as_real(alm)
+        if alm.dtype != torch.float64:
+            raise TypeError("real layout needs float64 a_lm")
+        alm = alm.contiguous()
+        if alm.numel() != ncomp * self.nreal:
+            raise ValueError("a_lm size does not match (ncomp, lmax)")
+        return alm
+
+    # -- transforms -----------------------------------------------------------------
+    def alm2map(self, alm, ncomp=None, layout="real", out=None):
+        """alm [ncomp, n] -> maps [ncomp, Npix].  ncomp 1: T; 2: (E,B)->(Q,U);
+        3: (T,E,B)->(T,Q,U)."""
+        if ncomp is None:
+            ncomp = 1 if alm.dim() == 1 else alm.shape[0]
+        a = self._alm_view(alm, layout, ncomp)
+        if out is None:
+            out = torch.empty((ncomp, self.npix) if ncomp > 1 else (self.npix,), dtype=torch.float64,
+                              device=alm.device)
+        _capi.check(self.lib.gs_sht_alm2map(self.handle, ncomp, _LAYOUT[layout], _capi.ptr(a), _capi.ptr(out),
+                                            _capi.stream_ptr()), "gs_sht_alm2map")
+        return out
+
+    def map2alm(self, maps, iter=0, layout="real", ncomp=None, out=None):
+        """maps [ncomp, Npix] -> alm; (4pi/Npix) x adjoint, plus ``iter`` Jacobi steps."""
+        if ncomp is None:
+            ncomp = 1 if maps.dim() == 1 else maps.shape[0]
+        maps = maps.contiguous()
+        if maps.dtype != torch.float64 or maps.numel() != ncomp * self.npix:
+            raise ValueError("maps must be float64 [ncomp, 12 nside^2]")
+        if out is None:
+            if layout == "complex":
+                out = torch.empty((ncomp, self.ncomplex) if ncomp > 1 else (self.ncomplex,), dtype=torch.complex128,
+                                  device=maps.device)
+            else:
+                out = torch.empty((ncomp, self.nreal) if ncomp > 1 else (self.nreal,), dtype=torch.float64,
+                                  device=maps.device)
+        o = torch.view_as_real(out) if layout == "complex" else out
+        _capi.check(self.lib.gs_sht_map2alm(self.handle, ncomp, _LAYOUT[layout], _capi.ptr(maps), _capi.ptr(o),
+                                            int(iter), _capi.stream_ptr()), "gs_sht_map2alm")
+        return out
+
+    def adjoint_synthesis(self, maps, bl=None, iter=3):
+        """utils.adjoint_synthesis_hp (utils.py:79-111): map2alm(iter) rescaled by
+        Npix/(4pi), real layout, optionally times the per-slot beam ``bl``
+        (a length-(L+1)^2 tensor, or per-l of length L+1)."""
+        a = self.map2alm(maps, iter=iter, layout="real")
+        a = a * (self.npix / (4.0 * torch.pi))
+        if bl is not None:
+            if bl.numel() == self.lmax + 1:
+                from .problem import slot_ell
+                idx = torch.as_tensor(slot_ell(self.lmax), device=a.device)
+                bl = bl.to(a.device)[idx]
+            a = a * bl
+        return a

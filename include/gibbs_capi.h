@@ -157,6 +157,26 @@ int gs_record_trace(gs_plan* plan, const double* dl_binned, double* trace, int c
 /* device-side timing of the dominant kernel (hipEvents on the plan's stream) */
 int gs_sweep_timing(gs_plan* plan, int enable, double* total_ms, int* count);
 
+/* ---- HEALPix RING spherical-harmonic transforms (gs_sht.hip) ------------
+ * Replace healpy's hp.alm2map / hp.map2alm as called by the masked CR
+ * variants: CenteredGibbs.py:204,298,505,513,698,717,751,773,791,812,
+ * NonCenteredGibbs.py:155,350, utils.adjoint_synthesis_hp utils.py:79-111.
+ * ncomp: 1 = T (spin 0), 2 = (E,B) <-> (Q,U) (spin 2), 3 = (T,E,B) <-> (T,Q,U).
+ * alm layout: GS_ALM_REAL (real m-major, (L+1)^2 doubles per component,
+ * utils.py:49-76) or GS_ALM_COMPLEX (healpy order, (L+1)(L+2)/2 complex
+ * interleaved per component).  maps: [ncomp][12 nside^2] RING order.
+ * map2alm = (4 pi / Npix) x adjoint of alm2map (healpy, uniform weights);
+ * niter adds healpy's Jacobi refinements a += map2alm(m - alm2map(a)).
+ * One SHT plan serves one stream at a time (it owns the ring-phase workspace). */
+#define GS_ALM_REAL 0
+#define GS_ALM_COMPLEX 1
+typedef struct gs_sht gs_sht;
+int gs_sht_create(int nside, int lmax, gs_sht** out);
+int gs_sht_destroy(gs_sht* sht);
+int gs_sht_info(const gs_sht* sht, int* nside, int* lmax, long long* npix, long long* device_bytes);
+int gs_sht_alm2map(gs_sht* sht, int ncomp, int layout, const double* alm, double* maps, void* stream);
+int gs_sht_map2alm(gs_sht* sht, int ncomp, int layout, const double* maps, double* alm, int niter, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
