@@ -47,10 +47,7 @@ namespace {
 
 constexpr double PI = 3.14159265358979323846;
 constexpr int LEG_BLOCK = 256;
-constexpr int RING_BLOCK = 512;
-constexpr int ANA_R = 4;                    // ring pairs per lane (analysis Legendre)
-constexpr int ANA_C = 4;                    // l per reduction chunk
-constexpr int ANA_TILE = ANA_R * LEG_BLOCK; // ring pairs per analysis workgroup
+constexpr int ANA_C = 4;                    // l per reduction chunk (even)
 constexpr int LDS_FFT_MAX = 8192;           // complex points held in LDS
 constexpr double SC_UP = 0x1p768;
 constexpr double SC_DN = 0x1p-768;
@@ -195,18 +192,43 @@ __global__ __launch_bounds__(256) void k_sht_onset(ShtDev D, const double* __res
 }
 
 // ---------------------------------------------------------------------------
-// synthesis: Legendre stage
+// Legendre stages: shared layout
 // ---------------------------------------------------------------------------
-// NC = 1: T (spin 0); 2: E,B -> Q,U; 3: T,E,B -> T,Q,U.
+// A workgroup covers LTILE = 1024 consecutive ring pairs for one m pair
+// (m, L - m: balanced work); lane `lane` of wave `w` owns the SR = 4 ring
+// pairs tile*1024 + w*256 + r*64 + lane, so (wave, slot r) is exactly one
+// 64-pair onset group and every per-l coefficient / a_lm value is a
+// wave-uniform scalar load.  Each slot enters at its group's onset l with the
+// plan-time recurrence state; while any lane of a slot is still below the
+// representable range (k < 0) the slow path masks and rescales, afterwards
+// the parity-unrolled fast path runs the plain recurrence.
+// NC = 1: T (spin 0); 2: E,B <-> Q,U; 3: T,E,B <-> T,Q,U.
 // phi layout: [comp][ns][m][pair] (double2), ns 0 = north, 1 = south
-template <int NC>
+constexpr int SR = 4;
+constexpr int LTILE = SR * LEG_BLOCK;
+
+// a_lm in the caller's layout -> ain[comp][nlm] (healpy-ordered complex)
+__global__ void k_sht_alm_in(int L, int nlm, int ncomp, const double* __restrict__ alm, int layout,
+                             double2* __restrict__ ain) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= (long long)ncomp * nlm) return;
+    const int comp = (int)(g / nlm);
+    const long long i = g % nlm;
+    const double* a = alm + comp * alm_comp_stride(layout, L);
+    if (layout == GS_ALM_COMPLEX) { ain[g] = make_double2(a[2 * i], a[2 * i + 1]); return; }
+    if (i <= L) { ain[g] = make_double2(a[i], 0.0); return; }
+    constexpr double IS2 = 0.70710678118654752440;
+    const long long r = 2 * i - (L + 1);
+    ain[g] = make_double2(a[r] * IS2, a[r + 1] * IS2);
+}
+
 struct SynAcc {
     double tp[2], tn[2];        // T: parity + / -
     double sp[4], sn[4];        // Q re, Q im, U re, U im: parity + / -
 };
 
 template <int NC, bool EVEN>
-__device__ __forceinline__ void syn_accumulate(SynAcc<NC>& A, const LegCoef& c, double v0, double v1, double is2,
+__device__ __forceinline__ void syn_accumulate(SynAcc& A, const LegCoef& c, double v0, double v1, double is2,
                                                double xis2, double2 aT, double2 aE, double2 aB) {
     if constexpr (NC != 2) {
         if (EVEN) { A.tp[0] = fma(aT.x, v0, A.tp[0]); A.tp[1] = fma(aT.y, v0, A.tp[1]); }
@@ -224,105 +246,148 @@ __device__ __forceinline__ void syn_accumulate(SynAcc<NC>& A, const LegCoef& c, 
     }
 }
 
+__device__ __forceinline__ void rec_step(const LegCoef& c, double x, double& v0, double& v1) {
+    const double vn = c.a * fma(-c.b, v1, x * v0);
+    v1 = v0;
+    v0 = vn;
+}
+
 template <int NC>
-__global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const double* __restrict__ alm, int layout,
+__global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const LegCoef* __restrict__ coef,
+                                                             const double2* __restrict__ ain,
                                                              double2* __restrict__ phi) {
-    const int L = D.L, npair = D.npair;
-    const int q = blockIdx.x;
-    const int p = blockIdx.y * LEG_BLOCK + threadIdx.x;
-    const bool act = p < npair;
-    const int group = p >> 6;
-    double x = 0.0, is2 = 0.0;
-    if (act) { x = D.geom[p].x; is2 = D.geom[p].is2; }
-    const double xis2 = x * is2;
-    const long long cs = alm_comp_stride(layout, L);
-    const double* aT = alm;
-    const double* aE = alm + (NC == 3 ? cs : 0);
-    const double* aB = aE + cs;
+    const int L = D.L, npair = D.npair, nlm = D.nlm;
+    const int q = blockIdx.x, tile = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g0 = tile * (LTILE / 64) + wave * SR;        // onset group of slot 0
+    double x[SR], is2[SR], xis2[SR];
+    int pr[SR];
+    bool act[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        pr[r] = (g0 + r) * 64 + lane;
+        act[r] = pr[r] < npair;
+        x[r] = act[r] ? D.geom[pr[r]].x : 0.0;
+        is2[r] = act[r] ? D.geom[pr[r]].is2 : 0.0;
+        xis2[r] = x[r] * is2[r];
+    }
+    const double2 z2 = make_double2(0.0, 0.0);
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
         if (h == 1 && m <= q) break;
-        SynAcc<NC> A;
+        int ls[SR];
+        int lmin = L + 1;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) { A.tp[i] = 0.0; A.tn[i] = 0.0; }
+        for (int r = 0; r < SR; ++r) {
+            ls[r] = __builtin_amdgcn_readfirstlane(g0 + r < D.ngroup ? D.lstart[(long long)m * D.ngroup + g0 + r]
+                                                                     : L + 1);
+            lmin = min(lmin, ls[r]);
+        }
+        SynAcc A[SR];
+        double v0[SR], v1[SR];
+        int kk[SR];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { A.sp[i] = 0.0; A.sn[i] = 0.0; }
-        const int ls = group < D.ngroup ? D.lstart[(long long)m * D.ngroup + group] : L + 1;
-        if (ls <= L) {
-            double2 s0 = make_double2(0.0, 0.0);
-            int k = 0;
-            if (act) { s0 = D.st[(long long)m * npair + p]; k = D.stk[(long long)m * npair + p]; }
-            double v1 = s0.x, v0 = s0.y;
-            const LegCoef* cf = D.coef + cidx(L, m, m) - m;   // cf[l] = coefficients of (l, m)
-            int l = ls;
-            const double2 z2 = make_double2(0.0, 0.0);
-            auto ld = [&](const double* a, int ll) { return alm_get(a, layout, L, ll, m); };
-            // phase A: some lane still below the representable range
-            while (l <= L && __any(k < 0)) {
-                const LegCoef c = cf[l];
-                const double2 t = NC != 2 ? ld(aT, l) : z2;
-                const double2 e = NC != 1 ? ld(aE, l) : z2;
-                const double2 b = NC != 1 ? ld(aB, l) : z2;
-                const double w0 = k == 0 ? v0 : 0.0, w1 = k == 0 ? v1 : 0.0;
-                if (((l - m) & 1) == 0) syn_accumulate<NC, true>(A, c, w0, w1, is2, xis2, t, e, b);
-                else syn_accumulate<NC, false>(A, c, w0, w1, is2, xis2, t, e, b);
+        for (int r = 0; r < SR; ++r) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) { A[r].tp[i] = 0.0; A[r].tn[i] = 0.0; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { A[r].sp[i] = 0.0; A[r].sn[i] = 0.0; }
+            v0[r] = 0.0; v1[r] = 0.0; kk[r] = 0;
+        }
+        const long long base = cidx(L, m, m) - m;              // + l = complex index of (l, m)
+        const LegCoef* cf = coef + base;
+        const double2* aT = ain + base;
+        const double2* aE = ain + (NC == 3 ? nlm : 0) + base;
+        const double2* aB = aE + nlm;
+        int l = lmin;
+        // ---- slow path: slot activation and scaled lanes ----
+        while (l <= L) {
+            bool live = true;
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (l == ls[r] && act[r]) {
+                    const double2 s0 = D.st[(long long)m * npair + pr[r]];
+                    v1[r] = s0.x; v0[r] = s0.y;
+                    kk[r] = D.stk[(long long)m * npair + pr[r]];
+                }
+                if (ls[r] <= L && (l < ls[r] || __any(kk[r] < 0))) live = false;
+            }
+            if (live) break;
+            const LegCoef c = cf[l];
+            const double2 t = NC != 2 ? aT[l] : z2;
+            const double2 e = NC != 1 ? aE[l] : z2;
+            const double2 b = NC != 1 ? aB[l] : z2;
+            const bool even = ((l - m) & 1) == 0;
+            const LegCoef cn = cf[min(l + 1, L)];
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (l < ls[r]) continue;
+                const double w0 = kk[r] == 0 ? v0[r] : 0.0, w1 = kk[r] == 0 ? v1[r] : 0.0;
+                if (even) syn_accumulate<NC, true>(A[r], c, w0, w1, is2[r], xis2[r], t, e, b);
+                else syn_accumulate<NC, false>(A[r], c, w0, w1, is2[r], xis2[r], t, e, b);
                 if (l < L) {
-                    const LegCoef cn = cf[l + 1];
-                    const double vn = cn.a * (x * v0 - cn.b * v1);
-                    v1 = v0; v0 = vn;
-                    if (k < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
-                }
-                ++l;
-            }
-            // phase B: plain recurrence, parity unrolled
-            if (l <= L && ((l - m) & 1)) {
-                const LegCoef c = cf[l];
-                syn_accumulate<NC, false>(A, c, v0, v1, is2, xis2, NC != 2 ? ld(aT, l) : z2,
-                                          NC != 1 ? ld(aE, l) : z2, NC != 1 ? ld(aB, l) : z2);
-                if (l < L) {
-                    const LegCoef cn = cf[l + 1];
-                    const double vn = cn.a * (x * v0 - cn.b * v1);
-                    v1 = v0; v0 = vn;
-                }
-                ++l;
-            }
-            for (; l + 1 <= L; l += 2) {
-                const LegCoef c0 = cf[l];
-                const LegCoef c1 = cf[l + 1];
-                syn_accumulate<NC, true>(A, c0, v0, v1, is2, xis2, NC != 2 ? ld(aT, l) : z2,
-                                         NC != 1 ? ld(aE, l) : z2, NC != 1 ? ld(aB, l) : z2);
-                double vn = c1.a * (x * v0 - c1.b * v1);
-                v1 = v0; v0 = vn;
-                syn_accumulate<NC, false>(A, c1, v0, v1, is2, xis2, NC != 2 ? ld(aT, l + 1) : z2,
-                                          NC != 1 ? ld(aE, l + 1) : z2, NC != 1 ? ld(aB, l + 1) : z2);
-                if (l + 2 <= L) {
-                    const LegCoef c2 = cf[l + 2];
-                    vn = c2.a * (x * v0 - c2.b * v1);
-                    v1 = v0; v0 = vn;
+                    rec_step(cn, x[r], v0[r], v1[r]);
+                    if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
                 }
             }
-            if (l <= L) {
-                const LegCoef c = cf[l];
-                syn_accumulate<NC, true>(A, c, v0, v1, is2, xis2, NC != 2 ? ld(aT, l) : z2,
-                                         NC != 1 ? ld(aE, l) : z2, NC != 1 ? ld(aB, l) : z2);
+            ++l;
+        }
+        // ---- fast path: every live slot active and representable ----
+        if (l <= L && ((l - m) & 1)) {
+            const LegCoef c = cf[l];
+            const LegCoef cn = cf[min(l + 1, L)];
+            const double2 t = NC != 2 ? aT[l] : z2, e = NC != 1 ? aE[l] : z2, b = NC != 1 ? aB[l] : z2;
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (ls[r] > L) continue;
+                syn_accumulate<NC, false>(A[r], c, v0[r], v1[r], is2[r], xis2[r], t, e, b);
+                if (l < L) rec_step(cn, x[r], v0[r], v1[r]);
+            }
+            ++l;
+        }
+        for (; l + 1 <= L; l += 2) {
+            const LegCoef c0 = cf[l], c1 = cf[l + 1], c2 = cf[min(l + 2, L)];
+            const double2 t0 = NC != 2 ? aT[l] : z2, e0 = NC != 1 ? aE[l] : z2, b0 = NC != 1 ? aB[l] : z2;
+            const double2 t1 = NC != 2 ? aT[l + 1] : z2, e1 = NC != 1 ? aE[l + 1] : z2, b1 = NC != 1 ? aB[l + 1] : z2;
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (ls[r] > L) continue;
+                syn_accumulate<NC, true>(A[r], c0, v0[r], v1[r], is2[r], xis2[r], t0, e0, b0);
+                rec_step(c1, x[r], v0[r], v1[r]);
+                syn_accumulate<NC, false>(A[r], c1, v0[r], v1[r], is2[r], xis2[r], t1, e1, b1);
+                rec_step(c2, x[r], v0[r], v1[r]);
             }
         }
-        if (!act) continue;
+        if (l <= L) {
+            const LegCoef c = cf[l];
+            const double2 t = NC != 2 ? aT[l] : z2, e = NC != 1 ? aE[l] : z2, b = NC != 1 ? aB[l] : z2;
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (ls[r] > L) continue;
+                syn_accumulate<NC, true>(A[r], c, v0[r], v1[r], is2[r], xis2[r], t, e, b);
+            }
+        }
+        // ---- outputs ----
         const long long plane = (long long)(L + 1) * npair;
-        const long long o = (long long)m * npair + p;
-        int comp = 0;
-        if constexpr (NC != 2) {
-            phi[(2 * comp + 0) * plane + o] = make_double2(A.tp[0] + A.tn[0], A.tp[1] + A.tn[1]);
-            phi[(2 * comp + 1) * plane + o] = make_double2(A.tp[0] - A.tn[0], A.tp[1] - A.tn[1]);
-            ++comp;
-        }
-        if constexpr (NC != 1) {
-            // Q = -(...), U = -(...)
-            phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[0] + A.sn[0]), -(A.sp[1] + A.sn[1]));
-            phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[0] - A.sn[0]), -(A.sp[1] - A.sn[1]));
-            ++comp;
-            phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[2] + A.sn[2]), -(A.sp[3] + A.sn[3]));
-            phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[2] - A.sn[2]), -(A.sp[3] - A.sn[3]));
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+            if (!act[r]) continue;
+            const long long o = (long long)m * npair + pr[r];
+            int comp = 0;
+            if constexpr (NC != 2) {
+                phi[(2 * comp + 0) * plane + o] = make_double2(A[r].tp[0] + A[r].tn[0], A[r].tp[1] + A[r].tn[1]);
+                phi[(2 * comp + 1) * plane + o] = make_double2(A[r].tp[0] - A[r].tn[0], A[r].tp[1] - A[r].tn[1]);
+                ++comp;
+            }
+            if constexpr (NC != 1) {
+                // Q = -(...), U = -(...)
+                phi[(2 * comp + 0) * plane + o] = make_double2(-(A[r].sp[0] + A[r].sn[0]), -(A[r].sp[1] + A[r].sn[1]));
+                phi[(2 * comp + 1) * plane + o] = make_double2(-(A[r].sp[0] - A[r].sn[0]), -(A[r].sp[1] - A[r].sn[1]));
+                ++comp;
+                phi[(2 * comp + 0) * plane + o] = make_double2(-(A[r].sp[2] + A[r].sn[2]), -(A[r].sp[3] + A[r].sn[3]));
+                phi[(2 * comp + 1) * plane + o] = make_double2(-(A[r].sp[2] - A[r].sn[2]), -(A[r].sp[3] - A[r].sn[3]));
+            }
         }
     }
 }
@@ -331,16 +396,17 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const dou
 // ring FFTs (block-wide, in place, buffer in LDS or global scratch)
 // ---------------------------------------------------------------------------
 // forward (dir = -1): X_k = sum_j x_j e^{-2 pi i jk/M};  dir = +1: conjugate
-// twiddles; tw[k] = e^{-2 pi i k / Mmax}, k < Mmax/2
+// twiddles; tw[k] = e^{-2 pi i k / Mmax}, k < Mmax/2.  Each thread owns at most
+// NB butterflies per stage (M / 2 <= NB * blockDim).
+template <int NB>
 __device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
-    constexpr int NBMAX = 16;   // M/2 / blockDim <= 16 (M <= 16384, blockDim 512)
     const int half = M >> 1;
     for (int Ns = 1; Ns < M; Ns <<= 1) {
-        double2 o0[NBMAX], o1[NBMAX];
-        int id[NBMAX];
+        double2 o0[NB], o1[NB];
+        int id[NB];
         const int tstride = Mmax / (2 * Ns);
 #pragma unroll
-        for (int t = 0; t < NBMAX; ++t) {
+        for (int t = 0; t < NB; ++t) {
             const int j = threadIdx.x + t * blockDim.x;
             if (j < half) {
                 const double2 a = buf[j];
@@ -354,7 +420,7 @@ __device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict
         }
         __syncthreads();
 #pragma unroll
-        for (int t = 0; t < NBMAX; ++t) {
+        for (int t = 0; t < NB; ++t) {
             const int j = threadIdx.x + t * blockDim.x;
             if (j < half) { buf[id[t]] = o0[t]; buf[id[t] + Ns] = o1[t]; }
         }
@@ -362,22 +428,23 @@ __device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict
     }
 }
 
-// forward DFT of length n held in buf[0..n) (M = Bluestein length, kern = FFT of
-// the chirp kernel); result in buf[0..n)
+// forward DFT of length n held in buf[0..n) (Bluestein when n is not a power
+// of two: M = g.M, kernel V = FFT of the chirp); result in buf[0..n)
+template <int NB>
 __device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
                             const double2* __restrict__ bsk) {
     const int n = g.nphi, M = g.M;
-    if (g.bs_off < 0) { fft_pow2(buf, M, -1, tw, Mmax); return; }
+    if (g.bs_off < 0) { fft_pow2<NB>(buf, M, -1, tw, Mmax); return; }
     const double2* V = bsk + g.bs_off;
     for (int j = threadIdx.x; j < M; j += blockDim.x) {
         if (j < n) buf[j] = cmul(buf[j], expi_pi_frac(-(long long)j * j, n));   // c_j = e^{-i pi j^2/n}
         else buf[j] = make_double2(0.0, 0.0);
     }
     __syncthreads();
-    fft_pow2(buf, M, -1, tw, Mmax);
+    fft_pow2<NB>(buf, M, -1, tw, Mmax);
     for (int j = threadIdx.x; j < M; j += blockDim.x) buf[j] = cmul(buf[j], V[j]);
     __syncthreads();
-    fft_pow2(buf, M, +1, tw, Mmax);
+    fft_pow2<NB>(buf, M, +1, tw, Mmax);
     const double inv = 1.0 / M;
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
         const double2 c = expi_pi_frac(-(long long)j * j, n);
@@ -388,21 +455,22 @@ __device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __re
 }
 
 // inverse (unnormalised) DFT: y_j = sum_k Z_k e^{+2 pi i jk/n}
+template <int NB>
 __device__ void dft_inverse(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
                             const double2* __restrict__ bsk) {
-    if (g.bs_off < 0) { fft_pow2(buf, g.M, +1, tw, Mmax); return; }
+    if (g.bs_off < 0) { fft_pow2<NB>(buf, g.M, +1, tw, Mmax); return; }
     for (int j = threadIdx.x; j < g.nphi; j += blockDim.x) buf[j].y = -buf[j].y;
     __syncthreads();
-    dft_forward(buf, g, tw, Mmax, bsk);
+    dft_forward<NB>(buf, g, tw, Mmax, bsk);
     for (int j = threadIdx.x; j < g.nphi; j += blockDim.x) buf[j].y = -buf[j].y;
     __syncthreads();
 }
 
 // plan time: V = FFT_M(w), w_t = e^{+i pi t^2/n} for |t| < n (cyclic)
-__global__ __launch_bounds__(RING_BLOCK) void k_sht_bluestein_setup(const int* __restrict__ pairs,
-                                                                    const PairGeom* __restrict__ geom,
-                                                                    const double2* __restrict__ tw, int Mmax,
-                                                                    double2* __restrict__ bsk) {
+__global__ __launch_bounds__(1024) void k_sht_bluestein_setup(const int* __restrict__ pairs,
+                                                              const PairGeom* __restrict__ geom,
+                                                              const double2* __restrict__ tw, int Mmax,
+                                                              double2* __restrict__ bsk) {
     const PairGeom g = geom[pairs[blockIdx.x]];
     double2* buf = bsk + g.bs_off;
     const int n = g.nphi, M = g.M;
@@ -413,7 +481,7 @@ __global__ __launch_bounds__(RING_BLOCK) void k_sht_bluestein_setup(const int* _
         buf[t] = tt >= 0 ? expi_pi_frac(tt * tt, n) : make_double2(0.0, 0.0);
     }
     __syncthreads();
-    fft_pow2(buf, M, -1, tw, Mmax);
+    fft_pow2<8>(buf, M, -1, tw, Mmax);
 }
 
 __global__ void k_sht_twiddles(int Mmax, double2* __restrict__ tw) {
@@ -424,59 +492,93 @@ __global__ void k_sht_twiddles(int Mmax, double2* __restrict__ tw) {
     tw[k] = make_double2(cs, sn);
 }
 
+// threads per FFT workgroup for a class of length M, and butterflies per thread
+inline int ring_block(int M) { return std::min(1024, std::max(64, M / 8)); }
+
 // ---------------------------------------------------------------------------
 // synthesis: ring stage.  grid (pairs of this M class, ncomp)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double2 fold_phi(const double2* __restrict__ ph, long long plane_off, int npair, int p, int L,
-                                            int k, int n, int h) {
-    // G_k = sum_{m = k mod n, m <= L} c_m Phi_m e^{i m phi0},  phi0 = h pi / n
-    double2 acc = make_double2(0.0, 0.0);
-    for (int m = k; m <= L; m += n) {
-        const double2 v = ph[plane_off + (long long)m * npair + p];
-        const double cm = m == 0 ? 1.0 : 2.0;
-        const double2 e = h ? expi_pi_frac(m, n) : make_double2(1.0, 0.0);
-        const double2 t = cmul(v, e);
-        acc.x = fma(cm, t.x, acc.x);
-        acc.y = fma(cm, t.y, acc.y);
-    }
-    return acc;
-}
+// Fold: G_k = sum_{m = k mod n, m <= L} c_m Phi_m e^{i m phi0} (c_0 = 1, else 2),
+// for north and south; the Hermitian parts of both go into one complex FFT:
+// Z_k = (G^N_k + conj G^N_-k)/2 + i (G^S_k + conj G^S_-k)/2.  Thread slot s owns
+// the bin pair (k, n-k), k = s mod K (K = n/2 + 1) and the aliases j = s / K
+// (mod J); J > 1 only for short rings, reduced in LDS in a fixed order.
+struct Fold4 { double2 nk, nmk, sk, smk; };
 
-__global__ __launch_bounds__(RING_BLOCK) void k_sht_synth_ring(int L, int npair, long long npix,
-                                                               const int* __restrict__ pairs,
-                                                               const PairGeom* __restrict__ geom,
-                                                               const double2* __restrict__ phi,
-                                                               const double2* __restrict__ tw, int Mmax,
-                                                               const double2* __restrict__ bsk,
-                                                               double2* __restrict__ gscratch, double* __restrict__ maps) {
+template <int NB>
+__global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long long npix,
+                                                         const int* __restrict__ pairs,
+                                                         const PairGeom* __restrict__ geom,
+                                                         const double2* __restrict__ phi,
+                                                         const double2* __restrict__ tw, int Mmax,
+                                                         const double2* __restrict__ bsk,
+                                                         double2* __restrict__ gscratch, double* __restrict__ maps) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
     const PairGeom g = geom[p];
+    const int BD = blockDim.x;
     double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
+    Fold4* red = reinterpret_cast<Fold4*>(lbuf + (gscratch ? 0 : g.M));   // J > 1 only (short rings)
     const int n = g.nphi;
     const long long plane = (long long)(L + 1) * npair;
-    const long long offN = (2LL * comp + 0) * plane, offS = (2LL * comp + 1) * plane;
+    const double2* PN = phi + (2LL * comp + 0) * plane + p;
+    const double2* PS = phi + (2LL * comp + 1) * plane + p;
     const bool eq = g.startS < 0;
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const int nk = k == 0 ? 0 : n - k;
-        const double2 a = fold_phi(phi, offN, npair, p, L, k, n, g.phi_half);
-        const double2 b = fold_phi(phi, offN, npair, p, L, nk, n, g.phi_half);
-        // Hermitian part of the north spectrum: (G_k + conj G_{-k}) / 2
-        double2 z = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
-        if (!eq) {
-            const double2 c = fold_phi(phi, offS, npair, p, L, k, n, g.phi_half);
-            const double2 d = fold_phi(phi, offS, npair, p, L, nk, n, g.phi_half);
-            const double2 s = make_double2(0.5 * (c.x + d.x), 0.5 * (c.y - d.y));
-            z.x -= s.y;   // z += i s
-            z.y += s.x;
+    const int K = n / 2 + 1;
+    const int J = K >= BD ? 1 : BD / K;          // threads per bin pair
+    auto H = [&](const double2* P, int m) {
+        const double2 v = P[(long long)m * npair];
+        const double cm = m == 0 ? 1.0 : 2.0;
+        const double2 t = g.phi_half ? cmul(v, expi_pi_frac(m, n)) : v;
+        return make_double2(cm * t.x, cm * t.y);
+    };
+    for (int s0 = 0; s0 < K * J; s0 += BD) {
+        const int sl = s0 + threadIdx.x;
+        Fold4 f = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
+        const int k = sl % K, j0 = sl / K;
+        const int nk = (n - k) % n;
+        if (sl < K * J) {
+            for (int m = k + j0 * n; m <= L; m += J * n) {
+                const double2 a = H(PN, m);
+                f.nk.x += a.x; f.nk.y += a.y;
+                if (!eq) { const double2 b = H(PS, m); f.sk.x += b.x; f.sk.y += b.y; }
+            }
+            if (nk != k)
+                for (int m = nk + j0 * n; m <= L; m += J * n) {
+                    const double2 a = H(PN, m);
+                    f.nmk.x += a.x; f.nmk.y += a.y;
+                    if (!eq) { const double2 b = H(PS, m); f.smk.x += b.x; f.smk.y += b.y; }
+                }
         }
-        buf[k] = z;
+        if (J > 1) {
+            red[threadIdx.x] = f;
+            __syncthreads();
+            if (sl < K * J && j0 == 0) {
+                for (int jj = 1; jj < J; ++jj) {
+                    const Fold4 o = red[threadIdx.x + jj * K];
+                    f.nk.x += o.nk.x; f.nk.y += o.nk.y; f.nmk.x += o.nmk.x; f.nmk.y += o.nmk.y;
+                    f.sk.x += o.sk.x; f.sk.y += o.sk.y; f.smk.x += o.smk.x; f.smk.y += o.smk.y;
+                }
+            }
+            __syncthreads();
+        }
+        if (sl < K * J && j0 == 0) {
+            if (nk == k) { f.nmk = f.nk; f.smk = f.sk; }
+            // Z_k = hN_k + i hS_k, hX_k = (G_k + conj G_-k)/2
+            const double2 hn = make_double2(0.5 * (f.nk.x + f.nmk.x), 0.5 * (f.nk.y - f.nmk.y));
+            const double2 hs = make_double2(0.5 * (f.sk.x + f.smk.x), 0.5 * (f.sk.y - f.smk.y));
+            buf[k] = make_double2(hn.x - hs.y, hn.y + hs.x);
+            if (nk != k) {
+                const double2 hn2 = make_double2(hn.x, -hn.y), hs2 = make_double2(hs.x, -hs.y);
+                buf[nk] = make_double2(hn2.x - hs2.y, hn2.y + hs2.x);
+            }
+        }
     }
     __syncthreads();
-    dft_inverse(buf, g, tw, Mmax, bsk);
+    dft_inverse<NB>(buf, g, tw, Mmax, bsk);
     double* mc = maps + (long long)comp * npix;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    for (int j = threadIdx.x; j < n; j += BD) {
         const double2 y = buf[j];
         mc[g.startN + j] = y.x;
         if (!eq) mc[g.startS + j] = y.y;
@@ -486,13 +588,14 @@ __global__ __launch_bounds__(RING_BLOCK) void k_sht_synth_ring(int L, int npair,
 // ---------------------------------------------------------------------------
 // analysis: ring stage.  grid (pairs of this M class, ncomp)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(RING_BLOCK) void k_sht_anal_ring(int L, int npair, long long npix,
-                                                              const int* __restrict__ pairs,
-                                                              const PairGeom* __restrict__ geom,
-                                                              const double* __restrict__ maps,
-                                                              const double2* __restrict__ tw, int Mmax,
-                                                              const double2* __restrict__ bsk,
-                                                              double2* __restrict__ gscratch, double2* __restrict__ phi) {
+template <int NB>
+__global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long long npix,
+                                                        const int* __restrict__ pairs,
+                                                        const PairGeom* __restrict__ geom,
+                                                        const double* __restrict__ maps,
+                                                        const double2* __restrict__ tw, int Mmax,
+                                                        const double2* __restrict__ bsk,
+                                                        double2* __restrict__ gscratch, double2* __restrict__ phi) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -504,7 +607,7 @@ __global__ __launch_bounds__(RING_BLOCK) void k_sht_anal_ring(int L, int npair, 
     for (int j = threadIdx.x; j < n; j += blockDim.x)
         buf[j] = make_double2(mc[g.startN + j], eq ? 0.0 : mc[g.startS + j]);
     __syncthreads();
-    dft_forward(buf, g, tw, Mmax, bsk);
+    dft_forward<NB>(buf, g, tw, Mmax, bsk);
     const long long plane = (long long)(L + 1) * npair;
     double2* oN = phi + (2LL * comp + 0) * plane;
     double2* oS = phi + (2LL * comp + 1) * plane;
@@ -527,12 +630,43 @@ __global__ __launch_bounds__(RING_BLOCK) void k_sht_anal_ring(int L, int npair, 
 }
 
 // ---------------------------------------------------------------------------
-// analysis: Legendre stage.  grid (m pairs, tiles of ANA_TILE ring pairs)
+// analysis: Legendre stage.  grid (m pairs, tiles of LTILE ring pairs)
 // out: part[tile][comp][nlm] (double2), unweighted sums
 //   T: sum lambda Phi_T ;  E: sum (Q F1 + i U F2) ;  B: sum (U F1 - i Q F2)
+// Per chunk of ANA_C l (aligned to m's parity) every lane sums its 4 ring
+// pairs in registers; the workgroup then reduces the chunk's NO x ANA_C
+// partial sums over its 256 lanes in LDS in a fixed order.
 // ---------------------------------------------------------------------------
+template <int NC, bool EVEN, bool SLOW>
+__device__ __forceinline__ void ana_term(double* a, const LegCoef& c, double v0, double v1, int k, double is2,
+                                         double xis2, const double2* fp, const double2* fn) {
+    const double lam = SLOW ? (k == 0 ? v0 : 0.0) : v0;
+    const double lam1 = SLOW ? (k == 0 ? v1 : 0.0) : v1;
+    int o = 0;
+    if constexpr (NC != 2) {
+        const double2 t = EVEN ? fp[0] : fn[0];
+        a[0] = fma(lam, t.x, a[0]);
+        a[1] = fma(lam, t.y, a[1]);
+        o = 2;
+    }
+    if constexpr (NC != 1) {
+        constexpr int cq = NC == 3 ? 1 : 0;
+        const double F1 = fma(c.R * xis2, lam1, -fma(c.P, is2, c.Q) * lam);
+        const double F2 = fma(c.Rm * is2, lam1, -(c.T * xis2) * lam);
+        const double2 Q1 = EVEN ? fp[cq] : fn[cq];          // F1 parity
+        const double2 U1 = EVEN ? fp[cq + 1] : fn[cq + 1];
+        const double2 Q2 = EVEN ? fn[cq] : fp[cq];          // F2 parity
+        const double2 U2 = EVEN ? fn[cq + 1] : fp[cq + 1];
+        a[o + 0] = fma(F1, Q1.x, fma(-F2, U2.y, a[o + 0]));
+        a[o + 1] = fma(F1, Q1.y, fma(F2, U2.x, a[o + 1]));
+        a[o + 2] = fma(F1, U1.x, fma(F2, Q2.y, a[o + 2]));
+        a[o + 3] = fma(F1, U1.y, fma(-F2, Q2.x, a[o + 3]));
+    }
+}
+
 template <int NC>
-__global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const double2* __restrict__ phi,
+__global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegCoef* __restrict__ coef,
+                                                            const double2* __restrict__ phi,
                                                             double2* __restrict__ part) {
     constexpr int NO = NC == 1 ? 2 : (NC == 2 ? 4 : 6);   // real outputs per l
     constexpr int NV = NO * ANA_C;
@@ -540,38 +674,40 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const doub
     __shared__ double red[NV * RS];
     const int L = D.L, npair = D.npair;
     const int q = blockIdx.x, tile = blockIdx.y;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g0 = tile * (LTILE / 64) + wave * SR;
     const long long plane = (long long)(L + 1) * npair;
-    double x[ANA_R], is2[ANA_R];
-    int pr[ANA_R];
-    bool act[ANA_R];
+    double x[SR], is2[SR], xis2[SR];
+    int pr[SR];
+    bool act[SR];
 #pragma unroll
-    for (int r = 0; r < ANA_R; ++r) {
-        pr[r] = tile * ANA_TILE + r * LEG_BLOCK + tid;
+    for (int r = 0; r < SR; ++r) {
+        pr[r] = (g0 + r) * 64 + lane;
         act[r] = pr[r] < npair;
         x[r] = act[r] ? D.geom[pr[r]].x : 0.0;
         is2[r] = act[r] ? D.geom[pr[r]].is2 : 0.0;
+        xis2[r] = x[r] * is2[r];
     }
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
         if (h == 1 && m <= q) break;
-        // per-slot onset l (uniform per wave) and the workgroup's first l
-        int ls[ANA_R];
+        int ls[SR];
+#pragma unroll
+        for (int r = 0; r < SR; ++r)
+            ls[r] = __builtin_amdgcn_readfirstlane(g0 + r < D.ngroup ? D.lstart[(long long)m * D.ngroup + g0 + r]
+                                                                     : L + 1);
         int lmin = L + 1;
-#pragma unroll
-        for (int r = 0; r < ANA_R; ++r) {
-            const int gq = (tile * ANA_TILE + r * LEG_BLOCK) / 64 + wave;
-            ls[r] = gq < D.ngroup ? D.lstart[(long long)m * D.ngroup + gq] : L + 1;
-        }
-        for (int gq = tile * ANA_TILE / 64; gq < min(D.ngroup, (tile + 1) * ANA_TILE / 64); ++gq)
+        for (int gq = tile * (LTILE / 64); gq < min(D.ngroup, (tile + 1) * (LTILE / 64)); ++gq)
             lmin = min(lmin, D.lstart[(long long)m * D.ngroup + gq]);
-        // per-slot parity-combined ring phases: [+]: N + S, [-]: N - S
-        double2 fp[ANA_R][NC], fn[ANA_R][NC];
-        double v0[ANA_R], v1[ANA_R];
-        int kk[ANA_R];
+        lmin = __builtin_amdgcn_readfirstlane(lmin);
+        // parity-combined ring phases: [+]: N + S, [-]: N - S
+        double2 fp[SR][NC], fn[SR][NC];
+        double v0[SR], v1[SR];
+        int kk[SR];
 #pragma unroll
-        for (int r = 0; r < ANA_R; ++r) {
-            v0[r] = 0.0; v1[r] = 0.0; kk[r] = -1;
+        for (int r = 0; r < SR; ++r) {
+            v0[r] = 0.0; v1[r] = 0.0; kk[r] = 0;
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 double2 a = make_double2(0.0, 0.0), b = a;
@@ -583,55 +719,61 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const doub
                 fn[r][c] = make_double2(a.x - b.x, a.y - b.y);
             }
         }
-        const LegCoef* cf = D.coef + cidx(L, m, m) - m;
         const long long obase = cidx(L, m, m) - m;
-        for (int l0 = lmin; l0 <= L; l0 += ANA_C) {
+        const LegCoef* cf = coef + obase;
+        bool slow = true;
+        // chunks start on m's parity so positions 0, 2 of a chunk are even
+        const int lstart0 = lmin - ((lmin - m) & 1);
+        for (int l0 = lstart0; l0 <= L; l0 += ANA_C) {
             double acc[NV];
 #pragma unroll
             for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+            // activations inside the chunk force the slow path
 #pragma unroll
-            for (int cc = 0; cc < ANA_C; ++cc) {
-                const int l = l0 + cc;
-                if (l > L) break;
-                const LegCoef c = cf[l];
-                const bool even = ((l - m) & 1) == 0;
+            for (int r = 0; r < SR; ++r)
+                if (ls[r] >= l0 && ls[r] < l0 + ANA_C && ls[r] <= L) slow = true;
+            if (slow) {
 #pragma unroll
-                for (int r = 0; r < ANA_R; ++r) {
-                    if (l < ls[r]) continue;                 // uniform per wave
-                    if (l == ls[r] && act[r]) {
-                        const double2 s0 = D.st[(long long)m * npair + pr[r]];
-                        v1[r] = s0.x; v0[r] = s0.y;
-                        kk[r] = D.stk[(long long)m * npair + pr[r]];
+                for (int cc = 0; cc < ANA_C; ++cc) {
+                    const int l = l0 + cc;
+                    if (l > L) break;
+                    const LegCoef c = cf[l];
+                    const LegCoef cn = cf[min(l + 1, L)];
+#pragma unroll
+                    for (int r = 0; r < SR; ++r) {
+                        if (l < ls[r]) continue;                 // uniform per wave
+                        if (l == ls[r] && act[r]) {
+                            const double2 s0 = D.st[(long long)m * npair + pr[r]];
+                            v1[r] = s0.x; v0[r] = s0.y;
+                            kk[r] = D.stk[(long long)m * npair + pr[r]];
+                        }
+                        if ((cc & 1) == 0) ana_term<NC, true, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
+                        else ana_term<NC, false, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
+                        if (l < L) {
+                            rec_step(cn, x[r], v0[r], v1[r]);
+                            if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
+                        }
                     }
-                    const double lam = kk[r] == 0 ? v0[r] : 0.0;
-                    const double lam1 = kk[r] == 0 ? v1[r] : 0.0;
-                    double* a = acc + cc * NO;
-                    int o = 0;
-                    if constexpr (NC != 2) {
-                        const double2 t = even ? fp[r][0] : fn[r][0];
-                        a[0] = fma(lam, t.x, a[0]);
-                        a[1] = fma(lam, t.y, a[1]);
-                        o = 2;
-                    }
-                    if constexpr (NC != 1) {
-                        constexpr int cq = NC == 3 ? 1 : 0;
-                        const double xis2 = x[r] * is2[r];
-                        const double F1 = fma(c.R * xis2, lam1, -fma(c.P, is2[r], c.Q) * lam);
-                        const double F2 = fma(c.Rm * is2[r], lam1, -(c.T * xis2) * lam);
-                        const double2 Q1 = even ? fp[r][cq] : fn[r][cq];       // F1 parity
-                        const double2 U1 = even ? fp[r][cq + 1] : fn[r][cq + 1];
-                        const double2 Q2 = even ? fn[r][cq] : fp[r][cq];       // F2 parity
-                        const double2 U2 = even ? fn[r][cq + 1] : fp[r][cq + 1];
-                        a[o + 0] = fma(F1, Q1.x, fma(-F2, U2.y, a[o + 0]));
-                        a[o + 1] = fma(F1, Q1.y, fma(F2, U2.x, a[o + 1]));
-                        a[o + 2] = fma(F1, U1.x, fma(F2, Q2.y, a[o + 2]));
-                        a[o + 3] = fma(F1, U1.y, fma(-F2, Q2.x, a[o + 3]));
-                    }
-                    if (l < L) {
-                        const LegCoef cn = cf[l + 1];
-                        const double vn = cn.a * (x[r] * v0[r] - cn.b * v1[r]);
-                        v1[r] = v0[r]; v0[r] = vn;
-                        if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
+                }
+                // leave the slow path once every live slot is active and representable
+                bool live = true;
+#pragma unroll
+                for (int r = 0; r < SR; ++r)
+                    if (ls[r] <= L && (l0 + ANA_C <= ls[r] || __any(kk[r] < 0))) live = false;
+                slow = !live;
+            } else {
+#pragma unroll
+                for (int cc = 0; cc < ANA_C; ++cc) {
+                    const int l = l0 + cc;
+                    if (l > L) break;
+                    const LegCoef c = cf[l];
+                    const LegCoef cn = cf[min(l + 1, L)];
+#pragma unroll
+                    for (int r = 0; r < SR; ++r) {
+                        if (ls[r] > L) continue;
+                        if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
+                        else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
+                        if (l < L) rec_step(cn, x[r], v0[r], v1[r]);
                     }
                 }
             }
@@ -652,7 +794,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const doub
             if (v < NV && g == 0) {
                 const int cc = v / NO, o = v % NO;
                 const int l = l0 + cc;
-                if (l <= L) {
+                if (l >= m && l <= L) {
                     const int comp = o >> 1;
                     double* dst = reinterpret_cast<double*>(part + ((long long)tile * NC + comp) * D.nlm + obase + l);
                     dst[o & 1] = sum;
@@ -660,11 +802,10 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const doub
             }
             __syncthreads();
         }
-        // l below the workgroup's onset: exact zeros
-        for (int l = m + tid; l < min(lmin, L + 1); l += LEG_BLOCK)
+        // l below the workgroup's first chunk: exact zeros
+        for (int l = m + tid; l < min(lstart0, L + 1); l += LEG_BLOCK)
             for (int c = 0; c < NC; ++c) part[((long long)tile * NC + c) * D.nlm + obase + l] = make_double2(0.0, 0.0);
     }
-    (void)lane;
 }
 
 // sum tiles in fixed order, weight, sign, write the caller's layout (accumulate
@@ -733,6 +874,7 @@ struct gs_sht {
     double2* part = nullptr;     // [ntile][3][nlm]
     double2* gscr = nullptr;     // global FFT scratch for M > LDS_FFT_MAX
     double* mapw = nullptr;      // [3][npix] Jacobi residual maps
+    double2* ain = nullptr;      // [3][nlm] a_lm in healpy complex order
     // ring classes by FFT length
     std::vector<int> cls_M;      // M of each class
     std::vector<int> cls_n;      // pairs in the class
@@ -756,7 +898,7 @@ int sht_alloc(gs_sht* p, T** dst, size_t n) {
 }
 
 void sht_free(gs_sht* p) {
-    void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->mapw};
+    void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->mapw, p->ain};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (int* b : p->cls_pairs)
@@ -782,7 +924,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     p->nside = N; p->L = L; p->npair = 2 * N; p->ngroup = (p->npair + 63) / 64;
     p->nlm = (L + 1) * (L + 2) / 2;
     p->npix = 12LL * N * N;
-    p->ntile = (p->npair + ANA_TILE - 1) / ANA_TILE;
+    p->ntile = (p->npair + LTILE - 1) / LTILE;
     // ---- geometry (ring pair r: north ring r+1, south ring 4N-1-r) ----
     std::vector<PairGeom> geom(p->npair);
     int Mmax = 2;
@@ -856,6 +998,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     rc |= sht_alloc(p, &p->phi, (size_t)3 * 2 * (L + 1) * p->npair);
     rc |= sht_alloc(p, &p->part, (size_t)p->ntile * 3 * p->nlm);
     rc |= sht_alloc(p, &p->mapw, (size_t)3 * p->npix);
+    rc |= sht_alloc(p, &p->ain, (size_t)3 * p->nlm);
     if (rc) { sht_free(p); return -1; }
     // ring classes by M
     std::vector<int> Ms;
@@ -893,10 +1036,12 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         sht_free(p);
         return set_error("gs_sht_create: out of device memory");
     }
-    if (hipFuncSetAttribute((const void*)k_sht_synth_ring, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            LDS_FFT_MAX * (int)sizeof(double2)) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_sht_anal_ring, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            LDS_FFT_MAX * (int)sizeof(double2)) != hipSuccess) {
+    {
+        const void* fns[] = {(const void*)k_sht_synth_ring<4>, (const void*)k_sht_synth_ring<8>,
+                             (const void*)k_sht_anal_ring<4>, (const void*)k_sht_anal_ring<8>};
+        for (const void* f : fns)
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      LDS_FFT_MAX * (int)sizeof(double2) + 64 * 4 * (int)sizeof(double2));
         (void)hipGetLastError();
     }
     hipLaunchKernelGGL(k_sht_twiddles, dim3(nblocks(Mmax / 2, 256)), dim3(256), 0, 0, Mmax, p->tw);
@@ -907,7 +1052,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         int* dp = nullptr;
         if (hipMalloc((void**)&dp, bs_pairs.size() * sizeof(int)) == hipSuccess &&
             hipMemcpy(dp, bs_pairs.data(), bs_pairs.size() * sizeof(int), hipMemcpyHostToDevice) == hipSuccess) {
-            hipLaunchKernelGGL(k_sht_bluestein_setup, dim3((unsigned)bs_pairs.size()), dim3(RING_BLOCK), 0, 0, dp,
+            hipLaunchKernelGGL(k_sht_bluestein_setup, dim3((unsigned)bs_pairs.size()), dim3(1024), 0, 0, dp,
                                p->geom, p->tw, Mmax, p->bsk);
         }
         (void)hipDeviceSynchronize();
@@ -942,15 +1087,27 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
     for (size_t c = 0; c < p->cls_M.size(); ++c) {
         const int M = p->cls_M[c];
         const bool glob = M > LDS_FFT_MAX;
-        const size_t lds = glob ? 0 : (size_t)M * sizeof(double2);
+        const int bd = ring_block(M);
+        const bool nb8 = M / 2 > 4 * bd;
+        // LDS: FFT buffer (+ fold reduction slots for short rings)
+        const size_t lds = glob ? 0 : (size_t)M * sizeof(double2) + (M < 8 * bd ? (size_t)bd * 4 * sizeof(double2) : 0);
         const dim3 grid(p->cls_n[c], ncomp);
         double2* scr = glob ? p->gscr : nullptr;
-        if (synth)
-            hipLaunchKernelGGL(k_sht_synth_ring, grid, dim3(RING_BLOCK), lds, S(stream), p->L, p->npair, p->npix,
-                               p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out);
-        else
-            hipLaunchKernelGGL(k_sht_anal_ring, grid, dim3(RING_BLOCK), lds, S(stream), p->L, p->npair, p->npix,
-                               p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi);
+        if (synth) {
+            if (nb8)
+                hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out);
+            else
+                hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out);
+        } else {
+            if (nb8)
+                hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi);
+            else
+                hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi);
+        }
         GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
     }
     return 0;
@@ -961,8 +1118,12 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_alm2map: ncomp must be 1 (T), 2 (E,B) or 3 (T,E,B)");
     if (layout != GS_ALM_REAL && layout != GS_ALM_COMPLEX) return set_error("gs_sht_alm2map: bad layout");
     if (!alm || !maps) return set_error("gs_sht_alm2map: null argument");
-    const dim3 grid(p->L / 2 + 1, (p->npair + LEG_BLOCK - 1) / LEG_BLOCK);
-#define GS_SL(NC) hipLaunchKernelGGL((k_sht_synth_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), alm, layout, p->phi)
+    const long long nin = (long long)ncomp * p->nlm;
+    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, ncomp, alm, layout,
+                       p->ain);
+    GS_LAUNCH_CHECK("k_sht_alm_in");
+    const dim3 grid(p->L / 2 + 1, p->ntile);
+#define GS_SL(NC) hipLaunchKernelGGL((k_sht_synth_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->ain, p->phi)
     if (ncomp == 1) GS_SL(1); else if (ncomp == 2) GS_SL(2); else GS_SL(3);
 #undef GS_SL
     GS_LAUNCH_CHECK("k_sht_synth_leg");
@@ -972,7 +1133,7 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
 static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream) {
     if (sht_rings(p, false, ncomp, maps, nullptr, stream)) return -1;
     const dim3 grid(p->L / 2 + 1, p->ntile);
-#define GS_AL(NC) hipLaunchKernelGGL((k_sht_anal_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->phi, p->part)
+#define GS_AL(NC) hipLaunchKernelGGL((k_sht_anal_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->phi, p->part)
     if (ncomp == 1) GS_AL(1); else if (ncomp == 2) GS_AL(2); else GS_AL(3);
 #undef GS_AL
     GS_LAUNCH_CHECK("k_sht_anal_leg");
