@@ -1,0 +1,273 @@
+"""numpy restatement of the MASKED constrained-realization samplers (TEST INFRASTRUCTURE).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may import
+this module; the product path never does.
+
+Restates (Gabriel-Ducrocq/GibbsSampler, EB / "polarization" class):
+  * the constructor's constants         CenteredGibbs.py:258-306
+      N^-1 = mask / noise_pol, mu = max(N^-1) + 1e-14, second_part_grad =
+      b * complex_to_real(map2alm([0, Q N^-1, U N^-1], iter=0)) * Npix/4pi
+  * sample_gibbs_change_variable (a9)   CenteredGibbs.py:676-729
+  * overrelaxation_sampler (a10)        CenteredGibbs.py:733-825
+  * compute_gradient_mala / propose_new_mala / compute_log_proposal /
+    compute_log_density / sample_mala (a11)   CenteredGibbs.py:494-603
+  * the dispatch ladder of sample (a12)  CenteredGibbs.py:828-850
+with the build's SHT oracle (oracle/sht.py) in place of healpy.  Pinned by
+tests/golden/reference_masked_eb_*.npz, produced by running the reference
+itself (tools/gen_golden_masked.py) with that same SHT behind its healpy
+import: these fixtures pin the samplers' algebra, scalings and draw order,
+not healpy's transform (parity unpinned).
+
+TEB generalisation (not in the reference): T uses its own N_T^-1 and
+mu_T = max(N_T^-1) + 1e-14; the s|v draw is the per-l 3x3 centered block of
+oracle.harmonic with kappa_f = mu_f / w; over-relaxation uses the Cholesky
+factor of that block.
+
+Draws come from a ``Draws`` source: ``ReplayDraws`` consumes numpy's legacy
+global stream in the reference's order (parity with the fixtures);
+``NativeDraws`` restates the device's counter-based Philox streams.
+"""
+import math
+
+import numpy as np
+
+from . import harmonic as H
+from . import sht as O
+
+FOURPI = 4.0 * math.pi
+TAG_AUX_V = 8        # pixel normals of v | s; c0 = pixel, c1 = map (0 T, 1 Q, 2 U)
+TAG_MALA_U = 9       # MALA accept uniform
+SUB_S = 16           # CR substep base of the s | v draws: SUB_S + 2k (+1: second OR draw)
+SUB_V_INIT = 255     # substep of the over-relaxation's initial v | s
+SUB_MALA = 200       # CR substep of the MALA proposal normals (+ call index)
+
+
+class ReplayDraws:
+    """numpy legacy global RNG, in the reference's order."""
+
+    def __init__(self, seed=None):
+        if seed is not None:
+            np.random.seed(seed)
+
+    def pixel_normals(self, nmaps, npix, **kw):
+        return np.stack([np.random.normal(size=npix) for _ in range(nmaps)])
+
+    def slot_normals(self, nfields, nreal, **kw):
+        return np.stack([np.random.normal(size=nreal) for _ in range(nfields)])
+
+    def uniform(self, **kw):
+        return np.random.uniform()
+
+
+class NativeDraws:
+    """The device's Philox4x32-10 streams (gibbssampler_amd/csrc/gs_masked.hip)."""
+
+    def __init__(self, seed, chain, iteration, L, npix):
+        self.seed, self.chain, self.it, self.L, self.npix = int(seed), int(chain), int(iteration), L, npix
+
+    def pixel_normals(self, nmaps, npix, maps=(1, 2), substep=0):
+        k0, k1 = H.chain_key(self.seed, self.chain)
+        p = np.arange(npix, dtype=np.uint64)
+        out = []
+        for f in maps:
+            w = H.philox4x32_10(p, f, TAG_AUX_V | (substep << 8), self.it, k0, k1)
+            out.append(H.box_muller(*w)[0])
+        return np.stack(out)
+
+    def slot_normals(self, nfields, nreal, substep=0):
+        return np.stack([H.cr_normals(self.seed, self.chain, self.it, substep, f, self.L) for f in range(nfields)])
+
+    def uniform(self, substep=0):
+        k0, k1 = H.chain_key(self.seed, self.chain)
+        return H._uniform1(k0, k1, 0, substep, TAG_MALA_U, self.it)
+
+
+class MaskedModel:
+    """Pixel-domain data and noise of one masked problem.
+
+    maps: [3, Npix] (T, Q, U); inv_noise: [3, Npix] mask-multiplied N^-1
+    (T row ignored for nfields = 2)."""
+
+    def __init__(self, L, nside, nfields, bl, maps, inv_noise):
+        self.L, self.nside, self.F = int(L), int(nside), int(nfields)
+        self.Npix = 12 * self.nside ** 2
+        self.w = FOURPI / self.Npix
+        self.bl = np.asarray(bl, dtype=np.float64)
+        self.maps = np.asarray(maps, dtype=np.float64)
+        self.inv_noise = np.asarray(inv_noise, dtype=np.float64)
+        # CenteredGibbs.py:276 (pol); TEB: the same rule for T
+        self.mu = np.array([self.inv_noise[k].max() + 1e-14 for k in range(3)])
+        self.slot_ell = H.slot_ell(self.L)
+
+    # fields -> map rows: F=2: E,B <-> Q,U (rows 1,2); F=3: T,E,B <-> T,Q,U
+    @property
+    def rows(self):
+        return (1, 2) if self.F == 2 else (0, 1, 2)
+
+    def synth(self, s_real):
+        """maps of b * s (s real layout [F, NR]) -> [F, Npix] for the field rows."""
+        a = np.zeros((3, O._cidx(self.L)[0].shape[0]), dtype=np.complex128)
+        ls = O._cidx(self.L)[0]
+        for k, r in enumerate(self.rows):
+            a[r] = H.real_to_complex(s_real[k], self.L) * self.bl[ls]
+        m = O.alm2map(a, self.nside, self.L)
+        return np.stack([m[r] for r in self.rows])
+
+    def analysis(self, mp):
+        """complex_to_real(map2alm(maps, iter=0)) for the field rows: [F, NR]."""
+        full = np.zeros((3, self.Npix))
+        for k, r in enumerate(self.rows):
+            full[r] = mp[k]
+        a = O.map2alm(full, self.nside, self.L, iter=0)
+        return np.stack([H.complex_to_real(a[r], self.L) for r in self.rows])
+
+    def second_part_grad(self):
+        """b A^T N^-1 d (CenteredGibbs.py:298-306)."""
+        nd = np.stack([self.inv_noise[r] * self.maps[r] for r in self.rows])
+        return self.analysis(nd) * (self.Npix / FOURPI) * self.bl[self.slot_ell][None]
+
+    def aux_model(self, bins):
+        """oracle.harmonic Model whose kappa_f = mu_f / w (the s | v block)."""
+        mu = [self.mu[r] for r in self.rows]
+        return H.Model(self.L, self.nside, self.F, self.bl, [1.0 / m for m in mu], bins)
+
+
+# ----------------------------------------------------------------------------
+# a9 / a10: auxiliary-variable CR
+# ----------------------------------------------------------------------------
+def _v_given_s(mm, s, z, v_old=None, alpha=None):
+    """v | s  (CenteredGibbs.py:693-700): v = gamma A b s + sqrt(gamma) z,
+    gamma = mu - N^-1; over-relaxed (801-802): v' = m + alpha (v - m) +
+    sqrt(1 - alpha^2) sqrt(gamma) z."""
+    mp = mm.synth(s)
+    out = []
+    for k, r in enumerate(mm.rows):
+        gam = mm.mu[r] - mm.inv_noise[r]
+        mean = gam * mp[k]
+        if alpha is None:
+            out.append(z[k] * np.sqrt(gam) + mean)
+        else:
+            out.append(mean + alpha * (v_old[k] - mean) + math.sqrt(1 - alpha ** 2) * z[k] * np.sqrt(gam))
+    return np.stack(out)
+
+
+def _s_given_v(mm, dl_unbinned, v, z, s_old=None, alpha=None):
+    """s | v  (CenteredGibbs.py:703-726): per slot (EB) or per-l block (TEB)
+    var_s = (C^+ + (mu/w) b^2)^-1, mean = var_s b map2alm(v + N^-1 d)/w."""
+    rhs = np.stack([v[k] + mm.inv_noise[r] * mm.maps[r] for k, r in enumerate(mm.rows)])
+    r_real = mm.analysis(rhs)
+    ell = mm.slot_ell
+    if mm.F == 2:
+        out = []
+        var = H.var_from_dl(dl_unbinned)
+        for k, r in enumerate(mm.rows):
+            var_s = 1.0 / ((mm.mu[r] / mm.w) * mm.bl[ell] ** 2 + H.inv_var(var[k][ell]))
+            mean = var_s * (r_real[k] / mm.w * mm.bl[ell])
+            if alpha is None:
+                out.append(z[k] * np.sqrt(var_s) + mean)
+            else:
+                out.append(mean + alpha * (s_old[k] - mean) + math.sqrt(1 - alpha ** 2) * z[k] * np.sqrt(var_s))
+        return np.stack(out)
+    model = mm.aux_model({s: np.arange(mm.L + 2) for s in H.SPECTRA[3]})
+    M, Lc = H.centered_params(model, dl_unbinned)
+    d_eff = np.stack([r_real[k] / mm.mu[r] for k, r in enumerate(mm.rows)])
+    mean = H.cr_apply(model, M, np.zeros_like(M), d_eff, np.zeros_like(d_eff))
+    fl = H.cr_apply(model, np.zeros_like(M), Lc, d_eff, z)
+    if alpha is None:
+        return mean + fl
+    return mean + alpha * (s_old - mean) + math.sqrt(1 - alpha ** 2) * fl
+
+
+def aux_variable(mm, dl_unbinned, s_old, n_gibbs, draws):
+    """sample_gibbs_change_variable (a9): n_gibbs x (v | s, s | v); accept 1."""
+    s = np.array(s_old, dtype=np.float64)
+    nr = (mm.L + 1) ** 2
+    for k in range(n_gibbs):
+        zv = draws.pixel_normals(mm.F, mm.Npix, maps=mm.rows, substep=k)
+        v = _v_given_s(mm, s, zv)
+        zs = draws.slot_normals(mm.F, nr, substep=SUB_S + 2 * k)
+        s = _s_given_v(mm, dl_unbinned, v, zs)
+    return s, 1
+
+
+def overrelaxation(mm, dl_unbinned, s_old, n_gibbs, draws, alpha=-0.995):
+    """overrelaxation_sampler (a10): v | s plain, then n_gibbs x
+    (s | v, v | s, s | v) all over-relaxed; accept 1."""
+    s = np.array(s_old, dtype=np.float64)
+    nr = (mm.L + 1) ** 2
+    v = _v_given_s(mm, s, draws.pixel_normals(mm.F, mm.Npix, maps=mm.rows, substep=SUB_V_INIT))
+    for k in range(n_gibbs):
+        s = _s_given_v(mm, dl_unbinned, v, draws.slot_normals(mm.F, nr, substep=SUB_S + 2 * k), s_old=s, alpha=alpha)
+        v = _v_given_s(mm, s, draws.pixel_normals(mm.F, mm.Npix, maps=mm.rows, substep=k), v_old=v, alpha=alpha)
+        s = _s_given_v(mm, dl_unbinned, v, draws.slot_normals(mm.F, nr, substep=SUB_S + 2 * k + 1), s_old=s,
+                       alpha=alpha)
+    return s, 1
+
+
+# ----------------------------------------------------------------------------
+# a11: MALA (EB, CenteredGibbs.py:494-603)
+# ----------------------------------------------------------------------------
+def mala_sigma(mm, dl_unbinned, noise_pol0):
+    """sigma = 1/((Npix/(noise_pol[0] 4pi)) b^2 + C^-1) per slot (571-572)."""
+    var = H.var_from_dl(dl_unbinned)
+    ell = mm.slot_ell
+    return np.stack([1.0 / ((mm.Npix / (noise_pol0 * FOURPI)) * mm.bl[ell] ** 2 + H.inv_var(var[k][ell]))
+                     for k in range(mm.F)])
+
+
+def mala_gradient(mm, dl_unbinned, s, g2):
+    """grad = -C^-1 s - b A^T N^-1 A b s + b A^T N^-1 d; also returns A b s."""
+    var = H.var_from_dl(dl_unbinned)
+    ell = mm.slot_ell
+    pix = mm.synth(s)
+    nq = np.stack([mm.inv_noise[r] * pix[k] for k, r in enumerate(mm.rows)])
+    second = -(mm.analysis(nq) / mm.w) * mm.bl[ell][None]
+    first = -np.stack([H.inv_var(var[k][ell]) * s[k] for k in range(mm.F)])
+    return first + second + g2, pix
+
+
+def mala_log_density(mm, dl_unbinned, s, pix, g2):
+    var = H.var_from_dl(dl_unbinned)
+    ell = mm.slot_ell
+    t1 = sum(-0.5 * np.sum(H.inv_var(var[k][ell]) * s[k] ** 2) for k in range(mm.F))
+    t2 = sum(-0.5 * np.sum(pix[k] ** 2 * mm.inv_noise[r]) for k, r in enumerate(mm.rows))
+    return t1 + t2 + float(np.sum(s * g2))
+
+
+def mala_log_proposal(s_new, s_old, grad_old, sigma, tau):
+    return float(np.sum(-0.5 * (s_new - s_old - tau * sigma * grad_old) ** 2 / (2 * tau * sigma)))
+
+
+def mala(mm, dl_unbinned, s_old, draws, noise_pol0, tau=0.02, call=0):
+    """sample_mala: one proposal, accept/reject; returns (s, accept, log_ratio)."""
+    s_old = np.array(s_old, dtype=np.float64)
+    g2 = mm.second_part_grad()
+    sigma = mala_sigma(mm, dl_unbinned, noise_pol0)
+    grad_old, pix_old = mala_gradient(mm, dl_unbinned, s_old, g2)
+    z = draws.slot_normals(mm.F, (mm.L + 1) ** 2, substep=SUB_MALA + call)
+    s_new = s_old + tau * sigma * grad_old + np.sqrt(2 * tau * sigma) * z
+    grad_new, pix_new = mala_gradient(mm, dl_unbinned, s_new, g2)
+    lr = (mala_log_density(mm, dl_unbinned, s_new, pix_new, g2) + mala_log_proposal(s_old, s_new, grad_new, sigma, tau)
+          - (mala_log_density(mm, dl_unbinned, s_old, pix_old, g2)
+             + mala_log_proposal(s_new, s_old, grad_old, sigma, tau)))
+    u = draws.uniform(substep=call)
+    if math.log(u) < lr:
+        return s_new, 1, lr
+    return s_old, 0, lr
+
+
+def sample_dispatch(mm, dl_unbinned, s_old, draws, gibbs_cr, overrelaxation_flag, ula, n_gibbs, noise_pol0,
+                    alpha=-0.995, tau=0.02):
+    """CenteredGibbs.py:828-850 for a masked run with a previous map."""
+    if gibbs_cr and overrelaxation_flag:
+        return overrelaxation(mm, dl_unbinned, s_old, n_gibbs, draws, alpha)
+    if gibbs_cr and not ula:
+        return aux_variable(mm, dl_unbinned, s_old, n_gibbs, draws)
+    if gibbs_cr and ula:
+        s_mid, _ = aux_variable(mm, dl_unbinned, s_old, n_gibbs, draws)
+        s, acc, _ = mala(mm, dl_unbinned, s_mid, draws, noise_pol0, tau)
+        return s, acc
+    if ula:
+        s, acc, _ = mala(mm, dl_unbinned, s_old, draws, noise_pol0, tau)
+        return s, acc
+    raise NotImplementedError("PCG CR (sample_mask, qcinv) is SURVEY.md 8 row f1")
