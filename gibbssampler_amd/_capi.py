@@ -18,6 +18,7 @@ GS_QUIRK_ASIS_RECENTRE_CENTERED = 1
 GS_NPARAM = 10
 GS_ALM_REAL = 0
 GS_ALM_COMPLEX = 1
+GS_MCR_AUX, GS_MCR_OVERRELAX, GS_MCR_MALA, GS_MCR_AUX_MALA = 0, 1, 2, 3
 NSTAT = {1: 2, 2: 4, 3: 8}
 
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -40,6 +41,19 @@ class GsModelDesc(ctypes.Structure):
         ("blocks", c_int_p * 4),
         ("nblock_edges", ctypes.c_int * 4),
         ("prop_var", c_double_p * 4),
+    ]
+
+
+class GsMaskedDesc(ctypes.Structure):
+    _fields_ = [
+        ("lmax", ctypes.c_int),
+        ("nside", ctypes.c_int),
+        ("nfields", ctypes.c_int),
+        ("bl", c_double_p),
+        ("n_gibbs", ctypes.c_int),
+        ("alpha", ctypes.c_double),
+        ("tau", ctypes.c_double),
+        ("noise_pol0", ctypes.c_double),
     ]
 
 
@@ -87,6 +101,12 @@ _SIGS = [
                                    ctypes.POINTER(ctypes.c_longlong)]),
     ("gs_sht_alm2map", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_sht_map2alm", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP]),
+    ("gs_masked_create", ctypes.c_int, [ctypes.POINTER(GsMaskedDesc), _VP, _VP, ctypes.POINTER(_VP)]),
+    ("gs_masked_destroy", ctypes.c_int, [_VP]),
+    ("gs_masked_info", ctypes.c_int, [_VP, c_double_p, _VP]),
+    ("gs_masked_gradient", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+    ("gs_masked_cr", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,
+                                    ctypes.c_uint32, ctypes.c_int, _VP, _VP, _VP]),
 ]
 
 EXPORTED = [n for n, _, _ in _SIGS]

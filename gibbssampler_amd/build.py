@@ -4,8 +4,9 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", "gs_kernels.hip"), os.path.join(HERE, "csrc", "gs_sht.hip")]
-HEADERS = [os.path.join(HERE, "csrc", h) for h in ("gs_rng.h", "gs_common.h", "gs_bm_tables.h")] + \
+SOURCES = [os.path.join(HERE, "csrc", "gs_kernels.hip"), os.path.join(HERE, "csrc", "gs_sht.hip"),
+           os.path.join(HERE, "csrc", "gs_masked.hip")]
+HEADERS = [os.path.join(HERE, "csrc", h) for h in ("gs_rng.h", "gs_common.h", "gs_bm_tables.h", "gs_block.h")] + \
     [os.path.join(ROOT, "include", "gibbs_capi.h")]
 LIB = os.path.join(HERE, "libgibbs_hip.so")
 ARCH = os.environ.get("GIBBS_OFFLOAD_ARCH", "gfx950")

@@ -1,0 +1,565 @@
+// gs_masked.hip -- masked (pixel-domain) constrained-realization steps on gfx950.
+//
+// Device versions of the reference's masked CR samplers (EB class
+// PolarizedCenteredConstrainedRealization, CenteredGibbs.py:241-850), TEB
+// generalised for the auxiliary-variable scheme:
+//   a9  sample_gibbs_change_variable   CenteredGibbs.py:676-729
+//   a10 overrelaxation_sampler         CenteredGibbs.py:733-825
+//   a11 sample_mala (+ gradient, log density, log proposal) 494-603
+//   a12 the dispatch ladder of sample  CenteredGibbs.py:828-850
+// One chain per call; the HEALPix SHTs run through gs_sht (gs_sht.hip); every
+// pixel- and slot-wise step is one fused kernel; the MALA accept test reduces
+// its eight sums in a fixed order (bitwise reproducible).
+//
+// Per-pixel arrays are [F][Npix] over the field rows (F = 2: Q, U; F = 3:
+// T, Q, U); a_lm are real m-major [F][(L+1)^2].  Native draws: pixel normals
+// Philox(c0 = pixel, c1 = map row (0 T, 1 Q, 2 U), c2 = TAG_AUX_V | sub << 8,
+// c3 = iteration); slot normals are the CR stream of the full-sky sweep with
+// substep SUB_S + 2k (+1 for the second over-relaxed s draw) or SUB_MALA;
+// the MALA uniform is Philox(0, call, TAG_MALA_U, iteration).  The same
+// streams are restated in oracle/masked.py (NativeDraws).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "gibbs_capi.h"
+#include "gs_rng.h"
+#include "gs_common.h"
+#include "gs_block.h"
+
+using namespace gs;
+using gs_detail::set_error;
+
+namespace {
+
+constexpr double PI = 3.14159265358979323846;
+constexpr uint32_t TAG_AUX_V = 8;
+constexpr uint32_t TAG_MALA_U = 9;
+constexpr int SUB_S = 16;
+constexpr int SUB_V_INIT = 255;
+constexpr int SUB_MALA = 200;
+constexpr int NSUM = 8;
+constexpr int RED_BLOCK = 256;
+
+inline unsigned nblocks(long long n, int bs) { return (unsigned)std::max<long long>(1, (n + bs - 1) / bs); }
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+struct Rows { int r[3]; };
+
+// (l, m) of complex index i (healpy m-major)
+__device__ __forceinline__ void cidx_lm(int L, long long i, int& l, int& m) {
+    const double b = 2.0 * L + 3.0;
+    m = (int)floor((b - sqrt(fmax(b * b - 8.0 * (double)i, 0.0))) / 2.0);
+    m = max(0, min(m, L));
+    while (m > 0 && (long long)m * (2 * L + 3 - m) / 2 > i) --m;
+    while (m < L && (long long)(m + 1) * (2 * L + 2 - m) / 2 <= i) ++m;
+    l = (int)(i - (long long)m * (2 * L + 1 - m) / 2);
+}
+
+// x = b_l s (real layout, per field)
+__global__ void k_mc_beam(int L, int F, const double* __restrict__ bl, const double* __restrict__ s,
+                          double* __restrict__ x) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= F * nlm) return;
+    const int f = (int)(g / nlm);
+    const long long i = g % nlm;
+    int l, m;
+    cidx_lm(L, i, l, m);
+    const double b = bl[l];
+    if (m == 0) { x[f * NR + l] = b * s[f * NR + l]; return; }
+    const long long r = 2 * i - (L + 1);
+    x[f * NR + r] = b * s[f * NR + r];
+    x[f * NR + r + 1] = b * s[f * NR + r + 1];
+}
+
+// v | s (CenteredGibbs.py:693-700; over-relaxed 797-802) and the s | v input
+// y = v + N^-1 d (711-713), per pixel and field row
+__global__ void k_mc_v(long long npix, int F, Rows rows, int over, double alpha, const double* __restrict__ Abs,
+                       const double* __restrict__ ninv, const double* __restrict__ dpix, double mu0, double mu1,
+                       double mu2, const double* __restrict__ zv, uint32_t seed_lo, uint32_t seed_hi, uint32_t chain,
+                       uint32_t sub, uint32_t iter, double* __restrict__ v, double* __restrict__ y) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= F * npix) return;
+    const int k = (int)(g / npix);
+    const long long p = g % npix;
+    const int row = rows.r[k];
+    const double mu = row == 0 ? mu0 : (row == 1 ? mu1 : mu2);
+    const double ni = ninv[g];
+    const double gam = mu - ni;
+    const double mean = gam * Abs[g];
+    double z;
+    if (zv) z = zv[g];
+    else z = normal1(chain_key(seed_lo, seed_hi, chain), (uint32_t)p, (uint32_t)row, TAG_AUX_V | (sub << 8), iter);
+    double vn;
+    if (!over) vn = z * sqrt(gam) + mean;
+    else vn = mean + alpha * (v[g] - mean) + sqrt(1.0 - alpha * alpha) * z * sqrt(gam);
+    v[g] = vn;
+    y[g] = vn + ni * dpix[g];
+}
+
+__device__ __forceinline__ void slot_normals(const double* __restrict__ zs, long long NR, int F, long long r, int nv,
+                                             Key key, long long i, uint32_t sub, uint32_t iter, double (&z)[3][2]) {
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        if (f >= F) break;
+        if (zs) {
+            z[f][0] = zs[f * NR + r];
+            z[f][1] = nv == 2 ? zs[f * NR + r + 1] : 0.0;
+        } else {
+            box_muller(philox((uint32_t)i, (uint32_t)f, TAG_CR | (sub << 8), iter, key), z[f][0], z[f][1]);
+        }
+    }
+}
+
+// s | v (CenteredGibbs.py:703-726; over-relaxed 778-781): per slot
+// s = mean + L z with mean = M d_eff, d_eff = complex_to_real(map2alm(y)) / mu_f,
+// (M, L) the centered per-l block for kappa_f = mu_f / w; over-relaxed
+// s' = mean + alpha (s - mean) + sqrt(1 - alpha^2) L z
+template <int F>
+__global__ void k_mc_s(int L, const double* __restrict__ params, const double* __restrict__ r_alm, double imu0,
+                       double imu1, double imu2, const double* __restrict__ zs, uint32_t seed_lo, uint32_t seed_hi,
+                       uint32_t chain, uint32_t sub, uint32_t iter, int over, double alpha, double* __restrict__ s) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= nlm) return;
+    int l, m;
+    cidx_lm(L, i, l, m);
+    const long long r = m == 0 ? l : 2 * i - (L + 1);
+    const int nv = m == 0 ? 1 : 2;
+    const double* p = params + (long long)l * GS_NPARAM;
+    const double imu[3] = {imu0, imu1, imu2};
+    double z[3][2];
+    slot_normals(zs, NR, F, r, nv, chain_key(seed_lo, seed_hi, chain), i, sub, iter, z);
+    const double c1 = sqrt(1.0 - alpha * alpha);
+    for (int c = 0; c < nv; ++c) {
+        double d[3], mean[3], fl[3];
+#pragma unroll
+        for (int f = 0; f < F; ++f) d[f] = r_alm[f * NR + r + c] * imu[f];
+        if constexpr (F != 3) {
+#pragma unroll
+            for (int f = 0; f < F; ++f) { mean[f] = p[f] * d[f]; fl[f] = p[F + f] * z[f][c]; }
+        } else {
+            mean[0] = p[0] * d[0] + p[1] * d[1];
+            mean[1] = p[2] * d[0] + p[3] * d[1];
+            mean[2] = p[4] * d[2];
+            fl[0] = p[5] * z[0][c];
+            fl[1] = p[6] * z[0][c] + p[7] * z[1][c];
+            fl[2] = p[8] * z[2][c];
+        }
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            double* sp = s + f * NR + r + c;
+            *sp = over ? mean[f] + alpha * (*sp - mean[f]) + c1 * fl[f] : fl[f] + mean[f];
+        }
+    }
+}
+
+__global__ void k_set_one(int32_t* a) { *a = 1; }
+
+__global__ void k_mc_mul(long long n, const double* __restrict__ a, const double* __restrict__ b,
+                         double* __restrict__ out) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g < n) out[g] = a[g] * b[g];
+}
+
+// per-slot inverse prior variance (zero-variance rule) of field f at l (EB)
+__device__ __forceinline__ double inv_prior(const double* __restrict__ dl, int L, int f, int l) {
+    const double v = var_from_dl(dl[f * (L + 1) + l], l);
+    return v != 0.0 ? 1.0 / v : 0.0;
+}
+
+// grad = -C^+ s - (b / w) r + g2,  r = complex_to_real(map2alm(N^-1 A b s))  (494-520)
+__global__ void k_mc_grad(int L, int F, const double* __restrict__ dl, const double* __restrict__ bl,
+                          const double* __restrict__ s, const double* __restrict__ r_alm, const double* __restrict__ g2,
+                          double inv_w, double* __restrict__ grad) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= F * nlm) return;
+    const int f = (int)(g / nlm);
+    const long long i = g % nlm;
+    int l, m;
+    cidx_lm(L, i, l, m);
+    const long long r = m == 0 ? l : 2 * i - (L + 1);
+    const int nv = m == 0 ? 1 : 2;
+    const double ip = inv_prior(dl, L, f, l);
+    for (int c = 0; c < nv; ++c) {
+        const long long o = f * NR + r + c;
+        grad[o] = -ip * s[o] + -(r_alm[o] * inv_w * bl[l]) + g2[o];
+    }
+}
+
+// s_new = s + tau sigma grad + sqrt(2 tau sigma) z  (523-527), sigma = p[F+f]^2
+__global__ void k_mc_propose(int L, int F, const double* __restrict__ params, const double* __restrict__ s,
+                             const double* __restrict__ grad, double tau, const double* __restrict__ zm,
+                             uint32_t seed_lo, uint32_t seed_hi, uint32_t chain, uint32_t sub, uint32_t iter,
+                             double* __restrict__ snew) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= nlm) return;
+    int l, m;
+    cidx_lm(L, i, l, m);
+    const long long r = m == 0 ? l : 2 * i - (L + 1);
+    const int nv = m == 0 ? 1 : 2;
+    double z[3][2];
+    slot_normals(zm, NR, F, r, nv, chain_key(seed_lo, seed_hi, chain), i, sub, iter, z);
+    for (int f = 0; f < F; ++f) {
+        const double sq = params[(long long)l * GS_NPARAM + F + f];
+        const double sig = sq * sq;
+        for (int c = 0; c < nv; ++c) {
+            const long long o = f * NR + r + c;
+            snew[o] = s[o] + tau * sig * grad[o] + sqrt(2.0 * tau * sig) * z[f][c];
+        }
+    }
+}
+
+// MALA sums (fixed-order partials per block):
+//  0: sum C^+ s0^2   1: sum C^+ s1^2   2: s0 . g2   3: s1 . g2
+//  4: sum (s0 - s1 - tau sig g1)^2 / (2 tau sig)   5: sum (s1 - s0 - tau sig g0)^2 / (2 tau sig)
+//  6: sum N^-1 pix0^2   7: sum N^-1 pix1^2
+__global__ __launch_bounds__(RED_BLOCK) void k_mc_sums(int L, int F, long long npix, const double* __restrict__ dl,
+                                                       const double* __restrict__ params, double tau,
+                                                       const double* __restrict__ s0, const double* __restrict__ s1,
+                                                       const double* __restrict__ g0, const double* __restrict__ g1,
+                                                       const double* __restrict__ g2, const double* __restrict__ ninv,
+                                                       const double* __restrict__ p0, const double* __restrict__ p1,
+                                                       double* __restrict__ partial) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nslot = F * NR, npx = F * npix;
+    double a[NSUM] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < nslot; g += stride) {
+        const int f = (int)(g / NR);
+        const long long r = g % NR;
+        int l;
+        if (r <= L) l = (int)r;
+        else { int m; cidx_lm(L, (r + L + 1) / 2, l, m); }
+        const double ip = inv_prior(dl, L, f, l);
+        const double sq = params[(long long)l * GS_NPARAM + F + f];
+        const double ts = tau * (sq * sq);
+        const double x0 = s0[g], x1 = s1[g];
+        a[0] += ip * x0 * x0;
+        a[1] += ip * x1 * x1;
+        a[2] += x0 * g2[g];
+        a[3] += x1 * g2[g];
+        const double e01 = x0 - x1 - ts * g1[g];
+        const double e10 = x1 - x0 - ts * g0[g];
+        a[4] += e01 * e01 / (2.0 * ts);
+        a[5] += e10 * e10 / (2.0 * ts);
+    }
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < npx; g += stride) {
+        const double q0 = p0[g], q1 = p1[g];
+        a[6] += q0 * q0 * ninv[g];
+        a[7] += q1 * q1 * ninv[g];
+    }
+    __shared__ double red[NSUM][RED_BLOCK];
+#pragma unroll
+    for (int k = 0; k < NSUM; ++k) red[k][threadIdx.x] = a[k];
+    __syncthreads();
+    for (int h = RED_BLOCK / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h)
+#pragma unroll
+            for (int k = 0; k < NSUM; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x < NSUM) partial[blockIdx.x * NSUM + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// accept with log u < log pi(s1) + log q(s0|s1) - log pi(s0) - log q(s1|s0) (577-603)
+__global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long long nslot, const double* __restrict__ um,
+                            uint32_t seed_lo, uint32_t seed_hi, uint32_t chain, uint32_t call, uint32_t iter,
+                            const double* __restrict__ s1, double* __restrict__ s0, int32_t* __restrict__ accept,
+                            double* __restrict__ log_ratio) {
+    __shared__ int acc;
+    if (threadIdx.x == 0) {
+        double t[NSUM];
+        for (int k = 0; k < NSUM; ++k) {
+            double v = 0.0;
+            for (int b = 0; b < nblk; ++b) v += partial[b * NSUM + k];
+            t[k] = v;
+        }
+        const double lp1 = -0.5 * t[1] + -0.5 * t[7] + t[3];
+        const double lp0 = -0.5 * t[0] + -0.5 * t[6] + t[2];
+        const double lr = lp1 + (-0.5 * t[4]) - (lp0 + (-0.5 * t[5]));
+        const double u = um ? um[0] : uniform1(chain_key(seed_lo, seed_hi, chain), 0u, call, TAG_MALA_U, iter);
+        acc = log(u) < lr ? 1 : 0;
+        if (accept) *accept = acc;
+        if (log_ratio) *log_ratio = lr;
+    }
+    __syncthreads();
+    if (acc)
+        for (long long g = threadIdx.x; g < nslot; g += blockDim.x) s0[g] = s1[g];
+}
+
+}  // namespace
+
+// ============================================================================
+// context
+// ============================================================================
+struct gs_masked {
+    int L = 0, nside = 0, F = 0, n_gibbs = 1, nblk = 0;
+    long long npix = 0, NR = 0, nlm = 0;
+    double w = 0, alpha = -0.995, tau = 0.02, noise_pol0 = 1.0;
+    double mu[3] = {0, 0, 0};
+    Rows rows{{1, 2, 0}};
+    gs_sht* sht = nullptr;
+    double *bl = nullptr, *dpix = nullptr, *ninv = nullptr, *g2 = nullptr;
+    double *params = nullptr, *params_mala = nullptr;
+    int* ell2bin = nullptr;
+    double *x = nullptr, *Abs = nullptr, *y = nullptr, *r = nullptr;
+    double *grad0 = nullptr, *grad1 = nullptr, *snew = nullptr, *pix0 = nullptr, *pix1 = nullptr, *vtmp = nullptr;
+    double *partial = nullptr, *lr = nullptr;
+};
+
+namespace {
+
+void mc_free(gs_masked* c) {
+    if (c->sht) gs_sht_destroy(c->sht);
+    double* bufs[] = {c->bl, c->dpix, c->ninv, c->g2, c->params, c->params_mala, c->x, c->Abs, c->y, c->r,
+                      c->grad0, c->grad1, c->snew, c->pix0, c->pix1, c->vtmp, c->partial, c->lr};
+    for (double* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->ell2bin) (void)hipFree(c->ell2bin);
+    delete c;
+}
+
+template <typename T>
+int mc_alloc(T** p, size_t n) {
+    GS_CHECK(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+    GS_CHECK(hipMemset(*p, 0, std::max<size_t>(n, 1) * sizeof(T)));
+    return 0;
+}
+
+// centered per-l blocks of a plan-less model: kappa_f for unbinned D_l [nspec][L+1]
+template <int F>
+__global__ void k_mc_params(int L, const double* __restrict__ dl, const int* __restrict__ ell2bin,
+                            const double* __restrict__ bl, double k0, double k1, double k2, double* __restrict__ params) {
+    block_params_at<F, GS_MODE_CENTERED>(blockIdx.x * blockDim.x + threadIdx.x, L, 1, L + 1, dl, ell2bin, bl, k0, k1,
+                                         k2, params);
+}
+
+int mc_params(gs_masked* c, const double* dl, const double* kap, double* out, hipStream_t st) {
+    const dim3 g(nblocks(c->L + 1, 256)), b(256);
+    if (c->F == 2)
+        hipLaunchKernelGGL(k_mc_params<2>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
+    else
+        hipLaunchKernelGGL(k_mc_params<3>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
+    GS_LAUNCH_CHECK("k_mc_params");
+    return 0;
+}
+
+// maps of b s  -> Abs
+int mc_synth(gs_masked* c, const double* s, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_mc_beam, dim3(nblocks(c->F * c->nlm, 256)), dim3(256), 0, st, c->L, c->F, c->bl, s, c->x);
+    GS_LAUNCH_CHECK("k_mc_beam");
+    return gs_sht_alm2map(c->sht, c->F, GS_ALM_REAL, c->x, out, st);
+}
+
+// one v | s then s | v pass (plain or over-relaxed)
+int mc_v(gs_masked* c, int over, const double* s, double* v, const double* zv, uint32_t slo, uint32_t shi,
+         uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
+    if (mc_synth(c, s, c->Abs, st)) return -1;
+    hipLaunchKernelGGL(k_mc_v, dim3(nblocks(c->F * c->npix, 256)), dim3(256), 0, st, c->npix, c->F, c->rows, over,
+                       c->alpha, c->Abs, c->ninv, c->dpix, c->mu[0], c->mu[1], c->mu[2], zv, slo, shi, chain, sub, it,
+                       v, c->y);
+    GS_LAUNCH_CHECK("k_mc_v");
+    return 0;
+}
+
+int mc_s(gs_masked* c, int over, double* s, const double* zs, uint32_t slo, uint32_t shi, uint32_t chain,
+         uint32_t sub, uint32_t it, hipStream_t st) {
+    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
+    double imu[3] = {0, 0, 0};
+    for (int k = 0; k < c->F; ++k) imu[k] = 1.0 / c->mu[c->rows.r[k]];
+    const dim3 g(nblocks(c->nlm, 256)), b(256);
+    if (c->F == 2)
+        hipLaunchKernelGGL(k_mc_s<2>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, slo, shi, chain,
+                           sub, it, over, c->alpha, s);
+    else
+        hipLaunchKernelGGL(k_mc_s<3>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, slo, shi, chain,
+                           sub, it, over, c->alpha, s);
+    GS_LAUNCH_CHECK("k_mc_s");
+    return 0;
+}
+
+int mc_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, hipStream_t st) {
+    if (mc_synth(c, s, pix, st)) return -1;
+    const long long n = c->F * c->npix;
+    hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->ninv, pix, c->y);
+    GS_LAUNCH_CHECK("k_mc_mul");
+    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
+    hipLaunchKernelGGL(k_mc_grad, dim3(nblocks(c->F * c->nlm, 256)), dim3(256), 0, st, c->L, c->F, dl, c->bl, s, c->r,
+                       c->g2, 1.0 / c->w, grad);
+    GS_LAUNCH_CHECK("k_mc_grad");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_masked_create(const gs_masked_desc* desc, const double* maps, const double* inv_noise, gs_masked** out) {
+    if (!desc || !maps || !inv_noise || !out) return set_error("gs_masked_create: null argument");
+    *out = nullptr;
+    if (desc->nfields != 2 && desc->nfields != 3) return set_error("gs_masked_create: nfields must be 2 (EB) or 3 (TEB)");
+    if (!desc->bl) return set_error("gs_masked_create: null beam");
+    gs_masked* c = new gs_masked();
+    c->L = desc->lmax; c->nside = desc->nside; c->F = desc->nfields;
+    c->n_gibbs = std::max(1, desc->n_gibbs);
+    c->alpha = desc->alpha; c->tau = desc->tau; c->noise_pol0 = desc->noise_pol0;
+    c->npix = 12LL * c->nside * c->nside;
+    c->NR = (long long)(c->L + 1) * (c->L + 1);
+    c->nlm = (long long)(c->L + 1) * (c->L + 2) / 2;
+    c->w = 4.0 * PI / (double)c->npix;
+    c->rows = c->F == 2 ? Rows{{1, 2, 0}} : Rows{{0, 1, 2}};
+    c->nblk = (int)std::min<long long>(512, nblocks(std::max(c->F * c->NR, c->F * c->npix), RED_BLOCK));
+    if (gs_sht_create(c->nside, c->L, &c->sht)) { mc_free(c); return -1; }
+    const long long FR = c->F * c->NR, FP = c->F * c->npix;
+    int rc = 0;
+    rc |= mc_alloc(&c->bl, c->L + 1);
+    rc |= mc_alloc(&c->dpix, FP);
+    rc |= mc_alloc(&c->ninv, FP);
+    rc |= mc_alloc(&c->g2, FR);
+    rc |= mc_alloc(&c->params, (size_t)(c->L + 1) * GS_NPARAM);
+    rc |= mc_alloc(&c->params_mala, (size_t)(c->L + 1) * GS_NPARAM);
+    rc |= mc_alloc(&c->ell2bin, (size_t)4 * (c->L + 1));
+    rc |= mc_alloc(&c->x, FR);
+    rc |= mc_alloc(&c->Abs, FP);
+    rc |= mc_alloc(&c->y, FP);
+    rc |= mc_alloc(&c->r, FR);
+    rc |= mc_alloc(&c->grad0, FR);
+    rc |= mc_alloc(&c->grad1, FR);
+    rc |= mc_alloc(&c->snew, FR);
+    rc |= mc_alloc(&c->pix0, FP);
+    rc |= mc_alloc(&c->pix1, FP);
+    rc |= mc_alloc(&c->vtmp, FP);
+    rc |= mc_alloc(&c->partial, (size_t)c->nblk * NSUM);
+    rc |= mc_alloc(&c->lr, 1);
+    if (rc) { mc_free(c); return -1; }
+    std::vector<int> e2b((size_t)4 * (c->L + 1));
+    for (int sp = 0; sp < 4; ++sp)
+        for (int l = 0; l <= c->L; ++l) e2b[(size_t)sp * (c->L + 1) + l] = l;
+    // field rows of the caller's [3][Npix] maps; mu = max(N^-1) + 1e-14 (CenteredGibbs.py:276)
+    std::vector<double> host((size_t)c->npix);
+    bool ok = hipMemcpy(c->bl, desc->bl, (c->L + 1) * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(c->ell2bin, e2b.data(), e2b.size() * sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+    for (int k = 0; ok && k < c->F; ++k) {
+        const int row = c->rows.r[k];
+        ok = hipMemcpy(c->dpix + k * c->npix, maps + row * c->npix, c->npix * sizeof(double),
+                       hipMemcpyDeviceToDevice) == hipSuccess &&
+             hipMemcpy(c->ninv + k * c->npix, inv_noise + row * c->npix, c->npix * sizeof(double),
+                       hipMemcpyDeviceToDevice) == hipSuccess &&
+             hipMemcpy(host.data(), inv_noise + row * c->npix, c->npix * sizeof(double), hipMemcpyDeviceToHost) ==
+                 hipSuccess;
+        if (ok) c->mu[row] = *std::max_element(host.begin(), host.end()) + 1e-14;
+    }
+    if (!ok) { mc_free(c); return set_error("gs_masked_create: copy failed"); }
+    // second_part_grad = b * complex_to_real(map2alm(N^-1 d)) * Npix/(4 pi)  (CenteredGibbs.py:298-306)
+    const long long n = c->F * c->npix;
+    hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, 0, n, c->ninv, c->dpix, c->y);
+    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, nullptr)) { mc_free(c); return -1; }
+    hipLaunchKernelGGL(k_mc_beam, dim3(nblocks(c->F * c->nlm, 256)), dim3(256), 0, 0, c->L, c->F, c->bl, c->r, c->g2);
+    const long long nr = c->F * c->NR;
+    std::vector<double> g2h((size_t)nr);
+    if (hipMemcpy(g2h.data(), c->g2, nr * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+        mc_free(c);
+        return set_error("gs_masked_create: setup failed");
+    }
+    const double resc = (double)c->npix / (4.0 * PI);
+    for (auto& v : g2h) v *= resc;
+    if (hipMemcpy(c->g2, g2h.data(), nr * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+        mc_free(c);
+        return set_error("gs_masked_create: setup failed");
+    }
+    *out = c;
+    return 0;
+}
+
+int gs_masked_destroy(gs_masked* c) {
+    if (c) mc_free(c);
+    return 0;
+}
+
+int gs_masked_info(const gs_masked* c, double* mu3, double* second_part_grad) {
+    if (!c) return set_error("null masked context");
+    if (mu3)
+        for (int k = 0; k < 3; ++k) mu3[k] = c->mu[k];
+    if (second_part_grad)
+        GS_CHECK(hipMemcpy(second_part_grad, c->g2, c->F * c->NR * sizeof(double), hipMemcpyDeviceToDevice));
+    return 0;
+}
+
+int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, void* stream) {
+    if (!c) return set_error("null masked context");
+    return mc_gradient(c, dl, s, grad, pix, S(stream));
+}
+
+int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v, const double* zv, const double* zs,
+                 const double* zm, const double* um, uint64_t seed, uint32_t iteration, int chain, int32_t* accept,
+                 double* log_ratio, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (!dl || !s) return set_error("gs_masked_cr: null argument");
+    if (kind < GS_MCR_AUX || kind > GS_MCR_AUX_MALA) return set_error("gs_masked_cr: bad kind");
+    if ((kind == GS_MCR_MALA || kind == GS_MCR_AUX_MALA) && c->F != 2)
+        return set_error("gs_masked_cr: MALA is defined for the EB model only (CenteredGibbs.py:560-603)");
+    const hipStream_t st = S(stream);
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32), ch = (uint32_t)chain;
+    const long long FP = c->F * c->npix, FR = c->F * c->NR;
+    double* vv = v ? v : c->vtmp;
+    if (kind != GS_MCR_MALA) {
+        const double kap[3] = {c->mu[c->rows.r[0]] / c->w, c->mu[c->rows.r[1]] / c->w,
+                               c->F == 3 ? c->mu[c->rows.r[2]] / c->w : 0.0};
+        if (mc_params(c, dl, kap, c->params, st)) return -1;
+        if (kind == GS_MCR_OVERRELAX) {
+            // v | s plain, then n_gibbs x (s | v, v | s, s | v) over-relaxed
+            if (mc_v(c, 0, s, vv, zv, slo, shi, ch, SUB_V_INIT, iteration, st)) return -1;
+            for (int k = 0; k < c->n_gibbs; ++k) {
+                const double* zs1 = zs ? zs + (2LL * k) * FR : nullptr;
+                const double* zs2 = zs ? zs + (2LL * k + 1) * FR : nullptr;
+                const double* zvk = zv ? zv + (1LL + k) * FP : nullptr;
+                if (mc_s(c, 1, s, zs1, slo, shi, ch, SUB_S + 2 * k, iteration, st)) return -1;
+                if (mc_v(c, 1, s, vv, zvk, slo, shi, ch, k, iteration, st)) return -1;
+                if (mc_s(c, 1, s, zs2, slo, shi, ch, SUB_S + 2 * k + 1, iteration, st)) return -1;
+            }
+        } else {
+            for (int k = 0; k < c->n_gibbs; ++k) {
+                if (mc_v(c, 0, s, vv, zv ? zv + k * FP : nullptr, slo, shi, ch, k, iteration, st)) return -1;
+                if (mc_s(c, 0, s, zs ? zs + k * FR : nullptr, slo, shi, ch, SUB_S + 2 * k, iteration, st)) return -1;
+            }
+        }
+        if (kind != GS_MCR_AUX_MALA) {
+            // the auxiliary-variable samplers always accept (CenteredGibbs.py:729,825)
+            if (accept) {
+                hipLaunchKernelGGL(k_set_one, dim3(1), dim3(1), 0, st, accept);
+                GS_LAUNCH_CHECK("k_set_one");
+            }
+            return 0;
+        }
+    }
+    // MALA (CenteredGibbs.py:560-603): sigma from the full-sky kappa of noise_pol[0]
+    const double km = (double)c->npix / (4.0 * PI * c->noise_pol0);
+    const double kapm[3] = {km, km, km};
+    if (mc_params(c, dl, kapm, c->params_mala, st)) return -1;
+    if (mc_gradient(c, dl, s, c->grad0, c->pix0, st)) return -1;
+    const uint32_t call = 0;
+    hipLaunchKernelGGL(k_mc_propose, dim3(nblocks(c->nlm, 256)), dim3(256), 0, st, c->L, c->F, c->params_mala, s,
+                       c->grad0, c->tau, zm, slo, shi, ch, (uint32_t)(SUB_MALA + call), iteration, c->snew);
+    GS_LAUNCH_CHECK("k_mc_propose");
+    if (mc_gradient(c, dl, c->snew, c->grad1, c->pix1, st)) return -1;
+    hipLaunchKernelGGL(k_mc_sums, dim3(c->nblk), dim3(RED_BLOCK), 0, st, c->L, c->F, c->npix, dl, c->params_mala,
+                       c->tau, s, c->snew, c->grad0, c->grad1, c->g2, c->ninv, c->pix0, c->pix1, c->partial);
+    GS_LAUNCH_CHECK("k_mc_sums");
+    hipLaunchKernelGGL(k_mc_accept, dim3(1), dim3(256), 0, st, c->nblk, c->partial, FR, um, slo, shi, ch, call,
+                       iteration, c->snew, s, accept, log_ratio ? log_ratio : c->lr);
+    GS_LAUNCH_CHECK("k_mc_accept");
+    return 0;
+}
+
+}  // extern "C"

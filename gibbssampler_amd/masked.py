@@ -1,0 +1,183 @@
+"""Masked (pixel-domain) constrained realisation on the GPU: the reference's
+PolarizedCenteredConstrainedRealization masked samplers (CenteredGibbs.py:241-850).
+
+``MaskedCR`` keeps the reference's method names and return conventions
+(dict of real-layout arrays, accept flag) so a caller of the reference finds
+the same surface:
+
+  sample_gibbs_change_variable(all_dls, s_old)   a9   CenteredGibbs.py:676-729
+  overrelaxation_sampler(all_dls, s_old)         a10  CenteredGibbs.py:733-825
+  sample_mala(all_dls, s_old)                    a11  CenteredGibbs.py:560-603
+  compute_gradient_mala(all_dls, s_old)               CenteredGibbs.py:494-520
+  sample(all_dls, s_old=None)                    a12  CenteredGibbs.py:828-850
+
+All arithmetic runs in libgibbs_hip.so (gs_masked_cr + gs_sht); this module
+only moves arrays and, in replay mode, draws numpy's legacy global stream in
+the reference's order (A.5 of SURVEY.md) so results match the reference for
+the same ``np.random.seed``.  There is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _capi
+
+FIELDS = {2: ("EE", "BB"), 3: ("TT", "EE", "BB")}
+
+
+class MaskedCR:
+    """pix_map: dict with "Q", "U" (and "T" for nfields = 3) pixel maps;
+    noise_temp / noise_pol: per-pixel noise variances (arrays or scalars);
+    mask: per-pixel mask multiplying N^-1 (CenteredGibbs.py:266-274) or None."""
+
+    def __init__(self, pix_map, noise_temp, noise_pol, bl, lmax, nside, mask=None, nfields=2, gibbs_cr=True,
+                 n_gibbs=1, alpha=-0.995, overrelaxation=False, ula=False, tau=0.02, rng="replay", seed=0, chain=0,
+                 device="cuda"):
+        if nfields not in (2, 3):
+            raise ValueError("nfields must be 2 (EB, the reference) or 3 (TEB)")
+        self.lib = _capi.load()
+        self.L, self.nside, self.F = int(lmax), int(nside), int(nfields)
+        self.Npix = 12 * self.nside ** 2
+        self.NR = (self.L + 1) ** 2
+        self.gibbs_cr, self.overrelaxation, self.ula = bool(gibbs_cr), bool(overrelaxation), bool(ula)
+        self.n_gibbs, self.alpha, self.tau = int(n_gibbs), float(alpha), float(tau)
+        if rng not in ("replay", "native"):
+            raise ValueError(rng)
+        self.rng, self.seed, self.chain = rng, int(seed), int(chain)
+        self.iteration = 0
+        self.device = device
+        npol = np.broadcast_to(np.asarray(noise_pol, dtype=np.float64), (self.Npix,))
+        ntemp = np.broadcast_to(np.asarray(noise_temp, dtype=np.float64), (self.Npix,))
+        m = np.ones(self.Npix) if mask is None else np.asarray(mask, dtype=np.float64)
+        inv = np.stack([m / ntemp, m / npol, m / npol])
+        maps = np.stack([np.asarray(pix_map.get("T", np.zeros(self.Npix)), dtype=np.float64),
+                         np.asarray(pix_map["Q"], dtype=np.float64), np.asarray(pix_map["U"], dtype=np.float64)])
+        self._maps = torch.from_numpy(np.ascontiguousarray(maps)).to(device)
+        self._inv = torch.from_numpy(np.ascontiguousarray(inv)).to(device)
+        self.bl = np.ascontiguousarray(np.asarray(bl, dtype=np.float64)[: self.L + 1])
+        desc = _capi.GsMaskedDesc()
+        desc.lmax, desc.nside, desc.nfields = self.L, self.nside, self.F
+        desc.bl = self.bl.ctypes.data_as(_capi.c_double_p)
+        desc.n_gibbs, desc.alpha, desc.tau, desc.noise_pol0 = self.n_gibbs, self.alpha, self.tau, float(npol[0])
+        h = ctypes.c_void_p()
+        _capi.check(self.lib.gs_masked_create(ctypes.byref(desc), _capi.ptr(self._maps), _capi.ptr(self._inv),
+                                              ctypes.byref(h)), "gs_masked_create")
+        self.handle = h
+        mu = (ctypes.c_double * 3)()
+        _capi.check(self.lib.gs_masked_info(h, mu, None), "gs_masked_info")
+        self.mu = np.array(mu[:])
+        self.v = torch.zeros((self.F, self.Npix), dtype=torch.float64, device=device)
+        self._acc = torch.zeros(1, dtype=torch.int32, device=device)
+        self._lr = torch.zeros(1, dtype=torch.float64, device=device)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self.lib.gs_masked_destroy(h)
+            self.handle = None
+
+    # -- conversions -------------------------------------------------------------------
+    def _dl(self, all_dls):
+        specs = ("EE", "BB") if self.F == 2 else ("TT", "EE", "BB", "TE")
+        arr = np.stack([np.asarray(all_dls[s], dtype=np.float64)[: self.L + 1] for s in specs])
+        return torch.from_numpy(np.ascontiguousarray(arr)).to(self.device)
+
+    def _s(self, s):
+        if isinstance(s, torch.Tensor):
+            return s.to(self.device, torch.float64).contiguous().clone()
+        return torch.from_numpy(np.ascontiguousarray(np.stack([np.asarray(s[k], dtype=np.float64)
+                                                              for k in FIELDS[self.F]]))).to(self.device)
+
+    def _out(self, s):
+        a = s.cpu().numpy()
+        return {k: a[i].copy() for i, k in enumerate(FIELDS[self.F])}
+
+    def second_part_grad(self):
+        out = torch.empty((self.F, self.NR), dtype=torch.float64, device=self.device)
+        _capi.check(self.lib.gs_masked_info(self.handle, None, _capi.ptr(out)), "gs_masked_info")
+        return out
+
+    # -- replay draws (reference order) -----------------------------------
+    def _pix(self, n):
+        return np.stack([np.stack([np.random.normal(size=self.Npix) for _ in range(self.F)]) for _ in range(n)])
+
+    def _slots(self):
+        return np.stack([np.random.normal(size=self.NR) for _ in range(self.F)])
+
+    def _replay(self, kind):
+        zv = zs = zm = um = None
+        if kind == _capi.GS_MCR_AUX or kind == _capi.GS_MCR_AUX_MALA:
+            v, s = [], []
+            for _ in range(self.n_gibbs):
+                v.append(self._pix(1)[0])
+                s.append(self._slots())
+            zv, zs = np.stack(v), np.stack(s)
+        elif kind == _capi.GS_MCR_OVERRELAX:
+            v, s = [self._pix(1)[0]], []
+            for _ in range(self.n_gibbs):
+                s.append(self._slots())
+                v.append(self._pix(1)[0])
+                s.append(self._slots())
+            zv, zs = np.stack(v), np.stack(s)
+        if kind in (_capi.GS_MCR_MALA, _capi.GS_MCR_AUX_MALA):
+            zm = self._slots()
+            um = np.array([np.random.uniform()])
+        dev = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+        return dev(zv), dev(zs), dev(zm), dev(um)
+
+    # -- the device step -------------------------------------------------------------------
+    def step(self, kind, dl, s, iteration=None):
+        """One CR call on device tensors (dl [nspec, L+1] unbinned, s [F, NR] in place)."""
+        it = self.iteration if iteration is None else int(iteration)
+        zv = zs = zm = um = None
+        if self.rng == "replay":
+            zv, zs, zm, um = self._replay(kind)
+        _capi.check(self.lib.gs_masked_cr(self.handle, kind, _capi.ptr(dl), _capi.ptr(s), _capi.ptr(self.v),
+                                          _capi.ptr(zv), _capi.ptr(zs), _capi.ptr(zm), _capi.ptr(um), self.seed, it,
+                                          self.chain, _capi.ptr(self._acc), _capi.ptr(self._lr),
+                                          _capi.stream_ptr()), "gs_masked_cr")
+        return s
+
+    def _run(self, kind, all_dls, s_old):
+        s = self._s(s_old)
+        self.step(kind, self._dl(all_dls), s)
+        return self._out(s), int(self._acc.item())
+
+    # -- reference surface ----------------------------------------------------------------
+    def sample_gibbs_change_variable(self, all_dls, old_s):
+        return self._run(_capi.GS_MCR_AUX, all_dls, old_s)
+
+    def overrelaxation_sampler(self, all_dls, old_s):
+        return self._run(_capi.GS_MCR_OVERRELAX, all_dls, old_s)
+
+    def sample_mala(self, all_dls, s_old):
+        return self._run(_capi.GS_MCR_MALA, all_dls, s_old)
+
+    def compute_gradient_mala(self, all_dls, s_old):
+        s = self._s(s_old)
+        grad = torch.empty_like(s)
+        pix = torch.empty((self.F, self.Npix), dtype=torch.float64, device=self.device)
+        _capi.check(self.lib.gs_masked_gradient(self.handle, _capi.ptr(self._dl(all_dls)), _capi.ptr(s),
+                                                _capi.ptr(grad), _capi.ptr(pix), _capi.stream_ptr()),
+                    "gs_masked_gradient")
+        g, p = grad.cpu().numpy(), pix.cpu().numpy()
+        return (*[g[i] for i in range(self.F)], *[p[i] for i in range(self.F)])
+
+    def last_log_ratio(self):
+        return float(self._lr.item())
+
+    def sample(self, all_dls, s_old=None):
+        """CenteredGibbs.py:828-850 (masked): the flag ladder."""
+        if s_old is None:
+            raise NotImplementedError("the init CR without a previous map is the qcinv PCG (SURVEY.md 8 row f1); "
+                                      "pass a start map")
+        if self.gibbs_cr and self.overrelaxation:
+            return self.overrelaxation_sampler(all_dls, s_old)
+        if self.gibbs_cr and not self.ula:
+            return self.sample_gibbs_change_variable(all_dls, s_old)
+        if self.gibbs_cr and self.ula:
+            return self._run(_capi.GS_MCR_AUX_MALA, all_dls, s_old)
+        if self.ula:
+            return self.sample_mala(all_dls, s_old)
+        raise NotImplementedError("PCG CR (sample_mask, qcinv) is SURVEY.md 8 row f1")

@@ -177,6 +177,43 @@ int gs_sht_info(const gs_sht* sht, int* nside, int* lmax, long long* npix, long 
 int gs_sht_alm2map(gs_sht* sht, int ncomp, int layout, const double* alm, double* maps, void* stream);
 int gs_sht_map2alm(gs_sht* sht, int ncomp, int layout, const double* maps, double* alm, int niter, void* stream);
 
+/* ---- masked (pixel-domain) constrained realisation (gs_masked.hip) -------
+ * Replaces PolarizedCenteredConstrainedRealization's masked samplers:
+ *   GS_MCR_AUX        sample_gibbs_change_variable  CenteredGibbs.py:676-729
+ *   GS_MCR_OVERRELAX  overrelaxation_sampler        CenteredGibbs.py:733-825
+ *   GS_MCR_MALA       sample_mala                   CenteredGibbs.py:560-603 (EB only)
+ *   GS_MCR_AUX_MALA   the ula composition of sample CenteredGibbs.py:832-836
+ * One chain per call.  maps / inv_noise (create): DEVICE [3][Npix] rows T, Q, U
+ * (inv_noise mask-multiplied, CenteredGibbs.py:266-274; the T row is read
+ * only for nfields = 3).  dl: DEVICE unbinned D_l [nspec][L+1]; s: [F][(L+1)^2]
+ * real layout, updated in place; v: [F][Npix] the auxiliary map (needed
+ * across calls only by GS_MCR_OVERRELAX; may be NULL).  Replay variates
+ * (NULL = native Philox streams): zv [n][F][Npix] pixel normals, zs [n][F][NR]
+ * slot normals in the reference's draw order (AUX: per inner iteration v then
+ * s; OVERRELAX: initial v, then per iteration s, v, s; MALA: zm [F][NR], um[1]).
+ * accept (device int32, optional): 1 for the auxiliary samplers, the MALA
+ * decision otherwise; log_ratio (device double, optional). */
+#define GS_MCR_AUX 0
+#define GS_MCR_OVERRELAX 1
+#define GS_MCR_MALA 2
+#define GS_MCR_AUX_MALA 3
+typedef struct gs_masked gs_masked;
+typedef struct gs_masked_desc {
+    int lmax, nside, nfields;      /* nfields 2 (E,B) or 3 (T,E,B)                */
+    const double* bl;              /* HOST [L+1] beam                             */
+    int n_gibbs;                   /* inner iterations (CenteredGibbs.py:250)     */
+    double alpha;                  /* over-relaxation, -0.995 (CenteredGibbs.py:244) */
+    double tau;                    /* MALA step, 0.02 (CenteredGibbs.py:294)      */
+    double noise_pol0;             /* noise_pol[0] of the MALA sigma (571-572)    */
+} gs_masked_desc;
+int gs_masked_create(const gs_masked_desc* desc, const double* maps, const double* inv_noise, gs_masked** out);
+int gs_masked_destroy(gs_masked* ctx);
+int gs_masked_info(const gs_masked* ctx, double* mu3 /* HOST [3] */, double* second_part_grad /* DEVICE [F][NR] */);
+int gs_masked_gradient(gs_masked* ctx, const double* dl, const double* s, double* grad, double* pix, void* stream);
+int gs_masked_cr(gs_masked* ctx, int kind, const double* dl, double* s, double* v, const double* zv, const double* zs,
+                 const double* zm, const double* um, uint64_t seed, uint32_t iteration, int chain, int32_t* accept,
+                 double* log_ratio, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,160 @@
+"""GPU: the masked CR samplers (gs_masked_cr through gibbssampler_amd.masked.MaskedCR).
+
+Replay mode against the reference-generated fixtures (same numpy draws, same
+algebra: a9 aux-variable, a10 over-relaxation, a11 MALA incl. both accept
+branches, a12 composition) and native mode against the oracle's restatement
+of the device Philox streams (EB and the TEB generalisation)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import masked as MK
+from oracle import sht as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_masked_eb_N8_L16.npz")
+TOL = dict(rtol=1e-9)
+
+
+@pytest.fixture(scope="module")
+def g():
+    return dict(np.load(GOLDEN))
+
+
+def _cr(g, **kw):
+    from gibbssampler_amd.masked import MaskedCR
+    pix = {"Q": g["Q"], "U": g["U"]}
+    return MaskedCR(pix, 40.0 ** 2, g["noise_pol"], g["bl"], int(g["L"]), int(g["nside"]), mask=g["mask"], **kw)
+
+
+def _dls(g):
+    return {"EE": g["dl_EE"], "BB": g["dl_BB"]}
+
+
+def _sold(g):
+    return {"EE": g["s_old_E"].copy(), "BB": g["s_old_B"].copy()}
+
+
+def _close(got, want):
+    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-11 * np.abs(want).max())
+
+
+def test_constants(g):
+    cr = _cr(g)
+    assert cr.mu[1] == pytest.approx(float(g["mu"]), rel=1e-15)
+    g2 = cr.second_part_grad().cpu().numpy()
+    _close(g2[0], g["second_part_grad_E"])
+    _close(g2[1], g["second_part_grad_B"])
+
+
+def test_a9_replay(g):
+    cr = _cr(g, n_gibbs=int(g["a9_ngibbs"]))
+    np.random.seed(int(g["a9_seed"]))
+    s, acc = cr.sample_gibbs_change_variable(_dls(g), _sold(g))
+    assert acc == 1
+    _close(s["EE"], g["a9_E"])
+    _close(s["BB"], g["a9_B"])
+
+
+def test_a10_replay(g):
+    cr = _cr(g, n_gibbs=int(g["a10_ngibbs"]), overrelaxation=True, alpha=float(g["a10_alpha"]))
+    np.random.seed(int(g["a10_seed"]))
+    s, acc = cr.overrelaxation_sampler(_dls(g), _sold(g))
+    assert acc == 1
+    _close(s["EE"], g["a10_E"])
+    _close(s["BB"], g["a10_B"])
+
+
+def test_a11_gradient(g):
+    cr = _cr(g, gibbs_cr=False, ula=True)
+    gE, gB, pE, pB = cr.compute_gradient_mala(_dls(g), _sold(g))
+    _close(gE, g["a11_gradE"])
+    _close(gB, g["a11_gradB"])
+    _close(pE, g["a11_sEpix"])
+    _close(pB, g["a11_sBpix"])
+
+
+@pytest.mark.parametrize("variant", ["a11", "a11b"])
+def test_a11_mala_replay(g, variant):
+    tau = float(g["a11_tau"]) if variant == "a11" else float(g["a11b_tau"])
+    cr = _cr(g, gibbs_cr=False, ula=True, tau=tau)
+    start = _sold(g) if variant == "a11" else {"EE": g["a9_E"], "BB": g["a9_B"]}
+    for k, sd in enumerate(g[variant + "_seeds"]):
+        np.random.seed(int(sd))
+        s, acc = cr.sample_mala(_dls(g), start)
+        assert acc == int(g[variant + "_accept"][k])
+        _close(s["EE"], g[variant + "_E"][k])
+        _close(s["BB"], g[variant + "_B"][k])
+
+
+def test_a12_composition_replay(g):
+    cr = _cr(g, gibbs_cr=True, ula=True, n_gibbs=int(g["a12_ngibbs"]))
+    np.random.seed(int(g["a12_seed"]))
+    s, acc = cr.sample(_dls(g), _sold(g))
+    assert acc == int(g["a12_accept"])
+    _close(s["EE"], g["a12_E"])
+    _close(s["BB"], g["a12_B"])
+
+
+def _teb_problem(N=8, L=16, seed=3):
+    rng = np.random.default_rng(seed)
+    npix = 12 * N * N
+    th, _ = O.pixel_angles(N)
+    mask = (np.abs(np.cos(th)) > 0.2).astype(float)
+    maps = rng.standard_normal((3, npix)) * np.array([[30.0], [0.3], [0.3]])
+    ntemp = np.full(npix, 40.0 ** 2) * np.linspace(0.9, 1.1, npix)
+    npol = np.full(npix, 0.2 ** 2) * np.linspace(1.2, 0.8, npix)
+    ell = np.arange(L + 1)
+    bl = np.exp(-0.5 * ell * (ell + 1) * (0.07 / np.sqrt(8 * np.log(2))) ** 2)
+    dl = {"TT": np.where(ell >= 2, 1000.0, 0.0), "EE": np.where(ell >= 2, 10.0 * (np.maximum(ell, 1) / 100) ** 0.5, 0),
+          "BB": np.where(ell >= 2, 0.01, 0.0)}
+    dl["TE"] = 0.5 * np.sqrt(dl["TT"] * dl["EE"])
+    s0 = rng.standard_normal((3, (L + 1) ** 2)) * np.array([[3.0], [0.05], [0.005]])
+    return N, L, mask, maps, ntemp, npol, bl, dl, s0
+
+
+@pytest.mark.parametrize("F", [2, 3])
+@pytest.mark.parametrize("over", [False, True])
+def test_aux_native_vs_oracle(F, over):
+    from gibbssampler_amd.masked import MaskedCR
+    N, L, mask, maps, ntemp, npol, bl, dl, s0 = _teb_problem()
+    seed, it, chain, ng = 4242, 7, 3, 2
+    pix = {"T": maps[0], "Q": maps[1], "U": maps[2]}
+    cr = MaskedCR(pix, ntemp, npol, bl, L, N, mask=mask, nfields=F, n_gibbs=ng, overrelaxation=over, rng="native",
+                  seed=seed, chain=chain)
+    cr.iteration = it
+    rows = (1, 2) if F == 2 else (0, 1, 2)
+    fields = ("EE", "BB") if F == 2 else ("TT", "EE", "BB")
+    s_in = {k: s0[r] for k, r in zip(fields, rows)}
+    s, acc = (cr.overrelaxation_sampler if over else cr.sample_gibbs_change_variable)(dl, s_in)
+    inv = np.stack([mask / ntemp, mask / npol, mask / npol])
+    mm = MK.MaskedModel(L, N, F, bl, maps, inv)
+    spec = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
+    dlu = np.stack([dl[k] for k in spec])
+    draws = MK.NativeDraws(seed, chain, it, L, 12 * N * N)
+    start = np.stack([s0[r] for r in rows])
+    if over:
+        want, _ = MK.overrelaxation(mm, dlu, start, ng, draws)
+    else:
+        want, _ = MK.aux_variable(mm, dlu, start, ng, draws)
+    for k, f in enumerate(fields):
+        _close(s[f], want[k])
+
+
+def test_mala_native_vs_oracle():
+    from gibbssampler_amd.masked import MaskedCR
+    N, L, mask, maps, ntemp, npol, bl, dl, s0 = _teb_problem(seed=5)
+    seed, it, chain = 99, 4, 1
+    for tau in (1e-4, 0.6):
+        cr = MaskedCR({"Q": maps[1], "U": maps[2]}, ntemp, npol, bl, L, N, mask=mask, nfields=2, gibbs_cr=False,
+                      ula=True, tau=tau, rng="native", seed=seed, chain=chain)
+        cr.iteration = it
+        s, acc = cr.sample_mala(dl, {"EE": s0[1], "BB": s0[2]})
+        mm = MK.MaskedModel(L, N, 2, bl, maps, np.stack([mask / ntemp, mask / npol, mask / npol]))
+        want, wacc, lr = MK.mala(mm, np.stack([dl["EE"], dl["BB"]]), s0[1:], MK.NativeDraws(seed, chain, it, L, 12 * N * N),
+                                 float(npol[0]), tau=tau)
+        assert acc == wacc
+        np.testing.assert_allclose(cr.last_log_ratio(), lr, rtol=1e-8, atol=1e-8)
+        _close(s["EE"], want[0])
+        _close(s["BB"], want[1])
