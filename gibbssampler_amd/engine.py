@@ -190,6 +190,12 @@ class GibbsPlan:
                 "gs_cr_sweep")
         return s_out, stats
 
+    def sweep_stats(self, d, s, stats=None):
+        """per-l statistics of a given map s [nchains, F, NR] (no draw)."""
+        stats = self.zeros(self.nchains, self.nstat, self.L + 1) if stats is None else stats
+        C.check(self.lib.gs_sweep_stats(self._h, C.ptr(d), C.ptr(s), C.ptr(stats), self._s()), "gs_sweep_stats")
+        return stats
+
     def cls_draw(self, stats, variates=None, seed=0, iteration=0, out=None):
         out = self.zeros(self.nchains, self.nspec, self.maxbins) if out is None else out
         C.check(self.lib.gs_cls_draw(self._h, C.ptr(stats), C.ptr(variates), int(seed), int(iteration),

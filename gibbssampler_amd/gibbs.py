@@ -15,9 +15,13 @@ T-only, EB (the reference's polarization runs) and TEB.  The reference's
 centered full-sky runs go through its PCG branch (CenteredGibbs.py:845-850,
 qcinv); on the full sky with isotropic noise that system is diagonal and the
 closed form (CenteredGibbs.py:317-353) is its exact solution, which is what
-runs here.  Masked / pixel-domain variants (PCG, auxiliary-variable, MALA,
-over-relaxation, pixel-domain MH likelihood) need the spherical-harmonic
-transform and raise NotImplementedError.
+runs here.  Masked centered runs (``mask_path`` = mask array or .npy file)
+use the device SHT and the auxiliary-variable / over-relaxation / MALA
+samplers of gibbssampler_amd.masked (CenteredGibbs.py:494-850, the a12 flag
+ladder); the qcinv PCG (init CR and ``gibbs_cr=False, ula=False``) and the
+pixel-domain non-centered likelihood raise NotImplementedError (SURVEY.md 8f
+rows f1/f2).  Masked-only keywords: ``n_gibbs``, ``alpha``, ``tau``,
+``skymap_init`` (the start map the reference's PCG init would provide).
 
 Extra keyword arguments (all optional): ``nchains`` (batched chains on one
 GPU), ``rng`` ("native" Philox or "replay" = numpy's global RNG in the
@@ -68,6 +72,22 @@ def _harmonic_data(pix_map, nfields, lmax):
     return {k: np.asarray(pix_map[k], dtype=np.float64) for k in keys}
 
 
+def _load_mask(mask_path, nside):
+    """The mask of CenteredGibbs.py:266-271 (hp.ud_grade(hp.read_map(path), nside)).
+    Accepted: an array at the run's N_side, or a .npy file of one.  FITS
+    reading and ud_grade are SURVEY.md 8 row f3."""
+    if isinstance(mask_path, np.ndarray):
+        m = np.asarray(mask_path, dtype=np.float64)
+    elif isinstance(mask_path, str) and mask_path.endswith(".npy"):
+        m = np.load(mask_path, allow_pickle=False).astype(np.float64)
+    else:
+        raise NotImplementedError("mask_path: FITS masks and ud_grade are SURVEY.md 8 row f3; pass an array or "
+                                  "a .npy file at the run's N_side")
+    if m.shape != (12 * nside ** 2,):
+        raise NotImplementedError("mask resolution differs from N_side: ud_grade is SURVEY.md 8 row f3")
+    return m
+
+
 def _default_bins(lmax, nfields):
     return {s: np.arange(0, lmax + 2) for s in _SPECTRA[nfields]}
 
@@ -86,8 +106,12 @@ class GibbsSampler:
                  gibbs_cr=False, rj_step=False, ula=False, *, nchains=1, rng="native", seed=0, fields=None,
                  chain0=0, reference_quirks=True, noise_pol=None, proposal_variances=None,
                  metropolis_blocks=None, n_iter_metropolis=1, mask_path=None):
+        self.mask = None
         if mask_path is not None:
-            raise NotImplementedError("masked (cut-sky) samplers need the SHT path (SURVEY.md 8f f1/f2)")
+            if self._kind != "centered":
+                raise NotImplementedError("masked non-centered / ASIS runs need the pixel-domain MH likelihood "
+                                          "(NonCenteredGibbs.py:333-355; SURVEY.md 8 row f2)")
+            self.mask = _load_mask(mask_path, nside)
         self.noise = noise
         self.beam = beam_fwhm_deg
         self.nside = nside
@@ -110,13 +134,21 @@ class GibbsSampler:
         else:
             self.bins = {self.spectra[0]: np.asarray(bins)}
         self.dls_to_cls_array = np.array([2 * np.pi / (l * (l + 1)) if l != 0 else 0 for l in range(lmax + 1)])
-        nt = _scalar_noise(noise, "noise")
-        if self.nfields == 1:
+        self.noise_pol = noise_pol
+        if self.mask is not None:
+            nt = float(np.atleast_1d(noise)[0])
+        else:
+            nt = _scalar_noise(noise, "noise")
+        if self.mask is not None:
+            npol = float(np.atleast_1d(noise_pol if noise_pol is not None else noise)[0])
+            self.noise_var = np.array([npol, npol] if self.nfields == 2 else [nt, npol, npol])
+        elif self.nfields == 1:
             noise_var = [nt]
         else:
             npol = _scalar_noise(noise_pol if noise_pol is not None else noise, "noise_pol")
             noise_var = [npol, npol] if self.nfields == 2 else [nt, npol, npol]
-        self.noise_var = np.array(noise_var)
+        if self.mask is None:
+            self.noise_var = np.array(noise_var)
         self.nchains = int(nchains)
         self.rng = rng
         self.seed = seed
@@ -197,20 +229,52 @@ class CenteredGibbs(GibbsSampler):
     def __init__(self, pix_map, noise_temp, noise_pol, beam, nside, lmax, Npix, mask_path=None,
                  polarization=False, bins=None, n_iter=100000, rj_step=False, all_sph=False, gibbs_cr=False,
                  overrelaxation=False, ula=False, **kw):
-        if gibbs_cr or overrelaxation or rj_step:
-            if mask_path is not None:
-                raise NotImplementedError("auxiliary-variable / over-relaxation / RJPO CR need the SHT path")
+        if rj_step and mask_path is not None:
+            raise NotImplementedError("RJPO CR (sample_mask_rj) is disabled at HEAD (CenteredGibbs.py:839) and "
+                                      "needs the qcinv PCG (SURVEY.md 8 row f1)")
+        self.n_gibbs = int(kw.pop("n_gibbs", 1))
+        self.alpha = float(kw.pop("alpha", -0.995))
+        self.tau = float(kw.pop("tau", 0.02))
+        self.skymap_init = kw.pop("skymap_init", None)
         super().__init__(pix_map, noise_temp, beam, nside, lmax, polarization=polarization, bins=bins,
                          n_iter=n_iter, gibbs_cr=gibbs_cr, rj_step=rj_step, mask_path=mask_path,
                          noise_pol=noise_pol, **kw)
         self.all_sph = all_sph
         self.overrelaxation = overrelaxation
-        self.constrained_sampler = CenteredConstrainedRealization(self)
+        self.cr_ula = ula
+        if self.mask is not None:
+            from .masked import MaskedCR
+            if not polarization:
+                raise NotImplementedError("masked temperature-only runs: the reference's TT masked path is broken "
+                                          "at HEAD (SURVEY.md Appendix B.7); use fields='TEB'")
+            self.constrained_sampler = MaskedCR(pix_map, noise_temp, noise_pol, self.bl_gauss, lmax, nside,
+                                                mask=self.mask, nfields=self.nfields, gibbs_cr=gibbs_cr,
+                                                n_gibbs=self.n_gibbs, alpha=self.alpha,
+                                                overrelaxation=overrelaxation, ula=ula, tau=self.tau, rng=self.rng,
+                                                seed=self.seed, chain=self.chain0)
+        else:
+            self.constrained_sampler = CenteredConstrainedRealization(self)
         self.cls_sampler = CenteredClsSampler(self)
+
+    def _run_masked(self, dls_init):
+        from .masked import MaskedRunner
+        if self.nchains != 1:
+            raise NotImplementedError("masked runs batch one chain per process (shard chains over GPUs)")
+        runner = MaskedRunner(self.constrained_sampler, self.bins)
+        F = self.nfields
+        s0 = self.skymap_init
+        if s0 is None:
+            s0 = np.zeros((F, (self.lmax + 1) ** 2))
+        elif isinstance(s0, dict):
+            s0 = np.stack([np.asarray(s0[k]) for k in (("EE", "BB") if F == 2 else ("TT", "EE", "BB"))])
+        init = dls_init if isinstance(dls_init, dict) else {self.spectra[0]: dls_init}
+        return runner.run(init, self.n_iter, s0)
 
     def run_polarization(self, dls_init):
         """GibbsSampler.run_polarization (GibbsSampler.py:118-180): returns
         (h_dls, h_accept_cr, h_duration_cr, h_duration_cls_sampling)."""
+        if self.mask is not None:
+            return self._run_masked(dls_init)
         h, _, t = self._run_common(dls_init)
         n = len(t)
         return h, np.ones(n, dtype=int), np.asarray(t), np.zeros(n)

@@ -17,6 +17,7 @@ the reference's order (A.5 of SURVEY.md) so results match the reference for
 the same ``np.random.seed``.  There is no CPU fallback.
 """
 import ctypes
+import time
 
 import numpy as np
 import torch
@@ -86,6 +87,8 @@ class MaskedCR:
     def _s(self, s):
         if isinstance(s, torch.Tensor):
             return s.to(self.device, torch.float64).contiguous().clone()
+        if isinstance(s, np.ndarray):
+            return torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64).reshape(self.F, self.NR)).to(self.device)
         return torch.from_numpy(np.ascontiguousarray(np.stack([np.asarray(s[k], dtype=np.float64)
                                                               for k in FIELDS[self.F]]))).to(self.device)
 
@@ -181,3 +184,66 @@ class MaskedCR:
         if self.ula:
             return self.sample_mala(all_dls, s_old)
         raise NotImplementedError("PCG CR (sample_mask, qcinv) is SURVEY.md 8 row f1")
+
+
+def cr_kind(gibbs_cr, overrelaxation, ula):
+    """The flag ladder of CenteredGibbs.py:828-850 for a masked run with a map."""
+    if gibbs_cr and overrelaxation:
+        return _capi.GS_MCR_OVERRELAX
+    if gibbs_cr and not ula:
+        return _capi.GS_MCR_AUX
+    if gibbs_cr and ula:
+        return _capi.GS_MCR_AUX_MALA
+    if ula:
+        return _capi.GS_MCR_MALA
+    raise NotImplementedError("PCG CR (sample_mask, qcinv) is SURVEY.md 8 row f1")
+
+
+class MaskedRunner:
+    """GibbsSampler.run_polarization (GibbsSampler.py:118-180) for a masked run on
+    one chain: per iteration the masked CR (MaskedCR, the a12 ladder) and the
+    centered C_l draw (gs_sweep_stats + gs_cls_draw), everything resident on
+    the device.  The reference's first CR (GibbsSampler.py:136-138) is the
+    qcinv PCG (row f1); the start map is given instead (``s_init``)."""
+
+    def __init__(self, cr, bins, kind=None):
+        from .engine import GibbsPlan
+        self.cr = cr
+        self.kind = cr_kind(cr.gibbs_cr, cr.overrelaxation, cr.ula) if kind is None else kind
+        F = cr.F
+        self.spectra = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
+        self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
+        self.plan = GibbsPlan(cr.L, cr.nside, F, 1, cr.bl, [1.0] * F, self.bins)
+        self.d0 = self.plan.zeros(F, cr.NR)
+
+    def _unfold(self, binned):
+        out = np.zeros((len(self.spectra), self.cr.L + 1))
+        for k, s in enumerate(self.spectra):
+            b = self.bins[s]
+            for i in range(len(b) - 1):
+                out[k, b[i]:b[i + 1]] = binned[s][i]
+        return torch.from_numpy(out).to(self.cr.device)
+
+    def run(self, dls_init, n_iter, s_init):
+        cr, plan = self.cr, self.plan
+        binned = {s: np.asarray(dls_init[s], dtype=np.float64) for s in self.spectra}
+        h = {s: [binned[s].copy()] for s in self.spectra}
+        acc, t_cr, t_cls = [], [], []
+        s = cr._s(s_init)
+        for i in range(n_iter):
+            it = i + 1
+            cr.iteration = it
+            t0 = time.perf_counter()
+            cr.step(self.kind, self._unfold(binned), s, iteration=it)
+            acc.append(int(cr._acc.item()))
+            t1 = time.perf_counter()
+            stats = plan.sweep_stats(self.d0, s[None])
+            var = plan.replay_invgamma() if cr.rng == "replay" else None
+            dlt = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)
+            binned = plan.dl_dicts(dlt)[0]
+            t_cls.append(time.perf_counter() - t1)
+            t_cr.append(t1 - t0)
+            for sp in self.spectra:
+                h[sp].append(binned[sp])
+        self.s = s
+        return {sp: np.array(v) for sp, v in h.items()}, np.array(acc), np.array(t_cr), np.array(t_cls)
