@@ -47,7 +47,15 @@ namespace {
 
 constexpr double PI = 3.14159265358979323846;
 constexpr int LEG_BLOCK = 256;
-constexpr int ANA_C = 4;                    // l per reduction chunk (even)
+#ifndef GS_ANA_C
+#define GS_ANA_C 4
+#endif
+#ifndef GS_ANA_SR
+#define GS_ANA_SR 4
+#endif
+constexpr int ANA_C = GS_ANA_C;             // l per reduction chunk (even)
+constexpr int ASR = GS_ANA_SR;              // ring pairs per lane, analysis
+constexpr int ATILE = ASR * 256;            // ring pairs per analysis workgroup
 constexpr int LDS_FFT_MAX = 8192;           // complex points held in LDS
 constexpr double SC_UP = 0x1p768;
 constexpr double SC_DN = 0x1p-768;
@@ -670,19 +678,21 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                                                             double2* __restrict__ part) {
     constexpr int NO = NC == 1 ? 2 : (NC == 2 ? 4 : 6);   // real outputs per l
     constexpr int NV = NO * ANA_C;
-    constexpr int RS = LEG_BLOCK + 1;                      // padded LDS row
-    __shared__ double red[NV * RS];
+    constexpr int NVP = NV <= 8 ? 8 : (NV <= 16 ? 16 : 32);   // rows per wave, power of two
+    constexpr int RS = 65;                                     // padded row of 64 partials
+    static_assert(NV <= 32, "chunk too large for the wave reduction");
+    __shared__ double red_all[4][NVP * RS];
     const int L = D.L, npair = D.npair;
     const int q = blockIdx.x, tile = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g0 = tile * (LTILE / 64) + wave * SR;
+    const int g0 = tile * (ATILE / 64) + wave * ASR;
     const long long plane = (long long)(L + 1) * npair;
-    double x[SR], is2[SR], xis2[SR];
-    int pr[SR];
-    bool act[SR];
+    double x[ASR], is2[ASR], xis2[ASR];
+    int pr[ASR];
+    bool act[ASR];
 #pragma unroll
-    for (int r = 0; r < SR; ++r) {
+    for (int r = 0; r < ASR; ++r) {
         pr[r] = (g0 + r) * 64 + lane;
         act[r] = pr[r] < npair;
         x[r] = act[r] ? D.geom[pr[r]].x : 0.0;
@@ -692,21 +702,21 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
         if (h == 1 && m <= q) break;
-        int ls[SR];
+        int ls[ASR];
 #pragma unroll
-        for (int r = 0; r < SR; ++r)
+        for (int r = 0; r < ASR; ++r)
             ls[r] = __builtin_amdgcn_readfirstlane(g0 + r < D.ngroup ? D.lstart[(long long)m * D.ngroup + g0 + r]
                                                                      : L + 1);
+        // each wave walks l from its own slots' first onset (no workgroup sync)
         int lmin = L + 1;
-        for (int gq = tile * (LTILE / 64); gq < min(D.ngroup, (tile + 1) * (LTILE / 64)); ++gq)
-            lmin = min(lmin, D.lstart[(long long)m * D.ngroup + gq]);
-        lmin = __builtin_amdgcn_readfirstlane(lmin);
-        // parity-combined ring phases: [+]: N + S, [-]: N - S
-        double2 fp[SR][NC], fn[SR][NC];
-        double v0[SR], v1[SR];
-        int kk[SR];
 #pragma unroll
-        for (int r = 0; r < SR; ++r) {
+        for (int r = 0; r < ASR; ++r) lmin = min(lmin, ls[r]);
+        // parity-combined ring phases: [+]: N + S, [-]: N - S
+        double2 fp[ASR][NC], fn[ASR][NC];
+        double v0[ASR], v1[ASR];
+        int kk[ASR];
+#pragma unroll
+        for (int r = 0; r < ASR; ++r) {
             v0[r] = 0.0; v1[r] = 0.0; kk[r] = 0;
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -730,9 +740,9 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
             for (int i = 0; i < NV; ++i) acc[i] = 0.0;
             // activations inside the chunk force the slow path
 #pragma unroll
-            for (int r = 0; r < SR; ++r)
+            for (int r = 0; r < ASR; ++r)
                 if (ls[r] >= l0 && ls[r] < l0 + ANA_C && ls[r] <= L) slow = true;
-            if (slow) {
+            if (slow || l0 + ANA_C - 1 > L) {
 #pragma unroll
                 for (int cc = 0; cc < ANA_C; ++cc) {
                     const int l = l0 + cc;
@@ -740,7 +750,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                     const LegCoef c = cf[l];
                     const LegCoef cn = cf[min(l + 1, L)];
 #pragma unroll
-                    for (int r = 0; r < SR; ++r) {
+                    for (int r = 0; r < ASR; ++r) {
                         if (l < ls[r]) continue;                 // uniform per wave
                         if (l == ls[r] && act[r]) {
                             const double2 s0 = D.st[(long long)m * npair + pr[r]];
@@ -758,53 +768,63 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                 // leave the slow path once every live slot is active and representable
                 bool live = true;
 #pragma unroll
-                for (int r = 0; r < SR; ++r)
+                for (int r = 0; r < ASR; ++r)
                     if (ls[r] <= L && (l0 + ANA_C <= ls[r] || __any(kk[r] < 0))) live = false;
                 slow = !live;
             } else {
 #pragma unroll
+                // full chunk, every live slot active and representable: no guards
+                // (cf[L + 1] exists: the coefficient table is padded by one entry)
                 for (int cc = 0; cc < ANA_C; ++cc) {
                     const int l = l0 + cc;
-                    if (l > L) break;
                     const LegCoef c = cf[l];
-                    const LegCoef cn = cf[min(l + 1, L)];
+                    const LegCoef cn = cf[l + 1];
 #pragma unroll
-                    for (int r = 0; r < SR; ++r) {
+                    for (int r = 0; r < ASR; ++r) {
                         if (ls[r] > L) continue;
                         if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
                         else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
-                        if (l < L) rec_step(cn, x[r], v0[r], v1[r]);
+                        rec_step(cn, x[r], v0[r], v1[r]);
                     }
                 }
             }
-            // fixed-order workgroup reduction of the chunk
+            // fixed-order wave reduction of the chunk (wave-private LDS rows, no
+            // workgroup barrier): lane -> (row o = lane % NVP, segment lane / NVP)
+            double* red = red_all[wave];
 #pragma unroll
-            for (int i = 0; i < NV; ++i) red[i * RS + tid] = acc[i];
-            __syncthreads();
-            // thread -> (output v, segment g of 32 partials); 8 segments per output
-            const int v = tid >> 3, g = tid & 7;
+            for (int i = 0; i < NV; ++i) red[i * RS + lane] = acc[i];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            constexpr int SEG = 64 / NVP;               // segments per row
+            constexpr int SLEN = 64 / SEG;              // partials per segment
+            const int o = lane % NVP, sg = lane / NVP;
             double sum = 0.0;
-            if (v < NV) {
-                const double* row = red + v * RS + g * 32;
-                for (int i = 0; i < 32; ++i) sum += row[(i + g * 4) & 31];
+            if (o < NV) {
+                const double* row = red + o * RS + sg * SLEN;
+#pragma unroll 8
+                for (int i = 0; i < SLEN; ++i) sum += row[i];
             }
-            sum += __shfl_xor(sum, 1, 64);
-            sum += __shfl_xor(sum, 2, 64);
-            sum += __shfl_xor(sum, 4, 64);
-            if (v < NV && g == 0) {
-                const int cc = v / NO, o = v % NO;
+#pragma unroll
+            for (int d = NVP; d < 64; d <<= 1) sum += __shfl_xor(sum, d, 64);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < NV) {
+                const int cc = lane / NO, oo = lane % NO;
                 const int l = l0 + cc;
                 if (l >= m && l <= L) {
-                    const int comp = o >> 1;
-                    double* dst = reinterpret_cast<double*>(part + ((long long)tile * NC + comp) * D.nlm + obase + l);
-                    dst[o & 1] = sum;
+                    const int comp = oo >> 1;
+                    double* dst = reinterpret_cast<double*>(
+                        part + (((long long)tile * 4 + wave) * NC + comp) * D.nlm + obase + l);
+                    dst[oo & 1] = sum;
                 }
             }
-            __syncthreads();
         }
-        // l below the workgroup's first chunk: exact zeros
-        for (int l = m + tid; l < min(lstart0, L + 1); l += LEG_BLOCK)
-            for (int c = 0; c < NC; ++c) part[((long long)tile * NC + c) * D.nlm + obase + l] = make_double2(0.0, 0.0);
+        // l below the wave's first chunk: exact zeros
+        for (int l = m + lane; l < min(lstart0, L + 1); l += 64)
+            for (int c = 0; c < NC; ++c)
+                part[(((long long)tile * 4 + wave) * NC + c) * D.nlm + obase + l] = make_double2(0.0, 0.0);
     }
 }
 
@@ -924,7 +944,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     p->nside = N; p->L = L; p->npair = 2 * N; p->ngroup = (p->npair + 63) / 64;
     p->nlm = (L + 1) * (L + 2) / 2;
     p->npix = 12LL * N * N;
-    p->ntile = (p->npair + LTILE - 1) / LTILE;
+    p->ntile = (p->npair + ATILE - 1) / ATILE;
     // ---- geometry (ring pair r: north ring r+1, south ring 4N-1-r) ----
     std::vector<PairGeom> geom(p->npair);
     int Mmax = 2;
@@ -989,14 +1009,14 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     }
     int rc = 0;
     rc |= sht_alloc(p, &p->geom, geom.size());
-    rc |= sht_alloc(p, &p->coef, coef.size());
+    rc |= sht_alloc(p, &p->coef, coef.size() + 1);   // + one zero entry past (L, L)
     rc |= sht_alloc(p, &p->lstart, (size_t)(L + 1) * p->ngroup);
     rc |= sht_alloc(p, &p->st, (size_t)(L + 1) * p->npair);
     rc |= sht_alloc(p, &p->stk, (size_t)(L + 1) * p->npair);
     rc |= sht_alloc(p, &p->tw, (size_t)Mmax / 2);
     rc |= sht_alloc(p, &p->bsk, (size_t)std::max<long long>(bs_total, 1));
     rc |= sht_alloc(p, &p->phi, (size_t)3 * 2 * (L + 1) * p->npair);
-    rc |= sht_alloc(p, &p->part, (size_t)p->ntile * 3 * p->nlm);
+    rc |= sht_alloc(p, &p->part, (size_t)p->ntile * 4 * 3 * p->nlm);   // one partial per analysis wave
     rc |= sht_alloc(p, &p->mapw, (size_t)3 * p->npix);
     rc |= sht_alloc(p, &p->ain, (size_t)3 * p->nlm);
     if (rc) { sht_free(p); return -1; }
@@ -1023,7 +1043,8 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     }
     if (gscr_need && sht_alloc(p, &p->gscr, (size_t)gscr_need)) { sht_free(p); return -1; }
     if (hipMemcpy(p->geom, geom.data(), geom.size() * sizeof(PairGeom), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->coef, coef.data(), coef.size() * sizeof(LegCoef), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(p->coef, coef.data(), coef.size() * sizeof(LegCoef), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(p->coef + coef.size(), 0, sizeof(LegCoef)) != hipSuccess) {
         sht_free(p);
         return set_error("gs_sht_create: table upload failed");
     }
@@ -1140,7 +1161,7 @@ static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, do
     const double w = 4.0 * PI / (double)p->npix;
     const long long n = (long long)ncomp * p->nlm;
 #define GS_AF(NC) hipLaunchKernelGGL((k_sht_anal_finish<NC>), dim3(nblocks(n, 256)), dim3(256), 0, S(stream), p->L, p->nlm, \
-                                     p->ntile, p->part, w, layout, acc, alm)
+                                     p->ntile * 4, p->part, w, layout, acc, alm)
     if (ncomp == 1) GS_AF(1); else if (ncomp == 2) GS_AF(2); else GS_AF(3);
 #undef GS_AF
     GS_LAUNCH_CHECK("k_sht_anal_finish");
