@@ -354,6 +354,9 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
             }
             ++l;
         }
+#if defined(GS_ASM_MARKERS)
+        asm volatile("; SYN_FAST_BEGIN");
+#endif
         for (; l + 1 <= L; l += 2) {
             const LegCoef c0 = cf[l], c1 = cf[l + 1], c2 = cf[min(l + 2, L)];
             const double2 t0 = NC != 2 ? aT[l] : z2, e0 = NC != 1 ? aE[l] : z2, b0 = NC != 1 ? aB[l] : z2;
@@ -772,22 +775,29 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                     if (ls[r] <= L && (l0 + ANA_C <= ls[r] || __any(kk[r] < 0))) live = false;
                 slow = !live;
             } else {
-#pragma unroll
                 // full chunk, every live slot active and representable: no guards
                 // (cf[L + 1] exists: the coefficient table is padded by one entry)
+#if defined(GS_ASM_MARKERS)
+                asm volatile("; ANA_FAST_BEGIN");
+#endif
+#pragma unroll
                 for (int cc = 0; cc < ANA_C; ++cc) {
                     const int l = l0 + cc;
                     const LegCoef c = cf[l];
                     const LegCoef cn = cf[l + 1];
 #pragma unroll
                     for (int r = 0; r < ASR; ++r) {
-                        if (ls[r] > L) continue;
+                        // no per-slot branch: a dead slot (ls > L) has zero phases and
+                        // zero state, so it adds exact zeros (keeps acc[] in place)
                         if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
                         else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
                         rec_step(cn, x[r], v0[r], v1[r]);
                     }
                 }
             }
+#if defined(GS_ASM_MARKERS)
+            asm volatile("; ANA_CHUNK_END");
+#endif
             // fixed-order wave reduction of the chunk (wave-private LDS rows, no
             // workgroup barrier): lane -> (row o = lane % NVP, segment lane / NVP)
             double* red = red_all[wave];
