@@ -212,7 +212,10 @@ __global__ __launch_bounds__(256) void k_sht_onset(ShtDev D, const double* __res
 // the parity-unrolled fast path runs the plain recurrence.
 // NC = 1: T (spin 0); 2: E,B <-> Q,U; 3: T,E,B <-> T,Q,U.
 // phi layout: [comp][ns][m][pair] (double2), ns 0 = north, 1 = south
-constexpr int SR = 4;
+#ifndef GS_SYN_SR
+#define GS_SYN_SR 2
+#endif
+constexpr int SR = GS_SYN_SR;               // ring pairs per lane, synthesis
 constexpr int LTILE = SR * LEG_BLOCK;
 
 // a_lm in the caller's layout -> ain[comp][nlm] (healpy-ordered complex)
@@ -1153,7 +1156,7 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, ncomp, alm, layout,
                        p->ain);
     GS_LAUNCH_CHECK("k_sht_alm_in");
-    const dim3 grid(p->L / 2 + 1, p->ntile);
+    const dim3 grid(p->L / 2 + 1, (p->npair + LTILE - 1) / LTILE);
 #define GS_SL(NC) hipLaunchKernelGGL((k_sht_synth_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->ain, p->phi)
     if (ncomp == 1) GS_SL(1); else if (ncomp == 2) GS_SL(2); else GS_SL(3);
 #undef GS_SL
