@@ -105,6 +105,10 @@ _SIGS = [
     ("gs_masked_destroy", ctypes.c_int, [_VP]),
     ("gs_masked_info", ctypes.c_int, [_VP, c_double_p, _VP]),
     ("gs_masked_gradient", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+    ("gs_masked_pcg_rhs", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, _VP,
+                                         _VP]),
+    ("gs_masked_pcg_solve", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_double, ctypes.c_int, c_int_p,
+                                           c_double_p, _VP]),
     ("gs_masked_cr", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,
                                     ctypes.c_uint32, ctypes.c_int, _VP, _VP, _VP]),
 ]

@@ -41,6 +41,8 @@ constexpr uint32_t TAG_MALA_U = 9;
 constexpr int SUB_S = 16;
 constexpr int SUB_V_INIT = 255;
 constexpr int SUB_MALA = 200;
+constexpr int SUB_PCG_S = 250;     // CR substep of the PCG's C^-1/2 slot normals
+constexpr int SUB_PCG_V = 254;     // TAG_AUX_V substep of the PCG's pixel normals
 constexpr int NSUM = 8;
 constexpr int RED_BLOCK = 256;
 
@@ -298,6 +300,177 @@ __global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long l
         for (long long g = threadIdx.x; g < nslot; g += blockDim.x) s0[g] = s1[g];
 }
 
+// ---------------------------------------------------------------------------
+// f1: PCG CR (CenteredGibbs.py:448-491) -- Q x = C^+ x + b A^T N^-1 A b x
+// ---------------------------------------------------------------------------
+// prior pseudo-inverse factors at l: EB per field sqrt(inv_var); TEB the lower
+// factor A^+ = [[i00, 0], [t10, i11]] of the TE block (C^+ = (A^+)^T A^+) and iB
+struct PriorPinv { double i00, t10, i11, iB, ie, ib; };
+
+template <int F>
+__device__ __forceinline__ PriorPinv prior_pinv(const double* __restrict__ dl, int L, int l) {
+    PriorPinv q{0, 0, 0, 0, 0, 0};
+    if constexpr (F == 2) {
+        const double ve = var_from_dl(dl[l], l), vb = var_from_dl(dl[(L + 1) + l], l);
+        q.ie = ve != 0.0 ? sqrt(1.0 / ve) : 0.0;
+        q.ib = vb != 0.0 ? sqrt(1.0 / vb) : 0.0;
+    } else {
+        const double tt = var_from_dl(dl[l], l), ee = var_from_dl(dl[(L + 1) + l], l);
+        const double bb = var_from_dl(dl[2 * (L + 1) + l], l), te = var_from_dl(dl[3 * (L + 1) + l], l);
+        const CovChol A = cov_chol_teb(tt, ee, te, bb);
+        q.i00 = A.a00 != 0.0 ? 1.0 / A.a00 : 0.0;
+        q.i11 = A.a11 != 0.0 ? 1.0 / A.a11 : 0.0;
+        q.t10 = -A.a10 * q.i00 * q.i11;
+        q.iB = A.aB != 0.0 ? 1.0 / A.aB : 0.0;
+    }
+    return q;
+}
+
+// y = sqrt(N^-1) z per pixel (the pixel half of the fluctuations, 467-471)
+__global__ void k_pcg_zpix(long long npix, int F, Rows rows, const double* __restrict__ ninv,
+                           const double* __restrict__ zv, uint32_t seed_lo, uint32_t seed_hi, uint32_t chain,
+                           uint32_t iter, double* __restrict__ y) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= F * npix) return;
+    const int k = (int)(g / npix);
+    const long long p = g % npix;
+    const double z = zv ? zv[g]
+                        : normal1(chain_key(seed_lo, seed_hi, chain), (uint32_t)p, (uint32_t)rows.r[k],
+                                  TAG_AUX_V | ((uint32_t)SUB_PCG_V << 8), iter);
+    y[g] = z * sqrt(ninv[g]);
+}
+
+// rhs = b A^T N^-1 d (g2) + b * map2alm(y, iter=3) * Npix/4pi + (A^+)^T z_slot
+template <int F>
+__global__ void k_pcg_rhs(int L, const double* __restrict__ dl, const double* __restrict__ bl,
+                          const double* __restrict__ g2, const double* __restrict__ r_alm, double resc,
+                          const double* __restrict__ zs, uint32_t seed_lo, uint32_t seed_hi, uint32_t chain,
+                          uint32_t iter, double* __restrict__ rhs) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= nlm) return;
+    int l, m;
+    cidx_lm(L, i, l, m);
+    const long long r = m == 0 ? l : 2 * i - (L + 1);
+    const int nv = m == 0 ? 1 : 2;
+    double z[3][2];
+    slot_normals(zs, NR, F, r, nv, chain_key(seed_lo, seed_hi, chain), i, SUB_PCG_S, iter, z);
+    const PriorPinv q = prior_pinv<F>(dl, L, l);
+    const double b = bl[l];
+    for (int c = 0; c < nv; ++c) {
+        double h[3];
+        if constexpr (F == 2) { h[0] = q.ie * z[0][c]; h[1] = q.ib * z[1][c]; }
+        else { h[0] = q.i00 * z[0][c] + q.t10 * z[1][c]; h[1] = q.i11 * z[1][c]; h[2] = q.iB * z[2][c]; }
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const long long o = f * NR + r + c;
+            rhs[o] = g2[o] + (r_alm[o] * resc * b + h[f]);
+        }
+    }
+}
+
+// out = C^+ x + (b / w) r,  r = complex_to_real(map2alm(N^-1 A b x))
+template <int F>
+__global__ void k_pcg_qfinish(int L, const double* __restrict__ dl, const double* __restrict__ bl,
+                              const double* __restrict__ x, const double* __restrict__ r_alm, double inv_w,
+                              double* __restrict__ out) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= nlm) return;
+    int l, m;
+    cidx_lm(L, i, l, m);
+    const long long r = m == 0 ? l : 2 * i - (L + 1);
+    const int nv = m == 0 ? 1 : 2;
+    const PriorPinv q = prior_pinv<F>(dl, L, l);
+    const double bw = bl[l] * inv_w;
+    for (int c = 0; c < nv; ++c) {
+        double cx[3];
+        if constexpr (F == 2) {
+            cx[0] = q.ie * q.ie * x[r + c];
+            cx[1] = q.ib * q.ib * x[NR + r + c];
+        } else {
+            const double xt = x[r + c], xe = x[NR + r + c];
+            const double y0 = q.i00 * xt, y1 = q.t10 * xt + q.i11 * xe;
+            cx[0] = q.i00 * y0 + q.t10 * y1;
+            cx[1] = q.i11 * y1;
+            cx[2] = q.iB * q.iB * x[2 * NR + r + c];
+        }
+#pragma unroll
+        for (int f = 0; f < F; ++f) out[f * NR + r + c] = cx[f] + r_alm[f * NR + r + c] * bw;
+    }
+}
+
+// z = Sigma r, Sigma = L L^T the centered block for kappa_f = nbar_f / w
+template <int F>
+__global__ void k_pcg_prec(int L, const double* __restrict__ params, const double* __restrict__ rr,
+                           double* __restrict__ z) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= NR) return;
+    int l;
+    if (g <= L) l = (int)g;
+    else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
+    const double* p = params + (long long)l * GS_NPARAM;
+    if constexpr (F == 2) {
+        z[g] = p[2] * p[2] * rr[g];
+        z[NR + g] = p[3] * p[3] * rr[NR + g];
+    } else {
+        const double r0 = rr[g], r1 = rr[NR + g], r2 = rr[2 * NR + g];
+        const double t0 = p[5] * r0 + p[6] * r1, t1 = p[7] * r1;        // L^T r
+        z[g] = p[5] * t0;
+        z[NR + g] = p[6] * t0 + p[7] * t1;
+        z[2 * NR + g] = p[8] * p[8] * r2;
+    }
+}
+
+// x += a p ; r -= a q
+__global__ void k_pcg_update(long long n, double a, const double* __restrict__ p, const double* __restrict__ q,
+                             double* __restrict__ x, double* __restrict__ r) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    x[g] += a * p[g];
+    r[g] -= a * q[g];
+}
+
+// p = z + b p
+__global__ void k_pcg_dir(long long n, double b, const double* __restrict__ z, double* __restrict__ p) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g < n) p[g] = z[g] + b * p[g];
+}
+
+// fixed-order dot products: out[0] = a.b, out[1] = c.d (per-block partials, then one block)
+__global__ __launch_bounds__(RED_BLOCK) void k_dot2(long long n, const double* __restrict__ a,
+                                                    const double* __restrict__ b, const double* __restrict__ c,
+                                                    const double* __restrict__ d, double* __restrict__ partial) {
+    double s0 = 0.0, s1 = 0.0;
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x) {
+        s0 += a[g] * b[g];
+        s1 += c[g] * d[g];
+    }
+    __shared__ double red[2][RED_BLOCK];
+    red[0][threadIdx.x] = s0;
+    red[1][threadIdx.x] = s1;
+    __syncthreads();
+    for (int h = RED_BLOCK / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + h];
+            red[1][threadIdx.x] += red[1][threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { partial[2 * blockIdx.x] = red[0][0]; partial[2 * blockIdx.x + 1] = red[1][0]; }
+}
+
+__global__ void k_dot2_finish(int nblk, const double* __restrict__ partial, double* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    double s0 = 0.0, s1 = 0.0;
+    for (int b = 0; b < nblk; ++b) { s0 += partial[2 * b]; s1 += partial[2 * b + 1]; }
+    out[0] = s0;
+    out[1] = s1;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -308,6 +481,7 @@ struct gs_masked {
     long long npix = 0, NR = 0, nlm = 0;
     double w = 0, alpha = -0.995, tau = 0.02, noise_pol0 = 1.0;
     double mu[3] = {0, 0, 0};
+    double nbar[3] = {0, 0, 0};      // mean N^-1 per map row (PCG preconditioner)
     Rows rows{{1, 2, 0}};
     gs_sht* sht = nullptr;
     double *bl = nullptr, *dpix = nullptr, *ninv = nullptr, *g2 = nullptr;
@@ -316,6 +490,7 @@ struct gs_masked {
     double *x = nullptr, *Abs = nullptr, *y = nullptr, *r = nullptr;
     double *grad0 = nullptr, *grad1 = nullptr, *snew = nullptr, *pix0 = nullptr, *pix1 = nullptr, *vtmp = nullptr;
     double *partial = nullptr, *lr = nullptr;
+    double *pr = nullptr, *pz = nullptr, *pp = nullptr, *pq = nullptr, *params_pcg = nullptr, *dots = nullptr;
 };
 
 namespace {
@@ -323,7 +498,8 @@ namespace {
 void mc_free(gs_masked* c) {
     if (c->sht) gs_sht_destroy(c->sht);
     double* bufs[] = {c->bl, c->dpix, c->ninv, c->g2, c->params, c->params_mala, c->x, c->Abs, c->y, c->r,
-                      c->grad0, c->grad1, c->snew, c->pix0, c->pix1, c->vtmp, c->partial, c->lr};
+                      c->grad0, c->grad1, c->snew, c->pix0, c->pix1, c->vtmp, c->partial, c->lr,
+                      c->pr, c->pz, c->pp, c->pq, c->params_pcg, c->dots};
     for (double* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ell2bin) (void)hipFree(c->ell2bin);
@@ -442,6 +618,12 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     rc |= mc_alloc(&c->vtmp, FP);
     rc |= mc_alloc(&c->partial, (size_t)c->nblk * NSUM);
     rc |= mc_alloc(&c->lr, 1);
+    rc |= mc_alloc(&c->pr, FR);
+    rc |= mc_alloc(&c->pz, FR);
+    rc |= mc_alloc(&c->pp, FR);
+    rc |= mc_alloc(&c->pq, FR);
+    rc |= mc_alloc(&c->params_pcg, (size_t)(c->L + 1) * GS_NPARAM);
+    rc |= mc_alloc(&c->dots, 2);
     if (rc) { mc_free(c); return -1; }
     std::vector<int> e2b((size_t)4 * (c->L + 1));
     for (int sp = 0; sp < 4; ++sp)
@@ -458,7 +640,12 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
                        hipMemcpyDeviceToDevice) == hipSuccess &&
              hipMemcpy(host.data(), inv_noise + row * c->npix, c->npix * sizeof(double), hipMemcpyDeviceToHost) ==
                  hipSuccess;
-        if (ok) c->mu[row] = *std::max_element(host.begin(), host.end()) + 1e-14;
+        if (ok) {
+            c->mu[row] = *std::max_element(host.begin(), host.end()) + 1e-14;
+            double acc = 0.0;
+            for (double v : host) acc += v;
+            c->nbar[row] = acc / (double)c->npix;
+        }
     }
     if (!ok) { mc_free(c); return set_error("gs_masked_create: copy failed"); }
     // second_part_grad = b * complex_to_real(map2alm(N^-1 d)) * Npix/(4 pi)  (CenteredGibbs.py:298-306)
@@ -499,6 +686,110 @@ int gs_masked_info(const gs_masked* c, double* mu3, double* second_part_grad) {
 int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, void* stream) {
     if (!c) return set_error("null masked context");
     return mc_gradient(c, dl, s, grad, pix, S(stream));
+}
+
+// ---- f1 PCG ----------------------------------------------------------------
+static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, hipStream_t st) {
+    if (mc_synth(c, x, c->pix0, st)) return -1;
+    const long long n = c->F * c->npix;
+    hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->ninv, c->pix0, c->y);
+    GS_LAUNCH_CHECK("k_mc_mul");
+    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
+    const dim3 g(nblocks(c->nlm, 256)), b(256);
+    if (c->F == 2) hipLaunchKernelGGL(k_pcg_qfinish<2>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
+    else hipLaunchKernelGGL(k_pcg_qfinish<3>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
+    GS_LAUNCH_CHECK("k_pcg_qfinish");
+    return 0;
+}
+
+static int pcg_dots(gs_masked* c, const double* a, const double* b, const double* d, const double* e, double* host2,
+                    hipStream_t st) {
+    const long long n = c->F * c->NR;
+    const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
+    hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(RED_BLOCK), 0, st, n, a, b, d, e, c->partial);
+    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(64), 0, st, nb, c->partial, c->dots);
+    GS_LAUNCH_CHECK("k_dot2");
+    GS_CHECK(hipMemcpyAsync(host2, c->dots, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    GS_CHECK(hipStreamSynchronize(st));
+    return 0;
+}
+
+int gs_masked_pcg_rhs(gs_masked* c, const double* dl, const double* zv, const double* zs, uint64_t seed,
+                      uint32_t iteration, int chain, double* rhs, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (!dl || !rhs) return set_error("gs_masked_pcg_rhs: null argument");
+    const hipStream_t st = S(stream);
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32), ch = (uint32_t)chain;
+    const long long n = c->F * c->npix;
+    hipLaunchKernelGGL(k_pcg_zpix, dim3(nblocks(n, 256)), dim3(256), 0, st, c->npix, c->F, c->rows, c->ninv, zv,
+                       slo, shi, ch, iteration, c->y);
+    GS_LAUNCH_CHECK("k_pcg_zpix");
+    // adjoint_synthesis_hp: map2alm with healpy's default iter = 3 (utils.py:89,104)
+    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 3, st)) return -1;
+    const dim3 g(nblocks(c->nlm, 256)), b(256);
+    const double resc = (double)c->npix / (4.0 * PI);
+    if (c->F == 2)
+        hipLaunchKernelGGL(k_pcg_rhs<2>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, zs, slo, shi, ch,
+                           iteration, rhs);
+    else
+        hipLaunchKernelGGL(k_pcg_rhs<3>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, zs, slo, shi, ch,
+                           iteration, rhs);
+    GS_LAUNCH_CHECK("k_pcg_rhs");
+    return 0;
+}
+
+int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
+                        int maxiter, int* iters, double* rel_residual, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (!dl || !rhs || !x) return set_error("gs_masked_pcg_solve: null argument");
+    const hipStream_t st = S(stream);
+    const long long n = c->F * c->NR;
+    // preconditioner: centered per-l block with kappa_f = nbar_f / w ("diag_cl")
+    double kap[3] = {0, 0, 0};
+    for (int k = 0; k < c->F; ++k) kap[k] = c->nbar[c->rows.r[k]] / c->w;
+    if (mc_params(c, dl, kap, c->params_pcg, st)) return -1;
+    if (x_is_guess) {
+        if (pcg_apply(c, dl, x, c->pq, st)) return -1;
+        hipLaunchKernelGGL(k_pcg_dir, dim3(nblocks(n, 256)), dim3(256), 0, st, n, -1.0, rhs, c->pq);   // pq = rhs - Qx
+        GS_CHECK(hipMemcpyAsync(c->pr, c->pq, n * sizeof(double), hipMemcpyDeviceToDevice, st));
+    } else {
+        GS_CHECK(hipMemsetAsync(x, 0, n * sizeof(double), st));
+        GS_CHECK(hipMemcpyAsync(c->pr, rhs, n * sizeof(double), hipMemcpyDeviceToDevice, st));
+    }
+    const dim3 gp(nblocks(c->NR, 256)), b(256);
+    auto prec = [&](const double* r, double* z) -> int {
+        if (c->F == 2) hipLaunchKernelGGL(k_pcg_prec<2>, gp, b, 0, st, c->L, c->params_pcg, r, z);
+        else hipLaunchKernelGGL(k_pcg_prec<3>, gp, b, 0, st, c->L, c->params_pcg, r, z);
+        GS_LAUNCH_CHECK("k_pcg_prec");
+        return 0;
+    };
+    if (prec(c->pr, c->pz)) return -1;
+    GS_CHECK(hipMemcpyAsync(c->pp, c->pz, n * sizeof(double), hipMemcpyDeviceToDevice, st));
+    double d2[2];
+    if (pcg_dots(c, rhs, rhs, c->pr, c->pz, d2, st)) return -1;
+    const double bn = sqrt(d2[0]);
+    double rz = d2[1];
+    if (pcg_dots(c, c->pr, c->pr, c->pr, c->pr, d2, st)) return -1;
+    double rn = sqrt(d2[0]);
+    int it = 0;
+    while (it < maxiter && rn > tol * bn) {
+        if (pcg_apply(c, dl, c->pp, c->pq, st)) return -1;
+        if (pcg_dots(c, c->pp, c->pq, c->pp, c->pq, d2, st)) return -1;
+        const double alpha = rz / d2[0];
+        hipLaunchKernelGGL(k_pcg_update, dim3(nblocks(n, 256)), dim3(256), 0, st, n, alpha, c->pp, c->pq, x, c->pr);
+        GS_LAUNCH_CHECK("k_pcg_update");
+        if (prec(c->pr, c->pz)) return -1;
+        if (pcg_dots(c, c->pr, c->pz, c->pr, c->pr, d2, st)) return -1;
+        const double beta = d2[0] / rz;
+        rz = d2[0];
+        rn = sqrt(d2[1]);
+        hipLaunchKernelGGL(k_pcg_dir, dim3(nblocks(n, 256)), dim3(256), 0, st, n, beta, c->pz, c->pp);
+        GS_LAUNCH_CHECK("k_pcg_dir");
+        ++it;
+    }
+    if (iters) *iters = it;
+    if (rel_residual) *rel_residual = bn > 0 ? rn / bn : 0.0;
+    return 0;
 }
 
 int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v, const double* zv, const double* zs,

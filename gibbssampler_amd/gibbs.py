@@ -16,12 +16,12 @@ centered full-sky runs go through its PCG branch (CenteredGibbs.py:845-850,
 qcinv); on the full sky with isotropic noise that system is diagonal and the
 closed form (CenteredGibbs.py:317-353) is its exact solution, which is what
 runs here.  Masked centered runs (``mask_path`` = mask array or .npy file)
-use the device SHT and the auxiliary-variable / over-relaxation / MALA
-samplers of gibbssampler_amd.masked (CenteredGibbs.py:494-850, the a12 flag
-ladder); the qcinv PCG (init CR and ``gibbs_cr=False, ula=False``) and the
-pixel-domain non-centered likelihood raise NotImplementedError (SURVEY.md 8f
-rows f1/f2).  Masked-only keywords: ``n_gibbs``, ``alpha``, ``tau``,
-``skymap_init`` (the start map the reference's PCG init would provide).
+use the device SHT and the PCG / auxiliary-variable / over-relaxation /
+MALA samplers of gibbssampler_amd.masked (CenteredGibbs.py:448-850, the a12
+flag ladder; the PCG is the init CR as at HEAD); the pixel-domain
+non-centered likelihood raises NotImplementedError (SURVEY.md 8f
+row f2).  Masked-only keywords: ``n_gibbs``, ``alpha``, ``tau``,
+``skymap_init`` (a start map instead of the reference's PCG init CR).
 
 Extra keyword arguments (all optional): ``nchains`` (batched chains on one
 GPU), ``rng`` ("native" Philox or "replay" = numpy's global RNG in the
@@ -263,9 +263,7 @@ class CenteredGibbs(GibbsSampler):
         runner = MaskedRunner(self.constrained_sampler, self.bins)
         F = self.nfields
         s0 = self.skymap_init
-        if s0 is None:
-            s0 = np.zeros((F, (self.lmax + 1) ** 2))
-        elif isinstance(s0, dict):
+        if isinstance(s0, dict):
             s0 = np.stack([np.asarray(s0[k]) for k in (("EE", "BB") if F == 2 else ("TT", "EE", "BB"))])
         init = dls_init if isinstance(dls_init, dict) else {self.spectra[0]: dls_init}
         return runner.run(init, self.n_iter, s0)

@@ -9,6 +9,7 @@ the same surface:
   overrelaxation_sampler(all_dls, s_old)         a10  CenteredGibbs.py:733-825
   sample_mala(all_dls, s_old)                    a11  CenteredGibbs.py:560-603
   compute_gradient_mala(all_dls, s_old)               CenteredGibbs.py:494-520
+  sample_mask(all_dls)                           f1   CenteredGibbs.py:448-491 (PCG)
   sample(all_dls, s_old=None)                    a12  CenteredGibbs.py:828-850
 
 All arithmetic runs in libgibbs_hip.so (gs_masked_cr + gs_sht); this module
@@ -34,7 +35,7 @@ class MaskedCR:
 
     def __init__(self, pix_map, noise_temp, noise_pol, bl, lmax, nside, mask=None, nfields=2, gibbs_cr=True,
                  n_gibbs=1, alpha=-0.995, overrelaxation=False, ula=False, tau=0.02, rng="replay", seed=0, chain=0,
-                 device="cuda"):
+                 device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000):
         if nfields not in (2, 3):
             raise ValueError("nfields must be 2 (EB, the reference) or 3 (TEB)")
         self.lib = _capi.load()
@@ -43,6 +44,8 @@ class MaskedCR:
         self.NR = (self.L + 1) ** 2
         self.gibbs_cr, self.overrelaxation, self.ula = bool(gibbs_cr), bool(overrelaxation), bool(ula)
         self.n_gibbs, self.alpha, self.tau = int(n_gibbs), float(alpha), float(tau)
+        self.pcg_accuracy, self.pcg_maxiter = float(pcg_accuracy), int(pcg_maxiter)   # CenteredGibbs.py:279-283
+        self.pcg_iterations = []
         if rng not in ("replay", "native"):
             raise ValueError(rng)
         self.rng, self.seed, self.chain = rng, int(seed), int(chain)
@@ -167,14 +170,47 @@ class MaskedCR:
         g, p = grad.cpu().numpy(), pix.cpu().numpy()
         return (*[g[i] for i in range(self.F)], *[p[i] for i in range(self.F)])
 
+    # -- f1: PCG ------------------------------------------------------------------------
+    def pcg_rhs(self, dl, iteration=None):
+        """right-hand side b A^T N^-1 d + fluctuations (device tensor [F, NR])."""
+        it = self.iteration if iteration is None else int(iteration)
+        zv = zs = None
+        if self.rng == "replay":      # CenteredGibbs.py:467-478: z_Q, z_U, then z_E, z_B
+            zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
+            zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
+        rhs = torch.empty((self.F, self.NR), dtype=torch.float64, device=self.device)
+        _capi.check(self.lib.gs_masked_pcg_rhs(self.handle, _capi.ptr(dl), _capi.ptr(zv), _capi.ptr(zs), self.seed,
+                                               it, self.chain, _capi.ptr(rhs), _capi.stream_ptr()),
+                    "gs_masked_pcg_rhs")
+        return rhs
+
+    def pcg_solve(self, dl, rhs, x=None, tol=None, maxiter=None):
+        guess = x is not None
+        x = torch.empty_like(rhs) if x is None else x
+        iters = ctypes.c_int()
+        res = ctypes.c_double()
+        _capi.check(self.lib.gs_masked_pcg_solve(self.handle, _capi.ptr(dl), _capi.ptr(rhs), _capi.ptr(x),
+                                                 int(guess), self.pcg_accuracy if tol is None else float(tol),
+                                                 self.pcg_maxiter if maxiter is None else int(maxiter),
+                                                 ctypes.byref(iters), ctypes.byref(res), _capi.stream_ptr()),
+                    "gs_masked_pcg_solve")
+        self.pcg_iterations.append(iters.value)
+        self.pcg_residual = res.value
+        return x
+
+    def sample_mask(self, all_dls):
+        """CenteredGibbs.py:448-491: PCG constrained realisation; accept 1."""
+        dl = self._dl(all_dls)
+        x = self.pcg_solve(dl, self.pcg_rhs(dl))
+        return self._out(x), 1
+
     def last_log_ratio(self):
         return float(self._lr.item())
 
     def sample(self, all_dls, s_old=None):
         """CenteredGibbs.py:828-850 (masked): the flag ladder."""
         if s_old is None:
-            raise NotImplementedError("the init CR without a previous map is the qcinv PCG (SURVEY.md 8 row f1); "
-                                      "pass a start map")
+            return self.sample_mask(all_dls)
         if self.gibbs_cr and self.overrelaxation:
             return self.overrelaxation_sampler(all_dls, s_old)
         if self.gibbs_cr and not self.ula:
@@ -183,7 +219,10 @@ class MaskedCR:
             return self._run(_capi.GS_MCR_AUX_MALA, all_dls, s_old)
         if self.ula:
             return self.sample_mala(all_dls, s_old)
-        raise NotImplementedError("PCG CR (sample_mask, qcinv) is SURVEY.md 8 row f1")
+        return self.sample_mask(all_dls)
+
+
+KIND_PCG = -1     # sample_mask (f1), driven from the host (CG loop)
 
 
 def cr_kind(gibbs_cr, overrelaxation, ula):
@@ -196,7 +235,7 @@ def cr_kind(gibbs_cr, overrelaxation, ula):
         return _capi.GS_MCR_AUX_MALA
     if ula:
         return _capi.GS_MCR_MALA
-    raise NotImplementedError("PCG CR (sample_mask, qcinv) is SURVEY.md 8 row f1")
+    return KIND_PCG
 
 
 class MaskedRunner:
@@ -229,13 +268,24 @@ class MaskedRunner:
         binned = {s: np.asarray(dls_init[s], dtype=np.float64) for s in self.spectra}
         h = {s: [binned[s].copy()] for s in self.spectra}
         acc, t_cr, t_cls = [], [], []
-        s = cr._s(s_init)
+        if s_init is None:
+            # GibbsSampler.py:136-138: the first CR is sample(dls) without a map ->
+            # the PCG (sample_mask), iteration 0 of the native streams
+            dl0 = self._unfold(binned)
+            s = cr.pcg_solve(dl0, cr.pcg_rhs(dl0, iteration=0))
+        else:
+            s = cr._s(s_init)
         for i in range(n_iter):
             it = i + 1
             cr.iteration = it
             t0 = time.perf_counter()
-            cr.step(self.kind, self._unfold(binned), s, iteration=it)
-            acc.append(int(cr._acc.item()))
+            dl = self._unfold(binned)
+            if self.kind == KIND_PCG:
+                s = cr.pcg_solve(dl, cr.pcg_rhs(dl, iteration=it))
+                acc.append(1)
+            else:
+                cr.step(self.kind, dl, s, iteration=it)
+                acc.append(int(cr._acc.item()))
             t1 = time.perf_counter()
             stats = plan.sweep_stats(self.d0, s[None])
             var = plan.replay_invgamma() if cr.rng == "replay" else None

@@ -213,6 +213,17 @@ int gs_masked_gradient(gs_masked* ctx, const double* dl, const double* s, double
 int gs_masked_cr(gs_masked* ctx, int kind, const double* dl, double* s, double* v, const double* zv, const double* zs,
                  const double* zm, const double* um, uint64_t seed, uint32_t iteration, int chain, int32_t* accept,
                  double* log_ratio, void* stream);
+/* f1: the PCG CR (sample_mask, CenteredGibbs.py:448-491).  rhs = b A^T N^-1 d
+ * + b adjoint_synthesis_hp(sqrt(N^-1) z_pix) (map2alm iter=3, utils.py:79-111)
+ * + C^-1/2 z_slot; solve (C^+ + b A^T N^-1 A b) x = rhs by preconditioned CG
+ * (per-l preconditioner (C^+ + b^2 nbar/w)^-1) until |r| <= tol |rhs|.
+ * zv [F][Npix], zs [F][NR]: replay normals (reference order z_Q, z_U, z_E,
+ * z_B) or NULL for the native streams.  The solve synchronises the stream once
+ * per CG iteration (convergence test on the host). */
+int gs_masked_pcg_rhs(gs_masked* ctx, const double* dl, const double* zv, const double* zs, uint64_t seed,
+                      uint32_t iteration, int chain, double* rhs, void* stream);
+int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
+                        int maxiter, int* iters, double* rel_residual, void* stream);
 
 #ifdef __cplusplus
 }

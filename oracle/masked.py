@@ -271,3 +271,103 @@ def sample_dispatch(mm, dl_unbinned, s_old, draws, gibbs_cr, overrelaxation_flag
         s, acc, _ = mala(mm, dl_unbinned, s_old, draws, noise_pol0, tau)
         return s, acc
     raise NotImplementedError("PCG CR (sample_mask, qcinv) is SURVEY.md 8 row f1")
+
+
+# ----------------------------------------------------------------------------
+# f1: PCG constrained realisation (CenteredGibbs.py:448-491)
+# ----------------------------------------------------------------------------
+SUB_PCG_S = 250       # CR substep of the PCG's C^-1/2 slot normals
+SUB_PCG_V = 254       # TAG_AUX_V substep of the PCG's pixel normals
+
+
+def _prior_pinv_apply(mm, dl_unbinned, x, half=False):
+    """C^+ x per slot (EB: inv_var; TEB: 2x2 TE pseudo-inverse + BB); with
+    half=True the factor (A^+)^T (covariance C^+) used for the C^-1/2 draw."""
+    ell = mm.slot_ell
+    if mm.F == 2:
+        var = H.var_from_dl(dl_unbinned)
+        f = (lambda v: np.sqrt(H.inv_var(v))) if half else H.inv_var
+        return np.stack([f(var[k][ell]) * x[k] for k in range(2)])
+    model = H.Model(mm.L, mm.nside, 3, mm.bl, [1.0, 1.0, 1.0], {s: np.arange(mm.L + 2) for s in H.SPECTRA[3]})
+    A = H.cov_chol(model, dl_unbinned)
+    Ai = H.chol_pinv(A)                                    # A^+ (lower)
+    out = np.zeros_like(x)
+    if half:                                               # (A^+)^T x
+        Ms = np.transpose(Ai, (0, 2, 1))
+        for f in range(3):
+            for g in range(3):
+                out[f] += Ms[ell, f, g] * x[g]
+        return out
+    P = np.einsum("lji,ljk->lik", Ai, Ai)                  # C^+ = (A^+)^T A^+
+    for f in range(3):
+        for g in range(3):
+            out[f] += P[ell, f, g] * x[g]
+    return out
+
+
+def pcg_fluctuation(mm, dl_unbinned, z_pix, z_slot):
+    """b_fluctuations (CenteredGibbs.py:467-482): b * adjoint_synthesis_hp(sqrt(N^-1) z_pix)
+    (utils.py:79-111: map2alm iter=3 times Npix/4pi) + C^-1/2 z_slot."""
+    y = np.stack([np.sqrt(mm.inv_noise[r]) * z_pix[k] for k, r in enumerate(mm.rows)])
+    full = np.zeros((3, mm.Npix))
+    for k, r in enumerate(mm.rows):
+        full[r] = y[k]
+    a = O.map2alm(full, mm.nside, mm.L, iter=3)
+    adj = np.stack([H.complex_to_real(a[r], mm.L) for r in mm.rows]) * (mm.Npix / FOURPI)
+    return adj * mm.bl[mm.slot_ell][None] + _prior_pinv_apply(mm, dl_unbinned, z_slot, half=True)
+
+
+def pcg_operator(mm, dl_unbinned, x):
+    """Q x = C^+ x + b A^T N^-1 A b x, A^T = map2alm(iter=0) / w (exact adjoint)."""
+    pix = mm.synth(x)
+    nq = np.stack([mm.inv_noise[r] * pix[k] for k, r in enumerate(mm.rows)])
+    return _prior_pinv_apply(mm, dl_unbinned, x) + (mm.analysis(nq) / mm.w) * mm.bl[mm.slot_ell][None]
+
+
+def pcg_solve(mm, dl_unbinned, rhs, tol=1e-12, maxiter=2000, x0=None):
+    """Preconditioned CG on Q x = rhs; preconditioner (C^+ + diag(b^2 nbar/w))^-1
+    per l (nbar = mean N^-1 of the field's map).  Stops at |r| <= tol |rhs|."""
+    nbar = [mm.inv_noise[r].mean() for r in mm.rows]
+    model = H.Model(mm.L, mm.nside, mm.F, mm.bl, [1.0 / n if n > 0 else 1e300 for n in nbar],
+                    {s: np.arange(mm.L + 2) for s in H.SPECTRA[mm.F]})
+    _, Lc = H.centered_params(model, dl_unbinned)
+    ell = mm.slot_ell
+
+    def prec(r):
+        t = np.zeros_like(r)
+        for f in range(mm.F):                      # L^T r
+            for g in range(mm.F):
+                t[f] += Lc[ell, g, f] * r[g]
+        out = np.zeros_like(r)
+        for f in range(mm.F):                      # L (L^T r)
+            for g in range(mm.F):
+                out[f] += Lc[ell, f, g] * t[g]
+        return out
+
+    x = np.zeros_like(rhs) if x0 is None else np.array(x0, dtype=np.float64)
+    r = rhs - pcg_operator(mm, dl_unbinned, x)
+    z = prec(r)
+    p = z.copy()
+    rz = float(np.sum(r * z))
+    bn = float(np.sqrt(np.sum(rhs * rhs)))
+    it = 0
+    while it < maxiter and np.sqrt(np.sum(r * r)) > tol * bn:
+        q = pcg_operator(mm, dl_unbinned, p)
+        alpha = rz / float(np.sum(p * q))
+        x = x + alpha * p
+        r = r - alpha * q
+        z = prec(r)
+        rz_new = float(np.sum(r * z))
+        p = z + (rz_new / rz) * p
+        rz = rz_new
+        it += 1
+    return x, it
+
+
+def pcg_sample(mm, dl_unbinned, draws, tol=1e-12, maxiter=2000):
+    """sample_mask: rhs = b A^T N^-1 d + fluctuations; x = Q^-1 rhs; accept 1."""
+    z_pix = draws.pixel_normals(mm.F, mm.Npix, maps=mm.rows, substep=SUB_PCG_V)
+    z_slot = draws.slot_normals(mm.F, (mm.L + 1) ** 2, substep=SUB_PCG_S)
+    rhs = mm.second_part_grad() + pcg_fluctuation(mm, dl_unbinned, z_pix, z_slot)
+    x, it = pcg_solve(mm, dl_unbinned, rhs, tol, maxiter)
+    return x, 1, it

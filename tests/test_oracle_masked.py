@@ -116,3 +116,27 @@ def test_masked_centered_driver(g):
             hist[sp].append(binned[sp])
     for sp in ("EE", "BB"):
         _close(np.array(hist[sp]), g["drv_h_" + sp])
+
+
+def test_f1_pcg_fluctuations(g):
+    """the PCG right-hand-side fluctuations match what the reference hands
+    qcinv (captured by tools/gen_golden_masked.py), same numpy draws."""
+    mm = _mm(g)
+    np.random.seed(int(g["pcg_seed"]))
+    d = MK.ReplayDraws()
+    zp = d.pixel_normals(2, mm.Npix)
+    zs = d.slot_normals(2, (mm.L + 1) ** 2)
+    bf = MK.pcg_fluctuation(mm, _dl(g), zp, zs)
+    _close(bf[0], g["pcg_bfluct_E"])
+    _close(bf[1], g["pcg_bfluct_B"])
+
+
+def test_f1_pcg_solves_the_system(g):
+    mm = _mm(g)
+    rng = np.random.default_rng(1)
+    rhs = rng.standard_normal((2, (mm.L + 1) ** 2)) * 10
+    rhs[:, mm.slot_ell < 2] = 0.0        # spin-2: Q is singular on l < 2 (no prior, no data)
+    x, it = MK.pcg_solve(mm, _dl(g), rhs, tol=1e-12)
+    res = MK.pcg_operator(mm, _dl(g), x) - rhs
+    assert np.abs(res).max() < 1e-9 * np.abs(rhs).max()
+    assert it < 500
