@@ -109,6 +109,9 @@ _SIGS = [
                                          _VP]),
     ("gs_masked_pcg_solve", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_double, ctypes.c_int, c_int_p,
                                            c_double_p, _VP]),
+    ("gs_masked_center", ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
+    ("gs_masked_nc_loglik", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("gs_mh_propose", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP, _VP, _VP]),
     ("gs_masked_cr", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,
                                     ctypes.c_uint32, ctypes.c_int, _VP, _VP, _VP]),
 ]

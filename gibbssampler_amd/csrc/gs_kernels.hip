@@ -705,6 +705,27 @@ __global__ __launch_bounds__(256) void k_mh_accept(int L, int nchains, int maxbi
     }
 }
 
+// the native accept uniforms of every (chain, spectrum, block, attempt) in the
+// flat accept order of the plan (same counters as k_mh_fused / k_mh_accept)
+__global__ void k_mh_uniforms(int nchains, int nspec, int maxbins, const int* __restrict__ meta, int nacc,
+                              int n_iter_mh, uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, int chain0,
+                              double* __restrict__ out) {
+    const uint32_t iter = itarg.get();
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= (long long)nchains * nacc) return;
+    const int chain = (int)(g / nacc), flat = (int)(g % nacc);
+    const int* nblocks = meta + 4;
+    const int* acc_off = meta + 8;
+    int sp = -1;
+    for (int k = 0; k < nspec; ++k)
+        if (flat >= acc_off[k] && flat < acc_off[k] + nblocks[k] * n_iter_mh) sp = k;
+    if (sp < 0) return;
+    const int r = flat - acc_off[sp];
+    const int blk = r / n_iter_mh, att = r % n_iter_mh;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    out[g] = uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
+}
+
 // MH phases fused in one launch: one workgroup per chain walks the phases;
 // per phase the per-l terms go to LDS, the per-(block, attempt) uniforms are
 // drawn in parallel, blocks of <= 16 l are decided by one thread each and
@@ -1338,6 +1359,31 @@ int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_
 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
                      uint32_t iteration, int32_t* accept_out, void* stream);
+
+int gs_mh_propose(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t iteration,
+                  double* prop_out, double* logr_out, double* u_acc_out, void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->has_mh) return set_error("gs_mh_propose: plan has no MH blocks / proposal variances");
+    if (!dl || !prop_out || !logr_out) return set_error("gs_mh_propose: null argument");
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
+    GS_CHECK(hipMemsetAsync(prop_out, 0, nprop * sizeof(double), S(stream)));
+    GS_CHECK(hipMemsetAsync(logr_out, 0, nprop * sizeof(double), S(stream)));
+#define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
+                                     p->maxbins, p->meta, p->prop_sd, dl, prop_out, logr_out, u_prop, slo, shi,     \
+                                     IterArg{iteration, p->itp()}, p->chain0)
+    if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
+#undef GS_MP
+    GS_LAUNCH_CHECK("k_mh_propose");
+    if (u_acc_out) {
+        const long long n = (long long)p->nchains * p->nacc;
+        hipLaunchKernelGGL(k_mh_uniforms, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->nchains, p->nspec,
+                           p->maxbins, p->meta, p->nacc, p->n_iter_mh, slo, shi, IterArg{iteration, p->itp()},
+                           p->chain0, u_acc_out);
+        GS_LAUNCH_CHECK("k_mh_uniforms");
+    }
+    return 0;
+}
 
 int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, const double* u_acc, uint64_t seed,
              uint32_t iteration, int32_t* accept_out, void* stream) {

@@ -471,6 +471,69 @@ __global__ void k_dot2_finish(int nblk, const double* __restrict__ partial, doub
     out[1] = s1;
 }
 
+// ---------------------------------------------------------------------------
+// f2: pixel-domain non-centered likelihood (NonCenteredGibbs.py:333-355)
+// ---------------------------------------------------------------------------
+// out = C^(dir/2) in per slot: dir = +1 the centered map C^1/2 s_nc (EB
+// sqrt(var), TEB chol(C)); dir = -1 the non-centered map C^+1/2 s (EB
+// sqrt(inv_var) (NonCenteredGibbs.py:236-237, ASIS.py:185-189), TEB A^+)
+template <int F>
+__global__ void k_mc_center(int L, const double* __restrict__ dl, int dir, const double* __restrict__ in,
+                            double* __restrict__ out) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= NR) return;
+    int l;
+    if (g <= L) l = (int)g;
+    else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
+    if constexpr (F == 2) {
+        for (int f = 0; f < 2; ++f) {
+            const double v = var_from_dl(dl[f * (L + 1) + l], l);
+            const double fac = dir > 0 ? sqrt(v) : (v != 0.0 ? sqrt(1.0 / v) : 0.0);
+            out[f * NR + g] = fac * in[f * NR + g];
+        }
+    } else {
+        const double tt = var_from_dl(dl[l], l), ee = var_from_dl(dl[(L + 1) + l], l);
+        const double bb = var_from_dl(dl[2 * (L + 1) + l], l), te = var_from_dl(dl[3 * (L + 1) + l], l);
+        const CovChol A = cov_chol_teb(tt, ee, te, bb);
+        const double x0 = in[g], x1 = in[NR + g], x2 = in[2 * NR + g];
+        if (dir > 0) {
+            out[g] = A.a00 * x0;
+            out[NR + g] = A.a10 * x0 + A.a11 * x1;
+            out[2 * NR + g] = A.aB * x2;
+        } else {
+            const double i00 = A.a00 != 0.0 ? 1.0 / A.a00 : 0.0, i11 = A.a11 != 0.0 ? 1.0 / A.a11 : 0.0;
+            const double t10 = -A.a10 * i00 * i11, iB = A.aB != 0.0 ? 1.0 / A.aB : 0.0;
+            out[g] = i00 * x0;
+            out[NR + g] = t10 * x0 + i11 * x1;
+            out[2 * NR + g] = iB * x2;
+        }
+    }
+}
+
+// partial sums of N^-1 (d - m)^2 over all field rows
+__global__ __launch_bounds__(RED_BLOCK) void k_mc_resid(long long n, const double* __restrict__ d,
+                                                        const double* __restrict__ m, const double* __restrict__ w,
+                                                        double* __restrict__ partial) {
+    double s0 = 0.0;
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x) {
+        const double r = d[g] - m[g];
+        s0 += r * r * w[g];
+    }
+    __shared__ double red[RED_BLOCK];
+    red[threadIdx.x] = s0;
+    __syncthreads();
+    for (int h = RED_BLOCK / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { partial[2 * blockIdx.x] = red[0]; partial[2 * blockIdx.x + 1] = 0.0; }
+}
+
+__global__ void k_mc_halfneg(const double* __restrict__ two, double* __restrict__ out) {
+    if (threadIdx.x == 0) *out = -0.5 * two[0];
+}
+
 }  // namespace
 
 // ============================================================================
@@ -789,6 +852,32 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
     }
     if (iters) *iters = it;
     if (rel_residual) *rel_residual = bn > 0 ? rn / bn : 0.0;
+    return 0;
+}
+
+// ---- f2 --------------------------------------------------------------------
+int gs_masked_center(gs_masked* c, const double* dl, int dir, const double* in, double* out, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (!dl || !in || !out) return set_error("gs_masked_center: null argument");
+    const dim3 g(nblocks(c->NR, 256)), b(256);
+    if (c->F == 2) hipLaunchKernelGGL(k_mc_center<2>, g, b, 0, S(stream), c->L, dl, dir, in, out);
+    else hipLaunchKernelGGL(k_mc_center<3>, g, b, 0, S(stream), c->L, dl, dir, in, out);
+    GS_LAUNCH_CHECK("k_mc_center");
+    return 0;
+}
+
+int gs_masked_nc_loglik(gs_masked* c, const double* dl, const double* s_nc, double* lik, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (!dl || !s_nc || !lik) return set_error("gs_masked_nc_loglik: null argument");
+    const hipStream_t st = S(stream);
+    if (gs_masked_center(c, dl, +1, s_nc, c->snew, stream)) return -1;
+    if (mc_synth(c, c->snew, c->pix1, st)) return -1;
+    const long long n = c->F * c->npix;
+    const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
+    hipLaunchKernelGGL(k_mc_resid, dim3(nb), dim3(RED_BLOCK), 0, st, n, c->dpix, c->pix1, c->ninv, c->partial);
+    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(64), 0, st, nb, c->partial, c->dots);
+    hipLaunchKernelGGL(k_mc_halfneg, dim3(1), dim3(64), 0, st, c->dots, lik);
+    GS_LAUNCH_CHECK("k_mc_resid");
     return 0;
 }
 

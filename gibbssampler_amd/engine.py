@@ -202,6 +202,15 @@ class GibbsPlan:
                                      C.ptr(out), self._s()), "gs_cls_draw")
         return out
 
+    def mh_propose(self, dl, u_prop=None, seed=0, iteration=0, with_uniforms=False):
+        """(prop, logr[, native accept uniforms]) of the NC MH step (no decisions)."""
+        prop = self.zeros(self.nchains, self.nspec, self.maxbins)
+        logr = self.zeros(self.nchains, self.nspec, self.maxbins)
+        ua = self.zeros(self.nchains, max(self.nacc, 1)) if with_uniforms else None
+        C.check(self.lib.gs_mh_propose(self._h, C.ptr(dl), C.ptr(u_prop), int(seed), int(iteration), C.ptr(prop),
+                                       C.ptr(logr), C.ptr(ua), self._s()), "gs_mh_propose")
+        return prop, logr, ua
+
     def nc_mh(self, stats, dl, u_prop=None, u_acc=None, seed=0, iteration=0, accept=None):
         accept = self.zeros(self.nchains, max(self.nacc, 1), dtype=torch.int32) if accept is None else accept
         C.check(self.lib.gs_nc_mh(self._h, C.ptr(stats), C.ptr(dl), C.ptr(u_prop), C.ptr(u_acc), int(seed),

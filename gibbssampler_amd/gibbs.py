@@ -108,9 +108,6 @@ class GibbsSampler:
                  metropolis_blocks=None, n_iter_metropolis=1, mask_path=None):
         self.mask = None
         if mask_path is not None:
-            if self._kind != "centered":
-                raise NotImplementedError("masked non-centered / ASIS runs need the pixel-domain MH likelihood "
-                                          "(NonCenteredGibbs.py:333-355; SURVEY.md 8 row f2)")
             self.mask = _load_mask(mask_path, nside)
         self.noise = noise
         self.beam = beam_fwhm_deg
@@ -193,6 +190,29 @@ class GibbsSampler:
                                          n_iter_metropolis=self.n_iter_metropolis)
         return self._runner
 
+    def _masked_cr(self, noise_temp, noise_pol, gibbs_cr=False, n_gibbs=1, alpha=-0.995, overrelaxation=False,
+                   ula=False, tau=0.02):
+        from .masked import MaskedCR
+        if not self.polarization:
+            raise NotImplementedError("masked temperature-only runs: the reference's TT masked path is broken "
+                                      "at HEAD (SURVEY.md Appendix B.7); use fields='TEB'")
+        if self.nchains != 1:
+            raise NotImplementedError("masked runs batch one chain per process (shard chains over GPUs)")
+        return MaskedCR(self.pix_map, noise_temp, noise_pol, self.bl_gauss, self.lmax, self.nside, mask=self.mask,
+                        nfields=self.nfields, gibbs_cr=gibbs_cr, n_gibbs=n_gibbs, alpha=alpha,
+                        overrelaxation=overrelaxation, ula=ula, tau=tau, rng=self.rng, seed=self.seed,
+                        chain=self.chain0)
+
+    def _masked_mh_runner(self, kind, cr, cr_kind_):
+        from .masked import MaskedMHRunner
+        if self.nfields != 2:
+            raise NotImplementedError("masked non-centred sampling is the reference's EB model "
+                                      "(PolarizationNonCenteredClsSampler, NonCenteredGibbs.py:255-445)")
+        blocks = self.metropolis_blocks if self.metropolis_blocks is not None else _default_blocks(self.bins)
+        return MaskedMHRunner(kind, cr, self.bins, {s: np.asarray(blocks[s]) for s in self.spectra},
+                              self.proposal_variances, self.n_iter_metropolis, cr_kind_=cr_kind_,
+                              quirk=self.reference_quirks)
+
     def _squeeze(self, a):
         return a[:, 0] if self.nchains == 1 else a
 
@@ -243,23 +263,15 @@ class CenteredGibbs(GibbsSampler):
         self.overrelaxation = overrelaxation
         self.cr_ula = ula
         if self.mask is not None:
-            from .masked import MaskedCR
-            if not polarization:
-                raise NotImplementedError("masked temperature-only runs: the reference's TT masked path is broken "
-                                          "at HEAD (SURVEY.md Appendix B.7); use fields='TEB'")
-            self.constrained_sampler = MaskedCR(pix_map, noise_temp, noise_pol, self.bl_gauss, lmax, nside,
-                                                mask=self.mask, nfields=self.nfields, gibbs_cr=gibbs_cr,
-                                                n_gibbs=self.n_gibbs, alpha=self.alpha,
-                                                overrelaxation=overrelaxation, ula=ula, tau=self.tau, rng=self.rng,
-                                                seed=self.seed, chain=self.chain0)
+            self.constrained_sampler = self._masked_cr(noise_temp, noise_pol, gibbs_cr=gibbs_cr, n_gibbs=self.n_gibbs,
+                                                       alpha=self.alpha, overrelaxation=overrelaxation, ula=ula,
+                                                       tau=self.tau)
         else:
             self.constrained_sampler = CenteredConstrainedRealization(self)
         self.cls_sampler = CenteredClsSampler(self)
 
     def _run_masked(self, dls_init):
         from .masked import MaskedRunner
-        if self.nchains != 1:
-            raise NotImplementedError("masked runs batch one chain per process (shard chains over GPUs)")
         runner = MaskedRunner(self.constrained_sampler, self.bins)
         F = self.nfields
         s0 = self.skymap_init
@@ -297,9 +309,18 @@ class NonCenteredGibbs(GibbsSampler):
         self.all_sph = all_sph
         self.constrained_sampler = NonCenteredConstrainedRealization(self)
         self.cls_sampler = NonCenteredClsSampler(self)
+        if self.mask is not None:
+            # NonCenteredGibbs.py:104-131,178-196: PCG in the centred parametrisation, then C^-1/2
+            from .masked import KIND_PCG
+            self.masked_cr = self._masked_cr(noise_I, noise_Q)
+            self.masked_runner = self._masked_mh_runner("noncentered", self.masked_cr, KIND_PCG)
+            self.cls_sampler = self.masked_runner.mh
 
     def run_polarization(self, dls_init):
         """NonCenteredGibbs.py:529-571: (h_dls, total_accept, h_duration_cr, h_duration_cls)."""
+        if self.mask is not None:
+            h, acc = self.masked_runner.run(dls_init, self.n_iter)[:2]
+            return h, acc, np.array([]), np.array([])
         h, acc, t = self._run_common(dls_init)
         return h, acc, np.array([]), np.array([])
 
@@ -328,10 +349,23 @@ class ASIS(GibbsSampler):
         self.constrained_sampler.n_gibbs = n_gibbs
         self.centered_cls_sampler = CenteredClsSampler(self)
         self.non_centered_cls_sampler = NonCenteredClsSampler(self)
+        if self.mask is not None:
+            # ASIS.py:55-66: PolarizedCenteredConstrainedRealization(gibbs_cr, n_gibbs, overrelaxation) with its
+            # default ula=True (CenteredGibbs.py:243-244); PCG unless gibbs_cr / rj_step (ASIS.py:153-170)
+            from .masked import KIND_PCG, cr_kind
+            self.masked_cr = self._masked_cr(noise, noise_Q, gibbs_cr=gibbs_cr, n_gibbs=n_gibbs,
+                                             overrelaxation=overrelaxation, ula=True)
+            kind = cr_kind(gibbs_cr, overrelaxation, True) if (gibbs_cr or rj_step) else KIND_PCG
+            self.masked_runner = self._masked_mh_runner("asis", self.masked_cr, kind)
+            self.constrained_sampler = self.masked_cr
+            self.non_centered_cls_sampler = self.masked_runner.mh
 
     def run_polarization(self, dls_init):
         """ASIS.py:134-226: (h_dls, total_accept, accept_cr|None, h_iteration_duration,
         h_duration_cr, h_duration_cls_sampling, h_duration_cls_nc_sampling)."""
+        if self.mask is not None:
+            h, acc, acc_cr, t_it, t_cr, t_cls, t_nc = self.masked_runner.run(dls_init, self.n_iter)
+            return h, acc, (acc_cr if self.rj_step else None), t_it, t_cr, t_cls, t_nc
         h, acc, t = self._run_common(dls_init)
         z = np.zeros(len(t))
         return h, acc, None, np.asarray(t), z, z, z

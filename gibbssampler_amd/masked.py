@@ -252,7 +252,7 @@ class MaskedRunner:
         F = cr.F
         self.spectra = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
         self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
-        self.plan = GibbsPlan(cr.L, cr.nside, F, 1, cr.bl, [1.0] * F, self.bins)
+        self.plan = GibbsPlan(cr.L, cr.nside, F, 1, cr.bl, [1.0] * F, self.bins, chain0=cr.chain)
         self.d0 = self.plan.zeros(F, cr.NR)
 
     def _unfold(self, binned):
@@ -297,3 +297,193 @@ class MaskedRunner:
                 h[sp].append(binned[sp])
         self.s = s
         return {sp: np.array(v) for sp, v in h.items()}, np.array(acc), np.array(t_cr), np.array(t_cls)
+
+
+# ---------------------------------------------------------------------------------------
+# f2: pixel-domain non-centred likelihood (masked NonCenteredGibbs / ASIS)
+# ---------------------------------------------------------------------------------------
+class PixelMH:
+    """PolarizationNonCenteredClsSampler.sample with all_sph=False
+    (NonCenteredGibbs.py:401-445): truncated-normal proposals for every bin
+    (gs_mh_propose), then per Metropolis block the whole-map likelihood
+    -1/2 sum_pix N^-1 (d - A b C^1/2 s_nc)^2 (compute_log_likelihood,
+    NonCenteredGibbs.py:333-355) evaluated on the device by
+    gs_masked_nc_loglik (one C^1/2 scaling + one SHT synthesis + one
+    reduction).  The accept test needs the scalar on the host (one sync per
+    block, as the reference's own loop); everything else stays resident.
+    Replay: numpy draws truncnorm EE, BB then one uniform per block attempt,
+    the reference's order (the likelihood draws nothing)."""
+
+    def __init__(self, cr, bins, blocks, proposal_variances, n_iter_metropolis=1):
+        from .engine import GibbsPlan, MH_ORDER
+        if cr.F != 2:
+            raise NotImplementedError("the pixel-domain NC sampler is the reference's EB model "
+                                      "(PolarizationNonCenteredClsSampler); TEB masked NC is not defined there")
+        self.cr = cr
+        self.spectra = ("EE", "BB")
+        self.order = MH_ORDER[2]
+        self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
+        self.blocks = {s: np.asarray(blocks[s]) for s in self.spectra}
+        self.n_iter = int(n_iter_metropolis)
+        self.plan = GibbsPlan(cr.L, cr.nside, 2, 1, cr.bl, [1.0, 1.0], self.bins, blocks=self.blocks,
+                              proposal_variances=proposal_variances, chain0=cr.chain,
+                              n_iter_metropolis=self.n_iter)
+        L = cr.L
+        idx = np.full((2, L + 1), -1, dtype=np.int64)
+        for k, s in enumerate(self.spectra):
+            b = self.bins[s]
+            for i in range(len(b) - 1):
+                idx[k, b[i]:min(b[i + 1], L + 1)] = i
+        self._idx = torch.from_numpy(np.maximum(idx, 0)).to(cr.device)
+        self._valid = torch.from_numpy(idx >= 0).to(cr.device)
+        self._lik = torch.zeros(1, dtype=torch.float64, device=cr.device)
+
+    def unfold(self, binned_t):
+        """utils.unfold_bins on the device: [2, maxbins] -> [2, L+1]."""
+        return torch.where(self._valid, torch.gather(binned_t, 1, self._idx), 0.0).contiguous()
+
+    def noncentre(self, dl_unbinned, s):
+        """s_nc = C^-1/2 s (zero where C = 0; NonCenteredGibbs.py:186-191, ASIS.py:184-190)."""
+        out = torch.empty_like(s)
+        _capi.check(self.cr.lib.gs_masked_center(self.cr.handle, _capi.ptr(dl_unbinned), -1, _capi.ptr(s),
+                                                 _capi.ptr(out), _capi.stream_ptr()), "gs_masked_center")
+        return out
+
+    def centre(self, dl_unbinned, s):
+        """C^1/2 s."""
+        out = torch.empty_like(s)
+        _capi.check(self.cr.lib.gs_masked_center(self.cr.handle, _capi.ptr(dl_unbinned), 1, _capi.ptr(s),
+                                                 _capi.ptr(out), _capi.stream_ptr()), "gs_masked_center")
+        return out
+
+    def loglik_t(self, dl_unbinned, s_nc):
+        _capi.check(self.cr.lib.gs_masked_nc_loglik(self.cr.handle, _capi.ptr(dl_unbinned), _capi.ptr(s_nc),
+                                                    _capi.ptr(self._lik), _capi.stream_ptr()),
+                    "gs_masked_nc_loglik")
+        return self._lik
+
+    def compute_log_likelihood(self, dls, s_nonCentered):
+        """NonCenteredGibbs.py:333-355 (binned dict, dict / array map) -> float."""
+        bt = self.plan.dl_tensor(dls)[0]
+        return float(self.loglik_t(self.unfold(bt), self.cr._s(s_nonCentered)).item())
+
+    def sample_t(self, s_nc, binned_t, iteration):
+        """one sweep on device tensors: binned_t [2, maxbins] (updated copy
+        returned), s_nc [2, NR]; returns (binned_t, accept dict of lists)."""
+        plan, cr = self.plan, self.cr
+        dl = binned_t[None].contiguous()
+        if cr.rng == "replay":
+            up, ua = plan.replay_mh_uniforms()
+            prop, logr, _ = plan.mh_propose(dl, up, seed=cr.seed, iteration=iteration)
+            ua_h = ua[0].cpu().numpy()
+        else:
+            prop, logr, ua = plan.mh_propose(dl, None, seed=cr.seed, iteration=iteration, with_uniforms=True)
+            ua_h = ua[0].cpu().numpy()
+        prop, logr_h = prop[0], logr[0].cpu().numpy()
+        cur = binned_t.clone()
+        old_lik = float(self.loglik_t(self.unfold(cur), s_nc).item())
+        accept = {s: [] for s in self.spectra}
+        ui = 0
+        for s in self.order:
+            k = self.spectra.index(s)
+            blocks = self.blocks[s]
+            for bi in range(len(blocks) - 1):
+                lo, hi = int(blocks[bi]), int(blocks[bi + 1])
+                lr_all = float(np.sum(logr_h[k, lo:hi]))
+                for _ in range(self.n_iter):
+                    new = cur.clone()
+                    new[k, lo:hi] = prop[k, lo:hi]
+                    new_lik = float(self.loglik_t(self.unfold(new), s_nc).item())
+                    log_r = (new_lik - old_lik) + lr_all
+                    if np.log(ua_h[ui]) < log_r:
+                        cur, old_lik = new, new_lik
+                        accept[s].append(1)
+                    else:
+                        accept[s].append(0)
+                    ui += 1
+        return cur, accept
+
+    def sample(self, s_nonCentered, binned_dls_old, iteration=None):
+        """reference surface: dict maps / binned dicts in, (binned dict, accept dict) out."""
+        it = self.cr.iteration if iteration is None else int(iteration)
+        bt = self.plan.dl_tensor(binned_dls_old)[0]
+        cur, acc = self.sample_t(self.cr._s(s_nonCentered), bt, it)
+        return self.plan.dl_dicts(cur[None])[0], acc
+
+
+class MaskedMHRunner:
+    """Masked non-centred and interweaving drivers on one chain:
+
+    kind "noncentered": NonCenteredClsSampler.run_polarization
+      (NonCenteredGibbs.py:529-571) -- per iteration the PCG CR in the centred
+      parametrisation, s_nc = C^-1/2 s (sample_mask, :178-196), pixel MH.
+    kind "asis": ASIS.run_polarization (ASIS.py:134-226) -- the masked CR
+      ladder (PCG, or the a9-a12 samplers with a start map from the PCG),
+      centred C_l draw, non-centring with the intermediate D_l, pixel MH, and
+      the re-centring of ASIS.py:201-203 (``quirk``: the reference scales the
+      CENTRED map by C_new^1/2; otherwise C_new^1/2 s_nc)."""
+
+    def __init__(self, kind, cr, bins, blocks, proposal_variances, n_iter_metropolis=1, cr_kind_=KIND_PCG,
+                 quirk=True):
+        if kind not in ("noncentered", "asis"):
+            raise ValueError(kind)
+        self.kind, self.cr, self.quirk = kind, cr, bool(quirk)
+        self.mh = PixelMH(cr, bins, blocks, proposal_variances, n_iter_metropolis)
+        self.cr_kind = cr_kind_ if kind == "asis" else KIND_PCG
+        self.plan = self.mh.plan
+        self.d0 = self.plan.zeros(2, cr.NR)
+
+    def _pcg(self, dl, it):
+        return self.cr.pcg_solve(dl, self.cr.pcg_rhs(dl, iteration=it))
+
+    def run(self, dls_init, n_iter):
+        cr, mh, plan = self.cr, self.mh, self.plan
+        cur = plan.dl_tensor({s: np.asarray(dls_init[s], dtype=np.float64) for s in mh.spectra})[0]
+        h = {s: [np.asarray(dls_init[s], dtype=np.float64).copy()] for s in mh.spectra}
+        acc = {s: [] for s in mh.spectra}
+        acc_cr, t_it, t_cr, t_cls, t_nc = [], [], [], [], []
+        dl = mh.unfold(cur)
+        s = None
+        if self.kind == "asis" and self.cr_kind != KIND_PCG:
+            s = self._pcg(dl, 0)          # ASIS.py:153-156: the start map from the PCG
+        for i in range(n_iter):
+            it = i + 1
+            cr.iteration = it
+            t0 = time.perf_counter()
+            if self.kind == "noncentered":
+                s = self._pcg(dl, it)
+                s_nc = mh.noncentre(dl, s)
+                t1 = time.perf_counter()
+                cur, a = mh.sample_t(s_nc, cur, it)
+                t2 = t1
+            else:
+                if self.cr_kind == KIND_PCG:
+                    s = self._pcg(dl, it)
+                else:
+                    cr.step(self.cr_kind, dl, s, iteration=it)
+                    acc_cr.append(int(cr._acc.item()))
+                t1 = time.perf_counter()
+                stats = plan.sweep_stats(self.d0[None], s[None])
+                var = plan.replay_invgamma() if cr.rng == "replay" else None
+                tmp = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)[0]
+                dl_tmp = mh.unfold(tmp)
+                s_nc = mh.noncentre(dl_tmp, s)
+                t2 = time.perf_counter()
+                cur, a = mh.sample_t(s_nc, tmp, it)
+                dl = mh.unfold(cur)
+                s = mh.centre(dl, s if self.quirk else s_nc)
+            if self.kind == "noncentered":
+                dl = mh.unfold(cur)
+            t3 = time.perf_counter()
+            b = plan.dl_dicts(cur[None])[0]
+            for sp in mh.spectra:
+                acc[sp].append(a[sp])
+                h[sp].append(b[sp])
+            t_it.append(t3 - t0)
+            t_cr.append(t1 - t0)
+            t_cls.append(t2 - t1)
+            t_nc.append(t3 - t2)
+        self.s = s
+        out = ({sp: np.array(v) for sp, v in h.items()}, {sp: np.array(v) for sp, v in acc.items()})
+        return out + (np.array(acc_cr) if acc_cr else None, np.array(t_it), np.array(t_cr), np.array(t_cls),
+                      np.array(t_nc))

@@ -121,6 +121,12 @@ int gs_sweep_stats(gs_plan* plan, const double* d_alm, const double* s, double* 
 int gs_cls_draw(gs_plan* plan, const double* stats, const double* invgamma_replay,
                 uint64_t seed, uint32_t iteration, double* dl_binned_out, void* stream);
 /* non-centered Metropolis-within-Gibbs over blocks (in/out dl_binned) */
+/* proposals of the NC Metropolis step (NonCenteredGibbs.py:292-330) into caller
+ * buffers [nchains][nspec][maxbins] (prop, log proposal ratio) and, when
+ * u_acc_out != NULL, the native accept uniforms [nchains][nacc]; used by the
+ * pixel-domain (masked) MH whose block loop needs a full SHT per block. */
+int gs_mh_propose(gs_plan* plan, const double* dl, const double* u_prop, uint64_t seed, uint32_t iteration,
+                  double* prop_out, double* logr_out, double* u_acc_out, void* stream);
 int gs_nc_mh(gs_plan* plan, const double* stats, double* dl_binned,
              const double* u_prop_replay, const double* u_accept_replay,
              uint64_t seed, uint32_t iteration, int32_t* accept_out, void* stream);
@@ -224,6 +230,12 @@ int gs_masked_pcg_rhs(gs_masked* ctx, const double* dl, const double* zv, const 
                       uint32_t iteration, int chain, double* rhs, void* stream);
 int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
                         int maxiter, int* iters, double* rel_residual, void* stream);
+/* f2: pixel-domain non-centered likelihood (NonCenteredGibbs.py:333-355):
+ * lik = -1/2 sum_pix N^-1 (d - A b C^1/2(D) s_nc)^2 (device double).
+ * gs_masked_center: out = C^1/2 in (dir = +1) or C^+1/2 in (dir = -1) per slot
+ * (EB sqrt(var) / sqrt(inv_var), NonCenteredGibbs.py:236-237; TEB chol(C)). */
+int gs_masked_center(gs_masked* ctx, const double* dl, int dir, const double* in, double* out, void* stream);
+int gs_masked_nc_loglik(gs_masked* ctx, const double* dl, const double* s_nc, double* lik, void* stream);
 
 #ifdef __cplusplus
 }

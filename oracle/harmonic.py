@@ -681,7 +681,7 @@ def _psd_ok(model, dl_unbinned, ells):
 
 
 def nc_mh(model, dl_binned_old, stats, seed=0, chain=0, iteration=0,
-          u_prop=None, u_accept=None, n_iter=1):
+          u_prop=None, u_accept=None, n_iter=1, loglik=None):
     """One Metropolis-within-Gibbs sweep (PolarizationNonCenteredClsSampler.sample).
 
     Replay: u_prop[spec] are the truncnorm uniforms (bins >= 2, scipy draws
@@ -733,7 +733,11 @@ def nc_mh(model, dl_binned_old, stats, seed=0, chain=0, iteration=0,
                 lr_all = float(np.sum(logr[s][lo:hi]))
                 un_old = model.unfold(cur)
                 un_new = model.unfold(new)
-                if _psd_ok(model, un_new, ells):
+                if loglik is not None:
+                    # pixel-domain likelihood (NonCenteredGibbs.py:333-355,380-399):
+                    # new_lik - old_lik of the whole map
+                    log_r = (loglik(un_new) - loglik(un_old)) + lr_all
+                elif _psd_ok(model, un_new, ells):
                     f_old = nc_loglik_terms(model, un_old, stats)
                     f_new = nc_loglik_terms(model, un_new, stats)
                     dlik = float(np.sum(f_new[ells] - f_old[ells]))

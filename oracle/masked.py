@@ -371,3 +371,102 @@ def pcg_sample(mm, dl_unbinned, draws, tol=1e-12, maxiter=2000):
     rhs = mm.second_part_grad() + pcg_fluctuation(mm, dl_unbinned, z_pix, z_slot)
     x, it = pcg_solve(mm, dl_unbinned, rhs, tol, maxiter)
     return x, 1, it
+
+
+# ----------------------------------------------------------------------------
+# f2: pixel-domain non-centered likelihood (NonCenteredGibbs.py:333-355)
+# ----------------------------------------------------------------------------
+def nc_map(mm, dl_unbinned, s_nc):
+    """A b C^1/2(D) s_nc for the field rows (EB: sqrt(var) per slot; TEB: chol(C))."""
+    if mm.F == 2:
+        var = H.var_from_dl(dl_unbinned)
+        s = np.stack([np.sqrt(var[k][mm.slot_ell]) * s_nc[k] for k in range(2)])
+    else:
+        model = H.Model(mm.L, mm.nside, 3, mm.bl, [1.0] * 3, {x: np.arange(mm.L + 2) for x in H.SPECTRA[3]})
+        A = H.cov_chol(model, dl_unbinned)
+        s = np.zeros_like(s_nc)
+        for f in range(3):
+            for g in range(3):
+                s[f] += A[mm.slot_ell, f, g] * s_nc[g]
+    return mm.synth(s)
+
+
+def nc_loglik_pixel(mm, dl_unbinned, s_nc):
+    """-1/2 sum_pix N^-1 [(Q_d - Q)^2 + (U_d - U)^2]  (TEB adds the T row)."""
+    mp = nc_map(mm, dl_unbinned, s_nc)
+    return -0.5 * sum(float(np.sum((mm.maps[r] - mp[k]) ** 2 * mm.inv_noise[r])) for k, r in enumerate(mm.rows))
+
+
+def pixel_mh(mm, model, dl_binned_old, s_nc, seed=0, chain=0, iteration=0, u_prop=None, u_accept=None, n_iter=1):
+    """PolarizationNonCenteredClsSampler.sample with all_sph=False (401-445):
+    the truncated-normal proposals and block loop of oracle.harmonic.nc_mh,
+    each block scored by the full pixel-domain likelihood."""
+    return H.nc_mh(model, dl_binned_old, None, seed=seed, chain=chain, iteration=iteration, u_prop=u_prop,
+                   u_accept=u_accept, n_iter=n_iter, loglik=lambda dl: nc_loglik_pixel(mm, dl, s_nc))
+
+
+def noncentre(mm, dl_unbinned, s, inverse=True):
+    """EB: s_nc = C^-1/2 s with 1/var set to 0 where var = 0
+    (NonCenteredGibbs.py:186-194, ASIS.py:182-190); inverse=False: C^1/2 s
+    (the re-centring of ASIS.py:199-203)."""
+    var = H.var_from_dl(dl_unbinned)
+    out = np.zeros_like(s)
+    for k in range(2):
+        v = var[k][mm.slot_ell]
+        if inverse:
+            iv = np.zeros_like(v)
+            iv[v != 0] = 1.0 / v[v != 0]
+            out[k] = np.sqrt(iv) * s[k]
+        else:
+            out[k] = np.sqrt(v) * s[k]
+    return out
+
+
+def run_masked_mh_chain(kind, mm, model, dls_init, n_iter, draws, tol=1e-13, cr="pcg", n_gibbs=1, noise_pol0=1.0,
+                        quirk=True, native=None):
+    """The masked NonCenteredClsSampler.run_polarization (NonCenteredGibbs.py:529-571)
+    and ASIS.run_polarization (ASIS.py:134-226) chains in the reference's
+    draw order, for one chain.  cr: "pcg" or "aux_mala" (ASIS with gibbs_cr,
+    its default ula=True).  native: (seed, chain) to use the device streams
+    instead of numpy's (draws must then be a factory it -> NativeDraws)."""
+    from . import reference_eb as RE
+    binned = {s: np.array(dls_init[s], dtype=np.float64) for s in model.spectra}
+    hist = {s: [binned[s].copy()] for s in model.spectra}
+    accs = {s: [] for s in model.spectra}
+
+    def dr(it):
+        return draws(it) if native is not None else draws
+
+    def mh(s_nc, start, it):
+        if native is not None:
+            return pixel_mh(mm, model, start, s_nc, seed=native[0], chain=native[1], iteration=it)
+        u_prop, u_acc = RE.draw_mh_uniforms(model)
+        return pixel_mh(mm, model, start, s_nc, u_prop=u_prop, u_accept=u_acc)
+
+    s = None
+    if kind == "asis" and cr != "pcg":
+        s, _, _ = pcg_sample(mm, model.unfold(binned), dr(0), tol=tol)
+    for i in range(n_iter):
+        it = i + 1
+        dl = model.unfold(binned)
+        if kind == "noncentered":
+            s, _, _ = pcg_sample(mm, dl, dr(it), tol=tol)
+            binned, a = mh(noncentre(mm, dl, s), binned, it)
+        else:
+            if cr == "pcg":
+                s, _, _ = pcg_sample(mm, dl, dr(it), tol=tol)
+            else:
+                s, _ = sample_dispatch(mm, dl, s, dr(it), gibbs_cr=True, overrelaxation_flag=False, ula=True,
+                                       n_gibbs=n_gibbs, noise_pol0=noise_pol0)
+            if native is not None:
+                tmp = H.centered_cls_draw(model, H.sweep_stats(model, s, model.d_alm), seed=native[0],
+                                          chain=native[1], iteration=it)
+            else:
+                tmp = RE.cls_centered(model, s)
+            s_nc = noncentre(mm, model.unfold(tmp), s)
+            binned, a = mh(s_nc, tmp, it)
+            s = noncentre(mm, model.unfold(binned), s if quirk else s_nc, inverse=False)
+        for sp in model.spectra:
+            accs[sp].append(a[sp])
+            hist[sp].append(binned[sp].copy())
+    return {sp: np.array(v) for sp, v in hist.items()}, {sp: np.array(v) for sp, v in accs.items()}, s

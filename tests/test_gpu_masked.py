@@ -276,3 +276,108 @@ def test_f1_pcg_driver_replay_vs_oracle(g):
     assert np.all(acc == 1)
     for sp in ("EE", "BB"):
         np.testing.assert_allclose(h[sp], np.array(want[sp]), rtol=1e-7)
+
+
+# ---- f2: pixel-domain non-centred likelihood --------------------------------------------
+def _f2_parts(g):
+    bins = {"EE": g["bins_EE"], "BB": g["bins_BB"]}
+    blocks = {"EE": g["blocks_EE"], "BB": g["blocks_BB"]}
+    pv = {"EE": g["pv_EE"], "BB": g["pv_BB"]}
+    return bins, blocks, pv
+
+
+def _oracle_model(g):
+    from oracle import harmonic as H
+    L, N = int(g["L"]), int(g["nside"])
+    bins, blocks, pv = _f2_parts(g)
+    mm = MK.MaskedModel(L, N, 2, g["bl"], np.stack([np.zeros(768), g["Q"], g["U"]]),
+                        np.stack([np.zeros(768), g["inv_noise_pol"], g["inv_noise_pol"]]))
+    model = H.Model(L, N, 2, g["bl"], [1.0, 1.0], bins, blocks=blocks, proposal_variances=pv,
+                    d_alm=np.zeros((2, (L + 1) ** 2)))
+    return mm, model
+
+
+def test_f2_pixel_mh_replay(g):
+    """the device likelihood and one MH sweep = the reference's
+    PolarizationNonCenteredClsSampler.sample(all_sph=False) (fixture f2_*)."""
+    from gibbssampler_amd.masked import PixelMH
+    bins, blocks, pv = _f2_parts(g)
+    mh = PixelMH(_cr(g, gibbs_cr=False, ula=False), bins, blocks, pv)
+    snc = {"EE": g["f2_snc_E"], "BB": g["f2_snc_B"]}
+    init = {"EE": g["init_EE"].copy(), "BB": g["init_BB"].copy()}
+    assert mh.compute_log_likelihood(init, snc) == pytest.approx(float(g["f2_lik0"]), rel=1e-11)
+    np.random.seed(int(g["f2_seed"]))
+    new, acc = mh.sample(snc, init)
+    _close(new["EE"], g["f2_EE"])
+    _close(new["BB"], g["f2_BB"])
+    assert acc["EE"] == list(g["f2_acc_EE"]) and acc["BB"] == list(g["f2_acc_BB"])
+
+
+def test_f2_pixel_mh_native_vs_oracle(g):
+    from gibbssampler_amd.masked import PixelMH
+    bins, blocks, pv = _f2_parts(g)
+    seed, chain, it = 77, 3, 5
+    cr = _cr(g, gibbs_cr=False, ula=False, rng="native", seed=seed, chain=chain)
+    mh = PixelMH(cr, bins, blocks, pv)
+    snc = np.stack([g["f2_snc_E"], g["f2_snc_B"]])
+    init = {"EE": g["init_EE"].copy(), "BB": g["init_BB"].copy()}
+    new, acc = mh.sample(snc, init, iteration=it)
+    mm, model = _oracle_model(g)
+    want, wacc = MK.pixel_mh(mm, model, init, snc, seed=seed, chain=chain, iteration=it)
+    _close(new["EE"], want["EE"])
+    _close(new["BB"], want["BB"])
+    assert acc == wacc
+
+
+def _masked_mh_sampler(g, cls, n_iter, rng="replay", seed=0, **kw):
+    from gibbssampler_amd import gibbs as G
+    L, N = int(g["L"]), int(g["nside"])
+    bins, blocks, pv = _f2_parts(g)
+    args = ({"Q": g["Q"], "U": g["U"]}, np.full(12 * N * N, 40.0 ** 2), g["noise_pol"], float(g["fwhm_deg"]), N, L,
+            12 * N * N, pv)
+    smp = getattr(G, cls)(*args, metropolis_blocks=blocks, polarization=True, bins=bins, n_iter=n_iter,
+                          mask_path=g["mask"], rng=rng, seed=seed, **kw)
+    smp.masked_cr.pcg_accuracy = 1e-13
+    return smp
+
+
+@pytest.mark.parametrize("rng", ["replay", "native"])
+def test_f2_masked_noncentered_driver_vs_oracle(g, rng):
+    """NonCenteredGibbs(mask_path=...): per iteration the PCG CR, C^-1/2, the
+    pixel MH sweep (NonCenteredGibbs.py:529-571), against the oracle chain."""
+    smp = _masked_mh_sampler(g, "NonCenteredGibbs", 3, rng=rng, seed=19)
+    init = {"EE": g["init_EE"].copy(), "BB": g["init_BB"].copy()}
+    np.random.seed(808)
+    h, acc, _, _ = smp.run(init)
+    mm, model = _oracle_model(g)
+    np.random.seed(808)
+    if rng == "replay":
+        want, wacc, _ = MK.run_masked_mh_chain("noncentered", mm, model, init, 3, MK.ReplayDraws())
+    else:
+        want, wacc, _ = MK.run_masked_mh_chain("noncentered", mm, model, init, 3,
+                                               lambda it: MK.NativeDraws(19, 0, it, mm.L, mm.Npix), native=(19, 0))
+    for sp in ("EE", "BB"):
+        np.testing.assert_allclose(h[sp], want[sp], rtol=1e-7)
+        np.testing.assert_array_equal(acc[sp], wacc[sp])
+
+
+@pytest.mark.parametrize("gibbs_cr", [False, True])
+def test_f2_masked_asis_driver_vs_oracle(g, gibbs_cr):
+    """ASIS(mask_path=...): CR (PCG, or the aux + MALA composition with its
+    PCG start map), centred C_l draw, non-centring, pixel MH, re-centring with
+    the reference's quirk (ASIS.py:134-226), against the oracle chain."""
+    n_gibbs = 2
+    smp = _masked_mh_sampler(g, "ASIS", 3, gibbs_cr=gibbs_cr, n_gibbs=n_gibbs)
+    init = {"EE": g["init_EE"].copy(), "BB": g["init_BB"].copy()}
+    np.random.seed(909)
+    out = smp.run(init)
+    h, acc = out[0], out[1]
+    assert len(out) == 7
+    mm, model = _oracle_model(g)
+    np.random.seed(909)
+    want, wacc, _ = MK.run_masked_mh_chain("asis", mm, model, init, 3, MK.ReplayDraws(),
+                                           cr="aux_mala" if gibbs_cr else "pcg", n_gibbs=n_gibbs,
+                                           noise_pol0=float(g["noise_pol"][0]))
+    for sp in ("EE", "BB"):
+        np.testing.assert_allclose(h[sp], want[sp], rtol=1e-7)
+        np.testing.assert_array_equal(acc[sp], wacc[sp])

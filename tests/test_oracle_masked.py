@@ -140,3 +140,43 @@ def test_f1_pcg_solves_the_system(g):
     res = MK.pcg_operator(mm, _dl(g), x) - rhs
     assert np.abs(res).max() < 1e-9 * np.abs(rhs).max()
     assert it < 500
+
+
+def test_f2_pixel_likelihood_and_mh(g):
+    """pixel-domain NC likelihood and one MH sweep (all_sph=False, masked)
+    against the reference (tools/gen_golden_masked.py, seed f2_seed)."""
+    mm = _mm(g)
+    L = int(g["L"])
+    bins = {"EE": g["bins_EE"], "BB": g["bins_BB"]}
+    model = H.Model(L, int(g["nside"]), 2, g["bl"], [1.0, 1.0], bins,
+                    blocks={"EE": g["blocks_EE"], "BB": g["blocks_BB"]},
+                    proposal_variances={"EE": g["pv_EE"], "BB": g["pv_BB"]})
+    snc = np.stack([g["f2_snc_E"], g["f2_snc_B"]])
+    d_old = {"EE": g["init_EE"].copy(), "BB": g["init_BB"].copy()}
+    lik0 = MK.nc_loglik_pixel(mm, model.unfold(d_old), snc)
+    assert lik0 == pytest.approx(float(g["f2_lik0"]), rel=1e-11)
+    np.random.seed(int(g["f2_seed"]))
+    u_prop, u_acc = RE.draw_mh_uniforms(model)
+    new, acc = MK.pixel_mh(mm, model, d_old, snc, u_prop=u_prop, u_accept=u_acc)
+    _close(new["EE"], g["f2_EE"])
+    _close(new["BB"], g["f2_BB"])
+    assert acc["EE"] == list(g["f2_acc_EE"]) and acc["BB"] == list(g["f2_acc_BB"])
+
+
+def test_f2_noncentre_roundtrip_and_chain_runs(g):
+    mm = _mm(g)
+    L = int(g["L"])
+    bins = {"EE": g["bins_EE"], "BB": g["bins_BB"]}
+    model = H.Model(L, int(g["nside"]), 2, g["bl"], [1.0, 1.0], bins,
+                    blocks={"EE": g["blocks_EE"], "BB": g["blocks_BB"]},
+                    proposal_variances={"EE": g["pv_EE"], "BB": g["pv_BB"]}, d_alm=np.zeros((2, (L + 1) ** 2)))
+    dl = model.unfold({"EE": g["init_EE"], "BB": g["init_BB"]})
+    s = _s_old(g)
+    back = MK.noncentre(mm, dl, MK.noncentre(mm, dl, s), inverse=False)
+    keep = mm.slot_ell >= 2
+    _close(back[:, keep], s[:, keep])
+    np.random.seed(5)
+    h, acc, _ = MK.run_masked_mh_chain("noncentered", mm, model, {"EE": g["init_EE"], "BB": g["init_BB"]}, 1,
+                                       MK.ReplayDraws(), tol=1e-10)
+    assert h["EE"].shape == (2, len(g["init_EE"])) and np.all(np.isfinite(h["EE"]))
+    assert acc["EE"].shape == (1, len(g["blocks_EE"]) - 1)
