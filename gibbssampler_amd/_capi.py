@@ -111,6 +111,7 @@ _SIGS = [
                                            c_double_p, _VP]),
     ("gs_masked_center", ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_masked_nc_loglik", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("gs_synalm", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, _VP]),
     ("gs_mh_propose", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP, _VP, _VP]),
     ("gs_masked_cr", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,
                                     ctypes.c_uint32, ctypes.c_int, _VP, _VP, _VP]),

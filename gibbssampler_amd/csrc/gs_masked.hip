@@ -512,6 +512,30 @@ __global__ void k_mc_center(int L, const double* __restrict__ dl, int dir, const
 }
 
 // partial sums of N^-1 (d - m)^2 over all field rows
+// synalm: a_lm = b_l C_l^1/2 z per real slot (F = 1: TT; 2: EE, BB; 3: TEB with
+// the (T, E) Cholesky factor of [[TT, TE], [TE, EE]]); cl holds C_l (not D_l)
+template <int F>
+__global__ void k_synalm(int L, const double* __restrict__ cl, const double* __restrict__ beam,
+                         const double* __restrict__ z, double* __restrict__ out) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= NR) return;
+    int l;
+    if (g <= L) l = (int)g;
+    else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
+    const int Lp1 = L + 1;
+    if constexpr (F == 3) {
+        const CovChol A = cov_chol_teb(cl[l], cl[Lp1 + l], cl[3 * Lp1 + l], cl[2 * Lp1 + l]);
+        const double x0 = z[g], x1 = z[NR + g], x2 = z[2 * NR + g];
+        out[g] = beam[l] * (A.a00 * x0);
+        out[NR + g] = beam[Lp1 + l] * (A.a10 * x0 + A.a11 * x1);
+        out[2 * NR + g] = beam[2 * Lp1 + l] * (A.aB * x2);
+    } else {
+        for (int f = 0; f < F; ++f)
+            out[f * NR + g] = beam[f * Lp1 + l] * (sqrt(fmax(cl[f * Lp1 + l], 0.0)) * z[f * NR + g]);
+    }
+}
+
 __global__ __launch_bounds__(RED_BLOCK) void k_mc_resid(long long n, const double* __restrict__ d,
                                                         const double* __restrict__ m, const double* __restrict__ w,
                                                         double* __restrict__ partial) {
@@ -863,6 +887,19 @@ int gs_masked_center(gs_masked* c, const double* dl, int dir, const double* in, 
     if (c->F == 2) hipLaunchKernelGGL(k_mc_center<2>, g, b, 0, S(stream), c->L, dl, dir, in, out);
     else hipLaunchKernelGGL(k_mc_center<3>, g, b, 0, S(stream), c->L, dl, dir, in, out);
     GS_LAUNCH_CHECK("k_mc_center");
+    return 0;
+}
+
+int gs_synalm(int lmax, int nfields, const double* cl, const double* beam, const double* z, double* alm,
+              void* stream) {
+    if (lmax < 0 || nfields < 1 || nfields > 3) return set_error("gs_synalm: bad lmax / nfields");
+    if (!cl || !beam || !z || !alm) return set_error("gs_synalm: null argument");
+    const long long NR = (long long)(lmax + 1) * (lmax + 1);
+    const dim3 g(nblocks(NR, 256)), b(256);
+    if (nfields == 1) hipLaunchKernelGGL(k_synalm<1>, g, b, 0, S(stream), lmax, cl, beam, z, alm);
+    else if (nfields == 2) hipLaunchKernelGGL(k_synalm<2>, g, b, 0, S(stream), lmax, cl, beam, z, alm);
+    else hipLaunchKernelGGL(k_synalm<3>, g, b, 0, S(stream), lmax, cl, beam, z, alm);
+    GS_LAUNCH_CHECK("k_synalm");
     return 0;
 }
 

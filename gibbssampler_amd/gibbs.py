@@ -18,10 +18,13 @@ closed form (CenteredGibbs.py:317-353) is its exact solution, which is what
 runs here.  Masked centered runs (``mask_path`` = mask array or .npy file)
 use the device SHT and the PCG / auxiliary-variable / over-relaxation /
 MALA samplers of gibbssampler_amd.masked (CenteredGibbs.py:448-850, the a12
-flag ladder; the PCG is the init CR as at HEAD); the pixel-domain
-non-centered likelihood raises NotImplementedError (SURVEY.md 8f
-row f2).  Masked-only keywords: ``n_gibbs``, ``alpha``, ``tau``,
-``skymap_init`` (a start map instead of the reference's PCG init CR).
+flag ladder; the PCG is the init CR as at HEAD); masked NonCenteredGibbs and
+ASIS score the MH blocks with the pixel-domain likelihood
+(NonCenteredGibbs.py:333-355, gibbssampler_amd.masked.PixelMH).  ``mask_path``
+is a HEALPix FITS file (any N_side, ud_graded), a .npy file or an array.
+Masked-only keywords: ``n_gibbs``, ``alpha``, ``tau``, ``skymap_init`` (a
+start map instead of the reference's PCG init CR).  Full-sky data may be
+given as pixel maps (Q, U[, T]); they are analysed once with map2alm(iter=3).
 
 Extra keyword arguments (all optional): ``nchains`` (batched chains on one
 GPU), ``rng`` ("native" Philox or "replay" = numpy's global RNG in the
@@ -56,35 +59,62 @@ def _scalar_noise(noise, what):
     return float(a.flat[0])
 
 
-def _harmonic_data(pix_map, nfields, lmax):
+def _harmonic_data(pix_map, nfields, lmax, nside):
+    """Real-layout harmonic data d_alm per field.  Given as a_lm under
+    'TT'/'EE'/'BB' (the all_sph form, main_polarization.py:43-45), or as pixel
+    maps ('Q'/'U', plus 'T' or 'I' for TEB; an Npix array for TT), analysed
+    once on the device with map2alm(iter=3) -- the non-all_sph data term of
+    NonCenteredGibbs.py:155-159 / utils.adjoint_synthesis_hp, which the
+    reference recomputes every iteration."""
     keys = {1: ("TT",), 2: ("EE", "BB"), 3: ("TT", "EE", "BB")}[nfields]
+    npix = 12 * nside ** 2
     if nfields == 1 and not isinstance(pix_map, dict):
         arr = np.asarray(pix_map, dtype=np.float64)
         if arr.shape[-1] == (lmax + 1) ** 2:
             return {"TT": arr}
-        raise NotImplementedError("temperature data given as a pixel map needs the SHT (map2alm) path; "
-                                  "pass the real-layout a_lm (utils.complex_to_real of map2alm) instead")
-    missing = [k for k in keys if k not in pix_map]
-    if missing:
-        raise NotImplementedError(f"pix_map lacks harmonic data {missing}: pixel-domain maps (Q/U) need the "
-                                  "SHT path; pass real-layout a_lm under 'TT'/'EE'/'BB' (all_sph form, "
-                                  "main_polarization.py:43-45)")
-    return {k: np.asarray(pix_map[k], dtype=np.float64) for k in keys}
+        if arr.shape[-1] != npix:
+            raise ValueError("TT data must be a real-layout a_lm or an Npix map")
+        return {"TT": _analyse([arr], nside, lmax)[0]}
+    if all(k in pix_map for k in keys):
+        return {k: np.asarray(pix_map[k], dtype=np.float64) for k in keys}
+    if "Q" in pix_map and "U" in pix_map:
+        if nfields == 2:
+            a = _analyse([pix_map["Q"], pix_map["U"]], nside, lmax)
+            return {"EE": a[0], "BB": a[1]}
+        t = pix_map.get("T", pix_map.get("I"))
+        if t is not None:
+            a = _analyse([t, pix_map["Q"], pix_map["U"]], nside, lmax)
+            return {"TT": a[0], "EE": a[1], "BB": a[2]}
+    raise ValueError(f"pix_map needs harmonic data {keys} or pixel maps (Q, U[, T])")
+
+
+def _analyse(maps, nside, lmax):
+    import torch
+    from .sht import HealpixSHT
+    m = torch.as_tensor(np.ascontiguousarray(np.stack([np.asarray(x, dtype=np.float64) for x in maps])),
+                        device="cuda")
+    sht = HealpixSHT(nside, lmax)
+    a = sht.map2alm(m if len(maps) > 1 else m[0], iter=3, ncomp=len(maps))
+    return a.reshape(len(maps), -1).cpu().numpy()
 
 
 def _load_mask(mask_path, nside):
-    """The mask of CenteredGibbs.py:266-271 (hp.ud_grade(hp.read_map(path), nside)).
-    Accepted: an array at the run's N_side, or a .npy file of one.  FITS
-    reading and ud_grade are SURVEY.md 8 row f3."""
+    """The mask of CenteredGibbs.py:266-271 (hp.ud_grade(hp.read_map(path), nside)):
+    a HEALPix FITS map (io.read_map, RING or NESTED), a .npy file or an array,
+    brought to the run's N_side with io.ud_grade."""
+    from . import io as gio
     if isinstance(mask_path, np.ndarray):
         m = np.asarray(mask_path, dtype=np.float64)
     elif isinstance(mask_path, str) and mask_path.endswith(".npy"):
         m = np.load(mask_path, allow_pickle=False).astype(np.float64)
+    elif isinstance(mask_path, str):
+        m = gio.read_map(mask_path, 0)
     else:
-        raise NotImplementedError("mask_path: FITS masks and ud_grade are SURVEY.md 8 row f3; pass an array or "
-                                  "a .npy file at the run's N_side")
+        raise TypeError("mask_path: a FITS / .npy path or an array")
+    if m.ndim != 1:
+        raise ValueError("mask must be one HEALPix map")
     if m.shape != (12 * nside ** 2,):
-        raise NotImplementedError("mask resolution differs from N_side: ud_grade is SURVEY.md 8 row f3")
+        m = gio.ud_grade(m, nside)
     return m
 
 
@@ -170,7 +200,7 @@ class GibbsSampler:
     def _make_runner(self):
         from .samplers import BatchedRunner
         if self._runner is None:
-            d = _harmonic_data(self.pix_map, self.nfields, self.lmax)
+            d = _harmonic_data(self.pix_map, self.nfields, self.lmax, self.nside)
             blocks = None
             pv = None
             if self._kind in ("noncentered", "asis"):
@@ -402,7 +432,7 @@ class _StepBase:
             o = self.owner
             bins = {s: np.arange(0, o.lmax + 2) for s in o.spectra}
             self._plan = GibbsPlan(o.lmax, o.nside, o.nfields, 1, o.bl_gauss, o.noise_var, bins)
-            self._d = self._plan.data_tensor(_harmonic_data(o.pix_map, o.nfields, o.lmax))
+            self._d = self._plan.data_tensor(_harmonic_data(o.pix_map, o.nfields, o.lmax, o.nside))
         return self._plan
 
     def _binned_plan(self):

@@ -237,6 +237,15 @@ int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, dou
 int gs_masked_center(gs_masked* ctx, const double* dl, int dir, const double* in, double* out, void* stream);
 int gs_masked_nc_loglik(gs_masked* ctx, const double* dl, const double* s_nc, double* lik, void* stream);
 
+/* Gaussian sky draw for synthetic data (the synalm + smoothalm half of
+ * healpy.synfast, main_polarization.py:38): alm[f] = beam[f][l] * (C_l^1/2 z)[f]
+ * per real slot.  cl [nspec][lmax+1] is C_l (not D_l): nfields 1: TT;
+ * 2: EE, BB; 3: TT, EE, BB, TE (TEB uses the Cholesky factor of the (T, E)
+ * block).  beam [nfields][lmax+1]; z [nfields][(lmax+1)^2] unit normals
+ * supplied by the caller; alm [nfields][(lmax+1)^2].  Device pointers. */
+int gs_synalm(int lmax, int nfields, const double* cl, const double* beam, const double* z, double* alm,
+              void* stream);
+
 #ifdef __cplusplus
 }
 #endif
