@@ -80,8 +80,10 @@ def test_synfast_spectrum_statistics():
         chat = np.bincount(sl, weights=a[f] ** 2) / (2 * np.arange(L + 1) + 1)
         ratio = chat[2:] / c[k][2:]
         assert abs(ratio.mean() - 1) < 0.05
-    chat_te = np.bincount(sl, weights=a[0] * a[1]) / (2 * np.arange(L + 1) + 1)
-    assert abs(chat_te[2:].sum() / c[3][2:].sum() - 1) < 0.1
+    n = 2 * np.arange(L + 1) + 1
+    chat_te = np.bincount(sl, weights=a[0] * a[1]) / n
+    zte = (chat_te[2:] - c[3][2:]) / np.sqrt((c[0][2:] * c[1][2:] + c[3][2:] ** 2) / n[2:])
+    assert abs(zte.mean()) < 4 / np.sqrt(len(zte)) and 0.5 < zte.std() < 1.5
 
 
 def test_fits_mask_through_the_surface(tmp_path):
