@@ -54,6 +54,8 @@ class GsMaskedDesc(ctypes.Structure):
         ("alpha", ctypes.c_double),
         ("tau", ctypes.c_double),
         ("noise_pol0", ctypes.c_double),
+        ("mu_eps", ctypes.c_double),
+        ("adj_iter", ctypes.c_int),
     ]
 
 
@@ -111,6 +113,8 @@ _SIGS = [
                                            c_double_p, _VP]),
     ("gs_masked_center", ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_masked_nc_loglik", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("gs_masked_tt_fullsky", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.c_int, _VP, _VP]),
     ("gs_synalm", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, _VP]),
     ("gs_mh_propose", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP, _VP, _VP]),
     ("gs_masked_cr", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64,

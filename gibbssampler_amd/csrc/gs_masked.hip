@@ -310,10 +310,13 @@ struct PriorPinv { double i00, t10, i11, iB, ie, ib; };
 template <int F>
 __device__ __forceinline__ PriorPinv prior_pinv(const double* __restrict__ dl, int L, int l) {
     PriorPinv q{0, 0, 0, 0, 0, 0};
-    if constexpr (F == 2) {
-        const double ve = var_from_dl(dl[l], l), vb = var_from_dl(dl[(L + 1) + l], l);
+    if constexpr (F != 3) {
+        const double ve = var_from_dl(dl[l], l);
         q.ie = ve != 0.0 ? sqrt(1.0 / ve) : 0.0;
-        q.ib = vb != 0.0 ? sqrt(1.0 / vb) : 0.0;
+        if constexpr (F == 2) {
+            const double vb = var_from_dl(dl[(L + 1) + l], l);
+            q.ib = vb != 0.0 ? sqrt(1.0 / vb) : 0.0;
+        }
     } else {
         const double tt = var_from_dl(dl[l], l), ee = var_from_dl(dl[(L + 1) + l], l);
         const double bb = var_from_dl(dl[2 * (L + 1) + l], l), te = var_from_dl(dl[3 * (L + 1) + l], l);
@@ -360,7 +363,7 @@ __global__ void k_pcg_rhs(int L, const double* __restrict__ dl, const double* __
     const double b = bl[l];
     for (int c = 0; c < nv; ++c) {
         double h[3];
-        if constexpr (F == 2) { h[0] = q.ie * z[0][c]; h[1] = q.ib * z[1][c]; }
+        if constexpr (F != 3) { h[0] = q.ie * z[0][c]; h[1] = q.ib * (F == 2 ? z[1][c] : 0.0); }
         else { h[0] = q.i00 * z[0][c] + q.t10 * z[1][c]; h[1] = q.i11 * z[1][c]; h[2] = q.iB * z[2][c]; }
 #pragma unroll
         for (int f = 0; f < F; ++f) {
@@ -387,9 +390,9 @@ __global__ void k_pcg_qfinish(int L, const double* __restrict__ dl, const double
     const double bw = bl[l] * inv_w;
     for (int c = 0; c < nv; ++c) {
         double cx[3];
-        if constexpr (F == 2) {
+        if constexpr (F != 3) {
             cx[0] = q.ie * q.ie * x[r + c];
-            cx[1] = q.ib * q.ib * x[NR + r + c];
+            if constexpr (F == 2) cx[1] = q.ib * q.ib * x[NR + r + c];
         } else {
             const double xt = x[r + c], xe = x[NR + r + c];
             const double y0 = q.i00 * xt, y1 = q.t10 * xt + q.i11 * xe;
@@ -413,9 +416,9 @@ __global__ void k_pcg_prec(int L, const double* __restrict__ params, const doubl
     if (g <= L) l = (int)g;
     else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
     const double* p = params + (long long)l * GS_NPARAM;
-    if constexpr (F == 2) {
-        z[g] = p[2] * p[2] * rr[g];
-        z[NR + g] = p[3] * p[3] * rr[NR + g];
+    if constexpr (F != 3) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) z[f * NR + g] = p[F + f] * p[F + f] * rr[f * NR + g];
     } else {
         const double r0 = rr[g], r1 = rr[NR + g], r2 = rr[2 * NR + g];
         const double t0 = p[5] * r0 + p[6] * r1, t1 = p[7] * r1;        // L^T r
@@ -486,8 +489,8 @@ __global__ void k_mc_center(int L, const double* __restrict__ dl, int dir, const
     int l;
     if (g <= L) l = (int)g;
     else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
-    if constexpr (F == 2) {
-        for (int f = 0; f < 2; ++f) {
+    if constexpr (F != 3) {
+        for (int f = 0; f < F; ++f) {
             const double v = var_from_dl(dl[f * (L + 1) + l], l);
             const double fac = dir > 0 ? sqrt(v) : (v != 0.0 ? sqrt(1.0 / v) : 0.0);
             out[f * NR + g] = fac * in[f * NR + g];
@@ -558,6 +561,43 @@ __global__ void k_mc_halfneg(const double* __restrict__ two, double* __restrict_
     if (threadIdx.x == 0) *out = -0.5 * two[0];
 }
 
+// f4: temperature full-sky CR from pixel data (CenteredGibbs.py:108-132 centered,
+// NonCenteredGibbs.py:22-38 non-centered): per real slot, with g2 = b
+// adjoint_synthesis_hp(N^-1 d), f = b adjoint_synthesis_hp(sqrt(N^-1) z_pix)
+// (= b r Npix/4pi, r = map2alm(y, iter 3)) and kap = N^-1[0] Npix/4pi,
+//   centered:     s = (g2 + C^+1/2 z + f) / (C^+ + kap b^2)      (C^+ zero for l < 2: mask_inversion)
+//   non-centered: s = (sqrt(C) (g2 + f) + z) / (1 + C kap b^2)
+template <int NC>
+__global__ void k_tt_fullsky(int L, const double* __restrict__ dl, const double* __restrict__ bl,
+                             const double* __restrict__ g2, const double* __restrict__ r_alm, double resc, double kap,
+                             const double* __restrict__ zs, uint32_t seed_lo, uint32_t seed_hi, uint32_t chain,
+                             uint32_t iter, double* __restrict__ s) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= nlm) return;
+    int l, m;
+    cidx_lm(L, i, l, m);
+    const long long r = m == 0 ? l : 2 * i - (L + 1);
+    const int nv = m == 0 ? 1 : 2;
+    double z[3][2];
+    slot_normals(zs, NR, 1, r, nv, chain_key(seed_lo, seed_hi, chain), i, SUB_PCG_S, iter, z);
+    const double v = var_from_dl(dl[l], l);
+    const double b = bl[l];
+    for (int c = 0; c < nv; ++c) {
+        const double f = b * (r_alm[r + c] * resc);
+        if constexpr (NC) {
+            const double sv = sqrt(v);
+            const double sig = 1.0 / (1.0 + v * kap * b * b);
+            s[r + c] = sig * (sv * g2[r + c]) + sig * (z[0][c] + sv * f);
+        } else {
+            const double iv = (l >= 2 && v != 0.0) ? 1.0 / v : 0.0;
+            const double sig = 1.0 / (iv + kap * b * b);
+            s[r + c] = sig * g2[r + c] + sig * (z[0][c] * sqrt(iv) + f);
+        }
+    }
+}
+
 }  // namespace
 
 // ============================================================================
@@ -569,6 +609,9 @@ struct gs_masked {
     double w = 0, alpha = -0.995, tau = 0.02, noise_pol0 = 1.0;
     double mu[3] = {0, 0, 0};
     double nbar[3] = {0, 0, 0};      // mean N^-1 per map row (PCG preconditioner)
+    double ninv0[3] = {0, 0, 0};     // N^-1 of pixel 0 per map row (the TT closed forms' noise level)
+    double mu_eps = 1e-14;
+    int adj_iter = 0;
     Rows rows{{1, 2, 0}};
     gs_sht* sht = nullptr;
     double *bl = nullptr, *dpix = nullptr, *ninv = nullptr, *g2 = nullptr;
@@ -610,7 +653,9 @@ __global__ void k_mc_params(int L, const double* __restrict__ dl, const int* __r
 
 int mc_params(gs_masked* c, const double* dl, const double* kap, double* out, hipStream_t st) {
     const dim3 g(nblocks(c->L + 1, 256)), b(256);
-    if (c->F == 2)
+    if (c->F == 1)
+        hipLaunchKernelGGL(k_mc_params<1>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
+    else if (c->F == 2)
         hipLaunchKernelGGL(k_mc_params<2>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
     else
         hipLaunchKernelGGL(k_mc_params<3>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
@@ -638,11 +683,16 @@ int mc_v(gs_masked* c, int over, const double* s, double* v, const double* zv, u
 
 int mc_s(gs_masked* c, int over, double* s, const double* zs, uint32_t slo, uint32_t shi, uint32_t chain,
          uint32_t sub, uint32_t it, hipStream_t st) {
-    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
+    // s | v analysis: iter 0 explicit for EB/TEB (CenteredGibbs.py:717,773,812),
+    // healpy's default iter = 3 for TT (CenteredGibbs.py:208)
+    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, c->adj_iter, st)) return -1;
     double imu[3] = {0, 0, 0};
     for (int k = 0; k < c->F; ++k) imu[k] = 1.0 / c->mu[c->rows.r[k]];
     const dim3 g(nblocks(c->nlm, 256)), b(256);
-    if (c->F == 2)
+    if (c->F == 1)
+        hipLaunchKernelGGL(k_mc_s<1>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, slo, shi, chain,
+                           sub, it, over, c->alpha, s);
+    else if (c->F == 2)
         hipLaunchKernelGGL(k_mc_s<2>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, slo, shi, chain,
                            sub, it, over, c->alpha, s);
     else
@@ -671,17 +721,21 @@ extern "C" {
 int gs_masked_create(const gs_masked_desc* desc, const double* maps, const double* inv_noise, gs_masked** out) {
     if (!desc || !maps || !inv_noise || !out) return set_error("gs_masked_create: null argument");
     *out = nullptr;
-    if (desc->nfields != 2 && desc->nfields != 3) return set_error("gs_masked_create: nfields must be 2 (EB) or 3 (TEB)");
+    if (desc->nfields < 1 || desc->nfields > 3)
+        return set_error("gs_masked_create: nfields must be 1 (T), 2 (EB) or 3 (TEB)");
+    if (desc->adj_iter < 0 || desc->adj_iter > 16) return set_error("gs_masked_create: adj_iter out of range");
     if (!desc->bl) return set_error("gs_masked_create: null beam");
     gs_masked* c = new gs_masked();
     c->L = desc->lmax; c->nside = desc->nside; c->F = desc->nfields;
     c->n_gibbs = std::max(1, desc->n_gibbs);
     c->alpha = desc->alpha; c->tau = desc->tau; c->noise_pol0 = desc->noise_pol0;
+    c->mu_eps = desc->mu_eps > 0.0 ? desc->mu_eps : 1e-14;
+    c->adj_iter = desc->adj_iter;
     c->npix = 12LL * c->nside * c->nside;
     c->NR = (long long)(c->L + 1) * (c->L + 1);
     c->nlm = (long long)(c->L + 1) * (c->L + 2) / 2;
     c->w = 4.0 * PI / (double)c->npix;
-    c->rows = c->F == 2 ? Rows{{1, 2, 0}} : Rows{{0, 1, 2}};
+    c->rows = c->F == 2 ? Rows{{1, 2, 0}} : Rows{{0, 1, 2}};      // F = 1: the T row
     c->nblk = (int)std::min<long long>(512, nblocks(std::max(c->F * c->NR, c->F * c->npix), RED_BLOCK));
     if (gs_sht_create(c->nside, c->L, &c->sht)) { mc_free(c); return -1; }
     const long long FR = c->F * c->NR, FP = c->F * c->npix;
@@ -728,7 +782,8 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
              hipMemcpy(host.data(), inv_noise + row * c->npix, c->npix * sizeof(double), hipMemcpyDeviceToHost) ==
                  hipSuccess;
         if (ok) {
-            c->mu[row] = *std::max_element(host.begin(), host.end()) + 1e-14;
+            c->mu[row] = *std::max_element(host.begin(), host.end()) + c->mu_eps;
+            c->ninv0[row] = host[0];
             double acc = 0.0;
             for (double v : host) acc += v;
             c->nbar[row] = acc / (double)c->npix;
@@ -738,7 +793,7 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     // second_part_grad = b * complex_to_real(map2alm(N^-1 d)) * Npix/(4 pi)  (CenteredGibbs.py:298-306)
     const long long n = c->F * c->npix;
     hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, 0, n, c->ninv, c->dpix, c->y);
-    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, nullptr)) { mc_free(c); return -1; }
+    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, c->adj_iter, nullptr)) { mc_free(c); return -1; }
     hipLaunchKernelGGL(k_mc_beam, dim3(nblocks(c->F * c->nlm, 256)), dim3(256), 0, 0, c->L, c->F, c->bl, c->r, c->g2);
     const long long nr = c->F * c->NR;
     std::vector<double> g2h((size_t)nr);
@@ -783,7 +838,8 @@ static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* ou
     GS_LAUNCH_CHECK("k_mc_mul");
     if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
     const dim3 g(nblocks(c->nlm, 256)), b(256);
-    if (c->F == 2) hipLaunchKernelGGL(k_pcg_qfinish<2>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
+    if (c->F == 1) hipLaunchKernelGGL(k_pcg_qfinish<1>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
+    else if (c->F == 2) hipLaunchKernelGGL(k_pcg_qfinish<2>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
     else hipLaunchKernelGGL(k_pcg_qfinish<3>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
     GS_LAUNCH_CHECK("k_pcg_qfinish");
     return 0;
@@ -815,7 +871,10 @@ int gs_masked_pcg_rhs(gs_masked* c, const double* dl, const double* zv, const do
     if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 3, st)) return -1;
     const dim3 g(nblocks(c->nlm, 256)), b(256);
     const double resc = (double)c->npix / (4.0 * PI);
-    if (c->F == 2)
+    if (c->F == 1)
+        hipLaunchKernelGGL(k_pcg_rhs<1>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, zs, slo, shi, ch,
+                           iteration, rhs);
+    else if (c->F == 2)
         hipLaunchKernelGGL(k_pcg_rhs<2>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, zs, slo, shi, ch,
                            iteration, rhs);
     else
@@ -845,7 +904,8 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
     }
     const dim3 gp(nblocks(c->NR, 256)), b(256);
     auto prec = [&](const double* r, double* z) -> int {
-        if (c->F == 2) hipLaunchKernelGGL(k_pcg_prec<2>, gp, b, 0, st, c->L, c->params_pcg, r, z);
+        if (c->F == 1) hipLaunchKernelGGL(k_pcg_prec<1>, gp, b, 0, st, c->L, c->params_pcg, r, z);
+        else if (c->F == 2) hipLaunchKernelGGL(k_pcg_prec<2>, gp, b, 0, st, c->L, c->params_pcg, r, z);
         else hipLaunchKernelGGL(k_pcg_prec<3>, gp, b, 0, st, c->L, c->params_pcg, r, z);
         GS_LAUNCH_CHECK("k_pcg_prec");
         return 0;
@@ -884,7 +944,8 @@ int gs_masked_center(gs_masked* c, const double* dl, int dir, const double* in, 
     if (!c) return set_error("null masked context");
     if (!dl || !in || !out) return set_error("gs_masked_center: null argument");
     const dim3 g(nblocks(c->NR, 256)), b(256);
-    if (c->F == 2) hipLaunchKernelGGL(k_mc_center<2>, g, b, 0, S(stream), c->L, dl, dir, in, out);
+    if (c->F == 1) hipLaunchKernelGGL(k_mc_center<1>, g, b, 0, S(stream), c->L, dl, dir, in, out);
+    else if (c->F == 2) hipLaunchKernelGGL(k_mc_center<2>, g, b, 0, S(stream), c->L, dl, dir, in, out);
     else hipLaunchKernelGGL(k_mc_center<3>, g, b, 0, S(stream), c->L, dl, dir, in, out);
     GS_LAUNCH_CHECK("k_mc_center");
     return 0;
@@ -918,6 +979,30 @@ int gs_masked_nc_loglik(gs_masked* c, const double* dl, const double* s_nc, doub
     return 0;
 }
 
+int gs_masked_tt_fullsky(gs_masked* c, int noncentered, const double* dl, const double* zv, const double* zs,
+                         uint64_t seed, uint32_t iteration, int chain, double* s_out, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (c->F != 1) return set_error("gs_masked_tt_fullsky: temperature-only context required");
+    if (!dl || !s_out) return set_error("gs_masked_tt_fullsky: null argument");
+    const hipStream_t st = S(stream);
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32), ch = (uint32_t)chain;
+    hipLaunchKernelGGL(k_pcg_zpix, dim3(nblocks(c->npix, 256)), dim3(256), 0, st, c->npix, 1, c->rows, c->ninv, zv,
+                       slo, shi, ch, iteration, c->y);
+    GS_LAUNCH_CHECK("k_pcg_zpix");
+    if (gs_sht_map2alm(c->sht, 1, GS_ALM_REAL, c->y, c->r, 3, st)) return -1;
+    const double resc = (double)c->npix / (4.0 * PI);
+    const double kap = c->ninv0[0] * resc;
+    const dim3 g(nblocks(c->nlm, 256)), b(256);
+    if (noncentered)
+        hipLaunchKernelGGL(k_tt_fullsky<1>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, kap, zs, slo, shi, ch,
+                           iteration, s_out);
+    else
+        hipLaunchKernelGGL(k_tt_fullsky<0>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, kap, zs, slo, shi, ch,
+                           iteration, s_out);
+    GS_LAUNCH_CHECK("k_tt_fullsky");
+    return 0;
+}
+
 int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v, const double* zv, const double* zs,
                  const double* zm, const double* um, uint64_t seed, uint32_t iteration, int chain, int32_t* accept,
                  double* log_ratio, void* stream) {
@@ -931,7 +1016,7 @@ int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v,
     const long long FP = c->F * c->npix, FR = c->F * c->NR;
     double* vv = v ? v : c->vtmp;
     if (kind != GS_MCR_MALA) {
-        const double kap[3] = {c->mu[c->rows.r[0]] / c->w, c->mu[c->rows.r[1]] / c->w,
+        const double kap[3] = {c->mu[c->rows.r[0]] / c->w, c->F >= 2 ? c->mu[c->rows.r[1]] / c->w : 0.0,
                                c->F == 3 ? c->mu[c->rows.r[2]] / c->w : 0.0};
         if (mc_params(c, dl, kap, c->params, st)) return -1;
         if (kind == GS_MCR_OVERRELAX) {

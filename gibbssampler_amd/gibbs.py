@@ -162,7 +162,11 @@ class GibbsSampler:
             self.bins = {self.spectra[0]: np.asarray(bins)}
         self.dls_to_cls_array = np.array([2 * np.pi / (l * (l + 1)) if l != 0 else 0 for l in range(lmax + 1)])
         self.noise_pol = noise_pol
-        if self.mask is not None:
+        # TT from a pixel map keeps per-pixel noise (the f4 pixel path); the harmonic
+        # path needs isotropic noise and checks it when it is built
+        tt_pixel_map = self.nfields == 1 and not isinstance(pix_map, dict) and \
+            np.asarray(pix_map).shape[-1] == 12 * nside ** 2
+        if self.mask is not None or tt_pixel_map:
             nt = float(np.atleast_1d(noise)[0])
         else:
             nt = _scalar_noise(noise, "noise")
@@ -185,6 +189,34 @@ class GibbsSampler:
         self.metropolis_blocks = metropolis_blocks
         self.n_iter_metropolis = n_iter_metropolis
         self._runner = None
+        self._tt = None
+
+    # -- f4: temperature from pixel data (reference semantics, gibbssampler_amd.tt) -----------
+    def _tt_pixel_path(self, all_sph):
+        """TT runs on the pixel map itself (CenteredGibbs.py:103-236, NonCenteredGibbs.py:17-249)
+        unless the caller asks for the all_sph / harmonic form or gives a_lm."""
+        if self.nfields != 1 or all_sph:
+            return False
+        if self.mask is not None:
+            return True
+        return not isinstance(self.pix_map, dict) and np.asarray(self.pix_map).shape[-1] == self.Npix
+
+    def _tt_model(self, with_mh):
+        from .tt import TTModel
+        if self._tt is None:
+            if self.nchains != 1:
+                raise NotImplementedError("pixel-domain TT runs one chain per process (shard chains over GPUs)")
+            pm = self.pix_map["TT"] if isinstance(self.pix_map, dict) else self.pix_map
+            pv = blocks = None
+            if with_mh:
+                pv = self.proposal_variances
+                pv = pv["TT"] if isinstance(pv, dict) else pv
+                blocks = self.metropolis_blocks
+                blocks = blocks["TT"] if isinstance(blocks, dict) else blocks
+            self._tt = TTModel(pm, self.noise, self.bl_gauss, self.lmax, self.nside, self.bins["TT"], mask=self.mask,
+                               blocks=blocks, proposal_variances=pv, n_iter_metropolis=self.n_iter_metropolis,
+                               rng=self.rng, seed=self.seed, chain=self.chain0)
+        return self._tt
 
     # -- helpers of the reference base class --------------------------------------------
     def dls_to_cls(self, dls_):
@@ -292,6 +324,13 @@ class CenteredGibbs(GibbsSampler):
         self.all_sph = all_sph
         self.overrelaxation = overrelaxation
         self.cr_ula = ula
+        self.tt_pixel = self._tt_pixel_path(all_sph)
+        if self.tt_pixel:
+            from .tt import TTCenteredConstrainedRealization, TTCenteredClsSampler
+            m = self._tt_model(False)
+            self.constrained_sampler = TTCenteredConstrainedRealization(m)
+            self.cls_sampler = TTCenteredClsSampler(m)
+            return
         if self.mask is not None:
             self.constrained_sampler = self._masked_cr(noise_temp, noise_pol, gibbs_cr=gibbs_cr, n_gibbs=self.n_gibbs,
                                                        alpha=self.alpha, overrelaxation=overrelaxation, ula=ula,
@@ -321,6 +360,8 @@ class CenteredGibbs(GibbsSampler):
 
     def run_temperature(self, dls_init):
         """GibbsSampler.run_temperature (GibbsSampler.py:76-116)."""
+        if self.tt_pixel:
+            return self._tt.run_centered(dls_init, self.n_iter)
         h, _, t = self._run_common(dls_init)
         return h["TT"], np.ones(len(t), dtype=int), list(t)
 
@@ -337,6 +378,13 @@ class NonCenteredGibbs(GibbsSampler):
                          mask_path=mask_path, noise_pol=noise_Q, proposal_variances=proposal_variances,
                          metropolis_blocks=metropolis_blocks, n_iter_metropolis=n_iter_metropolis, **kw)
         self.all_sph = all_sph
+        self.tt_pixel = self._tt_pixel_path(all_sph)
+        if self.tt_pixel:
+            from .tt import TTNonCenteredConstrainedRealization, TTNonCenteredClsSampler
+            m = self._tt_model(True)
+            self.constrained_sampler = TTNonCenteredConstrainedRealization(m)
+            self.cls_sampler = TTNonCenteredClsSampler(m)
+            return
         self.constrained_sampler = NonCenteredConstrainedRealization(self)
         self.cls_sampler = NonCenteredClsSampler(self)
         if self.mask is not None:
@@ -356,6 +404,8 @@ class NonCenteredGibbs(GibbsSampler):
 
     def run_temperature(self, dls_init):
         """NonCenteredGibbs.py:488-527: (h_dl, total_accept, h_time_seconds)."""
+        if self.tt_pixel:
+            return self._tt.run_noncentered(dls_init, self.n_iter)
         h, acc, t = self._run_common(dls_init)
         return h["TT"][1:], acc["TT"], np.asarray(t)
 
@@ -375,6 +425,14 @@ class ASIS(GibbsSampler):
         self.all_sph = all_sph
         self.n_gibbs = n_gibbs
         self.overrelaxation = overrelaxation
+        self.tt_pixel = self._tt_pixel_path(all_sph)
+        if self.tt_pixel:
+            from .tt import TTCenteredConstrainedRealization, TTCenteredClsSampler, TTNonCenteredClsSampler
+            m = self._tt_model(True)
+            self.constrained_sampler = TTCenteredConstrainedRealization(m)
+            self.centered_cls_sampler = TTCenteredClsSampler(m)
+            self.non_centered_cls_sampler = TTNonCenteredClsSampler(m)
+            return
         self.constrained_sampler = CenteredConstrainedRealization(self)
         self.constrained_sampler.n_gibbs = n_gibbs
         self.centered_cls_sampler = CenteredClsSampler(self)
@@ -402,6 +460,8 @@ class ASIS(GibbsSampler):
 
     def run_temperature(self, dls_init):
         """ASIS.py:69-131: (h_dls, h_accept, h_accept_cr, h_time_seconds)."""
+        if self.tt_pixel:
+            return self._tt.run_asis(dls_init, self.n_iter, gibbs_cr=self.gibbs_cr)
         h, acc, t = self._run_common(dls_init)
         return h["TT"], acc["TT"], np.ones(len(t), dtype=int), np.asarray(t)
 

@@ -25,19 +25,24 @@ import torch
 
 from . import _capi
 
-FIELDS = {2: ("EE", "BB"), 3: ("TT", "EE", "BB")}
+FIELDS = {1: ("TT",), 2: ("EE", "BB"), 3: ("TT", "EE", "BB")}
+SPECS = {1: ("TT",), 2: ("EE", "BB"), 3: ("TT", "EE", "BB", "TE")}
 
 
 class MaskedCR:
-    """pix_map: dict with "Q", "U" (and "T" for nfields = 3) pixel maps;
+    """pix_map: dict with "Q", "U" (and "T" for nfields = 3) pixel maps, or for
+    nfields = 1 (temperature) the T map (array or dict with "T");
     noise_temp / noise_pol: per-pixel noise variances (arrays or scalars);
-    mask: per-pixel mask multiplying N^-1 (CenteredGibbs.py:266-274) or None."""
+    mask: per-pixel mask multiplying N^-1 (CenteredGibbs.py:266-274) or None.
+    Temperature contexts use the TT constants of ConstrainedRealization.py:44
+    (mu = max(N^-1) + 1e-7) and healpy's default iter = 3 for the data term
+    and the aux s | v analysis (utils.adjoint_synthesis_hp, CenteredGibbs.py:208)."""
 
     def __init__(self, pix_map, noise_temp, noise_pol, bl, lmax, nside, mask=None, nfields=2, gibbs_cr=True,
                  n_gibbs=1, alpha=-0.995, overrelaxation=False, ula=False, tau=0.02, rng="replay", seed=0, chain=0,
                  device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000):
-        if nfields not in (2, 3):
-            raise ValueError("nfields must be 2 (EB, the reference) or 3 (TEB)")
+        if nfields not in (1, 2, 3):
+            raise ValueError("nfields must be 1 (T), 2 (EB, the reference) or 3 (TEB)")
         self.lib = _capi.load()
         self.L, self.nside, self.F = int(lmax), int(nside), int(nfields)
         self.Npix = 12 * self.nside ** 2
@@ -55,8 +60,13 @@ class MaskedCR:
         ntemp = np.broadcast_to(np.asarray(noise_temp, dtype=np.float64), (self.Npix,))
         m = np.ones(self.Npix) if mask is None else np.asarray(mask, dtype=np.float64)
         inv = np.stack([m / ntemp, m / npol, m / npol])
-        maps = np.stack([np.asarray(pix_map.get("T", np.zeros(self.Npix)), dtype=np.float64),
-                         np.asarray(pix_map["Q"], dtype=np.float64), np.asarray(pix_map["U"], dtype=np.float64)])
+        zero = np.zeros(self.Npix)
+        if self.F == 1:
+            t = pix_map["T"] if isinstance(pix_map, dict) else pix_map
+            maps = np.stack([np.asarray(t, dtype=np.float64), zero, zero])
+        else:
+            maps = np.stack([np.asarray(pix_map.get("T", zero), dtype=np.float64),
+                             np.asarray(pix_map["Q"], dtype=np.float64), np.asarray(pix_map["U"], dtype=np.float64)])
         self._maps = torch.from_numpy(np.ascontiguousarray(maps)).to(device)
         self._inv = torch.from_numpy(np.ascontiguousarray(inv)).to(device)
         self.bl = np.ascontiguousarray(np.asarray(bl, dtype=np.float64)[: self.L + 1])
@@ -64,6 +74,8 @@ class MaskedCR:
         desc.lmax, desc.nside, desc.nfields = self.L, self.nside, self.F
         desc.bl = self.bl.ctypes.data_as(_capi.c_double_p)
         desc.n_gibbs, desc.alpha, desc.tau, desc.noise_pol0 = self.n_gibbs, self.alpha, self.tau, float(npol[0])
+        desc.mu_eps = 1e-7 if self.F == 1 else 1e-14
+        desc.adj_iter = 3 if self.F == 1 else 0
         h = ctypes.c_void_p()
         _capi.check(self.lib.gs_masked_create(ctypes.byref(desc), _capi.ptr(self._maps), _capi.ptr(self._inv),
                                               ctypes.byref(h)), "gs_masked_create")
@@ -83,7 +95,7 @@ class MaskedCR:
 
     # -- conversions -------------------------------------------------------------------
     def _dl(self, all_dls):
-        specs = ("EE", "BB") if self.F == 2 else ("TT", "EE", "BB", "TE")
+        specs = SPECS[self.F]
         arr = np.stack([np.asarray(all_dls[s], dtype=np.float64)[: self.L + 1] for s in specs])
         return torch.from_numpy(np.ascontiguousarray(arr)).to(self.device)
 
@@ -175,9 +187,13 @@ class MaskedCR:
         """right-hand side b A^T N^-1 d + fluctuations (device tensor [F, NR])."""
         it = self.iteration if iteration is None else int(iteration)
         zv = zs = None
-        if self.rng == "replay":      # CenteredGibbs.py:467-478: z_Q, z_U, then z_E, z_B
-            zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
-            zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
+        if self.rng == "replay":
+            if self.F == 1:           # TT (CenteredGibbs.py:153-155): z_alm, then z_pix
+                zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
+                zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
+            else:                     # CenteredGibbs.py:467-478: z_Q, z_U, then z_E, z_B
+                zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
+                zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
         rhs = torch.empty((self.F, self.NR), dtype=torch.float64, device=self.device)
         _capi.check(self.lib.gs_masked_pcg_rhs(self.handle, _capi.ptr(dl), _capi.ptr(zv), _capi.ptr(zs), self.seed,
                                                it, self.chain, _capi.ptr(rhs), _capi.stream_ptr()),
@@ -197,6 +213,21 @@ class MaskedCR:
         self.pcg_iterations.append(iters.value)
         self.pcg_residual = res.value
         return x
+
+    def tt_fullsky(self, dl, noncentered=False, iteration=None, out=None):
+        """temperature full-sky CR from the pixel map (gs_masked_tt_fullsky):
+        CenteredGibbs.py:108-132 or NonCenteredGibbs.py:22-38; replay draws
+        z_alm then z_pix."""
+        it = self.iteration if iteration is None else int(iteration)
+        zv = zs = None
+        if self.rng == "replay":
+            zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
+            zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
+        out = torch.empty((1, self.NR), dtype=torch.float64, device=self.device) if out is None else out
+        _capi.check(self.lib.gs_masked_tt_fullsky(self.handle, int(bool(noncentered)), _capi.ptr(dl), _capi.ptr(zv),
+                                                  _capi.ptr(zs), self.seed, it, self.chain, _capi.ptr(out),
+                                                  _capi.stream_ptr()), "gs_masked_tt_fullsky")
+        return out
 
     def sample_mask(self, all_dls):
         """CenteredGibbs.py:448-491: PCG constrained realisation; accept 1."""
@@ -316,20 +347,22 @@ class PixelMH:
 
     def __init__(self, cr, bins, blocks, proposal_variances, n_iter_metropolis=1):
         from .engine import GibbsPlan, MH_ORDER
-        if cr.F != 2:
-            raise NotImplementedError("the pixel-domain NC sampler is the reference's EB model "
-                                      "(PolarizationNonCenteredClsSampler); TEB masked NC is not defined there")
+        if cr.F == 3:
+            raise NotImplementedError("the pixel-domain NC sampler is the reference's EB / TT model "
+                                      "(PolarizationNonCenteredClsSampler, NonCenteredClsSampler); TEB is not "
+                                      "defined there")
+        F = cr.F
         self.cr = cr
-        self.spectra = ("EE", "BB")
-        self.order = MH_ORDER[2]
+        self.spectra = SPECS[F]
+        self.order = MH_ORDER[F]
         self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
         self.blocks = {s: np.asarray(blocks[s]) for s in self.spectra}
         self.n_iter = int(n_iter_metropolis)
-        self.plan = GibbsPlan(cr.L, cr.nside, 2, 1, cr.bl, [1.0, 1.0], self.bins, blocks=self.blocks,
+        self.plan = GibbsPlan(cr.L, cr.nside, F, 1, cr.bl, [1.0] * F, self.bins, blocks=self.blocks,
                               proposal_variances=proposal_variances, chain0=cr.chain,
                               n_iter_metropolis=self.n_iter)
         L = cr.L
-        idx = np.full((2, L + 1), -1, dtype=np.int64)
+        idx = np.full((F, L + 1), -1, dtype=np.int64)
         for k, s in enumerate(self.spectra):
             b = self.bins[s]
             for i in range(len(b) - 1):
@@ -339,7 +372,7 @@ class PixelMH:
         self._lik = torch.zeros(1, dtype=torch.float64, device=cr.device)
 
     def unfold(self, binned_t):
-        """utils.unfold_bins on the device: [2, maxbins] -> [2, L+1]."""
+        """utils.unfold_bins on the device: [nspec, maxbins] -> [nspec, L+1]."""
         return torch.where(self._valid, torch.gather(binned_t, 1, self._idx), 0.0).contiguous()
 
     def noncentre(self, dl_unbinned, s):
@@ -431,7 +464,7 @@ class MaskedMHRunner:
         self.mh = PixelMH(cr, bins, blocks, proposal_variances, n_iter_metropolis)
         self.cr_kind = cr_kind_ if kind == "asis" else KIND_PCG
         self.plan = self.mh.plan
-        self.d0 = self.plan.zeros(2, cr.NR)
+        self.d0 = self.plan.zeros(cr.F, cr.NR)
 
     def _pcg(self, dl, it):
         return self.cr.pcg_solve(dl, self.cr.pcg_rhs(dl, iteration=it))

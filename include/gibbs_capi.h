@@ -205,17 +205,31 @@ int gs_sht_map2alm(gs_sht* sht, int ncomp, int layout, const double* maps, doubl
 #define GS_MCR_AUX_MALA 3
 typedef struct gs_masked gs_masked;
 typedef struct gs_masked_desc {
-    int lmax, nside, nfields;      /* nfields 2 (E,B) or 3 (T,E,B)                */
+    int lmax, nside, nfields;      /* nfields 1 (T), 2 (E,B) or 3 (T,E,B)         */
     const double* bl;              /* HOST [L+1] beam                             */
     int n_gibbs;                   /* inner iterations (CenteredGibbs.py:250)     */
     double alpha;                  /* over-relaxation, -0.995 (CenteredGibbs.py:244) */
     double tau;                    /* MALA step, 0.02 (CenteredGibbs.py:294)      */
     double noise_pol0;             /* noise_pol[0] of the MALA sigma (571-572)    */
+    double mu_eps;                 /* mu = max(N^-1) + mu_eps; 0 -> 1e-14 (pol,   */
+                                   /* CenteredGibbs.py:276); TT: 1e-7              */
+                                   /* (ConstrainedRealization.py:44)              */
+    int adj_iter;                  /* map2alm iterations of the data term          */
+                                   /* b A^T N^-1 d and of the aux s|v analysis:    */
+                                   /* 0 (pol: iter=0) or 3 (TT: adjoint_synthesis_hp */
+                                   /* and healpy's default, CenteredGibbs.py:208)  */
 } gs_masked_desc;
 int gs_masked_create(const gs_masked_desc* desc, const double* maps, const double* inv_noise, gs_masked** out);
 int gs_masked_destroy(gs_masked* ctx);
 int gs_masked_info(const gs_masked* ctx, double* mu3 /* HOST [3] */, double* second_part_grad /* DEVICE [F][NR] */);
 int gs_masked_gradient(gs_masked* ctx, const double* dl, const double* s, double* grad, double* pix, void* stream);
+/* f4: temperature full-sky CR from pixel data (nfields = 1 context):
+ * centered CenteredConstrainedRealization.sample_no_mask (CenteredGibbs.py:108-132)
+ * or non-centered NonCenteredConstrainedRealization.sample_no_mask
+ * (NonCenteredGibbs.py:22-38); zv [Npix] / zs [NR] replay normals (reference
+ * order: zs then zv) or NULL for the native streams; s_out [NR]. */
+int gs_masked_tt_fullsky(gs_masked* ctx, int noncentered, const double* dl, const double* zv, const double* zs,
+                         uint64_t seed, uint32_t iteration, int chain, double* s_out, void* stream);
 int gs_masked_cr(gs_masked* ctx, int kind, const double* dl, double* s, double* v, const double* zv, const double* zs,
                  const double* zm, const double* um, uint64_t seed, uint32_t iteration, int chain, int32_t* accept,
                  double* log_ratio, void* stream);

@@ -88,21 +88,23 @@ class MaskedModel:
     maps: [3, Npix] (T, Q, U); inv_noise: [3, Npix] mask-multiplied N^-1
     (T row ignored for nfields = 2)."""
 
-    def __init__(self, L, nside, nfields, bl, maps, inv_noise):
+    def __init__(self, L, nside, nfields, bl, maps, inv_noise, mu_eps=1e-14, adj_iter=0):
         self.L, self.nside, self.F = int(L), int(nside), int(nfields)
+        self.adj_iter = int(adj_iter)
         self.Npix = 12 * self.nside ** 2
         self.w = FOURPI / self.Npix
         self.bl = np.asarray(bl, dtype=np.float64)
         self.maps = np.asarray(maps, dtype=np.float64)
         self.inv_noise = np.asarray(inv_noise, dtype=np.float64)
-        # CenteredGibbs.py:276 (pol); TEB: the same rule for T
-        self.mu = np.array([self.inv_noise[k].max() + 1e-14 for k in range(3)])
+        # CenteredGibbs.py:276 (pol, 1e-14); TEB: the same rule for T; TT (nfields 1):
+        # ConstrainedRealization.py:44 (1e-7)
+        self.mu = np.array([self.inv_noise[k].max() + mu_eps for k in range(3)])
         self.slot_ell = H.slot_ell(self.L)
 
-    # fields -> map rows: F=2: E,B <-> Q,U (rows 1,2); F=3: T,E,B <-> T,Q,U
+    # fields -> map rows: F=1: T; F=2: E,B <-> Q,U (rows 1,2); F=3: T,E,B <-> T,Q,U
     @property
     def rows(self):
-        return (1, 2) if self.F == 2 else (0, 1, 2)
+        return {1: (0,), 2: (1, 2), 3: (0, 1, 2)}[self.F]
 
     def synth(self, s_real):
         """maps of b * s (s real layout [F, NR]) -> [F, Npix] for the field rows."""
@@ -113,18 +115,18 @@ class MaskedModel:
         m = O.alm2map(a, self.nside, self.L)
         return np.stack([m[r] for r in self.rows])
 
-    def analysis(self, mp):
-        """complex_to_real(map2alm(maps, iter=0)) for the field rows: [F, NR]."""
+    def analysis(self, mp, iter=0):
+        """complex_to_real(map2alm(maps, iter)) for the field rows: [F, NR]."""
         full = np.zeros((3, self.Npix))
         for k, r in enumerate(self.rows):
             full[r] = mp[k]
-        a = O.map2alm(full, self.nside, self.L, iter=0)
+        a = O.map2alm(full, self.nside, self.L, iter=iter)
         return np.stack([H.complex_to_real(a[r], self.L) for r in self.rows])
 
     def second_part_grad(self):
-        """b A^T N^-1 d (CenteredGibbs.py:298-306)."""
+        """b A^T N^-1 d (CenteredGibbs.py:298-306; TT: adjoint_synthesis_hp, iter 3)."""
         nd = np.stack([self.inv_noise[r] * self.maps[r] for r in self.rows])
-        return self.analysis(nd) * (self.Npix / FOURPI) * self.bl[self.slot_ell][None]
+        return self.analysis(nd, self.adj_iter) * (self.Npix / FOURPI) * self.bl[self.slot_ell][None]
 
     def aux_model(self, bins):
         """oracle.harmonic Model whose kappa_f = mu_f / w (the s | v block)."""
@@ -155,9 +157,9 @@ def _s_given_v(mm, dl_unbinned, v, z, s_old=None, alpha=None):
     """s | v  (CenteredGibbs.py:703-726): per slot (EB) or per-l block (TEB)
     var_s = (C^+ + (mu/w) b^2)^-1, mean = var_s b map2alm(v + N^-1 d)/w."""
     rhs = np.stack([v[k] + mm.inv_noise[r] * mm.maps[r] for k, r in enumerate(mm.rows)])
-    r_real = mm.analysis(rhs)
+    r_real = mm.analysis(rhs, mm.adj_iter)
     ell = mm.slot_ell
-    if mm.F == 2:
+    if mm.F != 3:
         out = []
         var = H.var_from_dl(dl_unbinned)
         for k, r in enumerate(mm.rows):
@@ -284,10 +286,10 @@ def _prior_pinv_apply(mm, dl_unbinned, x, half=False):
     """C^+ x per slot (EB: inv_var; TEB: 2x2 TE pseudo-inverse + BB); with
     half=True the factor (A^+)^T (covariance C^+) used for the C^-1/2 draw."""
     ell = mm.slot_ell
-    if mm.F == 2:
+    if mm.F != 3:
         var = H.var_from_dl(dl_unbinned)
         f = (lambda v: np.sqrt(H.inv_var(v))) if half else H.inv_var
-        return np.stack([f(var[k][ell]) * x[k] for k in range(2)])
+        return np.stack([f(var[k][ell]) * x[k] for k in range(mm.F)])
     model = H.Model(mm.L, mm.nside, 3, mm.bl, [1.0, 1.0, 1.0], {s: np.arange(mm.L + 2) for s in H.SPECTRA[3]})
     A = H.cov_chol(model, dl_unbinned)
     Ai = H.chol_pinv(A)                                    # A^+ (lower)
@@ -378,9 +380,9 @@ def pcg_sample(mm, dl_unbinned, draws, tol=1e-12, maxiter=2000):
 # ----------------------------------------------------------------------------
 def nc_map(mm, dl_unbinned, s_nc):
     """A b C^1/2(D) s_nc for the field rows (EB: sqrt(var) per slot; TEB: chol(C))."""
-    if mm.F == 2:
+    if mm.F != 3:
         var = H.var_from_dl(dl_unbinned)
-        s = np.stack([np.sqrt(var[k][mm.slot_ell]) * s_nc[k] for k in range(2)])
+        s = np.stack([np.sqrt(var[k][mm.slot_ell]) * s_nc[k] for k in range(mm.F)])
     else:
         model = H.Model(mm.L, mm.nside, 3, mm.bl, [1.0] * 3, {x: np.arange(mm.L + 2) for x in H.SPECTRA[3]})
         A = H.cov_chol(model, dl_unbinned)
@@ -411,7 +413,7 @@ def noncentre(mm, dl_unbinned, s, inverse=True):
     (the re-centring of ASIS.py:199-203)."""
     var = H.var_from_dl(dl_unbinned)
     out = np.zeros_like(s)
-    for k in range(2):
+    for k in range(mm.F):
         v = var[k][mm.slot_ell]
         if inverse:
             iv = np.zeros_like(v)
@@ -470,3 +472,110 @@ def run_masked_mh_chain(kind, mm, model, dls_init, n_iter, draws, tol=1e-13, cr=
             accs[sp].append(a[sp])
             hist[sp].append(binned[sp].copy())
     return {sp: np.array(v) for sp, v in hist.items()}, {sp: np.array(v) for sp, v in accs.items()}, s
+
+
+# ----------------------------------------------------------------------------
+# f4: temperature-only samplers from pixel data (TT; full sky or masked)
+# ----------------------------------------------------------------------------
+def tt_model(L, nside, bl, tmap, inv_noise_t):
+    """the TT problem: N^-1 = (mask) / noise (ConstrainedRealization.py:22-37),
+    mu = max(N^-1) + 1e-7 (:44), data term adjoint_synthesis_hp (iter 3)."""
+    z = np.zeros_like(np.asarray(tmap, dtype=np.float64))
+    return MaskedModel(L, nside, 1, bl, np.stack([tmap, z, z]), np.stack([inv_noise_t, z, z]), mu_eps=1e-7,
+                       adj_iter=3)
+
+
+def tt_fullsky_cr(mm, dl_tt, z_slot, z_pix, noncentered=False):
+    """CenteredConstrainedRealization.sample_no_mask (CenteredGibbs.py:108-132) or
+    NonCenteredConstrainedRealization.sample_no_mask (NonCenteredGibbs.py:22-38):
+    the diagonal solve with N^-1[0] Npix/4pi for the noise precision."""
+    ell = mm.slot_ell
+    var = H.var_from_dl(np.atleast_2d(dl_tt))[0][ell]
+    b = mm.bl[ell]
+    kap = mm.inv_noise[0][0] * mm.Npix / FOURPI
+    g2 = mm.second_part_grad()[0]
+    y = np.sqrt(mm.inv_noise[0]) * z_pix
+    f = b * mm.analysis(y[None], 3)[0] * (mm.Npix / FOURPI)
+    if noncentered:
+        sig = 1.0 / (1.0 + var * kap * b * b)
+        return sig * (np.sqrt(var) * g2) + sig * (z_slot + np.sqrt(var) * f)
+    iv = np.where((ell >= 2) & (var != 0), 1.0 / np.where(var != 0, var, 1.0), 0.0)
+    sig = 1.0 / (iv + kap * b * b)
+    return sig * g2 + sig * (z_slot * np.sqrt(iv) + f)
+
+
+def tt_chain(kind, mm_cr, mm_mh, model, dls_init, n_iter, draws, gibbs_cr=False, tol=1e-13, native=None):
+    """The reference's TT drivers in their draw order (f4 semantics):
+    kind "centered": GibbsSampler.run_temperature (GibbsSampler.py:76-116);
+    "noncentered": NonCenteredGibbs.run_temperature (488-527);
+    "asis": ASIS.run_temperature (ASIS.py:69-131).  mm_cr: the CR problem
+    (tt_model, masked or not), mm_mh the MH likelihood problem.  Full sky ->
+    closed forms; masked -> PCG.  native: (seed, chain) with draws(it) ->
+    NativeDraws.  Returns (history, accepts, final map)."""
+    from . import reference_eb as RE
+    masked = bool(np.any(mm_cr.inv_noise[0] == 0))
+    nr = (mm_cr.L + 1) ** 2
+
+    def dr(it):
+        return draws(it) if native is not None else draws
+
+    def cr_c(dl, it):
+        if masked:
+            d = dr(it)
+            zs = d.slot_normals(1, nr, substep=SUB_PCG_S)
+            zp = d.pixel_normals(1, mm_cr.Npix, maps=(0,), substep=SUB_PCG_V)
+            x, _ = pcg_solve(mm_cr, dl, mm_cr.second_part_grad() + pcg_fluctuation(mm_cr, dl, zp, zs), tol)
+            return x
+        d = dr(it)
+        zs = d.slot_normals(1, nr, substep=SUB_PCG_S)
+        zp = d.pixel_normals(1, mm_cr.Npix, maps=(0,), substep=SUB_PCG_V)
+        return tt_fullsky_cr(mm_cr, dl, zs[0], zp[0])[None]
+
+    def cr_nc(dl, it):
+        if masked:
+            return noncentre(mm_cr, dl, cr_c(dl, it))
+        d = dr(it)
+        zs = d.slot_normals(1, nr, substep=SUB_PCG_S)
+        zp = d.pixel_normals(1, mm_cr.Npix, maps=(0,), substep=SUB_PCG_V)
+        return tt_fullsky_cr(mm_cr, dl, zs[0], zp[0], noncentered=True)[None]
+
+    def cls(s, it):
+        if native is not None:
+            return H.centered_cls_draw(model, H.sweep_stats(model, s, model.d_alm), seed=native[0], chain=native[1],
+                                       iteration=it)
+        return RE.cls_centered(model, s)
+
+    def mh(s_nc, start, it):
+        if native is not None:
+            return pixel_mh(mm_mh, model, start, s_nc, seed=native[0], chain=native[1], iteration=it)
+        u_prop, u_acc = RE.draw_mh_uniforms(model)
+        return pixel_mh(mm_mh, model, start, s_nc, u_prop=u_prop, u_accept=u_acc)
+
+    binned = {"TT": np.array(dls_init["TT"], dtype=np.float64)}
+    hist, accs = [], []
+    s = None
+    if kind in ("centered", "asis"):
+        hist.append(binned["TT"].copy())
+        s = cr_c(model.unfold(binned), 0)
+    for i in range(n_iter):
+        it = i + 1
+        dl = model.unfold(binned)
+        if kind == "centered":
+            s = cr_c(dl, it)
+            binned = cls(s, it)
+        elif kind == "noncentered":
+            s = cr_nc(dl, it)
+            binned, a = mh(s, binned, it)
+            accs.append(a["TT"])
+        else:
+            if gibbs_cr:
+                s, _ = aux_variable(mm_cr, dl, s, 1, dr(it))
+            else:
+                s = cr_c(dl, it)
+            tmp = cls(s, it)
+            s_nc = noncentre(mm_cr, model.unfold(tmp), s)
+            binned, a = mh(s_nc, tmp, it)
+            accs.append(a["TT"])
+            s = noncentre(mm_cr, model.unfold(binned), s_nc, inverse=False)
+        hist.append(binned["TT"].copy())
+    return np.array(hist), np.array(accs), s
