@@ -83,15 +83,15 @@ def main():
                            nchains=args.nchains, bl=P["bl"], noise_var=P["noise_var"], bins=P["bins"],
                            d_alm=P["d_alm"], blocks=P["blocks"], proposal_variances=P["proposal_variances"],
                            rng="native", seed=args.seed, chain0=rank * args.nchains)
-    plan = runner.plan
+    plans = (runner.plan,)
     runner.init(P["dls_init"])
+    traces = [p.zeros(args.steps, p.nchains, p.nspec, p.maxbins) for p in plans]
     for _ in range(args.warmup):
         runner.step()
-    trace = plan.zeros(args.steps, plan.nchains, plan.nspec, plan.maxbins)
     use_graph = not args.no_graph
     if use_graph:
         # one hipGraph per Gibbs iteration: the D_l trace is written on the device
-        runner.capture_graph(trace=trace, trace_capacity=args.steps)
+        runner.capture_graph(trace=traces[0], trace_capacity=args.steps)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -100,7 +100,7 @@ def main():
     for i in range(args.steps):
         runner.step()
         if not use_graph:
-            trace[i].copy_(runner.dl)
+            traces[0][i].copy_(runner.dl)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -109,12 +109,14 @@ def main():
     # dominant-kernel timing: hipEvents around every sweep launch (on its stream) of
     # eager steps of the same state right after the timed loop
     runner.graph = None
-    plan.iteration_counter(False)
-    plan.sweep_timing(True)
+    plans[0].iteration_counter(False)
+    for p in plans:
+        p.sweep_timing(True)
     for _ in range(args.timing_launches):
         runner.step()
     torch.cuda.synchronize()
-    sweep_ms, sweep_n = plan.sweep_timing(False)
+    timed = [p.sweep_timing(False) for p in plans]
+    trace = torch.cat(traces, 1)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -128,16 +130,19 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank == 0:
+        sweep_n = sum(n for _, n in timed)
+        sweep_ms = sum(ms for ms, _ in timed)
         sweep_avg_ms = sweep_ms / max(sweep_n, 1)
-        ntask = plan.ntask
-        alg_bytes = sweep_algorithmic_bytes(plan.L, plan.F, plan.nchains,
-                                            plan.nchains * ntask * plan.nstat * 64 * 8)
+        per_launch = [sweep_algorithmic_bytes(p.L, p.F, p.nchains, p.nchains * p.ntask * p.nstat * 64 * 8)
+                      for p in plans]
+        alg_bytes = int(round(sum(b * n for b, (_, n) in zip(per_launch, timed)) / max(sweep_n, 1)))
         achieved = alg_bytes / (sweep_avg_ms * 1e-3) / 1e9
+        plan = plans[0]
         traffic = None
         try:
             with open(args.profile_json) as f:
                 prof = json.load(f)
-            key = f"{args.workload}_L{args.lmax}_F{args.fields}_c{args.nchains}"
+            key = f"{args.workload}_L{args.lmax}_F{args.fields}_c{plan.nchains}"
             if key in prof:
                 traffic = prof[key].get("hbm_bytes_per_launch")
         except (OSError, ValueError):

@@ -1481,11 +1481,9 @@ int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out,
     return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
 }
 
-int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
-                        const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
-                        void* stream) {
+int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t it, void* stream) {
     if (check_plan(p)) return -1;
-    if (!p->has_mh) return set_error("gs_step_noncentered: plan has no MH blocks / proposal variances");
+    if (!p->has_mh) return set_error("gs_nc_prologue: plan has no MH blocks / proposal variances");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const int nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
     const int nbq = nblk((long long)p->nchains * (p->L + 1), 256);
@@ -1496,8 +1494,29 @@ int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_o
     if (p->F == 1) GS_PRO(1); else if (p->F == 2) GS_PRO(2); else GS_PRO(3);
 #undef GS_PRO
     GS_LAUNCH_CHECK("k_nc_prologue");
-    if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
+    return 0;
+}
+
+int gs_nc_sweep(gs_plan* p, const double* d_alm, double* s_out, const double* z, uint64_t seed, uint32_t it,
+                void* stream) {
+    if (check_plan(p)) return -1;
+    return gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream);
+}
+
+int gs_nc_decide(gs_plan* p, double* dl, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
+                 void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->has_mh) return set_error("gs_nc_decide: plan has no MH blocks / proposal variances");
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     return mh_decide(p, p->stats, dl, u_acc, slo, shi, it, accept_out, stream);
+}
+
+int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
+                        const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
+                        void* stream) {
+    if (gs_nc_prologue(p, dl, u_prop, seed, it, stream)) return -1;
+    if (gs_nc_sweep(p, d_alm, s_out, z, seed, it, stream)) return -1;
+    return gs_nc_decide(p, dl, u_acc, seed, it, accept_out, stream);
 }
 
 int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z, const double* igvar,

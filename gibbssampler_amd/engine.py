@@ -235,6 +235,19 @@ class GibbsPlan:
                                              C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept), self._s()),
                 "gs_step_noncentered")
 
+    # the three stages of step_noncentered (for pipelined schedules)
+    def nc_prologue(self, dl, u_prop=None, seed=0, iteration=0):
+        C.check(self.lib.gs_nc_prologue(self._h, C.ptr(dl), C.ptr(u_prop), int(seed), int(iteration), self._s()),
+                "gs_nc_prologue")
+
+    def nc_sweep(self, d, s_out, z=None, seed=0, iteration=0):
+        C.check(self.lib.gs_nc_sweep(self._h, C.ptr(d), C.ptr(s_out), C.ptr(z), int(seed), int(iteration),
+                                     self._s()), "gs_nc_sweep")
+
+    def nc_decide(self, dl, u_acc=None, seed=0, iteration=0, accept=None):
+        C.check(self.lib.gs_nc_decide(self._h, C.ptr(dl), C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept),
+                                      self._s()), "gs_nc_decide")
+
     def step_asis(self, d, dl, s_out, z=None, igvar=None, u_prop=None, u_acc=None, seed=0, iteration=0,
                   accept=None, dl_tmp=None, recentre=False):
         C.check(self.lib.gs_step_asis(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), C.ptr(z), C.ptr(igvar),

@@ -156,3 +156,4 @@ class BatchedRunner:
             quirk = True
             self.plan.recentre(self.dl, s, None if quirk else self.dl_tmp)
         return s
+

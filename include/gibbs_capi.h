@@ -142,6 +142,17 @@ int gs_step_centered(gs_plan* plan, const double* d_alm, double* dl_binned, doub
 int gs_step_noncentered(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
                         const double* z_replay, const double* u_prop_replay, const double* u_accept_replay,
                         uint64_t seed, uint32_t iteration, int32_t* accept_out, void* stream);
+/* the three stages of gs_step_noncentered, for callers that schedule them:
+ *   gs_nc_prologue  NC block parameters of dl and the MH proposals
+ *                   (NonCenteredGibbs.py:134-176 operator, 292-330 proposals)
+ *   gs_nc_sweep     the CR draw + sufficient statistics into the plan
+ *   gs_nc_decide    the Metropolis-within-Gibbs decisions (NonCenteredGibbs.py:401-445) */
+int gs_nc_prologue(gs_plan* plan, const double* dl_binned, const double* u_prop_replay, uint64_t seed,
+                   uint32_t iteration, void* stream);
+int gs_nc_sweep(gs_plan* plan, const double* d_alm, double* s_out, const double* z_replay, uint64_t seed,
+                uint32_t iteration, void* stream);
+int gs_nc_decide(gs_plan* plan, double* dl_binned, const double* u_accept_replay, uint64_t seed, uint32_t iteration,
+                 int32_t* accept_out, void* stream);
 /* dl_tmp_out: nullable, receives the centered draw; recentre: 0 lazy (s_out keeps the
  * centered CR draw), 1 materialise the re-centred map in s_out */
 int gs_step_asis(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
