@@ -742,6 +742,19 @@ struct MhPhases {
     int lmin;     // smallest multipole any MH block covers (terms below it are never read)
 };
 
+// optional tail of the fused MH kernel (graph-captured NC steps): record this
+// chain's D_l in the trace and advance the device iteration counter once the
+// last workgroup has finished (every workgroup read the counter at its start,
+// so the ticket is race-free).  (Computing the next step's prologue here as
+// well was measured slower: it puts that wide, latency-bound work on one
+// workgroup per chain.)
+struct MhEpi {
+    double* trace;          // nullable: trace[(it-1) % cap][chain][nspec][maxbins]
+    int cap;
+    uint32_t* counter;      // nullable: [0] iteration (advanced), [1] finished-workgroup ticket
+    int nchains;
+};
+
 template <int F>
 __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases ph, const int2* __restrict__ phase_tab,
                                                   const int4* __restrict__ phase_rng,
@@ -752,7 +765,8 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                                                   const double* __restrict__ stats, double* __restrict__ dl,
                                                   const double* __restrict__ prop, const double* __restrict__ logr,
                                                   const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
-                                                  IterArg itarg, int chain0, int32_t* __restrict__ accept_out) {
+                                                  IterArg itarg, int chain0, int32_t* __restrict__ accept_out,
+                                                  MhEpi epi) {
     const uint32_t iter = itarg.get();
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
@@ -867,6 +881,25 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
             }
         }
         __syncthreads();
+    }
+    // ---- epilogue (graph-captured NC steps) ----
+    const int nrow = NSP * maxbins;
+    if (epi.trace) {
+        const long long slot = (long long)((iter + (uint32_t)epi.cap - 1u) % (uint32_t)epi.cap);
+        double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
+        for (int k = tid; k < nrow; k += blockDim.x) tr[k] = D[k];
+    }
+    if (epi.counter) {
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence();
+            const uint32_t t = atomicAdd(&epi.counter[1], 1u);
+            if (t == gridDim.x - 1) {
+                epi.counter[1] = 0u;
+                __threadfence();
+                atomicAdd(&epi.counter[0], 1u);
+            }
+        }
     }
 }
 
@@ -1358,7 +1391,7 @@ int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_
 }
 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
-                     uint32_t iteration, int32_t* accept_out, void* stream);
+                     uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi = nullptr);
 
 int gs_mh_propose(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t iteration,
                   double* prop_out, double* logr_out, double* u_acc_out, void* stream) {
@@ -1405,8 +1438,10 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
 
 // the MH phases proper (proposals already in p->prop / p->logr)
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
-                     uint32_t iteration, int32_t* accept_out, void* stream) {
+                     uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi) {
     int maxnb = 0;
+    const MhEpi none{nullptr, 1, nullptr, p->nchains};
+    const MhEpi E = epi ? *epi : none;
     MhPhases ph{};
     ph.nphase = p->nphase;
     ph.lmin = p->mh_lmin;
@@ -1421,12 +1456,13 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
 #define GS_MF(FF) hipLaunchKernelGGL((k_mh_fused<FF>), dim3(p->nchains), dim3(1024), lds, S(stream), p->L, p->maxbins, ph, \
                                      p->phase_tab, p->phase_rng, p->bins, p->blocks, p->meta + 8, p->nacc, p->n_iter_mh, p->ell2blk,    \
                                      p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop,       \
-                                     p->logr, u_acc, slo, shi, IterArg{iteration, p->itp()}, p->chain0, accept_out)
+                                     p->logr, u_acc, slo, shi, IterArg{iteration, p->itp()}, p->chain0, accept_out, E)
         if (p->F == 1) GS_MF(1); else if (p->F == 2) GS_MF(2); else GS_MF(3);
 #undef GS_MF
         GS_LAUNCH_CHECK("k_mh_fused");
         return 0;
     }
+    if (epi) return set_error("mh_decide: the fused epilogue needs the single-launch MH (l_max too large)");
     // very large l_max: two launches per phase (terms in HBM, one wave per block)
     const long long nl = (long long)p->nchains * (p->L + 1);
     for (int ph = 0; ph < p->nphase; ++ph) {
@@ -1509,6 +1545,16 @@ int gs_nc_decide(gs_plan* p, double* dl, const double* u_acc, uint64_t seed, uin
     if (!p->has_mh) return set_error("gs_nc_decide: plan has no MH blocks / proposal variances");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     return mh_decide(p, p->stats, dl, u_acc, slo, shi, it, accept_out, stream);
+}
+
+int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32_t* accept_out, double* trace,
+                       int capacity, void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->has_mh) return set_error("gs_nc_decide_fused: plan has no MH blocks / proposal variances");
+    if (trace && capacity < 1) return set_error("gs_nc_decide_fused: capacity < 1");
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    const MhEpi epi{trace, std::max(capacity, 1), p->iter_dev_on ? p->iter_dev : nullptr, p->nchains};
+    return mh_decide(p, p->stats, dl, nullptr, slo, shi, it, accept_out, stream, &epi);
 }
 
 int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,

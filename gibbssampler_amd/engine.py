@@ -248,6 +248,10 @@ class GibbsPlan:
         C.check(self.lib.gs_nc_decide(self._h, C.ptr(dl), C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept),
                                       self._s()), "gs_nc_decide")
 
+    def nc_decide_fused(self, dl, seed=0, iteration=0, accept=None, trace=None, capacity=0):
+        C.check(self.lib.gs_nc_decide_fused(self._h, C.ptr(dl), int(seed), int(iteration), C.ptr(accept),
+                                            C.ptr(trace), int(capacity), self._s()), "gs_nc_decide_fused")
+
     def step_asis(self, d, dl, s_out, z=None, igvar=None, u_prop=None, u_acc=None, seed=0, iteration=0,
                   accept=None, dl_tmp=None, recentre=False):
         C.check(self.lib.gs_step_asis(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), C.ptr(z), C.ptr(igvar),

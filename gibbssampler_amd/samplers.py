@@ -82,10 +82,18 @@ class BatchedRunner:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._launch_step(0)
-            if trace is not None:
-                p.record_trace(self.dl, trace, trace_capacity)
-            p.advance_iteration()
+            if self.kind == "noncentered":
+                # NC: prologue, sweep (+ statistics), MH decisions with the trace record
+                # and the counter advance fused into the decision launch
+                p.nc_prologue(self.dl, seed=self.seed)
+                p.nc_sweep(self.d, self.s, seed=self.seed)
+                p.nc_decide_fused(self.dl, seed=self.seed, accept=self.accept, trace=trace,
+                                  capacity=trace_capacity or 0)
+            else:
+                self._launch_step(0)
+                if trace is not None:
+                    p.record_trace(self.dl, trace, trace_capacity)
+                p.advance_iteration()
         self.graph = g
         return g
 

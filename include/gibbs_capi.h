@@ -153,6 +153,13 @@ int gs_nc_sweep(gs_plan* plan, const double* d_alm, double* s_out, const double*
                 uint32_t iteration, void* stream);
 int gs_nc_decide(gs_plan* plan, double* dl_binned, const double* u_accept_replay, uint64_t seed, uint32_t iteration,
                  int32_t* accept_out, void* stream);
+/* gs_nc_decide with the step's bookkeeping fused into the same launch (native
+ * RNG, for graph-captured steps): after the decisions each chain's workgroup
+ * records its D_l in trace (nullable; trace[(it-1) % capacity]) and, with the
+ * device counter on, the last workgroup advances the counter (ticket; every
+ * workgroup read it at its start). */
+int gs_nc_decide_fused(gs_plan* plan, double* dl_binned, uint64_t seed, uint32_t iteration, int32_t* accept_out,
+                       double* trace, int capacity, void* stream);
 /* dl_tmp_out: nullable, receives the centered draw; recentre: 0 lazy (s_out keeps the
  * centered CR draw), 1 materialise the re-centred map in s_out */
 int gs_step_asis(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
