@@ -33,10 +33,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="noncentered", choices=["noncentered", "centered", "asis"])
-    ap.add_argument("--nchains", type=int, default=32, help="chains per GPU")
-    ap.add_argument("--lmax", type=int, default=1024)
-    ap.add_argument("--nside", type=int, default=512)
+    ap.add_argument("--workload", default="noncentered", choices=["noncentered", "centered", "asis", "masked"],
+                    help="masked = BASELINE configs[4]: CenteredGibbs TEB with an 80%% mask, aux-variable CR "
+                         "(n_gibbs 1), N_side 2048 / l_max 4096, 1 chain per GPU")
+    ap.add_argument("--nchains", type=int, default=None, help="chains per GPU (32; masked: 1)")
+    ap.add_argument("--lmax", type=int, default=None, help="1024 (masked: 4096)")
+    ap.add_argument("--nside", type=int, default=None, help="512 (masked: 2048)")
     ap.add_argument("--fields", type=int, default=3, choices=[1, 2, 3])
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -45,7 +47,12 @@ def parse():
     ap.add_argument("--timing-launches", type=int, default=20,
                     help="eager steps after the timed loop whose sweep launches are timed with hipEvents")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    masked = a.workload == "masked"
+    a.nchains = a.nchains or (1 if masked else 32)
+    a.lmax = a.lmax or (4096 if masked else 1024)
+    a.nside = a.nside or (2048 if masked else 512)
+    return a
 
 
 def sweep_algorithmic_bytes(L, F, nchains, ntask_stats):
@@ -75,6 +82,8 @@ def main():
         build()
     if dist is not None:
         dist.barrier()
+    if args.workload == "masked":
+        return run_masked(args, rank, world, dist)
     from gibbssampler_amd.problem import synthetic_problem
     from gibbssampler_amd.samplers import BatchedRunner
 
@@ -173,6 +182,120 @@ def main():
                          "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": round(sweep_avg_ms, 5), "launches": sweep_n},
             "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+FP64_VALU_PEAK_TFS = 78.6   # MI355X_MICROARCH.md: FP64 vector
+
+
+def sht_flops(nside, L, ncomp_c=20):
+    """N_ringpair * N_lm * c (c = 4 spin-0 + 16 spin-2 = 20 for TEB)."""
+    return 2 * nside * (L + 1) * (L + 2) // 2 * ncomp_c
+
+
+def run_masked(args, rank, world, dist):
+    """BASELINE configs[4]: CenteredGibbs TEB, masked (f_sky 0.8), aux-variable CR
+    with n_gibbs = 1 (a9, TEB) + inverse-Wishart / inverse-Gamma C_l draw, one
+    chain per GPU.  Per iteration: b s -> alm2map (TEB) -> v | s -> map2alm
+    (TEB) -> s | v, then the sweep statistics and the C_l draw; all on the device."""
+    from gibbssampler_amd import _capi
+    from gibbssampler_amd.data import band_mask, synfast
+    from gibbssampler_amd.engine import GibbsPlan
+    from gibbssampler_amd.masked import MaskedCR
+    from gibbssampler_amd.problem import fiducial_dl, gauss_beam
+    from gibbssampler_amd.sht import HealpixSHT
+    L, N = args.lmax, args.nside
+    Npix = 12 * N * N
+    NR = (L + 1) ** 2
+    if args.nchains != 1:
+        raise SystemExit("masked workload: one chain per GPU (chains shard over GPUs)")
+    dl = fiducial_dl(L, 3)
+    ell = np.arange(L + 1, dtype=np.float64)
+    fac = np.where(ell > 0, 2 * np.pi / np.maximum(ell * (ell + 1), 1), 0.0)
+    cls_ = np.stack([dl[k] * fac for k in ("TT", "EE", "BB", "TE")])
+    np.random.seed(0)
+    fwhm = np.radians(0.5)
+    maps = synfast(cls_, N, L, fwhm)                                   # [3, Npix] device
+    g = torch.Generator(device="cuda").manual_seed(1)
+    sig = torch.tensor([40.0, 0.2, 0.2], dtype=torch.float64, device="cuda")[:, None]
+    d = maps + sig * torch.randn(maps.shape, dtype=torch.float64, device="cuda", generator=g)
+    mask = band_mask(N)
+    mt = torch.from_numpy(mask).cuda()
+    d = (d * mt).cpu().numpy()
+    del maps
+    bl = gauss_beam(fwhm, L)
+    cr = MaskedCR({"T": d[0], "Q": d[1], "U": d[2]}, 40.0 ** 2, 0.2 ** 2, bl, L, N, mask=mask, nfields=3,
+                  gibbs_cr=True, n_gibbs=1, rng="native", seed=args.seed, chain=rank)
+    del d
+    bins = {s: np.arange(0, L + 2) for s in ("TT", "EE", "BB", "TE")}
+    plan = GibbsPlan(L, N, 3, 1, bl, [1.0, 1.0, 1.0], bins, chain0=rank)
+    d0 = plan.zeros(1, 3, NR)
+    dl_t = torch.from_numpy(np.stack([dl[k] for k in ("TT", "EE", "BB", "TE")])).cuda().contiguous()
+    s = torch.zeros((3, NR), dtype=torch.float64, device="cuda")
+    it = [0]
+
+    def step():
+        it[0] += 1
+        cr.step(_capi.GS_MCR_AUX, dl_t, s, iteration=it[0])
+        st = plan.sweep_stats(d0, s[None])
+        out = plan.cls_draw(st, None, seed=args.seed, iteration=it[0])
+        dl_t.copy_(out[0, :, :L + 1])          # unbinned bins: bin b = l
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # the transforms the step runs, timed with events on the launch stream
+    sht = HealpixSHT(N, L)
+    a = torch.zeros((3, NR), dtype=torch.float64, device="cuda")
+    mp = torch.zeros((3, Npix), dtype=torch.float64, device="cuda")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    reps = 3
+    ev[0].record()
+    for _ in range(reps):
+        sht.alm2map(a, ncomp=3, out=mp)
+    ev[1].record()
+    for _ in range(reps):
+        sht.map2alm(mp, iter=0, ncomp=3, out=a)
+    ev[2].record()
+    torch.cuda.synchronize()
+    t_syn = ev[0].elapsed_time(ev[1]) / reps
+    t_ana = ev[1].elapsed_time(ev[2]) / reps
+    if rank == 0:
+        fl = sht_flops(N, L)
+        achieved = 2 * fl / ((t_syn + t_ana) * 1e-3) / 1e12
+        line = {
+            "metric": "Gibbs iters/sec (constrained-realization + C_l draw), Nside=%d lmax=%d" % (N, L),
+            "value": round(args.steps * world / elapsed, 4),
+            "unit": "chain-iterations/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (analytic fiducial spectra, synfast on the device + white noise, 80% band mask)",
+            "config": {"workload": "centered TEB masked aux-variable CR (n_gibbs=1)", "nside": N, "lmax": L,
+                       "nfields": 3, "chains_per_gpu": 1, "global_chains": world,
+                       "rng": "native philox4x32-10", "parallelism": f"chains sharded over {world} GPU(s)"},
+            "roofline": {"bound": "fp64", "kernel": "gs_sht alm2map + map2alm (TEB)", "achieved": round(achieved, 2),
+                         "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFS, 4),
+                         "traffic": None, "algorithmic_flops_per_launch": fl,
+                         "avg_launch_ms": {"alm2map": round(t_syn, 3), "map2alm": round(t_ana, 3)}},
+            "cpu_baseline": None,
+            "notes": "healpy is absent, so no CPU SHT baseline at this size; see DESIGN.md",
         }
         print(json.dumps(line))
     if dist is not None:

@@ -25,6 +25,22 @@ from . import _capi
 from .sht import HealpixSHT
 
 
+def pixel_cos_theta(nside):
+    """cos(theta) of every HEALPix RING pixel (Gorski et al. 2005 ring latitudes)."""
+    N = int(nside)
+    i = np.arange(1, 4 * N, dtype=np.float64)
+    z = np.where(i < N, 1.0 - i * i / (3.0 * N * N),
+                 np.where(i <= 3 * N, 4.0 / 3.0 - 2.0 * i / (3.0 * N), -(1.0 - (4 * N - i) ** 2 / (3.0 * N * N))))
+    ii = np.arange(1, 4 * N, dtype=np.int64)
+    nphi = np.where(ii < N, 4 * ii, np.where(ii <= 3 * N, 4 * N, 4 * (4 * N - ii)))
+    return np.repeat(z, nphi)
+
+
+def band_mask(nside, cut=0.2):
+    """the synthetic 80% mask of SURVEY.md 8d: keep |cos theta| > cut."""
+    return (np.abs(pixel_cos_theta(nside)) > cut).astype(np.float64)
+
+
 def _beams(lmax, fwhm_rad, nfields):
     sigma = fwhm_rad / math.sqrt(8.0 * math.log(2.0))
     ell = np.arange(lmax + 1, dtype=np.float64)
