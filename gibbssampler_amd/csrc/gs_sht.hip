@@ -737,73 +737,12 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         }
         const long long obase = cidx(L, m, m) - m;
         const LegCoef* cf = coef + obase;
-        bool slow = true;
         // chunks start on m's parity so positions 0, 2 of a chunk are even
         const int lstart0 = lmin - ((lmin - m) & 1);
-        for (int l0 = lstart0; l0 <= L; l0 += ANA_C) {
-            double acc[NV];
-#pragma unroll
-            for (int i = 0; i < NV; ++i) acc[i] = 0.0;
-            // activations inside the chunk force the slow path
-#pragma unroll
-            for (int r = 0; r < ASR; ++r)
-                if (ls[r] >= l0 && ls[r] < l0 + ANA_C && ls[r] <= L) slow = true;
-            if (slow || l0 + ANA_C - 1 > L) {
-#pragma unroll
-                for (int cc = 0; cc < ANA_C; ++cc) {
-                    const int l = l0 + cc;
-                    if (l > L) break;
-                    const LegCoef c = cf[l];
-                    const LegCoef cn = cf[min(l + 1, L)];
-#pragma unroll
-                    for (int r = 0; r < ASR; ++r) {
-                        if (l < ls[r]) continue;                 // uniform per wave
-                        if (l == ls[r] && act[r]) {
-                            const double2 s0 = D.st[(long long)m * npair + pr[r]];
-                            v1[r] = s0.x; v0[r] = s0.y;
-                            kk[r] = D.stk[(long long)m * npair + pr[r]];
-                        }
-                        if ((cc & 1) == 0) ana_term<NC, true, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
-                        else ana_term<NC, false, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
-                        if (l < L) {
-                            rec_step(cn, x[r], v0[r], v1[r]);
-                            if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
-                        }
-                    }
-                }
-                // leave the slow path once every live slot is active and representable
-                bool live = true;
-#pragma unroll
-                for (int r = 0; r < ASR; ++r)
-                    if (ls[r] <= L && (l0 + ANA_C <= ls[r] || __any(kk[r] < 0))) live = false;
-                slow = !live;
-            } else {
-                // full chunk, every live slot active and representable: no guards
-                // (cf[L + 1] exists: the coefficient table is padded by one entry)
-#if defined(GS_ASM_MARKERS)
-                asm volatile("; ANA_FAST_BEGIN");
-#endif
-#pragma unroll
-                for (int cc = 0; cc < ANA_C; ++cc) {
-                    const int l = l0 + cc;
-                    const LegCoef c = cf[l];
-                    const LegCoef cn = cf[l + 1];
-#pragma unroll
-                    for (int r = 0; r < ASR; ++r) {
-                        // no per-slot branch: a dead slot (ls > L) has zero phases and
-                        // zero state, so it adds exact zeros (keeps acc[] in place)
-                        if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
-                        else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
-                        rec_step(cn, x[r], v0[r], v1[r]);
-                    }
-                }
-            }
-#if defined(GS_ASM_MARKERS)
-            asm volatile("; ANA_CHUNK_END");
-#endif
-            // fixed-order wave reduction of the chunk (wave-private LDS rows, no
-            // workgroup barrier): lane -> (row o = lane % NVP, segment lane / NVP)
-            double* red = red_all[wave];
+        double* red = red_all[wave];
+        // fixed-order wave reduction of a chunk (wave-private LDS rows, no
+        // workgroup barrier): lane -> (row o = lane % NVP, segment lane / NVP)
+        auto reduce_store = [&](const double (&acc)[NV], int l0) {
 #pragma unroll
             for (int i = 0; i < NV; ++i) red[i * RS + lane] = acc[i];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -833,6 +772,81 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                     dst[oo & 1] = sum;
                 }
             }
+        };
+        // guarded chunk: slot activation at its onset, scaled lanes masked and
+        // rescaled, l beyond L skipped
+        auto slow_chunk = [&](double (&acc)[NV], int l0) {
+#pragma unroll
+            for (int cc = 0; cc < ANA_C; ++cc) {
+                const int l = l0 + cc;
+                if (l > L) break;
+                const LegCoef c = cf[l];
+                const LegCoef cn = cf[min(l + 1, L)];
+#pragma unroll
+                for (int r = 0; r < ASR; ++r) {
+                    if (l < ls[r]) continue;                 // uniform per wave
+                    if (l == ls[r] && act[r]) {
+                        const double2 s0 = D.st[(long long)m * npair + pr[r]];
+                        v1[r] = s0.x; v0[r] = s0.y;
+                        kk[r] = D.stk[(long long)m * npair + pr[r]];
+                    }
+                    if ((cc & 1) == 0) ana_term<NC, true, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
+                    else ana_term<NC, false, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
+                    if (l < L) {
+                        rec_step(cn, x[r], v0[r], v1[r]);
+                        if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
+                    }
+                }
+            }
+        };
+        int l0 = lstart0;
+        // phase 1: guarded chunks until every live slot is active and representable
+        for (; l0 <= L; l0 += ANA_C) {
+            double acc[NV];
+#pragma unroll
+            for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+            slow_chunk(acc, l0);
+            reduce_store(acc, l0);
+            bool live = true;
+#pragma unroll
+            for (int r = 0; r < ASR; ++r)
+                if (ls[r] <= L && (l0 + ANA_C <= ls[r] || __any(kk[r] < 0))) live = false;
+            if (live) { l0 += ANA_C; break; }
+        }
+        // phase 2: full chunks, no guards (a dead slot, ls > L, has zero phases
+        // and zero state and adds exact zeros; cf[L + 1] exists: the coefficient
+        // table is padded by one entry)
+#if defined(GS_ASM_MARKERS)
+        asm volatile("; ANA_FAST_BEGIN");
+#endif
+        for (; l0 + ANA_C - 1 <= L; l0 += ANA_C) {
+            double acc[NV];
+#pragma unroll
+            for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+#pragma unroll
+            for (int cc = 0; cc < ANA_C; ++cc) {
+                const int l = l0 + cc;
+                const LegCoef c = cf[l];
+                const LegCoef cn = cf[l + 1];
+#pragma unroll
+                for (int r = 0; r < ASR; ++r) {
+                    if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
+                    else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
+                    rec_step(cn, x[r], v0[r], v1[r]);
+                }
+            }
+            reduce_store(acc, l0);
+        }
+#if defined(GS_ASM_MARKERS)
+        asm volatile("; ANA_CHUNK_END");
+#endif
+        // phase 3: the partial last chunk
+        if (l0 <= L) {
+            double acc[NV];
+#pragma unroll
+            for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+            slow_chunk(acc, l0);
+            reduce_store(acc, l0);
         }
         // l below the wave's first chunk: exact zeros
         for (int l = m + lane; l < min(lstart0, L + 1); l += 64)
