@@ -781,6 +781,8 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     const int chain = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    __shared__ double wsum[64];
+    __shared__ int wflag;
     double* D = dl + (long long)chain * NSP * maxbins;
     const double* P = prop + (long long)chain * NSP * maxbins;
     const double* R = logr + (long long)chain * NSP * maxbins;
@@ -856,29 +858,39 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                 if (accept_out) accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
             }
         }
-        // wide blocks: one wave each
+        // wide blocks: the whole workgroup per block, one block after the other
+        // (fixed-order sums: per-thread terms, wave sums, then the 16 wave sums
+        // in wave order), so a phase's few long blocks do not serialise on one wave
 #if defined(GS_ABL_MH_WIDE)
         if (false)
 #endif
-        for (int j = wv; j < nwide; j += nwv) {
+        for (int j = 0; j < nwide; ++j) {
             const int2 sb = tab[j];
             const int4 r = rng[j];
             const int sp = sb.x, blk = sb.y, k = sp == sp0 ? 0 : 1;
             const int lo = r.x, hi = r.y, l0 = r.z, l1 = r.w;
             double diff = 0.0, lrs = 0.0;
-            for (int l = l0 + lane; l < l1; l += 64) diff += g[k * Lp1 + l];
-            for (int b = lo + lane; b < hi; b += 64) lrs += R[sp * maxbins + b];
+            for (int l = l0 + tid; l < l1; l += blockDim.x) diff += g[k * Lp1 + l];
+            for (int b = lo + tid; b < hi; b += blockDim.x) lrs += R[sp * maxbins + b];
             diff = wave_sum(diff);
             lrs = wave_sum(lrs);
-            bool taken = false;
-            for (int att = 0; att < n_iter_mh; ++att) {
-                const bool acc = log(ub[j * n_iter_mh + att]) < (taken ? 0.0 : diff) + lrs;
-                if (acc && !taken)
-                    for (int b = lo + lane; b < hi; b += 64) D[sp * maxbins + b] = P[sp * maxbins + b];
-                taken = taken || acc;
-                if (lane == 0 && accept_out)
-                    accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
+            if (lane == 0) { wsum[wv] = diff; wsum[32 + wv] = lrs; }
+            __syncthreads();
+            if (tid == 0) {
+                double dsum = 0.0, lsum = 0.0;
+                for (int w = 0; w < nwv; ++w) { dsum += wsum[w]; lsum += wsum[32 + w]; }
+                bool taken = false;
+                for (int att = 0; att < n_iter_mh; ++att) {
+                    const bool acc = log(ub[j * n_iter_mh + att]) < (taken ? 0.0 : dsum) + lsum;
+                    taken = taken || acc;
+                    if (accept_out)
+                        accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
+                }
+                wflag = taken ? 1 : 0;
             }
+            __syncthreads();
+            if (wflag)
+                for (int b = lo + tid; b < hi; b += blockDim.x) D[sp * maxbins + b] = P[sp * maxbins + b];
         }
         __syncthreads();
     }
