@@ -788,6 +788,9 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     const double* R = logr + (long long)chain * NSP * maxbins;
     const double* st = stats + (long long)chain * NS * Lp1;
     for (int k = tid; k < NSP * Lp1; k += blockDim.x) e2b[k] = ell2bin[k];
+    // the chain's D_l lives in LDS for the whole sweep (written back at the end)
+    for (int k = tid; k < NSP * maxbins; k += blockDim.x) Ds[k] = D[k];
+    __syncthreads();
     for (int q = 0; q < ph.nphase; ++q) {
         const int nb = ph.n[q];
         if (nb == 0) continue;
@@ -795,8 +798,6 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         const int2* tab = phase_tab + ph.off[q];
         const int4* rng = phase_rng + ph.off[q];
         const int nwide = ph.nwide[q];
-        for (int k = tid; k < NSP * maxbins; k += blockDim.x) Ds[k] = D[k];
-        __syncthreads();
         // per-l likelihood differences of the phase's spectra
 #if defined(GS_ABL_MH_TERMS)
         for (int l = tid; l < Lp1; l += blockDim.x) { g[l] = 0.0; g[Lp1 + l] = 0.0; }
@@ -853,7 +854,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
             for (int att = 0; att < n_iter_mh; ++att) {
                 const bool acc = log(ub[j * n_iter_mh + att]) < (taken ? 0.0 : diff) + lrs;
                 if (acc && !taken)
-                    for (int b = lo; b < hi; ++b) D[sp * maxbins + b] = P[sp * maxbins + b];
+                    for (int b = lo; b < hi; ++b) Ds[sp * maxbins + b] = P[sp * maxbins + b];
                 taken = taken || acc;
                 if (accept_out) accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
             }
@@ -890,16 +891,17 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
             }
             __syncthreads();
             if (wflag)
-                for (int b = lo + tid; b < hi; b += blockDim.x) D[sp * maxbins + b] = P[sp * maxbins + b];
+                for (int b = lo + tid; b < hi; b += blockDim.x) Ds[sp * maxbins + b] = P[sp * maxbins + b];
         }
         __syncthreads();
     }
-    // ---- epilogue (graph-captured NC steps) ----
     const int nrow = NSP * maxbins;
+    for (int k = tid; k < nrow; k += blockDim.x) D[k] = Ds[k];
+    // ---- epilogue (graph-captured NC steps) ----
     if (epi.trace) {
         const long long slot = (long long)((iter + (uint32_t)epi.cap - 1u) % (uint32_t)epi.cap);
         double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
-        for (int k = tid; k < nrow; k += blockDim.x) tr[k] = D[k];
+        for (int k = tid; k < nrow; k += blockDim.x) tr[k] = Ds[k];
     }
     if (epi.counter) {
         __syncthreads();
