@@ -1338,6 +1338,26 @@ int gs_block_params(gs_plan* p, int mode, const double* dl, double* params, void
     return 0;
 }
 
+// an event record that also works while the stream is being captured into a
+// hipGraph (then it becomes an external event-record node, timed at replay)
+static int record_ev(hipEvent_t e, hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    GS_CHECK(hipStreamGetCaptureInfo_v2(s, &cs, &id, &graph, &deps, &ndeps));
+    if (cs != hipStreamCaptureStatusActive) {
+        GS_CHECK(hipEventRecord(e, s));
+        return 0;
+    }
+    // capturing: add an event-record node after the stream's current frontier
+    hipGraphNode_t node = nullptr;
+    GS_CHECK(hipGraphAddEventRecordNode(&node, graph, deps, ndeps, e));
+    GS_CHECK(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
+    return 0;
+}
+
 static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1) {
     if (!p->timing) return 0;
     if (p->ev_used + 2 > p->ev.size()) {
@@ -1350,13 +1370,20 @@ static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e
     *e0 = p->ev[p->ev_used];
     *e1 = p->ev[p->ev_used + 1];
     p->ev_used += 2;
-    GS_CHECK(hipEventRecord(*e0, s));
+    return record_ev(*e0, s);
+}
+
+static int stats_finish(gs_plan* p, double* stats, void* stream) {
+    const long long n = (long long)p->nchains * p->nstat * (p->L + 1);
+    hipLaunchKernelGGL(k_stats_finish, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
+                       p->nchunk, p->rows_per_task, p->nstat, p->partials, stats);
+    GS_LAUNCH_CHECK("k_stats_finish");
     return 0;
 }
 
 static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
                         uint32_t iteration, uint32_t substep, double* s_out, double* stats, bool given,
-                        void* stream) {
+                        void* stream, bool finish = true) {
     if (check_plan(p)) return -1;
     if (!d_alm || !stats || (!given && !params) || (given && !s_out)) return set_error("gs_cr_sweep: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
@@ -1374,12 +1401,8 @@ static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, c
 #undef GS_SWF
 #undef GS_SW
     GS_LAUNCH_CHECK("k_cr_sweep");
-    if (p->timing) GS_CHECK(hipEventRecord(e1, S(stream)));
-    const long long n = (long long)p->nchains * p->nstat * (p->L + 1);
-    hipLaunchKernelGGL(k_stats_finish, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
-                       p->nchunk, p->rows_per_task, p->nstat, p->partials, stats);
-    GS_LAUNCH_CHECK("k_stats_finish");
-    return 0;
+    if (p->timing && record_ev(e1, S(stream))) return -1;
+    return finish ? stats_finish(p, stats, stream) : 0;
 }
 
 int gs_cr_sweep(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
@@ -1548,9 +1571,14 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
 }
 
 int gs_nc_sweep(gs_plan* p, const double* d_alm, double* s_out, const double* z, uint64_t seed, uint32_t it,
-                void* stream) {
+                int finish, void* stream) {
     if (check_plan(p)) return -1;
-    return gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream);
+    return sweep_launch(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, false, stream, finish != 0);
+}
+
+int gs_nc_finish(gs_plan* p, void* stream) {
+    if (check_plan(p)) return -1;
+    return stats_finish(p, p->stats, stream);
 }
 
 int gs_nc_decide(gs_plan* p, double* dl, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
@@ -1575,7 +1603,7 @@ int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_o
                         const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
                         void* stream) {
     if (gs_nc_prologue(p, dl, u_prop, seed, it, stream)) return -1;
-    if (gs_nc_sweep(p, d_alm, s_out, z, seed, it, stream)) return -1;
+    if (gs_nc_sweep(p, d_alm, s_out, z, seed, it, 1, stream)) return -1;
     return gs_nc_decide(p, dl, u_acc, seed, it, accept_out, stream);
 }
 

@@ -240,9 +240,12 @@ class GibbsPlan:
         C.check(self.lib.gs_nc_prologue(self._h, C.ptr(dl), C.ptr(u_prop), int(seed), int(iteration), self._s()),
                 "gs_nc_prologue")
 
-    def nc_sweep(self, d, s_out, z=None, seed=0, iteration=0):
+    def nc_sweep(self, d, s_out, z=None, seed=0, iteration=0, finish=True):
         C.check(self.lib.gs_nc_sweep(self._h, C.ptr(d), C.ptr(s_out), C.ptr(z), int(seed), int(iteration),
-                                     self._s()), "gs_nc_sweep")
+                                     int(bool(finish)), self._s()), "gs_nc_sweep")
+
+    def nc_finish(self):
+        C.check(self.lib.gs_nc_finish(self._h, self._s()), "gs_nc_finish")
 
     def nc_decide(self, dl, u_acc=None, seed=0, iteration=0, accept=None):
         C.check(self.lib.gs_nc_decide(self._h, C.ptr(dl), C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept),

@@ -95,6 +95,31 @@ class BatchedRunner:
                     p.record_trace(self.dl, trace, trace_capacity)
                 p.advance_iteration()
         self.graph = g
+        self.graph_steps = 1
+        return g
+
+    def capture_steps(self, nsteps, trace=None, trace_capacity=None, time_sweeps=False):
+        """NonCentered, native RNG: capture ``nsteps`` whole iterations in ONE hipGraph
+        (one replay = nsteps steps).  time_sweeps: bracket every CR-sweep kernel by
+        event-record nodes (plan.sweep_timing), so the sweep's duration is measured
+        on its own stream inside the replay; collect with plan.sweep_timing(False)."""
+        if self.kind != "noncentered" or self.rng != "native":
+            raise ValueError("capture_steps: native NonCentered runs only")
+        p = self.plan
+        p.iteration_counter(True, self.iteration + 1)
+        torch.cuda.synchronize()
+        if time_sweeps:
+            p.sweep_timing(True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(nsteps):
+                p.nc_prologue(self.dl, seed=self.seed)
+                p.nc_sweep(self.d, self.s, seed=self.seed, finish=False)
+                p.nc_finish()
+                p.nc_decide_fused(self.dl, seed=self.seed, accept=self.accept, trace=trace,
+                                  capacity=trace_capacity or 0)
+        self.graph = g
+        self.graph_steps = nsteps
         return g
 
     def _launch_step(self, it, z=None, ig=None, up=None, ua=None):
@@ -111,7 +136,7 @@ class BatchedRunner:
     def step(self):
         if getattr(self, "graph", None) is not None:
             self.graph.replay()
-            self.iteration += 1
+            self.iteration += getattr(self, "graph_steps", 1)
             return
         p = self.plan
         it = self.iteration + 1

@@ -150,7 +150,10 @@ int gs_step_noncentered(gs_plan* plan, const double* d_alm, double* dl_binned, d
 int gs_nc_prologue(gs_plan* plan, const double* dl_binned, const double* u_prop_replay, uint64_t seed,
                    uint32_t iteration, void* stream);
 int gs_nc_sweep(gs_plan* plan, const double* d_alm, double* s_out, const double* z_replay, uint64_t seed,
-                uint32_t iteration, void* stream);
+                uint32_t iteration, int finish, void* stream);
+/* finish = 0 leaves the statistics as per-task partials; gs_nc_finish reduces them
+ * (fixed order) -- lets a caller bracket the sweep kernel alone with timing events */
+int gs_nc_finish(gs_plan* plan, void* stream);
 int gs_nc_decide(gs_plan* plan, double* dl_binned, const double* u_accept_replay, uint64_t seed, uint32_t iteration,
                  int32_t* accept_out, void* stream);
 /* gs_nc_decide with the step's bookkeeping fused into the same launch (native
@@ -178,7 +181,10 @@ int gs_advance_iteration(gs_plan* plan, void* stream);
 int gs_record_trace(gs_plan* plan, const double* dl_binned, double* trace, int capacity, uint32_t iteration,
                     void* stream);
 
-/* device-side timing of the dominant kernel (hipEvents on the plan's stream) */
+/* device-side timing of the dominant kernel: with enable = 1 every later CR-sweep
+ * launch is bracketed by hipEvents on its stream (also while the stream is
+ * captured into a hipGraph: external event-record nodes, timed at each replay);
+ * enable = 0 returns the summed duration and the number of launches timed */
 int gs_sweep_timing(gs_plan* plan, int enable, double* total_ms, int* count);
 
 /* ---- HEALPix RING spherical-harmonic transforms (gs_sht.hip) ------------

@@ -55,3 +55,32 @@ def test_graph_equals_eager(kind, F):
     g.step()
     eager.step()
     np.testing.assert_array_equal(g.dl.cpu().numpy(), eager.dl.cpu().numpy())
+
+
+@pytest.mark.parametrize("F", [3, 2])
+def test_multistep_graph_with_sweep_timing(F):
+    """bench.py's timed region: K NC iterations in ONE graph with the sweeps
+    bracketed by captured event nodes -- same chains as eager, K timings."""
+    import torch
+    n, w = 5, 2
+    eager = _runner("noncentered", F)
+    want = []
+    for _ in range(w + n):
+        eager.step()
+        want.append(eager.dl.cpu().numpy().copy())
+    g = _runner("noncentered", F)
+    for _ in range(w):
+        g.step()
+    p = g.plan
+    trace = p.zeros(n, p.nchains, p.nspec, p.maxbins)
+    g.capture_steps(n, trace=trace, trace_capacity=n, time_sweeps=True)
+    g.step()
+    torch.cuda.synchronize()
+    ms, cnt = p.sweep_timing(False)
+    assert cnt == n and ms > 0
+    tr = trace.cpu().numpy()
+    for k in range(n):
+        it = w + 1 + k
+        np.testing.assert_array_equal(tr[(it - 1) % n], want[w + k])
+    np.testing.assert_array_equal(g.dl.cpu().numpy(), want[-1])
+    assert g.iteration == w + n
