@@ -37,6 +37,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <cstdlib>
 
 #include "gibbs_capi.h"
 #include "gs_common.h"
@@ -73,6 +74,9 @@ struct PairGeom {
     int M;               // FFT length
     int logM;
     long long bs_off;    // Bluestein kernel offset (complex entries), -1 if nphi = M
+    int split;           // 1: DFT_nphi = two DFT_(nphi/2) (even / odd samples), each a
+                         //    Bluestein of length M held in LDS (instead of one M > LDS)
+    int sslot;           // index of the ring pair among the split ones (global scratch slot)
 };
 
 // per (l, m) recurrence + spin-2 coefficients (64 B, one scalar load)
@@ -445,11 +449,8 @@ __device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict
 // forward DFT of length n held in buf[0..n) (Bluestein when n is not a power
 // of two: M = g.M, kernel V = FFT of the chirp); result in buf[0..n)
 template <int NB>
-__device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
-                            const double2* __restrict__ bsk) {
-    const int n = g.nphi, M = g.M;
-    if (g.bs_off < 0) { fft_pow2<NB>(buf, M, -1, tw, Mmax); return; }
-    const double2* V = bsk + g.bs_off;
+__device__ void bluestein_forward(double2* buf, int n, int M, const double2* __restrict__ V,
+                                  const double2* __restrict__ tw, int Mmax) {
     for (int j = threadIdx.x; j < M; j += blockDim.x) {
         if (j < n) buf[j] = cmul(buf[j], expi_pi_frac(-(long long)j * j, n));   // c_j = e^{-i pi j^2/n}
         else buf[j] = make_double2(0.0, 0.0);
@@ -468,16 +469,30 @@ __device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __re
     __syncthreads();
 }
 
+// conj(DFT(conj x)) = unnormalised inverse DFT, Bluestein of length n
+template <int NB>
+__device__ void bluestein_inverse(double2* buf, int n, int M, const double2* __restrict__ V,
+                                  const double2* __restrict__ tw, int Mmax) {
+    for (int j = threadIdx.x; j < n; j += blockDim.x) buf[j].y = -buf[j].y;
+    __syncthreads();
+    bluestein_forward<NB>(buf, n, M, V, tw, Mmax);
+    for (int j = threadIdx.x; j < n; j += blockDim.x) buf[j].y = -buf[j].y;
+    __syncthreads();
+}
+
+template <int NB>
+__device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
+                            const double2* __restrict__ bsk) {
+    if (g.bs_off < 0) { fft_pow2<NB>(buf, g.M, -1, tw, Mmax); return; }
+    bluestein_forward<NB>(buf, g.nphi, g.M, bsk + g.bs_off, tw, Mmax);
+}
+
 // inverse (unnormalised) DFT: y_j = sum_k Z_k e^{+2 pi i jk/n}
 template <int NB>
 __device__ void dft_inverse(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
                             const double2* __restrict__ bsk) {
     if (g.bs_off < 0) { fft_pow2<NB>(buf, g.M, +1, tw, Mmax); return; }
-    for (int j = threadIdx.x; j < g.nphi; j += blockDim.x) buf[j].y = -buf[j].y;
-    __syncthreads();
-    dft_forward<NB>(buf, g, tw, Mmax, bsk);
-    for (int j = threadIdx.x; j < g.nphi; j += blockDim.x) buf[j].y = -buf[j].y;
-    __syncthreads();
+    bluestein_inverse<NB>(buf, g.nphi, g.M, bsk + g.bs_off, tw, Mmax);
 }
 
 // plan time: V = FFT_M(w), w_t = e^{+i pi t^2/n} for |t| < n (cyclic)
@@ -487,7 +502,7 @@ __global__ __launch_bounds__(1024) void k_sht_bluestein_setup(const int* __restr
                                                               double2* __restrict__ bsk) {
     const PairGeom g = geom[pairs[blockIdx.x]];
     double2* buf = bsk + g.bs_off;
-    const int n = g.nphi, M = g.M;
+    const int n = g.split ? g.nphi / 2 : g.nphi, M = g.M;
     for (int t = threadIdx.x; t < M; t += blockDim.x) {
         long long tt = -1;
         if (t < n) tt = t;
@@ -526,7 +541,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
                                                          const double2* __restrict__ phi,
                                                          const double2* __restrict__ tw, int Mmax,
                                                          const double2* __restrict__ bsk,
-                                                         double2* __restrict__ gscratch, double* __restrict__ maps) {
+                                                         double2* __restrict__ gscratch, double* __restrict__ maps,
+                                                         double2* __restrict__ sscr, int nsplit, int sstride) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -590,8 +606,46 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         }
     }
     __syncthreads();
-    dft_inverse<NB>(buf, g, tw, Mmax, bsk);
     double* mc = maps + (long long)comp * npix;
+    if (g.split) {
+        // y_j = A_(j mod h) + e^{2 pi i j / n} B_(j mod h), A / B = IDFT_h of the even /
+        // odd bins (each a Bluestein of length h in LDS; A and the odd bins wait in
+        // global scratch)
+        const int h = n / 2;
+        double2* A = sscr + ((long long)comp * nsplit + g.sslot) * sstride;
+        double2* Zo = A + h;
+        for (int k = threadIdx.x; k < h; k += BD) Zo[k] = buf[2 * k + 1];
+        double2 ev[NB];
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const int k = threadIdx.x + t * BD;
+            ev[t] = k < h ? buf[2 * k] : make_double2(0.0, 0.0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const int k = threadIdx.x + t * BD;
+            if (k < h) buf[k] = ev[t];
+        }
+        __syncthreads();
+        const double2* V = bsk + g.bs_off;
+        bluestein_inverse<NB>(buf, h, g.M, V, tw, Mmax);
+        for (int k = threadIdx.x; k < h; k += BD) A[k] = buf[k];
+        __syncthreads();
+        for (int k = threadIdx.x; k < h; k += BD) buf[k] = Zo[k];
+        __syncthreads();
+        bluestein_inverse<NB>(buf, h, g.M, V, tw, Mmax);
+        for (int k = threadIdx.x; k < h; k += BD) {
+            const double2 b = cmul(buf[k], expi_pi_frac(2LL * k, n));
+            const double2 a = A[k];
+            const double2 y0 = make_double2(a.x + b.x, a.y + b.y), y1 = make_double2(a.x - b.x, a.y - b.y);
+            mc[g.startN + k] = y0.x;
+            mc[g.startN + k + h] = y1.x;
+            if (!eq) { mc[g.startS + k] = y0.y; mc[g.startS + k + h] = y1.y; }
+        }
+        return;
+    }
+    dft_inverse<NB>(buf, g, tw, Mmax, bsk);
     for (int j = threadIdx.x; j < n; j += BD) {
         const double2 y = buf[j];
         mc[g.startN + j] = y.x;
@@ -609,7 +663,8 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
                                                         const double* __restrict__ maps,
                                                         const double2* __restrict__ tw, int Mmax,
                                                         const double2* __restrict__ bsk,
-                                                        double2* __restrict__ gscratch, double2* __restrict__ phi) {
+                                                        double2* __restrict__ gscratch, double2* __restrict__ phi,
+                                                        double2* __restrict__ sscr, int nsplit, int sstride) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -618,10 +673,35 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
     const int n = g.nphi;
     const bool eq = g.startS < 0;
     const double* mc = maps + (long long)comp * npix;
-    for (int j = threadIdx.x; j < n; j += blockDim.x)
-        buf[j] = make_double2(mc[g.startN + j], eq ? 0.0 : mc[g.startS + j]);
-    __syncthreads();
-    dft_forward<NB>(buf, g, tw, Mmax, bsk);
+    if (g.split) {
+        // X_k = E_k + e^{-2 pi i k / n} O_k, X_(k+h) = E_k - (...) O_k with E / O the
+        // length-h DFTs of the even / odd samples (Bluestein in LDS; O waits in scratch)
+        const int h = n / 2;
+        double2* O = sscr + ((long long)comp * nsplit + g.sslot) * sstride;
+        const double2* V = bsk + g.bs_off;
+        for (int k = threadIdx.x; k < h; k += blockDim.x)
+            buf[k] = make_double2(mc[g.startN + 2 * k + 1], eq ? 0.0 : mc[g.startS + 2 * k + 1]);
+        __syncthreads();
+        bluestein_forward<NB>(buf, h, g.M, V, tw, Mmax);
+        for (int k = threadIdx.x; k < h; k += blockDim.x) O[k] = buf[k];
+        __syncthreads();
+        for (int k = threadIdx.x; k < h; k += blockDim.x)
+            buf[k] = make_double2(mc[g.startN + 2 * k], eq ? 0.0 : mc[g.startS + 2 * k]);
+        __syncthreads();
+        bluestein_forward<NB>(buf, h, g.M, V, tw, Mmax);
+        for (int k = threadIdx.x; k < h; k += blockDim.x) {
+            const double2 e = buf[k];
+            const double2 o = cmul(O[k], expi_pi_frac(-2LL * k, n));
+            buf[k] = make_double2(e.x + o.x, e.y + o.y);
+            buf[k + h] = make_double2(e.x - o.x, e.y - o.y);
+        }
+        __syncthreads();
+    } else {
+        for (int j = threadIdx.x; j < n; j += blockDim.x)
+            buf[j] = make_double2(mc[g.startN + j], eq ? 0.0 : mc[g.startS + j]);
+        __syncthreads();
+        dft_forward<NB>(buf, g, tw, Mmax, bsk);
+    }
     const long long plane = (long long)(L + 1) * npair;
     double2* oN = phi + (2LL * comp + 0) * plane;
     double2* oS = phi + (2LL * comp + 1) * plane;
@@ -920,6 +1000,9 @@ struct gs_sht {
     double2* phi = nullptr;      // [3][2][L+1][npair]
     double2* part = nullptr;     // [ntile][3][nlm]
     double2* gscr = nullptr;     // global FFT scratch for M > LDS_FFT_MAX
+    double2* sscr = nullptr;     // split rings: [comp][slot][split_n] half-transform scratch
+    int nsplit = 0, split_n = 0;
+    int lds_fft_max = LDS_FFT_MAX;   // FFT lengths held in LDS (GS_SHT_LDS_FFT_MAX lowers it: tests)
     double* mapw = nullptr;      // [3][npix] Jacobi residual maps
     double2* ain = nullptr;      // [3][nlm] a_lm in healpy complex order
     // ring classes by FFT length
@@ -945,7 +1028,8 @@ int sht_alloc(gs_sht* p, T** dst, size_t n) {
 }
 
 void sht_free(gs_sht* p) {
-    void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->mapw, p->ain};
+    void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->sscr,
+                    p->mapw, p->ain};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (int* b : p->cls_pairs)
@@ -967,6 +1051,10 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     if (nside < 1 || nside > 8192 || (nside & (nside - 1))) return set_error("gs_sht_create: nside must be a power of two <= 8192");
     if (lmax < 0 || lmax > 4 * nside) return set_error("gs_sht_create: lmax out of range (0..4 nside)");
     gs_sht* p = new gs_sht();
+    if (const char* e = std::getenv("GS_SHT_LDS_FFT_MAX")) {
+        const int v = std::atoi(e);
+        if (v >= 16 && v <= LDS_FFT_MAX && (v & (v - 1)) == 0) p->lds_fft_max = v;
+    }
     const int N = nside, L = lmax;
     p->nside = N; p->L = L; p->npair = 2 * N; p->ngroup = (p->npair + 63) / 64;
     p->nlm = (L + 1) * (L + 2) / 2;
@@ -1001,6 +1089,12 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         }
         const bool pow2 = (g.nphi & (g.nphi - 1)) == 0;
         g.M = pow2 ? g.nphi : (1 << ilog2(2 * g.nphi - 1));
+        g.split = 0;
+        g.sslot = -1;
+        if (!pow2 && g.M > p->lds_fft_max && g.nphi % 2 == 0) {
+            const int Mh = 1 << ilog2(g.nphi - 1);          // Bluestein length for nphi / 2
+            if (Mh <= p->lds_fft_max && Mh >= g.nphi) { g.M = Mh; g.split = 1; }
+        }
         g.logM = ilog2(g.M);
         g.bs_off = -1;
         Mmax = std::max(Mmax, g.M);
@@ -1008,8 +1102,10 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     }
     long long bs_total = 0;
     std::vector<int> bs_pairs;
-    for (int r = 0; r < p->npair; ++r)
+    for (int r = 0; r < p->npair; ++r) {
         if (geom[r].M != geom[r].nphi) { geom[r].bs_off = bs_total; bs_total += geom[r].M; bs_pairs.push_back(r); }
+        if (geom[r].split) geom[r].sslot = p->nsplit++;
+    }
     p->Mmax = Mmax;
     // ---- recurrence coefficients ----
     std::vector<LegCoef> coef(p->nlm);
@@ -1066,9 +1162,15 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         p->cls_M.push_back(M);
         p->cls_n.push_back((int)lst.size());
         p->cls_pairs.push_back(d);
-        if (M > LDS_FFT_MAX) gscr_need = std::max<long long>(gscr_need, 3LL * (long long)lst.size() * Mmax);
+        if (M > p->lds_fft_max) gscr_need = std::max<long long>(gscr_need, 3LL * (long long)lst.size() * Mmax);
     }
     if (gscr_need && sht_alloc(p, &p->gscr, (size_t)gscr_need)) { sht_free(p); return -1; }
+    if (p->nsplit) {
+        int nmax = 0;
+        for (auto& g : geom) if (g.split) nmax = std::max(nmax, g.nphi);
+        if (sht_alloc(p, &p->sscr, (size_t)3 * p->nsplit * nmax)) { sht_free(p); return -1; }
+        p->split_n = nmax;
+    }
     if (hipMemcpy(p->geom, geom.data(), geom.size() * sizeof(PairGeom), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->coef, coef.data(), coef.size() * sizeof(LegCoef), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(p->coef + coef.size(), 0, sizeof(LegCoef)) != hipSuccess) {
@@ -1134,27 +1236,32 @@ int gs_sht_info(const gs_sht* p, int* nside, int* lmax, long long* npix, long lo
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream) {
     for (size_t c = 0; c < p->cls_M.size(); ++c) {
         const int M = p->cls_M[c];
-        const bool glob = M > LDS_FFT_MAX;
+        const bool glob = M > p->lds_fft_max;
         const int bd = ring_block(M);
         const bool nb8 = M / 2 > 4 * bd;
         // LDS: FFT buffer (+ fold reduction slots for short rings)
-        const size_t lds = glob ? 0 : (size_t)M * sizeof(double2) + (M < 8 * bd ? (size_t)bd * 4 * sizeof(double2) : 0);
+        const size_t red = M < 8 * bd ? (size_t)bd * 4 * sizeof(double2) : 0;   // fold reduction, short rings
+        const size_t lds = (glob ? 0 : (size_t)M * sizeof(double2)) + red;
         const dim3 grid(p->cls_n[c], ncomp);
         double2* scr = glob ? p->gscr : nullptr;
         if (synth) {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out);
+                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out,
+                                   p->sscr, p->nsplit, p->split_n);
             else
                 hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out);
+                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out,
+                                   p->sscr, p->nsplit, p->split_n);
         } else {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi);
+                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi,
+                                   p->sscr, p->nsplit, p->split_n);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi);
+                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi,
+                                   p->sscr, p->nsplit, p->split_n);
         }
         GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
     }

@@ -177,3 +177,31 @@ def test_single_modes_vs_scipy(N, L, modes):
             want = (coef * Y).real * (1.0 if m == 0 else 2.0)
             got = mp[start[r]:start[r] + nphi[r]]
             np.testing.assert_allclose(got, want, rtol=0, atol=1e-10 * max(1.0, np.abs(want).max()))
+
+
+@pytest.mark.parametrize("thr", [32, 64])
+@pytest.mark.parametrize("ncomp", [1, 3])
+def test_large_ring_fft_paths_vs_oracle(thr, ncomp, monkeypatch):
+    """The ring-FFT paths N_side >= 2048 takes (rings whose Bluestein length
+    exceeds the LDS: split into two half-length Bluesteins in LDS, or the
+    global-scratch FFT), exercised at N_side 16 by lowering the LDS threshold
+    of the plan (GS_SHT_LDS_FFT_MAX)."""
+    torch = _torch()
+    from gibbssampler_amd.sht import HealpixSHT
+    monkeypatch.setenv("GS_SHT_LDS_FFT_MAX", str(thr))
+    N, L = 16, 40
+    sht = HealpixSHT(N, L)
+    rng = np.random.default_rng(thr + ncomp)
+    a = _rand_alm(L, ncomp, rng)
+    want = _oracle_maps(a, N, L, ncomp)
+    got = sht.alm2map(torch.from_numpy(a).cuda(), ncomp=ncomp, layout="complex").cpu().numpy().reshape(ncomp, -1)
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-11 * np.abs(want).max())
+    maps = rng.standard_normal((ncomp, O.npix(N)))
+    want_a = _oracle_alm(maps, N, L, ncomp, 0)
+    got_a = sht.map2alm(torch.from_numpy(maps).cuda(), iter=0, layout="complex", ncomp=ncomp).cpu().numpy()
+    np.testing.assert_allclose(got_a.reshape(ncomp, -1), want_a, rtol=0, atol=1e-11 * np.abs(want_a).max())
+
+
+def test_adjointness_nside2048():
+    """exact adjointness at N_side 2048 (split-half Bluestein rings in play)."""
+    test_adjointness_fullsize(2048, 4096, 1)
