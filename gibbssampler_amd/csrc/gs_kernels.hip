@@ -239,12 +239,26 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
             // timing experiment only: Philox without the Box-Muller transform
             const uint4 w = philox(i, (uint32_t)f, tag, iter, key);
             zv[f][0] = (double)w.x - (double)w.y; zv[f][1] = (double)w.z - (double)w.w;
+#elif defined(GS_EXPERIMENT_ZIG_FAST)
+            // timing experiment only: the fast path of a 256-layer ziggurat per normal
+            {
+                const uint4 w = philox(i, (uint32_t)f, tag, iter, key);
+                const uint32_t lo0 = w.x, hi0 = w.y, lo1 = w.z, hi1 = w.w;
+                const int i0 = lo0 & 255, i1 = lo1 & 255;
+                const double u0 = ((double)(hi0 >> 5) * 67108864.0 + (double)(lo0 >> 6)) * (1.0 / 9007199254740992.0);
+                const double u1 = ((double)(hi1 >> 5) * 67108864.0 + (double)(lo1 >> 6)) * (1.0 / 9007199254740992.0);
+                double x0 = u0 * tab[i0], x1 = u1 * tab[i1];
+                if (u0 >= tab[256 + i0]) x0 *= 0.5;
+                if (u1 >= tab[256 + i1]) x1 *= 0.5;
+                zv[f][0] = (lo0 & 256) ? -x0 : x0;
+                zv[f][1] = (lo1 & 256) ? -x1 : x1;
+            }
 #elif defined(GS_EXPERIMENT_NO_RNG)
             zv[f][0] = (double)(i ^ f); zv[f][1] = (double)(i + iter);
 #elif defined(GS_OCML_BM)
             box_muller(philox(i, (uint32_t)f, tag, iter, key), zv[f][0], zv[f][1]);
 #else
-            box_muller_tab(philox(i, (uint32_t)f, tag, iter, key), tab, zv[f][0], zv[f][1]);
+            box_muller_tab(philox<true>(i, (uint32_t)f, tag, iter, key), tab, zv[f][0], zv[f][1]);
 #endif
 #if defined(GS_SERIAL_FIELDS)
             __builtin_amdgcn_sched_barrier(0);

@@ -23,6 +23,10 @@ __device__ __forceinline__ Key chain_key(uint32_t seed_lo, uint32_t seed_hi, uin
     return Key{seed_lo, seed_hi ^ chain};
 }
 
+// UKEY: the key is wave-uniform (one chain per workgroup), so the round key can
+// sit in an SGPR and each Philox word costs one gfx950 three-input XOR
+// (v_bitop3, truth table 0x96); with a per-lane key the plain two-XOR form.
+template <bool UKEY = false>
 __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, Key k) {
     uint32_t k0 = k.k0, k1 = k.k1;
 #pragma unroll
@@ -32,14 +36,14 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-#if defined(GS_XOR3)
         uint32_t n0, n2;
-        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c1), "s"(k0));
-        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c3), "s"(k1));
-#else
-        const uint32_t n0 = hi1 ^ c1 ^ k0;
-        const uint32_t n2 = hi0 ^ c3 ^ k1;
-#endif
+        if constexpr (UKEY) {
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c1), "s"(k0));
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c3), "s"(k1));
+        } else {
+            n0 = hi1 ^ c1 ^ k0;
+            n2 = hi0 ^ c3 ^ k1;
+        }
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
