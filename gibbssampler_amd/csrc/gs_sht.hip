@@ -98,6 +98,22 @@ struct ShtDev {
 
 __device__ __forceinline__ long long cidx(int L, int l, int m) { return (long long)m * (2 * L + 1 - m) / 2 + l; }
 
+// Ring phases Phi_m(pair), one plane per (comp, north/south): blocks of PHI_MB
+// consecutive m of one ring pair are contiguous ([m / MB][pair][m % MB]), so
+// the ring stage (threads = consecutive m of one pair) moves whole 128-B lines
+// while the Legendre stage (lanes = pairs at fixed m) keeps one element per
+// lane.  PHI_MB = 1 is the plain m-major layout.
+#ifndef GS_PHI_MB
+#define GS_PHI_MB 4
+#endif
+constexpr int PHI_MB = GS_PHI_MB;
+__host__ __device__ __forceinline__ long long phi_plane(int L, int npair) {
+    return (long long)((L + PHI_MB) / PHI_MB) * PHI_MB * npair;
+}
+__device__ __forceinline__ long long phi_at(int m, int p, int npair) {
+    return ((long long)(m / PHI_MB) * npair + p) * PHI_MB + (m % PHI_MB);
+}
+
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -387,11 +403,11 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
             }
         }
         // ---- outputs ----
-        const long long plane = (long long)(L + 1) * npair;
+        const long long plane = phi_plane(L, npair);
 #pragma unroll
         for (int r = 0; r < SR; ++r) {
             if (!act[r]) continue;
-            const long long o = (long long)m * npair + pr[r];
+            const long long o = phi_at(m, pr[r], npair);
             int comp = 0;
             if constexpr (NC != 2) {
                 phi[(2 * comp + 0) * plane + o] = make_double2(A[r].tp[0] + A[r].tn[0], A[r].tp[1] + A[r].tn[1]);
@@ -416,6 +432,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 // forward (dir = -1): X_k = sum_j x_j e^{-2 pi i jk/M};  dir = +1: conjugate
 // twiddles; tw[k] = e^{-2 pi i k / Mmax}, k < Mmax/2.  Each thread owns at most
 // NB butterflies per stage (M / 2 <= NB * blockDim).
+#if defined(GS_FFT_RADIX2)
 template <int NB>
 __device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
     const int half = M >> 1;
@@ -445,6 +462,102 @@ __device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict
         __syncthreads();
     }
 }
+#else
+// e^{dir 2 pi i t / Mmax} for 0 <= t < Mmax from the half-circle table
+__device__ __forceinline__ double2 twid(int t, int dir, const double2* __restrict__ tw, int Mmax) {
+    const int h = Mmax >> 1;
+    double2 w = tw[t < h ? t : t - h];
+    if (t >= h) { w.x = -w.x; w.y = -w.y; }
+    if (dir > 0) w.y = -w.y;
+    return w;
+}
+
+// v <- DFT_R(v) in registers, natural order: v_k = sum_n v_n e^{dir 2 pi i nk/R}
+// (R = 8: three radix-2 decimation-in-frequency levels, then the bit reversal)
+template <int R>
+__device__ __forceinline__ void dft_reg(double2* v, int dir) {
+    const double sg = dir > 0 ? 1.0 : -1.0;
+    auto bfly = [](double2& a, double2& b) {
+        const double2 t = make_double2(a.x - b.x, a.y - b.y);
+        a = make_double2(a.x + b.x, a.y + b.y);
+        b = t;
+    };
+    // multiply by e^{sg i pi / 2} = sg i
+    auto rot4 = [&](double2 a) { return make_double2(-sg * a.y, sg * a.x); };
+    if constexpr (R == 2) {
+        bfly(v[0], v[1]);
+    } else if constexpr (R == 4) {
+        bfly(v[0], v[2]); bfly(v[1], v[3]);
+        v[3] = rot4(v[3]);
+        bfly(v[0], v[1]); bfly(v[2], v[3]);
+        const double2 t = v[1]; v[1] = v[2]; v[2] = t;          // bit reversal
+    } else {
+        constexpr double C = 0.70710678118654752440;
+        bfly(v[0], v[4]); bfly(v[1], v[5]); bfly(v[2], v[6]); bfly(v[3], v[7]);
+        // v5 *= W8, v6 *= W8^2, v7 *= W8^3 (W8 = e^{sg i pi/4})
+        v[5] = make_double2(C * (v[5].x - sg * v[5].y), C * (v[5].y + sg * v[5].x));
+        v[6] = rot4(v[6]);
+        v[7] = make_double2(C * (-v[7].x - sg * v[7].y), C * (-v[7].y + sg * v[7].x));
+        bfly(v[0], v[2]); bfly(v[1], v[3]); bfly(v[4], v[6]); bfly(v[5], v[7]);
+        v[3] = rot4(v[3]); v[7] = rot4(v[7]);
+        bfly(v[0], v[1]); bfly(v[2], v[3]); bfly(v[4], v[5]); bfly(v[6], v[7]);
+        double2 t = v[1]; v[1] = v[4]; v[4] = t;                 // bit reversal (1 4)(3 6)
+        t = v[3]; v[3] = v[6]; v[6] = t;
+    }
+}
+
+// one Stockham stage of radix R at span Ns (Ns = product of the earlier
+// radices): butterfly j reads x[j + k M/R], twiddles by e^{dir 2 pi i (j mod Ns) k
+// / (Ns R)}, and writes y[(j - j mod Ns) R + j mod Ns + k Ns] (in place: all
+// reads, barrier, all writes).  NV complex values per thread at most.
+template <int R, int NV>
+__device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int dir, const double2* __restrict__ tw,
+                                               int Mmax) {
+    constexpr int NBF = NV / R;
+    const int nb = M / R;
+    const int step = Mmax / (Ns * R);
+    double2 v[NBF][R];
+#pragma unroll
+    for (int b = 0; b < NBF; ++b) {
+        const int j = threadIdx.x + b * blockDim.x;
+        if (j < nb) {
+#pragma unroll
+            for (int k = 0; k < R; ++k) v[b][k] = buf[j + k * nb];
+            if (Ns > 1) {
+                const int jm = j & (Ns - 1);
+#pragma unroll
+                for (int k = 1; k < R; ++k) v[b][k] = cmul(v[b][k], twid(jm * k * step, dir, tw, Mmax));
+            }
+            dft_reg<R>(v[b], dir);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NBF; ++b) {
+        const int j = threadIdx.x + b * blockDim.x;
+        if (j < nb) {
+            const int jm = j & (Ns - 1);
+            const int base = (j - jm) * R + jm;
+#pragma unroll
+            for (int k = 0; k < R; ++k) buf[base + k * Ns] = v[b][k];
+        }
+    }
+    __syncthreads();
+}
+
+// in-place power-of-two FFT in buf (LDS or global scratch), M <= 2 NB blockDim:
+// mixed-radix Stockham, one radix-2 or radix-4 stage first (M = 2^(3q+1) or
+// 2^(3q+2)), then radix-8 stages -- 5 block-wide passes at M = 8192 instead of 13
+template <int NB>
+__device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
+    constexpr int NV = 2 * NB;
+    const int p = 31 - __clz(M);
+    int Ns = 1;
+    if (p % 3 == 1) { stockham_stage<2, NV>(buf, M, 1, dir, tw, Mmax); Ns = 2; }
+    else if (p % 3 == 2) { stockham_stage<4, NV>(buf, M, 1, dir, tw, Mmax); Ns = 4; }
+    for (; Ns < M; Ns *= 8) stockham_stage<8, NV>(buf, M, Ns, dir, tw, Mmax);
+}
+#endif
 
 // forward DFT of length n held in buf[0..n) (Bluestein when n is not a power
 // of two: M = g.M, kernel V = FFT of the chirp); result in buf[0..n)
@@ -551,14 +664,14 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
     Fold4* red = reinterpret_cast<Fold4*>(lbuf + (gscratch ? 0 : g.M));   // J > 1 only (short rings)
     const int n = g.nphi;
-    const long long plane = (long long)(L + 1) * npair;
-    const double2* PN = phi + (2LL * comp + 0) * plane + p;
-    const double2* PS = phi + (2LL * comp + 1) * plane + p;
+    const long long plane = phi_plane(L, npair);
+    const double2* PN = phi + (2LL * comp + 0) * plane;
+    const double2* PS = phi + (2LL * comp + 1) * plane;
     const bool eq = g.startS < 0;
     const int K = n / 2 + 1;
     const int J = K >= BD ? 1 : BD / K;          // threads per bin pair
     auto H = [&](const double2* P, int m) {
-        const double2 v = P[(long long)m * npair];
+        const double2 v = P[phi_at(m, p, npair)];
         const double cm = m == 0 ? 1.0 : 2.0;
         const double2 t = g.phi_half ? cmul(v, expi_pi_frac(m, n)) : v;
         return make_double2(cm * t.x, cm * t.y);
@@ -702,7 +815,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         __syncthreads();
         dft_forward<NB>(buf, g, tw, Mmax, bsk);
     }
-    const long long plane = (long long)(L + 1) * npair;
+    const long long plane = phi_plane(L, npair);
     double2* oN = phi + (2LL * comp + 0) * plane;
     double2* oS = phi + (2LL * comp + 1) * plane;
     for (int m = threadIdx.x; m <= L; m += blockDim.x) {
@@ -718,8 +831,8 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
             xs = cmul(xs, e);
         }
         if (m == 0) { xn.y = 0.0; xs.y = 0.0; }
-        oN[(long long)m * npair + p] = xn;
-        oS[(long long)m * npair + p] = eq ? make_double2(0.0, 0.0) : xs;
+        oN[phi_at(m, p, npair)] = xn;
+        oS[phi_at(m, p, npair)] = eq ? make_double2(0.0, 0.0) : xs;
     }
 }
 
@@ -764,16 +877,14 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                                                             double2* __restrict__ part) {
     constexpr int NO = NC == 1 ? 2 : (NC == 2 ? 4 : 6);   // real outputs per l
     constexpr int NV = NO * ANA_C;
-    constexpr int NVP = NV <= 8 ? 8 : (NV <= 16 ? 16 : 32);   // rows per wave, power of two
-    constexpr int RS = 65;                                     // padded row of 64 partials
     static_assert(NV <= 32, "chunk too large for the wave reduction");
-    __shared__ double red_all[4][NVP * RS];
+    __shared__ double red_all[4][2 * 16 * (NV + 2)];   // per wave: two chunk buffers
     const int L = D.L, npair = D.npair;
     const int q = blockIdx.x, tile = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = tile * (ATILE / 64) + wave * ASR;
-    const long long plane = (long long)(L + 1) * npair;
+    const long long plane = phi_plane(L, npair);
     double x[ASR], is2[ASR], xis2[ASR];
     int pr[ASR];
     bool act[ASR];
@@ -808,8 +919,8 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
             for (int c = 0; c < NC; ++c) {
                 double2 a = make_double2(0.0, 0.0), b = a;
                 if (act[r] && ls[r] <= L) {
-                    a = phi[(2LL * c + 0) * plane + (long long)m * npair + pr[r]];
-                    b = phi[(2LL * c + 1) * plane + (long long)m * npair + pr[r]];
+                    a = phi[(2LL * c + 0) * plane + phi_at(m, pr[r], npair)];
+                    b = phi[(2LL * c + 1) * plane + phi_at(m, pr[r], npair)];
                 }
                 fp[r][c] = make_double2(a.x + b.x, a.y + b.y);
                 fn[r][c] = make_double2(a.x - b.x, a.y - b.y);
@@ -820,30 +931,56 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         // chunks start on m's parity so positions 0, 2 of a chunk are even
         const int lstart0 = lmin - ((lmin - m) & 1);
         double* red = red_all[wave];
-        // fixed-order wave reduction of a chunk (wave-private LDS rows, no
-        // workgroup barrier): lane -> (row o = lane % NVP, segment lane / NVP)
-        auto reduce_store = [&](const double (&acc)[NV], int l0) {
+        // ---- fixed-order wave reduction of a chunk's NV partial sums ----
+        // Two butterfly levels across the wave halves (v_permlane32_swap: lane ^ 32)
+        // and rows (v_permlane16_swap: lane ^ 16) leave each lane NV/4 sums of 4
+        // lanes (outputs block B = lane >> 4); the 16 lanes of a row then meet in
+        // wave-private LDS (one row of NV per lane, two buffers): two lanes per
+        // output sum 8 rows each and combine.  put_chunk writes a chunk, get_chunk
+        // issues its reads, fin_chunk sums and stores; the fast loop reads chunk
+        // k - 1 before computing chunk k, so the LDS latency hides under the
+        // Legendre work (LDS ops of one wave complete in order: no fences).
+        constexpr int H1 = NV / 2, H2 = NV / 4, RS2 = NV + 2, RBUF = 16 * RS2;
+        auto put_chunk = [&](const double (&acc)[NV], int bsel) {
+            double w1[H1], w2[H2];
 #pragma unroll
-            for (int i = 0; i < NV; ++i) red[i * RS + lane] = acc[i];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            constexpr int SEG = 64 / NVP;               // segments per row
-            constexpr int SLEN = 64 / SEG;              // partials per segment
-            const int o = lane % NVP, sg = lane / NVP;
-            double sum = 0.0;
-            if (o < NV) {
-                const double* row = red + o * RS + sg * SLEN;
-#pragma unroll 8
-                for (int i = 0; i < SLEN; ++i) sum += row[i];
+            for (int t = 0; t < H1; ++t) {
+                const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(acc[t]), __double2loint(acc[t + H1]),
+                                                                 false, false);
+                const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(acc[t]), __double2hiint(acc[t + H1]),
+                                                                 false, false);
+                w1[t] = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
             }
 #pragma unroll
-            for (int d = NVP; d < 64; d <<= 1) sum += __shfl_xor(sum, d, 64);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < NV) {
-                const int cc = lane / NO, oo = lane % NO;
+            for (int t = 0; t < H2; ++t) {
+                const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(w1[t]), __double2loint(w1[t + H2]),
+                                                                 false, false);
+                const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(w1[t]), __double2hiint(w1[t + H2]),
+                                                                 false, false);
+                w2[t] = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+            }
+            double* rowp = red + bsel * RBUF + (lane & 15) * RS2 + (lane >> 4) * H2;
+#pragma unroll
+            for (int t = 0; t < H2; t += 2)
+                *reinterpret_cast<double2*>(rowp + t) = make_double2(w2[t], w2[t + 1]);
+        };
+        auto get_chunk = [&](int bsel, double (&rv)[8]) {
+            const int o = min(lane >> 1, NV - 1), hh = lane & 1;
+            const double* col = red + bsel * RBUF + (hh * 8) * RS2 + o;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) rv[i] = col[i * RS2];
+        };
+        auto fin_chunk = [&](const double (&rv)[8], int l0) {
+            const int o = lane >> 1, hh = lane & 1;
+            double sum = rv[0];
+#pragma unroll
+            for (int i = 1; i < 8; ++i) sum += rv[i];
+            const int slo = __builtin_amdgcn_update_dpp(0, __double2loint(sum), 0xB1, 0xf, 0xf, false);
+            const int shi = __builtin_amdgcn_update_dpp(0, __double2hiint(sum), 0xB1, 0xf, 0xf, false);
+            const double other = __hiloint2double(shi, slo);
+            sum = hh ? other + sum : sum + other;   // rows 0-7 then 8-15 on both lanes
+            if (hh == 0 && o < NV) {
+                const int cc = o / NO, oo = o % NO;
                 const int l = l0 + cc;
                 if (l >= m && l <= L) {
                     const int comp = oo >> 1;
@@ -852,6 +989,12 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                     dst[oo & 1] = sum;
                 }
             }
+        };
+        auto reduce_store = [&](const double (&acc)[NV], int l0) {
+            double rv[8];
+            put_chunk(acc, 0);
+            get_chunk(0, rv);
+            fin_chunk(rv, l0);
         };
         // guarded chunk: slot activation at its onset, scaled lanes masked and
         // rescaled, l beyond L skipped
@@ -899,23 +1042,38 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
 #if defined(GS_ASM_MARKERS)
         asm volatile("; ANA_FAST_BEGIN");
 #endif
-        for (; l0 + ANA_C - 1 <= L; l0 += ANA_C) {
-            double acc[NV];
+        {
+            bool pend = false;
+            int pl0 = 0, cur = 0;
+            for (; l0 + ANA_C - 1 <= L; l0 += ANA_C) {
+                double rv[8];
+                if (pend) get_chunk(cur ^ 1, rv);
+                double acc[NV];
 #pragma unroll
-            for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+                for (int i = 0; i < NV; ++i) acc[i] = 0.0;
 #pragma unroll
-            for (int cc = 0; cc < ANA_C; ++cc) {
-                const int l = l0 + cc;
-                const LegCoef c = cf[l];
-                const LegCoef cn = cf[l + 1];
+                for (int cc = 0; cc < ANA_C; ++cc) {
+                    const int l = l0 + cc;
+                    const LegCoef c = cf[l];
+                    const LegCoef cn = cf[l + 1];
 #pragma unroll
-                for (int r = 0; r < ASR; ++r) {
-                    if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
-                    else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
-                    rec_step(cn, x[r], v0[r], v1[r]);
+                    for (int r = 0; r < ASR; ++r) {
+                        if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
+                        else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
+                        rec_step(cn, x[r], v0[r], v1[r]);
+                    }
                 }
+                if (pend) fin_chunk(rv, pl0);
+                put_chunk(acc, cur);
+                pend = true;
+                pl0 = l0;
+                cur ^= 1;
             }
-            reduce_store(acc, l0);
+            if (pend) {
+                double rv[8];
+                get_chunk(cur ^ 1, rv);
+                fin_chunk(rv, pl0);
+            }
         }
 #if defined(GS_ASM_MARKERS)
         asm volatile("; ANA_CHUNK_END");
@@ -997,7 +1155,7 @@ struct gs_sht {
     int* stk = nullptr;
     double2* tw = nullptr;
     double2* bsk = nullptr;
-    double2* phi = nullptr;      // [3][2][L+1][npair]
+    double2* phi = nullptr;      // [3][2] planes of phi_plane(L, npair) (phi_at)
     double2* part = nullptr;     // [ntile][3][nlm]
     double2* gscr = nullptr;     // global FFT scratch for M > LDS_FFT_MAX
     double2* sscr = nullptr;     // split rings: [comp][slot][split_n] half-transform scratch
@@ -1138,7 +1296,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     rc |= sht_alloc(p, &p->stk, (size_t)(L + 1) * p->npair);
     rc |= sht_alloc(p, &p->tw, (size_t)Mmax / 2);
     rc |= sht_alloc(p, &p->bsk, (size_t)std::max<long long>(bs_total, 1));
-    rc |= sht_alloc(p, &p->phi, (size_t)3 * 2 * (L + 1) * p->npair);
+    rc |= sht_alloc(p, &p->phi, (size_t)3 * 2 * phi_plane(L, p->npair));
     rc |= sht_alloc(p, &p->part, (size_t)p->ntile * 4 * 3 * p->nlm);   // one partial per analysis wave
     rc |= sht_alloc(p, &p->mapw, (size_t)3 * p->npix);
     rc |= sht_alloc(p, &p->ain, (size_t)3 * p->nlm);
