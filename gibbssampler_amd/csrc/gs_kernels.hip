@@ -1076,9 +1076,10 @@ void build_tasks(gs_plan* p) {
     };
     // rows per chunk: fixed (independent of the chain count), so the fixed-order
     // statistic sums -- and therefore every chain's trajectory -- are bit-identical
-    // whatever the batch size or GPU count; 32 rows measured best at the
-    // BASELINE size (tools/sweep_rows.sh)
-    int tm = 32;
+    // whatever the batch size or GPU count.  20-24 rows measured best at the
+    // BASELINE size (tools/sweep_rows.py, interleaved in one process: sweep +
+    // finish 264-267 us against 280-284 us at 32 rows, 271 us at 16)
+    int tm = 24;
     if (const char* env = getenv("GS_SWEEP_ROWS")) {
         const int v = atoi(env);
         if (v >= 1 && v <= 1024) tm = v;
