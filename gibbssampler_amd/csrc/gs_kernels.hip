@@ -428,8 +428,18 @@ __global__ void k_stats_finish(int L, int nchains, int ntile, int nchunk, int tm
     const int lane = ell - (L - WAVE * t - 63);
     const int cmax = (L - WAVE * t) / tm;
     const double* pp = partials + ((long long)chain * ntile + t) * nchunk * nstat * WAVE + q * WAVE + lane;
+    // loads issued 8 at a time (latency-bound otherwise), summed in chunk order
+    const long long cs = (long long)nstat * WAVE;
     double acc = 0.0;
-    for (int c = 0; c <= cmax; ++c) acc += pp[(long long)c * nstat * WAVE];
+    int c = 0;
+    for (; c + 8 <= cmax + 1; c += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = pp[(c + j) * cs];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+    for (; c <= cmax; ++c) acc += pp[c * cs];
     stats[g] = acc;
 }
 
