@@ -1167,6 +1167,10 @@ struct gs_sht {
     std::vector<int> cls_M;      // M of each class
     std::vector<int> cls_n;      // pairs in the class
     std::vector<int*> cls_pairs; // device lists
+    // the short-ring classes run on a side stream beside the largest class
+    // (fork / join by events, graph-capturable); 0 = all on the caller's stream
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     long long bytes = 0;
     ShtDev dev() const {
         ShtDev D;
@@ -1192,6 +1196,9 @@ void sht_free(gs_sht* p) {
         if (b) (void)hipFree(b);
     for (int* b : p->cls_pairs)
         if (b) (void)hipFree(b);
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+    if (p->side) (void)hipStreamDestroy(p->side);
     delete p;
 }
 
@@ -1373,6 +1380,13 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         sht_free(p);
         return set_error(std::string("gs_sht_create: setup kernels failed: ") + hipGetErrorString(e));
     }
+    if (!getenv("GS_SHT_NO_SIDE_STREAM") &&
+        (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
+         hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess)) {
+        sht_free(p);
+        return set_error("gs_sht_create: side stream / events");
+    }
     *out = p;
     return 0;
 }
@@ -1391,37 +1405,58 @@ int gs_sht_info(const gs_sht* p, int* nside, int* lmax, long long* npix, long lo
     return 0;
 }
 
+static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const double* maps_in, double* maps_out,
+                          hipStream_t st) {
+    const int M = p->cls_M[c];
+    const bool glob = M > p->lds_fft_max;
+    const int bd = ring_block(M);
+    const bool nb8 = M / 2 > 4 * bd;
+    // LDS: FFT buffer (+ fold reduction slots for short rings)
+    const size_t red = M < 8 * bd ? (size_t)bd * 4 * sizeof(double2) : 0;   // fold reduction, short rings
+    const size_t lds = (glob ? 0 : (size_t)M * sizeof(double2)) + red;
+    const dim3 grid(p->cls_n[c], ncomp);
+    double2* scr = glob ? p->gscr : nullptr;
+    if (synth) {
+        if (nb8)
+            hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
+                               p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n);
+        else
+            hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
+                               p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n);
+    } else {
+        if (nb8)
+            hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n);
+        else
+            hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n);
+    }
+    GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
+    return 0;
+}
+
+// Ring stage: one launch per FFT-length class.  The classes touch disjoint
+// rings (and disjoint scratch: split rings own their sscr slot, the one
+// global-scratch class stays on the caller's stream), so the short-ring
+// classes -- a dozen small, latency-bound launches -- run on the plan's side
+// stream while the largest class runs on the caller's.
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream) {
-    for (size_t c = 0; c < p->cls_M.size(); ++c) {
-        const int M = p->cls_M[c];
-        const bool glob = M > p->lds_fft_max;
-        const int bd = ring_block(M);
-        const bool nb8 = M / 2 > 4 * bd;
-        // LDS: FFT buffer (+ fold reduction slots for short rings)
-        const size_t red = M < 8 * bd ? (size_t)bd * 4 * sizeof(double2) : 0;   // fold reduction, short rings
-        const size_t lds = (glob ? 0 : (size_t)M * sizeof(double2)) + red;
-        const dim3 grid(p->cls_n[c], ncomp);
-        double2* scr = glob ? p->gscr : nullptr;
-        if (synth) {
-            if (nb8)
-                hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out,
-                                   p->sscr, p->nsplit, p->split_n);
-            else
-                hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out,
-                                   p->sscr, p->nsplit, p->split_n);
-        } else {
-            if (nb8)
-                hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi,
-                                   p->sscr, p->nsplit, p->split_n);
-            else
-                hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
-                                   p->cls_pairs[c], p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi,
-                                   p->sscr, p->nsplit, p->split_n);
-        }
-        GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
+    const size_t ncls = p->cls_M.size();
+    size_t big = 0;
+    for (size_t c = 1; c < ncls; ++c)
+        if ((long long)p->cls_n[c] * p->cls_M[c] > (long long)p->cls_n[big] * p->cls_M[big]) big = c;
+    const bool fork = p->side && ncls > 1;
+    if (fork) {
+        GS_CHECK(hipEventRecord(p->ev_fork, S(stream)));
+        GS_CHECK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
+    }
+    for (size_t c = 0; c < ncls; ++c) {
+        const bool on_side = fork && c != big && p->cls_M[c] <= p->lds_fft_max;
+        if (sht_ring_class(p, c, synth, ncomp, maps_in, maps_out, on_side ? p->side : S(stream))) return -1;
+    }
+    if (fork) {
+        GS_CHECK(hipEventRecord(p->ev_join, p->side));
+        GS_CHECK(hipStreamWaitEvent(S(stream), p->ev_join, 0));
     }
     return 0;
 }
