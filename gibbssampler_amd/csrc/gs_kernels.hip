@@ -779,7 +779,9 @@ struct MhEpi {
     int nchains;
 };
 
-template <int F>
+// SC: this chain's per-l statistics cached in LDS for the whole kernel (every
+// phase evaluates f_l from them; LDS instead of three passes over L2)
+template <int F, bool SC>
 __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases ph, const int2* __restrict__ phase_tab,
                                                   const int4* __restrict__ phase_rng,
                                                   const int* __restrict__ bins, const int* __restrict__ blocks,
@@ -801,16 +803,21 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     double* g = smem;                               // [2][L+1]
     double* ub = g + 2 * Lp1;                       // [phase blocks x n_iter]
     double* Ds = ub + maxnb * n_iter_mh;            // [NSP][maxbins] LDS copy of this chain's D_l
-    int* e2b = reinterpret_cast<int*>(Ds + NSP * maxbins);   // [NSP][L+1]
+    double* stl = Ds + NSP * maxbins;               // [NS][L+1] statistics (SC only)
+    int* e2b = reinterpret_cast<int*>(stl + (SC ? NS * Lp1 : 0));   // [NSP][L+1]
     const int chain = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
-    __shared__ double wsum[64];
-    __shared__ int wflag;
+    constexpr int MAXW = 4;                         // wide blocks decided together
+    __shared__ double wsum[MAXW][64];
+    __shared__ int wflag[MAXW];
     double* D = dl + (long long)chain * NSP * maxbins;
     const double* P = prop + (long long)chain * NSP * maxbins;
     const double* R = logr + (long long)chain * NSP * maxbins;
-    const double* st = stats + (long long)chain * NS * Lp1;
+    const double* stg = stats + (long long)chain * NS * Lp1;
+    if constexpr (SC)
+        for (int k = tid; k < NS * Lp1; k += blockDim.x) stl[k] = stg[k];
+    const double* st = SC ? stl : stg;
     for (int k = tid; k < NSP * Lp1; k += blockDim.x) e2b[k] = ell2bin[k];
     // the chain's D_l lives in LDS for the whole sweep (written back at the end)
     for (int k = tid; k < NSP * maxbins; k += blockDim.x) Ds[k] = D[k];
@@ -883,27 +890,35 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                 if (accept_out) accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
             }
         }
-        // wide blocks: the whole workgroup per block, one block after the other
-        // (fixed-order sums: per-thread terms, wave sums, then the 16 wave sums
-        // in wave order), so a phase's few long blocks do not serialise on one wave
+        // wide blocks: the whole workgroup, up to MAXW blocks together (fixed-order
+        // sums per block: per-thread terms, wave sums, then the 16 wave sums in
+        // wave order; the blocks of a phase are independent), so a phase's few
+        // long blocks share one pair of barriers and do not serialise on one wave
 #if defined(GS_ABL_MH_WIDE)
         if (false)
 #endif
-        for (int j = 0; j < nwide; ++j) {
-            const int2 sb = tab[j];
-            const int4 r = rng[j];
-            const int sp = sb.x, blk = sb.y, k = sp == sp0 ? 0 : 1;
-            const int lo = r.x, hi = r.y, l0 = r.z, l1 = r.w;
-            double diff = 0.0, lrs = 0.0;
-            for (int l = l0 + tid; l < l1; l += blockDim.x) diff += g[k * Lp1 + l];
-            for (int b = lo + tid; b < hi; b += blockDim.x) lrs += R[sp * maxbins + b];
-            diff = wave_sum(diff);
-            lrs = wave_sum(lrs);
-            if (lane == 0) { wsum[wv] = diff; wsum[32 + wv] = lrs; }
+        for (int j0 = 0; j0 < nwide; j0 += MAXW) {
+            const int nw = min(MAXW, nwide - j0);
+#pragma unroll
+            for (int jj = 0; jj < MAXW; ++jj) {
+                if (jj >= nw) break;
+                const int2 sb = tab[j0 + jj];
+                const int4 r = rng[j0 + jj];
+                const int k = sb.x == sp0 ? 0 : 1;
+                double diff = 0.0, lrs = 0.0;
+                for (int l = r.z + tid; l < r.w; l += blockDim.x) diff += g[k * Lp1 + l];
+                for (int b = r.x + tid; b < r.y; b += blockDim.x) lrs += R[sb.x * maxbins + b];
+                diff = wave_sum(diff);
+                lrs = wave_sum(lrs);
+                if (lane == 0) { wsum[jj][wv] = diff; wsum[jj][32 + wv] = lrs; }
+            }
             __syncthreads();
-            if (tid == 0) {
+            if (tid < nw) {
+                const int j = j0 + tid;
+                const int2 sb = tab[j];
+                const int sp = sb.x, blk = sb.y;
                 double dsum = 0.0, lsum = 0.0;
-                for (int w = 0; w < nwv; ++w) { dsum += wsum[w]; lsum += wsum[32 + w]; }
+                for (int w = 0; w < nwv; ++w) { dsum += wsum[tid][w]; lsum += wsum[tid][32 + w]; }
                 bool taken = false;
                 for (int att = 0; att < n_iter_mh; ++att) {
                     const bool acc = log(ub[j * n_iter_mh + att]) < (taken ? 0.0 : dsum) + lsum;
@@ -911,11 +926,15 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                     if (accept_out)
                         accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
                 }
-                wflag = taken ? 1 : 0;
+                wflag[tid] = taken ? 1 : 0;
             }
             __syncthreads();
-            if (wflag)
-                for (int b = lo + tid; b < hi; b += blockDim.x) Ds[sp * maxbins + b] = P[sp * maxbins + b];
+            for (int jj = 0; jj < nw; ++jj) {
+                if (!wflag[jj]) continue;
+                const int2 sb = tab[j0 + jj];
+                const int4 r = rng[j0 + jj];
+                for (int b = r.x + tid; b < r.y; b += blockDim.x) Ds[sb.x * maxbins + b] = P[sb.x * maxbins + b];
+            }
         }
         __syncthreads();
     }
@@ -1514,12 +1533,16 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
     }
     const size_t lds = (2 * (size_t)(p->L + 1) + (size_t)maxnb * p->n_iter_mh + (size_t)p->nspec * p->maxbins) *
                            sizeof(double) + (size_t)p->nspec * (p->L + 1) * sizeof(int);
+    const size_t lds_sc = lds + (size_t)p->nstat * (p->L + 1) * sizeof(double);
+    const bool sc = lds_sc <= 144 * 1024 && !getenv("GS_MH_NO_STATS_CACHE");
     if (lds <= 128 * 1024) {
-#define GS_MF(FF) hipLaunchKernelGGL((k_mh_fused<FF>), dim3(p->nchains), dim3(1024), lds, S(stream), p->L, p->maxbins, ph, \
+#define GS_MF(FF) if (sc) GS_MF2(FF, true, lds_sc); else GS_MF2(FF, false, lds)
+#define GS_MF2(FF, SCV, LDSV) hipLaunchKernelGGL((k_mh_fused<FF, SCV>), dim3(p->nchains), dim3(1024), LDSV, S(stream), p->L, p->maxbins, ph, \
                                      p->phase_tab, p->phase_rng, p->bins, p->blocks, p->meta + 8, p->nacc, p->n_iter_mh, p->ell2blk,    \
                                      p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop,       \
                                      p->logr, u_acc, slo, shi, IterArg{iteration, p->itp()}, p->chain0, accept_out, E)
-        if (p->F == 1) GS_MF(1); else if (p->F == 2) GS_MF(2); else GS_MF(3);
+        if (p->F == 1) { GS_MF(1); } else if (p->F == 2) { GS_MF(2); } else { GS_MF(3); }
+#undef GS_MF2
 #undef GS_MF
         GS_LAUNCH_CHECK("k_mh_fused");
         return 0;
