@@ -81,6 +81,8 @@ struct gs_plan {
     double* prop = nullptr;          // [nchains][nspec][maxbins]
     double* logr = nullptr;          // [nchains][nspec][maxbins]
     double* dl_tmp = nullptr;        // [nchains][nspec][maxbins]
+    double* u_nat = nullptr;         // [nchains][nacc] native MH accept uniforms drawn by the prologue
+    bool u_nat_ready = false;
     // device iteration counter (hipGraph replay of whole steps)
     uint32_t* iter_dev = nullptr;
     bool iter_dev_on = false;
@@ -617,17 +619,42 @@ __global__ __launch_bounds__(256) void k_mh_propose(int nchains, int maxbins, co
                      logr, u_prop, seed_lo, seed_hi, itarg, chain0);
 }
 
+// flat accept order of the plan (same counters as k_mh_fused / k_mh_accept)
+__device__ __forceinline__ void mh_uniform_at(long long g, int nchains, int nspec, const int* __restrict__ meta,
+                                              int nacc, int n_iter_mh, uint32_t seed_lo, uint32_t seed_hi,
+                                              uint32_t iter, int chain0, double* __restrict__ out) {
+    if (g >= (long long)nchains * nacc) return;
+    const int chain = (int)(g / nacc), flat = (int)(g % nacc);
+    const int* nblocks = meta + 4;
+    const int* acc_off = meta + 8;
+    int sp = -1;
+    for (int k = 0; k < nspec; ++k)
+        if (flat >= acc_off[k] && flat < acc_off[k] + nblocks[k] * n_iter_mh) sp = k;
+    if (sp < 0) return;
+    const int r = flat - acc_off[sp];
+    const int blk = r / n_iter_mh, att = r % n_iter_mh;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    out[g] = uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
+}
+
 // non-centered prologue: the MH proposals depend only on the current D_l, not
 // on the CR draw, so they are made in the same launch as the CR block
 // parameters (proposal workgroups first; both halves are latency-bound).
 template <int F>
-__global__ __launch_bounds__(256) void k_nc_prologue(int nblk_prop, int L, int nchains, int maxbins,
+__global__ __launch_bounds__(256) void k_nc_prologue(int nblk_prop, int nblk_par, double* __restrict__ u_out,
+                                                     int nspec, int nacc, int n_iter_mh, int L, int nchains, int maxbins,
                                                      const int* __restrict__ ell2bin, const double* __restrict__ bl,
                                                      double k0, double k1, double k2, double* __restrict__ params,
                                                      const int* __restrict__ nbins_arr, const double* __restrict__ prop_sd,
                                                      const double* __restrict__ dl, double* __restrict__ prop,
                                                      double* __restrict__ logr, const double* __restrict__ u_prop,
                                                      uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, int chain0) {
+    if ((int)blockIdx.x >= nblk_prop + nblk_par) {
+        // native accept uniforms of this step's MH (k_mh_fused reads them from LDS)
+        mh_uniform_at(((int)blockIdx.x - nblk_prop - nblk_par) * (long long)blockDim.x + threadIdx.x, nchains, nspec,
+                      nbins_arr, nacc, n_iter_mh, seed_lo, seed_hi, itarg.get(), chain0, u_out);
+        return;
+    }
     if ((int)blockIdx.x < nblk_prop)
         mh_propose_at<F>(blockIdx.x * (long long)blockDim.x + threadIdx.x, nchains, maxbins, nbins_arr, prop_sd, dl,
                          prop, logr, u_prop, seed_lo, seed_hi, itarg, chain0);
@@ -730,24 +757,11 @@ __global__ __launch_bounds__(256) void k_mh_accept(int L, int nchains, int maxbi
 }
 
 // the native accept uniforms of every (chain, spectrum, block, attempt) in the
-// flat accept order of the plan (same counters as k_mh_fused / k_mh_accept)
 __global__ void k_mh_uniforms(int nchains, int nspec, int maxbins, const int* __restrict__ meta, int nacc,
                               int n_iter_mh, uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, int chain0,
                               double* __restrict__ out) {
-    const uint32_t iter = itarg.get();
-    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g >= (long long)nchains * nacc) return;
-    const int chain = (int)(g / nacc), flat = (int)(g % nacc);
-    const int* nblocks = meta + 4;
-    const int* acc_off = meta + 8;
-    int sp = -1;
-    for (int k = 0; k < nspec; ++k)
-        if (flat >= acc_off[k] && flat < acc_off[k] + nblocks[k] * n_iter_mh) sp = k;
-    if (sp < 0) return;
-    const int r = flat - acc_off[sp];
-    const int blk = r / n_iter_mh, att = r % n_iter_mh;
-    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
-    out[g] = uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
+    mh_uniform_at(blockIdx.x * (long long)blockDim.x + threadIdx.x, nchains, nspec, meta, nacc, n_iter_mh, seed_lo,
+                  seed_hi, itarg.get(), chain0, out);
 }
 
 // MH phases fused in one launch: one workgroup per chain walks the phases;
@@ -781,6 +795,27 @@ struct MhEpi {
 
 // SC: this chain's per-l statistics cached in LDS for the whole kernel (every
 // phase evaluates f_l from them; LDS instead of three passes over L2)
+// workgroup copy global -> LDS with four independent loads per thread in flight
+template <typename T>
+__device__ __forceinline__ void lds_fill4(T* __restrict__ dst, const T* __restrict__ src, int n) {
+    const int bd = blockDim.x;
+    for (int k0 = threadIdx.x; k0 < n; k0 += 4 * bd) {
+        T v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = k0 + t * bd < n ? src[k0 + t * bd] : T(0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (k0 + t * bd < n) dst[k0 + t * bd] = v[t];
+    }
+}
+
+#if defined(GS_MH_STAMPS)
+// diagnostic build only: per-workgroup s_memtime stamps of the MH phases
+__device__ unsigned long long g_mh_stamps[64][24];
+#define MH_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_mh_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define MH_STAMP(k) do { } while (0)
+#endif
 template <int F, bool SC>
 __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases ph, const int2* __restrict__ phase_tab,
                                                   const int4* __restrict__ phase_rng,
@@ -793,6 +828,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                                                   const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
                                                   IterArg itarg, int chain0, int32_t* __restrict__ accept_out,
                                                   MhEpi epi) {
+    MH_STAMP(0);
     const uint32_t iter = itarg.get();
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
@@ -804,7 +840,8 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     double* ub = g + 2 * Lp1;                       // [phase blocks x n_iter]
     double* Ds = ub + maxnb * n_iter_mh;            // [NSP][maxbins] LDS copy of this chain's D_l
     double* stl = Ds + NSP * maxbins;               // [NS][L+1] statistics (SC only)
-    int* e2b = reinterpret_cast<int*>(stl + (SC ? NS * Lp1 : 0));   // [NSP][L+1]
+    double* ul = stl + (SC ? NS * Lp1 : 0);         // [nacc] this chain's accept uniforms (u_acc given)
+    int* e2b = reinterpret_cast<int*>(ul + (u_acc ? nacc : 0));   // [NSP][L+1]
     const int chain = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
@@ -815,14 +852,17 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     const double* P = prop + (long long)chain * NSP * maxbins;
     const double* R = logr + (long long)chain * NSP * maxbins;
     const double* stg = stats + (long long)chain * NS * Lp1;
-    if constexpr (SC)
-        for (int k = tid; k < NS * Lp1; k += blockDim.x) stl[k] = stg[k];
     const double* st = SC ? stl : stg;
-    for (int k = tid; k < NSP * Lp1; k += blockDim.x) e2b[k] = ell2bin[k];
-    // the chain's D_l lives in LDS for the whole sweep (written back at the end)
-    for (int k = tid; k < NSP * maxbins; k += blockDim.x) Ds[k] = D[k];
+    // LDS fill: the chain's D_l (kept in LDS for the whole sweep, written back at
+    // the end), statistics (SC), accept uniforms (u_acc) and the l -> bin map;
+    // four loads in flight per thread and array
+    lds_fill4(Ds, D, NSP * maxbins);
+    if constexpr (SC) lds_fill4(stl, stg, NS * Lp1);
+    if (u_acc) lds_fill4(ul, u_acc + (long long)chain * nacc, nacc);
+    lds_fill4(e2b, ell2bin, NSP * Lp1);
     __syncthreads();
     for (int q = 0; q < ph.nphase; ++q) {
+        MH_STAMP(1 + 5 * q);
         const int nb = ph.n[q];
         if (nb == 0) continue;
         const int sp0 = ph.sp[q][0], sp1 = ph.sp[q][1];
@@ -856,6 +896,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                 g[k * Lp1 + l] = out;
             }
         }
+        MH_STAMP(2 + 5 * q);
         // accept uniforms of every (block, attempt), in parallel
         for (int j = tid; j < nb * n_iter_mh; j += blockDim.x) {
             const int2 sb = tab[j / n_iter_mh];
@@ -864,11 +905,11 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
 #if defined(GS_ABL_MH_U)
             ub[j] = 0.5 + 1e-9 * flat;
 #else
-            ub[j] = u_acc ? u_acc[(long long)chain * nacc + flat]
-                          : uniform1(key, sb.y, (uint32_t)sb.x | ((uint32_t)att << 8), TAG_MH_U, iter);
+            ub[j] = u_acc ? ul[flat] : uniform1(key, sb.y, (uint32_t)sb.x | ((uint32_t)att << 8), TAG_MH_U, iter);
 #endif
         }
         __syncthreads();
+        MH_STAMP(3 + 5 * q);
         // narrow blocks: one thread each
 #if defined(GS_ABL_MH_NARROW)
         if (false)
@@ -890,6 +931,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                 if (accept_out) accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
             }
         }
+        MH_STAMP(4 + 5 * q);
         // wide blocks: the whole workgroup, up to MAXW blocks together (fixed-order
         // sums per block: per-thread terms, wave sums, then the 16 wave sums in
         // wave order; the blocks of a phase are independent), so a phase's few
@@ -938,6 +980,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         }
         __syncthreads();
     }
+    MH_STAMP(20);
     const int nrow = NSP * maxbins;
     for (int k = tid; k < nrow; k += blockDim.x) D[k] = Ds[k];
     // ---- epilogue (graph-captured NC steps) ----
@@ -946,6 +989,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
         for (int k = tid; k < nrow; k += blockDim.x) tr[k] = Ds[k];
     }
+    MH_STAMP(21);
     if (epi.counter) {
         __syncthreads();
         if (tid == 0) {
@@ -1160,6 +1204,11 @@ int check_plan(const gs_plan* p) {
 extern "C" {
 
 int gs_abi_version(void) { return GS_ABI_VERSION; }
+#if defined(GS_MH_STAMPS)
+int gs_debug_mh_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mh_stamps), sizeof(unsigned long long) * 64 * 24) == hipSuccess ? 0 : -1;
+}
+#endif
 const char* gs_last_error(void) { return gs_detail::g_last_error.c_str(); }
 
 int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
@@ -1288,6 +1337,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->prop, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->logr, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->dl_tmp, nc * p->nspec * maxbins);
+    rc |= dev_alloc(&p->u_nat, nc * std::max(p->nacc, 1));
     rc |= dev_alloc(&p->iter_dev, 4);
     if (rc) { gs_plan_destroy(p); return -1; }
     *out = p;
@@ -1296,7 +1346,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
-    void* bufs[] = {p->iter_dev, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials,
+    void* bufs[] = {p->iter_dev, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
                     p->params, p->stats, p->prop, p->logr, p->dl_tmp};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1533,10 +1583,11 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
     }
     const size_t lds = (2 * (size_t)(p->L + 1) + (size_t)maxnb * p->n_iter_mh + (size_t)p->nspec * p->maxbins) *
                            sizeof(double) + (size_t)p->nspec * (p->L + 1) * sizeof(int);
-    const size_t lds_sc = lds + (size_t)p->nstat * (p->L + 1) * sizeof(double);
-    const bool sc = lds_sc <= 144 * 1024 && !getenv("GS_MH_NO_STATS_CACHE");
+    const size_t lds_u = u_acc ? (size_t)p->nacc * sizeof(double) : 0;
+    const size_t lds_sc = lds + lds_u + (size_t)p->nstat * (p->L + 1) * sizeof(double);
+    const bool sc = lds_sc <= 156 * 1024 && !getenv("GS_MH_NO_STATS_CACHE");
     if (lds <= 128 * 1024) {
-#define GS_MF(FF) if (sc) GS_MF2(FF, true, lds_sc); else GS_MF2(FF, false, lds)
+#define GS_MF(FF) if (sc) GS_MF2(FF, true, lds_sc); else GS_MF2(FF, false, lds + lds_u)
 #define GS_MF2(FF, SCV, LDSV) hipLaunchKernelGGL((k_mh_fused<FF, SCV>), dim3(p->nchains), dim3(1024), LDSV, S(stream), p->L, p->maxbins, ph, \
                                      p->phase_tab, p->phase_rng, p->bins, p->blocks, p->meta + 8, p->nacc, p->n_iter_mh, p->ell2blk,    \
                                      p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop,       \
@@ -1608,7 +1659,11 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const int nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
     const int nbq = nblk((long long)p->nchains * (p->L + 1), 256);
-#define GS_PRO(FF) hipLaunchKernelGGL((k_nc_prologue<FF>), dim3(nbp + nbq), dim3(256), 0, S(stream), nbp, p->L,        \
+    // native mode: the MH accept uniforms are drawn here too (replay draws them on the host)
+    p->u_nat_ready = u_prop == nullptr && p->nacc > 0 && !getenv("GS_MH_INKERNEL_UNIFORMS");
+    const int nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
+#define GS_PRO(FF) hipLaunchKernelGGL((k_nc_prologue<FF>), dim3(nbp + nbq + nbu), dim3(256), 0, S(stream), nbp, nbq,   \
+                                      p->u_nat, p->nspec, p->nacc, p->n_iter_mh, p->L,                                  \
                                       p->nchains, p->maxbins, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], \
                                       p->params, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi,            \
                                       IterArg{it, p->itp()}, p->chain0)
@@ -1644,7 +1699,7 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
     if (trace && capacity < 1) return set_error("gs_nc_decide_fused: capacity < 1");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const MhEpi epi{trace, std::max(capacity, 1), p->iter_dev_on ? p->iter_dev : nullptr, p->nchains};
-    return mh_decide(p, p->stats, dl, nullptr, slo, shi, it, accept_out, stream, &epi);
+    return mh_decide(p, p->stats, dl, p->u_nat_ready ? p->u_nat : nullptr, slo, shi, it, accept_out, stream, &epi);
 }
 
 int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
