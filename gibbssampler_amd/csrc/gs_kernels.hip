@@ -448,20 +448,26 @@ __global__ void k_stats_finish(int L, int nchains, int ntile, int nchunk, int tm
 // ============================================================================
 // centered C_l draw (CenteredGibbs.py:54-93) + TEB inverse-Wishart
 // ============================================================================
-// grid: (nchains, nspec); IG spectra one bin per thread
+// grid: (nchains, nspec, bin chunks of blockDim), one bin per thread (the
+// gamma draws are latency chains: one per thread, not a loop per thread).
+// Optional epilogue of graph-captured centered steps (as MhEpi): the trace
+// record of every bin and the device counter advance by the last workgroup.
 template <int F>
-__global__ __launch_bounds__(256) void k_cls_draw(int L, int nchains, int maxbins, const int* __restrict__ bins,
-                                                  const int* __restrict__ nbins_arr, const double* __restrict__ stats,
-                                                  const double* __restrict__ variates, uint32_t seed_lo,
-                                                  uint32_t seed_hi, IterArg itarg, int chain0,
-                                                  double* __restrict__ dl_out) {
-    const uint32_t iter = itarg.get();
+__device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __restrict__ bins,
+                                              const int* __restrict__ nbins_arr, const double* __restrict__ stats,
+                                              const double* __restrict__ variates, uint32_t seed_lo, uint32_t seed_hi,
+                                              uint32_t iter, int chain0, double* __restrict__ dl_out,
+                                              double* __restrict__ trace, int cap, int nchains) {
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
     const int chain = blockIdx.x;
     const int sp = blockIdx.y;
     const int Lp1 = L + 1;
     const int nb = nbins_arr[sp];
+    const int b = blockIdx.z * blockDim.x + threadIdx.x;
+    // trace slot of this iteration: trace[(iter - 1) % cap][chain][nspec][maxbins]
+    double* tr = trace ? trace + ((long long)((iter + (uint32_t)cap - 1u) % (uint32_t)cap) * nchains + chain) * NSP * maxbins
+                       : nullptr;
     const int* be = bins + sp * (maxbins + 1);
     const double* st = stats + (long long)chain * NS * Lp1;
     double* out = dl_out + ((long long)chain * NSP + sp) * maxbins;
@@ -471,7 +477,14 @@ __global__ __launch_bounds__(256) void k_cls_draw(int L, int nchains, int maxbin
     const bool iw = (F == 3) && (sp != 2);
     if (iw) {
         if (sp != 0) return;        // the TT block draws TT, EE and TE together
-        for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        if (b >= maxbins) return;
+        if (b >= nb) {
+            if (tr) { tr[0 * maxbins + b] = dl_out[((long long)chain * NSP + 0) * maxbins + b];
+                      tr[1 * maxbins + b] = dl_out[((long long)chain * NSP + 1) * maxbins + b];
+                      tr[3 * maxbins + b] = dl_out[((long long)chain * NSP + 3) * maxbins + b]; }
+            return;
+        }
+        {
             double nu = 0.0, a = 0.0, dd = 0.0, c = 0.0;
             for (int l = be[b]; l < be[b + 1]; ++l) {
                 const double w = (double)l * (l + 1) / (2.0 * PI);
@@ -501,10 +514,16 @@ __global__ __launch_bounds__(256) void k_cls_draw(int L, int nchains, int maxbin
             dl_out[((long long)chain * NSP + 0) * maxbins + b] = tt;
             dl_out[((long long)chain * NSP + 1) * maxbins + b] = ee;
             dl_out[((long long)chain * NSP + 3) * maxbins + b] = te;
+            if (tr) { tr[0 * maxbins + b] = tt; tr[1 * maxbins + b] = ee; tr[3 * maxbins + b] = te; }
         }
         return;
     }
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    if (b >= maxbins) return;
+    if (b >= nb) {
+        if (tr) tr[sp * maxbins + b] = out[b];
+        return;
+    }
+    {
         double beta = 0.0, expo = 0.0;
         for (int l = be[b]; l < be[b + 1]; ++l) {
             const double chat = st[ssrow * Lp1 + l] / (2.0 * l + 1.0);
@@ -516,8 +535,35 @@ __global__ __launch_bounds__(256) void k_cls_draw(int L, int nchains, int maxbin
         if (variates) X = variates[((long long)chain * NSP + sp) * maxbins + b];
         else X = b < 2 ? 0.0 : 1.0 / gamma_mt(alpha, key, b, sp, iter, 0);
         out[b] = b < 2 ? 0.0 : beta * X;
+        if (tr) tr[sp * maxbins + b] = out[b];
     }
 }
+
+template <int F>
+__global__ __launch_bounds__(64) void k_cls_draw(int L, int nchains, int maxbins, const int* __restrict__ bins,
+                                                 const int* __restrict__ nbins_arr, const double* __restrict__ stats,
+                                                 const double* __restrict__ variates, uint32_t seed_lo,
+                                                 uint32_t seed_hi, IterArg itarg, int chain0,
+                                                 double* __restrict__ dl_out, double* __restrict__ trace, int cap,
+                                                 uint32_t* __restrict__ counter) {
+    const uint32_t iter = itarg.get();
+    cls_draw_body<F>(L, maxbins, bins, nbins_arr, stats, variates, seed_lo, seed_hi, iter, chain0, dl_out, trace,
+                     cap, nchains);
+    if (counter) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            const uint32_t nblk = gridDim.x * gridDim.y * gridDim.z;
+            const uint32_t t = atomicAdd(&counter[1], 1u);
+            if (t == nblk - 1) {
+                counter[1] = 0u;
+                __threadfence();
+                atomicAdd(&counter[0], 1u);
+            }
+        }
+    }
+}
+
 
 // ============================================================================
 // non-centered Metropolis-within-Gibbs (NonCenteredGibbs.py:292-445)
@@ -1152,7 +1198,10 @@ void build_tasks(gs_plan* p) {
     // whatever the batch size or GPU count.  20-24 rows measured best at the
     // BASELINE size (tools/sweep_rows.py, interleaved in one process: sweep +
     // finish 264-267 us against 280-284 us at 32 rows, 271 us at 16)
-    int tm = 24;
+    // smaller l_max: fewer tasks per chain, so shorter ones keep the chip busy
+    // (single-chain configs[1], L = 512: 8 rows 42 us per step vs 57 us at 24);
+    // a function of L only, never of the chain count
+    int tm = L >= 1024 ? 24 : (L > 512 ? 16 : 8);
     if (const char* env = getenv("GS_SWEEP_ROWS")) {
         const int v = atoi(env);
         if (v >= 1 && v <= 1024) tm = v;
@@ -1508,17 +1557,24 @@ int gs_sweep_stats(gs_plan* p, const double* d_alm, const double* s, double* sta
     return sweep_launch(p, d_alm, nullptr, nullptr, 0, 0, 0, const_cast<double*>(s), stats, true, stream);
 }
 
-int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_t seed, uint32_t iteration,
-                double* dl_out, void* stream) {
+static int cls_draw_launch(gs_plan* p, const double* stats, const double* variates, uint64_t seed,
+                           uint32_t iteration, double* dl_out, double* trace, int cap, uint32_t* counter,
+                           void* stream) {
     if (check_plan(p)) return -1;
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    const dim3 g(p->nchains, p->nspec), b(256);
+    const dim3 g(p->nchains, p->nspec, (p->maxbins + 63) / 64), b(64);
 #define GS_CD(FF) hipLaunchKernelGGL((k_cls_draw<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
-                                     stats, variates, slo, shi, IterArg{iteration, p->itp()}, p->chain0, dl_out)
+                                     stats, variates, slo, shi, IterArg{iteration, p->itp()}, p->chain0, dl_out, trace, \
+                                     cap, counter)
     if (p->F == 1) GS_CD(1); else if (p->F == 2) GS_CD(2); else GS_CD(3);
 #undef GS_CD
     GS_LAUNCH_CHECK("k_cls_draw");
     return 0;
+}
+
+int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_t seed, uint32_t iteration,
+                double* dl_out, void* stream) {
+    return cls_draw_launch(p, stats, variates, seed, iteration, dl_out, nullptr, 1, nullptr, stream);
 }
 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
@@ -1651,6 +1707,16 @@ int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out,
     if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
     if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
     return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
+}
+
+int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed, uint32_t it,
+                           double* trace, int capacity, void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->iter_dev_on) return set_error("gs_step_centered_fused: device iteration counter not enabled");
+    if (trace && capacity < 1) return set_error("gs_step_centered_fused: capacity < 1");
+    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
+    if (gs_cr_sweep(p, d_alm, p->params, nullptr, seed, it, 0, s_out, p->stats, stream)) return -1;
+    return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->iter_dev, stream);
 }
 
 int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t it, void* stream) {

@@ -230,6 +230,12 @@ class GibbsPlan:
         C.check(self.lib.gs_step_centered(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), C.ptr(z), C.ptr(igvar),
                                           int(seed), int(iteration), self._s()), "gs_step_centered")
 
+    def step_centered_fused(self, d, dl, s_out, seed=0, iteration=0, trace=None, capacity=0):
+        """gs_step_centered with the trace record and device-counter advance in the
+        C_l-draw launch (graph-captured native steps)."""
+        C.check(self.lib.gs_step_centered_fused(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), int(seed), int(iteration),
+                                                C.ptr(trace), int(capacity), self._s()), "gs_step_centered_fused")
+
     def step_noncentered(self, d, dl, s_out, z=None, u_prop=None, u_acc=None, seed=0, iteration=0, accept=None):
         C.check(self.lib.gs_step_noncentered(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), C.ptr(z), C.ptr(u_prop),
                                              C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept), self._s()),

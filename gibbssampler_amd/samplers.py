@@ -89,6 +89,10 @@ class BatchedRunner:
                 p.nc_sweep(self.d, self.s, seed=self.seed)
                 p.nc_decide_fused(self.dl, seed=self.seed, accept=self.accept, trace=trace,
                                   capacity=trace_capacity or 0)
+            elif self.kind == "centered":
+                # centered: the trace record and the counter advance ride in the C_l draw
+                p.step_centered_fused(self.d, self.dl, self.s, seed=self.seed, trace=trace,
+                                      capacity=trace_capacity or 0)
             else:
                 self._launch_step(0)
                 if trace is not None:

@@ -139,6 +139,11 @@ int gs_recentre(gs_plan* plan, const double* dl_new, const double* dl_old, doubl
 int gs_step_centered(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
                      const double* z_replay, const double* invgamma_replay,
                      uint64_t seed, uint32_t iteration, void* stream);
+/* native RNG, device iteration counter on (graph-captured steps): gs_step_centered
+ * with the D_l trace record (trace nullable: [capacity][nchains][nspec][maxbins],
+ * slot (iteration - 1) % capacity) and the counter advance in the C_l-draw launch */
+int gs_step_centered_fused(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
+                           uint64_t seed, uint32_t iteration, double* trace, int capacity, void* stream);
 int gs_step_noncentered(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
                         const double* z_replay, const double* u_prop_replay, const double* u_accept_replay,
                         uint64_t seed, uint32_t iteration, int32_t* accept_out, void* stream);

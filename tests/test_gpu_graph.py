@@ -1,7 +1,8 @@
 """GPU: hipGraph-captured steps (samplers.BatchedRunner.capture_graph) give
 bit-identical chains to eager steps -- the NC graph fuses the trace record
-and the counter advance into the MH decision launch; centered and ASIS graphs
-keep their launch sequence plus trace and advance."""
+and the counter advance into the MH decision launch, the centered graph into
+the C_l-draw launch (gs_step_centered_fused); ASIS graphs keep their launch
+sequence plus trace and advance."""
 import numpy as np
 import pytest
 
@@ -20,7 +21,7 @@ def _runner(kind, F, nchains=4):
 
 
 @pytest.mark.parametrize("kind,F", [("noncentered", 3), ("noncentered", 2), ("noncentered", 1),
-                                    ("centered", 3), ("asis", 2)])
+                                    ("centered", 3), ("centered", 2), ("centered", 1), ("asis", 2)])
 def test_graph_equals_eager(kind, F):
     import torch
     n, w = 6, 2
