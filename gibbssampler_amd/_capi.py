@@ -89,6 +89,8 @@ _SIGS = [
     ("gs_stats_to_noncentered", ctypes.c_int, [_VP, _VP, _VP, _VP]),
     ("gs_recentre", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     ("gs_step_centered", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP]),
+    ("gs_step_asis_fused", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP, ctypes.c_int,
+                                          _VP, ctypes.c_int, _VP]),
     ("gs_step_centered_fused", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, ctypes.c_int,
                                               _VP]),
     ("gs_step_noncentered", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,

@@ -1796,6 +1796,39 @@ int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, con
     return 0;
 }
 
+int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed, uint32_t it,
+                       int32_t* accept_out, double* dl_tmp_out, int recentre, double* trace, int capacity,
+                       void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->iter_dev_on) return set_error("gs_step_asis_fused: device iteration counter not enabled");
+    if (!p->has_mh) return set_error("gs_step_asis_fused: plan has no MH blocks / proposal variances");
+    if (trace && capacity < 1) return set_error("gs_step_asis_fused: capacity < 1");
+    double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
+    if (gs_cr_sweep(p, d_alm, p->params, nullptr, seed, it, 0, s_out, p->stats, stream)) return -1;
+    if (gs_cls_draw(p, p->stats, nullptr, seed, it, tmp, stream)) return -1;
+    if (gs_stats_to_noncentered(p, tmp, p->stats, stream)) return -1;
+    const size_t bytes = (size_t)p->nchains * p->nspec * p->maxbins * sizeof(double);
+    GS_CHECK(hipMemcpyAsync(dl, tmp, bytes, hipMemcpyDeviceToDevice, S(stream)));
+    const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
+#define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
+                                     p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, nullptr, slo, shi,        \
+                                     IterArg{it, p->itp()}, p->chain0)
+    if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
+#undef GS_MP
+    GS_LAUNCH_CHECK("k_mh_propose");
+    // the trace record and the counter advance ride in the MH launch (no kernel
+    // after it reads the counter: the re-centring uses D_l only)
+    const MhEpi epi{trace, trace ? capacity : 1, p->iter_dev, p->nchains};
+    if (mh_decide(p, p->stats, dl, nullptr, slo, shi, it, accept_out, stream, &epi)) return -1;
+    if (recentre && s_out) {
+        const bool quirk = (p->quirks & GS_QUIRK_ASIS_RECENTRE_CENTERED) != 0;
+        if (gs_recentre(p, dl, quirk ? nullptr : tmp, s_out, stream)) return -1;
+    }
+    return 0;
+}
+
 int gs_iteration_counter(gs_plan* p, int enable, uint32_t start) {
     if (check_plan(p)) return -1;
     p->iter_dev_on = enable != 0;

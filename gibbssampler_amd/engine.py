@@ -236,6 +236,13 @@ class GibbsPlan:
         C.check(self.lib.gs_step_centered_fused(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), int(seed), int(iteration),
                                                 C.ptr(trace), int(capacity), self._s()), "gs_step_centered_fused")
 
+    def step_asis_fused(self, d, dl, s_out, seed=0, iteration=0, accept=None, dl_tmp=None, recentre=False,
+                        trace=None, capacity=0):
+        """gs_step_asis with the trace record and device-counter advance in the MH launch."""
+        C.check(self.lib.gs_step_asis_fused(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), int(seed), int(iteration),
+                                            C.ptr(accept), C.ptr(dl_tmp), 1 if recentre else 0, C.ptr(trace),
+                                            int(capacity), self._s()), "gs_step_asis_fused")
+
     def step_noncentered(self, d, dl, s_out, z=None, u_prop=None, u_acc=None, seed=0, iteration=0, accept=None):
         C.check(self.lib.gs_step_noncentered(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), C.ptr(z), C.ptr(u_prop),
                                              C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept), self._s()),

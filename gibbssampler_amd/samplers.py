@@ -94,10 +94,9 @@ class BatchedRunner:
                 p.step_centered_fused(self.d, self.dl, self.s, seed=self.seed, trace=trace,
                                       capacity=trace_capacity or 0)
             else:
-                self._launch_step(0)
-                if trace is not None:
-                    p.record_trace(self.dl, trace, trace_capacity)
-                p.advance_iteration()
+                # ASIS: the trace record and the counter advance ride in the MH launch
+                p.step_asis_fused(self.d, self.dl, self.s, seed=self.seed, accept=self.accept, dl_tmp=self.dl_tmp,
+                                  recentre=self.materialize_recentre, trace=trace, capacity=trace_capacity or 0)
         self.graph = g
         self.graph_steps = 1
         return g

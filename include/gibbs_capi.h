@@ -144,6 +144,10 @@ int gs_step_centered(gs_plan* plan, const double* d_alm, double* dl_binned, doub
  * slot (iteration - 1) % capacity) and the counter advance in the C_l-draw launch */
 int gs_step_centered_fused(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
                            uint64_t seed, uint32_t iteration, double* trace, int capacity, void* stream);
+/* the same for gs_step_asis (native): trace record and counter advance in the MH launch */
+int gs_step_asis_fused(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
+                       uint64_t seed, uint32_t iteration, int32_t* accept_out, double* dl_tmp_out, int recentre,
+                       double* trace, int capacity, void* stream);
 int gs_step_noncentered(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
                         const double* z_replay, const double* u_prop_replay, const double* u_accept_replay,
                         uint64_t seed, uint32_t iteration, int32_t* accept_out, void* stream);

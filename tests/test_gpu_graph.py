@@ -1,8 +1,8 @@
 """GPU: hipGraph-captured steps (samplers.BatchedRunner.capture_graph) give
 bit-identical chains to eager steps -- the NC graph fuses the trace record
 and the counter advance into the MH decision launch, the centered graph into
-the C_l-draw launch (gs_step_centered_fused); ASIS graphs keep their launch
-sequence plus trace and advance."""
+the C_l-draw launch (gs_step_centered_fused), the ASIS graph into its MH
+launch (gs_step_asis_fused)."""
 import numpy as np
 import pytest
 
@@ -21,7 +21,7 @@ def _runner(kind, F, nchains=4):
 
 
 @pytest.mark.parametrize("kind,F", [("noncentered", 3), ("noncentered", 2), ("noncentered", 1),
-                                    ("centered", 3), ("centered", 2), ("centered", 1), ("asis", 2)])
+                                    ("centered", 3), ("centered", 2), ("centered", 1), ("asis", 2), ("asis", 3)])
 def test_graph_equals_eager(kind, F):
     import torch
     n, w = 6, 2
