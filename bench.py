@@ -43,9 +43,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
-    ap.add_argument("--timing-launches", type=int, default=20,
-                    help="eager steps after the timed loop whose sweep launches are timed with hipEvents")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph of the timed steps")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     masked = a.workload == "masked"
@@ -97,16 +95,12 @@ def main():
     traces = [p.zeros(args.steps, p.nchains, p.nspec, p.maxbins) for p in plans]
     for _ in range(args.warmup):
         runner.step()
-    use_graph = not args.no_graph
-    one_graph = use_graph and args.workload == "noncentered"
+    one_graph = not args.no_graph
     if one_graph:
         # the K timed iterations as ONE hipGraph (D_l trace written on the device);
         # every CR-sweep kernel is bracketed by event-record nodes inside the graph,
         # so its duration is measured on its stream over the timed region itself
         runner.capture_steps(args.steps, trace=traces[0], trace_capacity=args.steps, time_sweeps=True)
-    elif use_graph:
-        # one hipGraph per Gibbs iteration: the D_l trace is written on the device
-        runner.capture_graph(trace=traces[0], trace_capacity=args.steps)
     else:
         for p in plans:
             p.sweep_timing(True)        # events around every sweep launch of the timed loop
@@ -120,31 +114,15 @@ def main():
     else:
         for i in range(args.steps):
             runner.step()
-            if not use_graph:
-                traces[0][i].copy_(runner.dl)
+            traces[0][i].copy_(runner.dl)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
     elapsed = t1 - t0
-    if one_graph:
-        timed = [p.sweep_timing(False) for p in plans]
-        timing_mode = "hipEvents around each sweep inside the timed graph"
-    elif not use_graph:
-        timed = [p.sweep_timing(False) for p in plans]
-        timing_mode = "hipEvents around each sweep of the timed loop"
-    else:
-        # per-iteration graphs of the centered / ASIS steps: time the sweep launches of
-        # eager steps of the same state right after the timed loop
-        runner.graph = None
-        plans[0].iteration_counter(False)
-        for p in plans:
-            p.sweep_timing(True)
-        for _ in range(args.timing_launches):
-            runner.step()
-        torch.cuda.synchronize()
-        timed = [p.sweep_timing(False) for p in plans]
-        timing_mode = "hipEvents around the sweeps of eager steps after the timed loop"
+    timed = [p.sweep_timing(False) for p in plans]
+    timing_mode = ("hipEvents around each sweep inside the timed graph" if one_graph else
+                   "hipEvents around each sweep of the timed loop")
     trace = torch.cat(traces, 1)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -193,8 +171,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (analytic fiducial spectra, d = b s + n in harmonic space, seed 0)",
             "config": {"workload": f"{args.workload} TEB all_sph full-sky" if args.fields == 3 else args.workload,
-                       "launch": ("one hipGraph of all timed iterations" if one_graph else
-                                  "hipGraph per iteration" if use_graph else "eager"),
+                       "launch": "one hipGraph of all timed iterations" if one_graph else "eager",
                        "nside": args.nside, "lmax": args.lmax, "nfields": args.fields,
                        "chains_per_gpu": args.nchains, "global_chains": args.nchains * world,
                        "rng": "native philox4x32-10", "parallelism": f"chains sharded over {world} GPU(s)"},

@@ -102,12 +102,12 @@ class BatchedRunner:
         return g
 
     def capture_steps(self, nsteps, trace=None, trace_capacity=None, time_sweeps=False):
-        """NonCentered, native RNG: capture ``nsteps`` whole iterations in ONE hipGraph
-        (one replay = nsteps steps).  time_sweeps: bracket every CR-sweep kernel by
+        """Native RNG: capture ``nsteps`` whole iterations in ONE hipGraph (one
+        replay = nsteps steps).  time_sweeps: bracket every CR-sweep kernel by
         event-record nodes (plan.sweep_timing), so the sweep's duration is measured
         on its own stream inside the replay; collect with plan.sweep_timing(False)."""
-        if self.kind != "noncentered" or self.rng != "native":
-            raise ValueError("capture_steps: native NonCentered runs only")
+        if self.rng != "native":
+            raise ValueError("capture_steps: native RNG runs only")
         p = self.plan
         p.iteration_counter(True, self.iteration + 1)
         torch.cuda.synchronize()
@@ -116,11 +116,19 @@ class BatchedRunner:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for i in range(nsteps):
-                p.nc_prologue(self.dl, seed=self.seed)
-                p.nc_sweep(self.d, self.s, seed=self.seed, finish=False)
-                p.nc_finish()
-                p.nc_decide_fused(self.dl, seed=self.seed, accept=self.accept, trace=trace,
-                                  capacity=trace_capacity or 0)
+                if self.kind == "noncentered":
+                    p.nc_prologue(self.dl, seed=self.seed)
+                    p.nc_sweep(self.d, self.s, seed=self.seed, finish=False)
+                    p.nc_finish()
+                    p.nc_decide_fused(self.dl, seed=self.seed, accept=self.accept, trace=trace,
+                                      capacity=trace_capacity or 0)
+                elif self.kind == "centered":
+                    p.step_centered_fused(self.d, self.dl, self.s, seed=self.seed, trace=trace,
+                                          capacity=trace_capacity or 0)
+                else:
+                    p.step_asis_fused(self.d, self.dl, self.s, seed=self.seed, accept=self.accept,
+                                      dl_tmp=self.dl_tmp, recentre=self.materialize_recentre, trace=trace,
+                                      capacity=trace_capacity or 0)
         self.graph = g
         self.graph_steps = nsteps
         return g

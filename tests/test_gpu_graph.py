@@ -58,18 +58,18 @@ def test_graph_equals_eager(kind, F):
     np.testing.assert_array_equal(g.dl.cpu().numpy(), eager.dl.cpu().numpy())
 
 
-@pytest.mark.parametrize("F", [3, 2])
-def test_multistep_graph_with_sweep_timing(F):
-    """bench.py's timed region: K NC iterations in ONE graph with the sweeps
+@pytest.mark.parametrize("kind,F", [("noncentered", 3), ("noncentered", 2), ("centered", 3), ("asis", 3)])
+def test_multistep_graph_with_sweep_timing(kind, F):
+    """bench.py's timed region: K iterations in ONE graph with the sweeps
     bracketed by captured event nodes -- same chains as eager, K timings."""
     import torch
     n, w = 5, 2
-    eager = _runner("noncentered", F)
+    eager = _runner(kind, F)
     want = []
     for _ in range(w + n):
         eager.step()
         want.append(eager.dl.cpu().numpy().copy())
-    g = _runner("noncentered", F)
+    g = _runner(kind, F)
     for _ in range(w):
         g.step()
     p = g.plan
