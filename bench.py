@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph of the timed steps")
+    ap.add_argument("--time-every", type=int, default=1,
+                    help="bracket the CR sweep of every N-th timed step with hipEvents (graph mode)")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     masked = a.workload == "masked"
@@ -100,7 +102,9 @@ def main():
         # the K timed iterations as ONE hipGraph (D_l trace written on the device);
         # every CR-sweep kernel is bracketed by event-record nodes inside the graph,
         # so its duration is measured on its stream over the timed region itself
-        runner.capture_steps(args.steps, trace=traces[0], trace_capacity=args.steps, time_sweeps=True)
+        # (--time-every N brackets only every N-th sweep: an event node costs ~5 us)
+        runner.capture_steps(args.steps, trace=traces[0], trace_capacity=args.steps, time_sweeps=True,
+                             time_every=args.time_every)
     else:
         for p in plans:
             p.sweep_timing(True)        # events around every sweep launch of the timed loop

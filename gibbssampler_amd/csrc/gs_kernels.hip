@@ -1504,9 +1504,13 @@ static int record_ev(hipEvent_t e, hipStream_t s) {
 static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e1) {
     if (!p->timing) return 0;
     if (p->ev_used + 2 > p->ev.size()) {
+        // timing-only events: no system-scope fence at record (a fence per
+        // record writes back and invalidates the caches -- ~6 us between the
+        // graph's kernels and a slower next kernel); read after a device sync
+        static const bool fence = getenv("GS_TIMING_EVENT_FENCE") != nullptr;
         for (int k = 0; k < 64; ++k) {
             hipEvent_t e;
-            GS_CHECK(hipEventCreate(&e));
+            GS_CHECK(fence ? hipEventCreate(&e) : hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
             p->ev.push_back(e);
         }
     }
@@ -1856,6 +1860,10 @@ int gs_record_trace(gs_plan* p, const double* dl, double* trace, int capacity, u
 
 int gs_sweep_timing(gs_plan* p, int enable, double* total_ms, int* count) {
     if (check_plan(p)) return -1;
+    if (enable == 2 || enable == 3) {           // pause / resume, keeping the launches timed so far
+        p->timing = enable == 3;
+        return 0;
+    }
     if (enable) {
         p->timing = true;
         p->ev_used = 0;

@@ -287,9 +287,12 @@ class GibbsPlan:
 
     # ---- timing of the dominant kernel (hipEvents on the launch stream) ---------------
     def sweep_timing(self, enable):
+        """True: start bracketing every CR sweep with hipEvents; False: stop and
+        return (total ms, launches); "pause" / "resume" keep the launches timed so far."""
+        mode = {True: 1, False: 0, "pause": 2, "resume": 3}[enable]
         tot = ctypes.c_double()
         n = ctypes.c_int()
-        C.check(self.lib.gs_sweep_timing(self._h, 1 if enable else 0, ctypes.byref(tot), ctypes.byref(n)))
+        C.check(self.lib.gs_sweep_timing(self._h, mode, ctypes.byref(tot), ctypes.byref(n)))
         return tot.value, n.value
 
 

@@ -101,11 +101,12 @@ class BatchedRunner:
         self.graph_steps = 1
         return g
 
-    def capture_steps(self, nsteps, trace=None, trace_capacity=None, time_sweeps=False):
+    def capture_steps(self, nsteps, trace=None, trace_capacity=None, time_sweeps=False, time_every=1):
         """Native RNG: capture ``nsteps`` whole iterations in ONE hipGraph (one
-        replay = nsteps steps).  time_sweeps: bracket every CR-sweep kernel by
-        event-record nodes (plan.sweep_timing), so the sweep's duration is measured
-        on its own stream inside the replay; collect with plan.sweep_timing(False)."""
+        replay = nsteps steps).  time_sweeps: bracket the CR-sweep kernel of every
+        ``time_every``-th step by event-record nodes (plan.sweep_timing), so the
+        sweep's duration is measured on its own stream inside the replay (an event
+        node costs ~5 us of the step); collect with plan.sweep_timing(False)."""
         if self.rng != "native":
             raise ValueError("capture_steps: native RNG runs only")
         p = self.plan
@@ -116,6 +117,8 @@ class BatchedRunner:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for i in range(nsteps):
+                if time_sweeps:
+                    p.sweep_timing("resume" if i % time_every == 0 else "pause")
                 if self.kind == "noncentered":
                     p.nc_prologue(self.dl, seed=self.seed)
                     p.nc_sweep(self.d, self.s, seed=self.seed, finish=False)

@@ -193,6 +193,7 @@ int gs_record_trace(gs_plan* plan, const double* dl_binned, double* trace, int c
 /* device-side timing of the dominant kernel: with enable = 1 every later CR-sweep
  * launch is bracketed by hipEvents on its stream (also while the stream is
  * captured into a hipGraph: external event-record nodes, timed at each replay);
+ * enable = 2 / 3 pause / resume (launches in between are not bracketed);
  * enable = 0 returns the summed duration and the number of launches timed */
 int gs_sweep_timing(gs_plan* plan, int enable, double* total_ms, int* count);
 

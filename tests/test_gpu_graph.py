@@ -74,11 +74,11 @@ def test_multistep_graph_with_sweep_timing(kind, F):
         g.step()
     p = g.plan
     trace = p.zeros(n, p.nchains, p.nspec, p.maxbins)
-    g.capture_steps(n, trace=trace, trace_capacity=n, time_sweeps=True)
+    g.capture_steps(n, trace=trace, trace_capacity=n, time_sweeps=True, time_every=2)
     g.step()
     torch.cuda.synchronize()
     ms, cnt = p.sweep_timing(False)
-    assert cnt == n and ms > 0
+    assert cnt == (n + 1) // 2 and ms > 0
     tr = trace.cpu().numpy()
     for k in range(n):
         it = w + 1 + k
