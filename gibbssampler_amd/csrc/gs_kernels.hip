@@ -284,7 +284,20 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
 #pragma unroll
         for (int f = 0; f < F; ++f)
 #pragma unroll
-            for (int c = 0; c < NV; ++c) __builtin_nontemporal_store(sv[f][c], &sc[f * NR + r + c]);
+            for (int c = 0; c < NV; ++c) {
+#if defined(GS_EXPERIMENT_LINE_ALIGNED_WRONG)
+                // timing experiment only (wrong data): every wave store realigned to a 128-B line
+                double* q = &sc[f * NR + r + c];
+                if (NV == 2) {
+                    const uintptr_t a = reinterpret_cast<uintptr_t>(&sc[f * NR + r]);
+                    const uintptr_t a0 = __builtin_amdgcn_readfirstlane((unsigned)(a & 0xFFFFFFFFu)) & 127u;
+                    q = q - (a0 >> 3);
+                }
+                __builtin_nontemporal_store(sv[f][c], q);
+#else
+                __builtin_nontemporal_store(sv[f][c], &sc[f * NR + r + c]);
+#endif
+            }
     }
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
