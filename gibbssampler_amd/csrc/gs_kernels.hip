@@ -181,8 +181,6 @@ __global__ void k_alm2cl(int L, int n, const double* __restrict__ x, const doubl
 
 __global__ void k_unfold(int n, const double* __restrict__ binned, const int* __restrict__ bins, int nbins,
                          double* __restrict__ out) {
-    const int Lp1 = 0;
-    (void)Lp1;
     const int k = blockIdx.y;
     for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
         const double v = binned[(long long)k * nbins + b];
