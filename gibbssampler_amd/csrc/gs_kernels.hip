@@ -1433,7 +1433,16 @@ int gs_plan_sweep_info(const gs_plan* p, int* ntask, int* rows_per_task) {
 }
 
 // ---- stand-alone helpers ----------------------------------------------------
+// stateless helpers: lmax >= 0, n >= 0 (n == 0: nothing to do), non-null buffers
+static int check_lmax_n(const char* fn, int lmax, int n, const void* a, const void* b) {
+    if (lmax < 0 || n < 0) return set_error(std::string(fn) + ": lmax / n out of range");
+    if (n > 0 && (!a || !b)) return set_error(std::string(fn) + ": null argument");
+    return 0;
+}
+
 int gs_var_expand(int lmax, int n, const double* dl, double* var, void* stream) {
+    if (check_lmax_n("gs_var_expand", lmax, n, dl, var)) return -1;
+    if (n == 0) return 0;
     const long long nc = (long long)(lmax + 1) * (lmax + 2) / 2 * n;
     hipLaunchKernelGGL(k_var_expand, dim3(nblk(nc, 256)), dim3(256), 0, S(stream), lmax, n, dl, var);
     GS_LAUNCH_CHECK("k_var_expand");
@@ -1441,6 +1450,8 @@ int gs_var_expand(int lmax, int n, const double* dl, double* var, void* stream) 
 }
 
 int gs_real_to_complex(int lmax, int n, const double* re, double* cx, void* stream) {
+    if (check_lmax_n("gs_real_to_complex", lmax, n, re, cx)) return -1;
+    if (n == 0) return 0;
     const long long nc = (long long)(lmax + 1) * (lmax + 2) / 2 * n;
     hipLaunchKernelGGL(k_real_to_complex, dim3(nblk(nc, 256)), dim3(256), 0, S(stream), lmax, n, re, cx);
     GS_LAUNCH_CHECK("k_real_to_complex");
@@ -1448,6 +1459,8 @@ int gs_real_to_complex(int lmax, int n, const double* re, double* cx, void* stre
 }
 
 int gs_complex_to_real(int lmax, int n, const double* cx, double* re, void* stream) {
+    if (check_lmax_n("gs_complex_to_real", lmax, n, cx, re)) return -1;
+    if (n == 0) return 0;
     const long long nc = (long long)(lmax + 1) * (lmax + 2) / 2 * n;
     hipLaunchKernelGGL(k_complex_to_real, dim3(nblk(nc, 256)), dim3(256), 0, S(stream), lmax, n, cx, re);
     GS_LAUNCH_CHECK("k_complex_to_real");
@@ -1455,12 +1468,16 @@ int gs_complex_to_real(int lmax, int n, const double* cx, double* re, void* stre
 }
 
 int gs_remove_monopole_dipole(int lmax, int n, double* alm, void* stream) {
+    if (check_lmax_n("gs_remove_monopole_dipole", lmax, n, alm, alm)) return -1;
+    if (n == 0) return 0;
     hipLaunchKernelGGL(k_remove_md, dim3(nblk(n, 64)), dim3(64), 0, S(stream), lmax, n, alm);
     GS_LAUNCH_CHECK("k_remove_md");
     return 0;
 }
 
 int gs_alm2cl(int lmax, int n, const double* x, const double* y, double* cl, void* stream) {
+    if (check_lmax_n("gs_alm2cl", lmax, n, x, cl)) return -1;
+    if (n == 0) return 0;
     const int ntile = (lmax + WAVE) / WAVE;
     const long long waves = (long long)n * ntile;
     hipLaunchKernelGGL(k_alm2cl, dim3(nblk(waves, 4)), dim3(256), 0, S(stream), lmax, n, x, y ? y : x, cl);
@@ -1469,6 +1486,9 @@ int gs_alm2cl(int lmax, int n, const double* x, const double* y, double* cl, voi
 }
 
 int gs_unfold_bins(int n, const double* binned, const int* bins, int nbins, double* out, void* stream) {
+    if (n < 0 || nbins < 0) return set_error("gs_unfold_bins: n / nbins out of range");
+    if (n == 0 || nbins == 0) return 0;
+    if (!binned || !bins || !out) return set_error("gs_unfold_bins: null argument");
     hipLaunchKernelGGL(k_unfold, dim3(nblk(nbins, 256), n), dim3(256), 0, S(stream), n, binned, bins, nbins, out);
     GS_LAUNCH_CHECK("k_unfold");
     return 0;
@@ -1477,6 +1497,7 @@ int gs_unfold_bins(int n, const double* binned, const int* bins, int nbins, doub
 // ---- plan stages -----------------------------------------------------------------
 int gs_block_params(gs_plan* p, int mode, const double* dl, double* params, void* stream) {
     if (check_plan(p)) return -1;
+    if (!dl || !params) return set_error("gs_block_params: null argument");
     const long long n = (long long)p->nchains * (p->L + 1);
     const dim3 g(nblk(n, 256)), b(256);
 #define GS_BP(FF, MM) hipLaunchKernelGGL((k_block_params<FF, MM>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, dl, \
@@ -1577,6 +1598,7 @@ static int cls_draw_launch(gs_plan* p, const double* stats, const double* variat
                            uint32_t iteration, double* dl_out, double* trace, int cap, uint32_t* counter,
                            void* stream) {
     if (check_plan(p)) return -1;
+    if (!stats || !dl_out) return set_error("gs_cls_draw: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const dim3 g(p->nchains, p->nspec, (p->maxbins + 63) / 64), b(64);
 #define GS_CD(FF) hipLaunchKernelGGL((k_cls_draw<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
@@ -1625,6 +1647,7 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
              uint32_t iteration, int32_t* accept_out, void* stream) {
     if (check_plan(p)) return -1;
     if (!p->has_mh) return set_error("gs_nc_mh: plan has no MH blocks / proposal variances");
+    if (!stats || !dl) return set_error("gs_nc_mh: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
 #if defined(GS_ABL_MH_NOPROPOSE)
@@ -1699,6 +1722,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
 
 int gs_stats_to_noncentered(gs_plan* p, const double* dl, double* stats, void* stream) {
     if (check_plan(p)) return -1;
+    if (!dl || !stats) return set_error("gs_stats_to_noncentered: null argument");
     const long long n = (long long)p->nchains * (p->L + 1);
 #define GS_TN(FF) hipLaunchKernelGGL((k_stats_to_nc<FF>), dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, \
                                      p->maxbins, dl, p->ell2bin, stats)
@@ -1710,6 +1734,7 @@ int gs_stats_to_noncentered(gs_plan* p, const double* dl, double* stats, void* s
 
 int gs_recentre(gs_plan* p, const double* dl_new, const double* dl_old, double* s, void* stream) {
     if (check_plan(p)) return -1;
+    if (!dl_new || !s) return set_error("gs_recentre: null argument");
     const long long n = (long long)p->nchains * (p->L + 1) * (p->L + 2) / 2;
 #define GS_RC(FF) hipLaunchKernelGGL((k_recentre<FF>), dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, \
                                      p->maxbins, dl_new, dl_old, p->ell2bin, s)
@@ -1722,6 +1747,7 @@ int gs_recentre(gs_plan* p, const double* dl_new, const double* dl_old, double* 
 // ---- fused iterations ------------------------------------------------------
 int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
                      const double* igvar, uint64_t seed, uint32_t it, void* stream) {
+    if (check_plan(p)) return -1;
     if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
     if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
     return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
@@ -1740,6 +1766,7 @@ int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* 
 int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t it, void* stream) {
     if (check_plan(p)) return -1;
     if (!p->has_mh) return set_error("gs_nc_prologue: plan has no MH blocks / proposal variances");
+    if (!dl) return set_error("gs_nc_prologue: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const int nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
     const int nbq = nblk((long long)p->nchains * (p->L + 1), 256);
@@ -1772,6 +1799,7 @@ int gs_nc_decide(gs_plan* p, double* dl, const double* u_acc, uint64_t seed, uin
                  void* stream) {
     if (check_plan(p)) return -1;
     if (!p->has_mh) return set_error("gs_nc_decide: plan has no MH blocks / proposal variances");
+    if (!dl) return set_error("gs_nc_decide: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     return mh_decide(p, p->stats, dl, u_acc, slo, shi, it, accept_out, stream);
 }
@@ -1780,6 +1808,7 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
                        int capacity, void* stream) {
     if (check_plan(p)) return -1;
     if (!p->has_mh) return set_error("gs_nc_decide_fused: plan has no MH blocks / proposal variances");
+    if (!dl) return set_error("gs_nc_decide_fused: null argument");
     if (trace && capacity < 1) return set_error("gs_nc_decide_fused: capacity < 1");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const MhEpi epi{trace, std::max(capacity, 1), p->iter_dev_on ? p->iter_dev : nullptr, p->nchains};
@@ -1797,6 +1826,7 @@ int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_o
 int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z, const double* igvar,
                  const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
                  double* dl_tmp_out, int recentre, void* stream) {
+    if (check_plan(p)) return -1;
     double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
     if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
     if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
@@ -1865,6 +1895,7 @@ int gs_advance_iteration(gs_plan* p, void* stream) {
 int gs_record_trace(gs_plan* p, const double* dl, double* trace, int capacity, uint32_t iteration, void* stream) {
     if (check_plan(p)) return -1;
     if (capacity < 1) return set_error("gs_record_trace: capacity < 1");
+    if (!dl || !trace) return set_error("gs_record_trace: null argument");
     const long long n = (long long)p->nchains * p->nspec * p->maxbins;
     hipLaunchKernelGGL(k_record_trace, dim3(nblk(n, 256)), dim3(256), 0, S(stream), n, dl, trace, capacity,
                        IterArg{iteration, p->itp()});

@@ -827,6 +827,7 @@ int gs_masked_info(const gs_masked* c, double* mu3, double* second_part_grad) {
 
 int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, void* stream) {
     if (!c) return set_error("null masked context");
+    if (!dl || !s || !grad || !pix) return set_error("gs_masked_gradient: null argument");
     return mc_gradient(c, dl, s, grad, pix, S(stream));
 }
 

@@ -51,3 +51,63 @@ def test_abi_version_and_error_channel(lib):
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(_capi.GibbsHipError):
         _capi.load(str(tmp_path / "nope.so"))
+
+
+def _zero_args(argtypes):
+    ints = (ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_longlong)
+    return [0 if t in ints else (0.0 if t is ctypes.c_double else None) for t in argtypes]
+
+
+def test_null_handles_are_errors_not_crashes(lib):
+    """Every entry point taking a plan, SHT plan or masked context rejects a
+    NULL handle with -1 and a message before any HIP call (the reference
+    raises a Python exception where these return a status)."""
+    lib2 = _capi.load()
+    checked = 0
+    for name, _, argtypes in _capi._SIGS:
+        if not argtypes or argtypes[0] is not ctypes.c_void_p or name.endswith("_destroy"):
+            continue
+        rc = getattr(lib2, name)(*_zero_args(argtypes))
+        assert rc == -1, name
+        assert b"null" in lib2.gs_last_error(), (name, lib2.gs_last_error())
+        checked += 1
+    assert checked >= 30
+    for name in ("gs_plan_destroy", "gs_sht_destroy", "gs_masked_destroy"):
+        assert getattr(lib2, name)(None) == 0          # destroying NULL is a no-op
+
+
+def test_stateless_helpers_validate_before_launch(lib):
+    """Sizes and buffers are checked before any launch; an empty batch is a
+    no-op (no kernel, no GPU needed)."""
+    lib2 = _capi.load()
+    for name in ("gs_var_expand", "gs_real_to_complex", "gs_complex_to_real"):
+        fn = getattr(lib2, name)
+        assert fn(-1, 1, None, None, None) == -1
+        assert b"out of range" in lib2.gs_last_error()
+        assert fn(8, 1, None, None, None) == -1
+        assert b"null" in lib2.gs_last_error()
+        assert fn(8, 0, None, None, None) == 0
+    assert lib2.gs_remove_monopole_dipole(8, 0, None, None) == 0
+    assert lib2.gs_remove_monopole_dipole(8, -2, None, None) == -1
+    assert lib2.gs_alm2cl(8, 0, None, None, None, None) == 0
+    assert lib2.gs_alm2cl(8, 2, None, None, None, None) == -1
+    assert lib2.gs_unfold_bins(0, None, None, 5, None, None) == 0
+    assert lib2.gs_unfold_bins(2, None, None, 5, None, None) == -1
+    assert lib2.gs_synalm(-1, 3, None, None, None, None, None) == -1
+
+
+def test_create_rejects_bad_sizes(lib):
+    lib2 = _capi.load()
+    out = ctypes.c_void_p()
+    assert lib2.gs_plan_create(None, ctypes.byref(out)) == -1
+    d = _capi.GsModelDesc()
+    for lmax, nf, nch, msg in ((1, 3, 1, b"lmax"), (64, 4, 1, b"nfields"), (64, 3, 0, b"nchains")):
+        d.lmax, d.nfields, d.nchains = lmax, nf, nch
+        assert lib2.gs_plan_create(ctypes.byref(d), ctypes.byref(out)) == -1
+        assert msg in lib2.gs_last_error()
+    assert lib2.gs_sht_create(3, 6, ctypes.byref(out)) == -1
+    assert b"power of two" in lib2.gs_last_error()
+    assert lib2.gs_sht_create(8, 40, ctypes.byref(out)) == -1
+    assert b"lmax" in lib2.gs_last_error()
+    assert lib2.gs_masked_create(None, None, None, ctypes.byref(out)) == -1
+    assert not out.value
