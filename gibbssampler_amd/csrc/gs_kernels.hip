@@ -235,34 +235,7 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
 #pragma unroll
             for (int c = 0; c < NV; ++c) zv[f][c] = zc[f * NR + r + c];
         } else {
-#if defined(GS_EXPERIMENT_NO_BM)
-            // timing experiment only: Philox without the Box-Muller transform
-            const uint4 w = philox(i, (uint32_t)f, tag, iter, key);
-            zv[f][0] = (double)w.x - (double)w.y; zv[f][1] = (double)w.z - (double)w.w;
-#elif defined(GS_EXPERIMENT_ZIG_FAST)
-            // timing experiment only: the fast path of a 256-layer ziggurat per normal
-            {
-                const uint4 w = philox(i, (uint32_t)f, tag, iter, key);
-                const uint32_t lo0 = w.x, hi0 = w.y, lo1 = w.z, hi1 = w.w;
-                const int i0 = lo0 & 255, i1 = lo1 & 255;
-                const double u0 = ((double)(hi0 >> 5) * 67108864.0 + (double)(lo0 >> 6)) * (1.0 / 9007199254740992.0);
-                const double u1 = ((double)(hi1 >> 5) * 67108864.0 + (double)(lo1 >> 6)) * (1.0 / 9007199254740992.0);
-                double x0 = u0 * tab[i0], x1 = u1 * tab[i1];
-                if (u0 >= tab[256 + i0]) x0 *= 0.5;
-                if (u1 >= tab[256 + i1]) x1 *= 0.5;
-                zv[f][0] = (lo0 & 256) ? -x0 : x0;
-                zv[f][1] = (lo1 & 256) ? -x1 : x1;
-            }
-#elif defined(GS_EXPERIMENT_NO_RNG)
-            zv[f][0] = (double)(i ^ f); zv[f][1] = (double)(i + iter);
-#elif defined(GS_OCML_BM)
-            box_muller(philox(i, (uint32_t)f, tag, iter, key), zv[f][0], zv[f][1]);
-#else
             box_muller_tab(philox<true>(i, (uint32_t)f, tag, iter, key), tab, zv[f][0], zv[f][1]);
-#endif
-#if defined(GS_SERIAL_FIELDS)
-            __builtin_amdgcn_sched_barrier(0);
-#endif
         }
     }
 #pragma unroll
@@ -283,18 +256,7 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
         for (int f = 0; f < F; ++f)
 #pragma unroll
             for (int c = 0; c < NV; ++c) {
-#if defined(GS_EXPERIMENT_LINE_ALIGNED_WRONG)
-                // timing experiment only (wrong data): every wave store realigned to a 128-B line
-                double* q = &sc[f * NR + r + c];
-                if (NV == 2) {
-                    const uintptr_t a = reinterpret_cast<uintptr_t>(&sc[f * NR + r]);
-                    const uintptr_t a0 = __builtin_amdgcn_readfirstlane((unsigned)(a & 0xFFFFFFFFu)) & 127u;
-                    q = q - (a0 >> 3);
-                }
-                __builtin_nontemporal_store(sv[f][c], q);
-#else
                 __builtin_nontemporal_store(sv[f][c], &sc[f * NR + r + c]);
-#endif
             }
     }
 #pragma unroll
@@ -324,11 +286,8 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
 // workgroup is one contiguous 4 KiB run per field and chain; consecutive
 // workgroups are consecutive chains of the same (tiles, rows) block and
 // share the data reads in L2.
-#ifndef GS_SWEEP_WAVES_PER_SIMD
-#define GS_SWEEP_WAVES_PER_SIMD 1
-#endif
 template <int F, int ZM, bool STORE>
-__global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L, int nchains, int ntile, int nchunk, int tm,
+__global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunk, int tm,
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
                                                   const double* __restrict__ params, const double* __restrict__ z,
                                                   double* __restrict__ s, double* __restrict__ partials,
@@ -395,24 +354,11 @@ __global__ __launch_bounds__(256, GS_SWEEP_WAVES_PER_SIMD) void k_cr_sweep(int L
     if (m1 - 1 <= ell_lo && ell_lo >= 0) {
         // off-diagonal block: every lane active on every row; the next row's
         // data is loaded before this row's draw (register double buffer)
-#if !defined(GS_PREFETCH)
         for (; m < m1; ++m) {
             load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
             sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
             i += L - m;
         }
-#else
-        if (m < m1) load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
-        for (; m < m1; ++m) {
-            const long long inext = i + (L - m);
-            double dn[F][2];
-            if (m + 1 < m1) load_d<F, 2>(d, NR, 2 * inext - (L + 1), dn);
-            sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
-#pragma unroll
-            for (int f = 0; f < F; ++f) { dv[f][0] = dn[f][0]; dv[f][1] = dn[f][1]; }
-            i = inext;
-        }
-#endif
     } else {
         for (; m < m1; ++m) {
             if (lane_ok && ell >= m) {
@@ -867,13 +813,6 @@ __device__ __forceinline__ void lds_fill4(T* __restrict__ dst, const T* __restri
     }
 }
 
-#if defined(GS_MH_STAMPS)
-// diagnostic build only: per-workgroup s_memtime stamps of the MH phases
-__device__ unsigned long long g_mh_stamps[64][24];
-#define MH_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_mh_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define MH_STAMP(k) do { } while (0)
-#endif
 template <int F, bool SC>
 __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases ph, const int2* __restrict__ phase_tab,
                                                   const int4* __restrict__ phase_rng,
@@ -886,7 +825,6 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                                                   const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
                                                   IterArg itarg, int chain0, int32_t* __restrict__ accept_out,
                                                   MhEpi epi) {
-    MH_STAMP(0);
     const uint32_t iter = itarg.get();
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
@@ -920,7 +858,6 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     lds_fill4(e2b, ell2bin, NSP * Lp1);
     __syncthreads();
     for (int q = 0; q < ph.nphase; ++q) {
-        MH_STAMP(1 + 5 * q);
         const int nb = ph.n[q];
         if (nb == 0) continue;
         const int sp0 = ph.sp[q][0], sp1 = ph.sp[q][1];
@@ -928,10 +865,6 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         const int4* rng = phase_rng + ph.off[q];
         const int nwide = ph.nwide[q];
         // per-l likelihood differences of the phase's spectra
-#if defined(GS_ABL_MH_TERMS)
-        for (int l = tid; l < Lp1; l += blockDim.x) { g[l] = 0.0; g[Lp1 + l] = 0.0; }
-        if (false)
-#endif
         for (int l = ph.lmin + tid; l < Lp1; l += blockDim.x) {
             double vo[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -954,24 +887,15 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                 g[k * Lp1 + l] = out;
             }
         }
-        MH_STAMP(2 + 5 * q);
         // accept uniforms of every (block, attempt), in parallel
         for (int j = tid; j < nb * n_iter_mh; j += blockDim.x) {
             const int2 sb = tab[j / n_iter_mh];
             const int att = j % n_iter_mh;
             const int flat = acc_off[sb.x] + sb.y * n_iter_mh + att;
-#if defined(GS_ABL_MH_U)
-            ub[j] = 0.5 + 1e-9 * flat;
-#else
             ub[j] = u_acc ? ul[flat] : uniform1(key, sb.y, (uint32_t)sb.x | ((uint32_t)att << 8), TAG_MH_U, iter);
-#endif
         }
         __syncthreads();
-        MH_STAMP(3 + 5 * q);
         // narrow blocks: one thread each
-#if defined(GS_ABL_MH_NARROW)
-        if (false)
-#endif
         for (int j = nwide + tid; j < nb; j += blockDim.x) {
             const int2 sb = tab[j];
             const int4 r = rng[j];
@@ -989,14 +913,10 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
                 if (accept_out) accept_out[(long long)chain * nacc + acc_off[sp] + blk * n_iter_mh + att] = acc ? 1 : 0;
             }
         }
-        MH_STAMP(4 + 5 * q);
         // wide blocks: the whole workgroup, up to MAXW blocks together (fixed-order
         // sums per block: per-thread terms, wave sums, then the 16 wave sums in
         // wave order; the blocks of a phase are independent), so a phase's few
         // long blocks share one pair of barriers and do not serialise on one wave
-#if defined(GS_ABL_MH_WIDE)
-        if (false)
-#endif
         for (int j0 = 0; j0 < nwide; j0 += MAXW) {
             const int nw = min(MAXW, nwide - j0);
 #pragma unroll
@@ -1038,7 +958,6 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         }
         __syncthreads();
     }
-    MH_STAMP(20);
     const int nrow = NSP * maxbins;
     for (int k = tid; k < nrow; k += blockDim.x) D[k] = Ds[k];
     // ---- epilogue (graph-captured NC steps) ----
@@ -1047,7 +966,6 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
         for (int k = tid; k < nrow; k += blockDim.x) tr[k] = Ds[k];
     }
-    MH_STAMP(21);
     if (epi.counter) {
         __syncthreads();
         if (tid == 0) {
@@ -1265,11 +1183,6 @@ int check_plan(const gs_plan* p) {
 extern "C" {
 
 int gs_abi_version(void) { return GS_ABI_VERSION; }
-#if defined(GS_MH_STAMPS)
-int gs_debug_mh_stamps(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mh_stamps), sizeof(unsigned long long) * 64 * 24) == hipSuccess ? 0 : -1;
-}
-#endif
 const char* gs_last_error(void) { return gs_detail::g_last_error.c_str(); }
 
 int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
@@ -1650,9 +1563,6 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
     if (!stats || !dl) return set_error("gs_nc_mh: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
-#if defined(GS_ABL_MH_NOPROPOSE)
-    if (false)
-#endif
 #define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
                                      p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi, IterArg{iteration, p->itp()}, \
                                      p->chain0)
@@ -1748,6 +1658,7 @@ int gs_recentre(gs_plan* p, const double* dl_new, const double* dl_old, double* 
 int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
                      const double* igvar, uint64_t seed, uint32_t it, void* stream) {
     if (check_plan(p)) return -1;
+    if (!d_alm || !dl) return set_error("gs_step_centered: null argument");
     if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
     if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
     return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
@@ -1758,6 +1669,7 @@ int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* 
     if (check_plan(p)) return -1;
     if (!p->iter_dev_on) return set_error("gs_step_centered_fused: device iteration counter not enabled");
     if (trace && capacity < 1) return set_error("gs_step_centered_fused: capacity < 1");
+    if (!d_alm || !dl) return set_error("gs_step_centered_fused: null argument");
     if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
     if (gs_cr_sweep(p, d_alm, p->params, nullptr, seed, it, 0, s_out, p->stats, stream)) return -1;
     return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->iter_dev, stream);
@@ -1818,6 +1730,9 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
 int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
                         const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
                         void* stream) {
+    if (check_plan(p)) return -1;
+    if (!p->has_mh) return set_error("gs_step_noncentered: plan has no MH blocks / proposal variances");
+    if (!d_alm || !dl) return set_error("gs_step_noncentered: null argument");
     if (gs_nc_prologue(p, dl, u_prop, seed, it, stream)) return -1;
     if (gs_nc_sweep(p, d_alm, s_out, z, seed, it, 1, stream)) return -1;
     return gs_nc_decide(p, dl, u_acc, seed, it, accept_out, stream);
@@ -1827,6 +1742,9 @@ int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, con
                  const double* u_prop, const double* u_acc, uint64_t seed, uint32_t it, int32_t* accept_out,
                  double* dl_tmp_out, int recentre, void* stream) {
     if (check_plan(p)) return -1;
+    // validated before anything is launched (dl is overwritten mid-step)
+    if (!p->has_mh) return set_error("gs_step_asis: plan has no MH blocks / proposal variances");
+    if (!d_alm || !dl) return set_error("gs_step_asis: null argument");
     double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
     if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
     if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
@@ -1851,6 +1769,7 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
     if (!p->iter_dev_on) return set_error("gs_step_asis_fused: device iteration counter not enabled");
     if (!p->has_mh) return set_error("gs_step_asis_fused: plan has no MH blocks / proposal variances");
     if (trace && capacity < 1) return set_error("gs_step_asis_fused: capacity < 1");
+    if (!d_alm || !dl) return set_error("gs_step_asis_fused: null argument");
     double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;

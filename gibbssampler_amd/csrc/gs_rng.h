@@ -118,15 +118,9 @@ __device__ __forceinline__ void bm_sincos2pi(double u, double& sn, double& cs) {
 __device__ __forceinline__ void box_muller(uint4 w, double& z0, double& z1) {
     const double u1 = u53(w.x, w.y);
     const double u2 = u53(w.z, w.w);
-#if defined(GS_OCML_BM)
-    const double r = sqrt(-2.0 * log(u1));
-    double sn, cs;
-    sincospi(2.0 * u2, &sn, &cs);
-#else
     const double r = sqrt(-2.0 * bm_log(u1));
     double sn, cs;
     bm_sincos2pi(u2, sn, cs);
-#endif
     z0 = r * cs;
     z1 = r * sn;
 }
@@ -221,37 +215,12 @@ __device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const do
     cs = fma(ck, cph, -(sk * sph));
 }
 
-// sqrt(t), t >= 0: hardware reciprocal square root (~2^-29 relative) and one
-// Newton step (error ~2^-58), then r = t y; exact 0 at t = 0
-__device__ __forceinline__ double bm_sqrt(double t) {
-#if defined(GS_RSQ_SQRT)
-    double y = __builtin_amdgcn_rsq(t);
-    const double h = 0.5 * t;
-    y = y * fma(-h * y, y, 1.5);
-    return t > 0.0 ? t * y : 0.0;
-#else
-    return sqrt(t);
-#endif
-}
-
 __device__ __forceinline__ void box_muller_tab(uint4 w, const double* __restrict__ tab, double& z0, double& z1) {
     const double u1 = u53(w.x, w.y);
-#if defined(GS_ABL_NOLOG)
-    const double lg = u1 - 1.0;           // timing ablation only
-#else
     const double lg = bm_log_tab(u1, tab);
-#endif
-#if defined(GS_ABL_NOSQRT)
-    const double r = -2.0 * lg;           // timing ablation only
-#else
-    const double r = bm_sqrt(-2.0 * lg);
-#endif
+    const double r = sqrt(-2.0 * lg);
     double sn, cs;
-#if defined(GS_ABL_NOTRIG)
-    sn = (double)w.z * 2.3283064365386963e-10; cs = (double)w.w * 2.3283064365386963e-10;   // ablation
-#else
     bm_sincos_tab(w.z, w.w, tab, sn, cs);
-#endif
     z0 = r * cs;
     z1 = r * sn;
 }

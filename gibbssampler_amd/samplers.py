@@ -21,6 +21,7 @@ import time
 import numpy as np
 import torch
 
+from . import _capi as C
 from .engine import GibbsPlan, MH_ORDER
 
 INIT_ITER = 0xFFFFFFFF
@@ -35,6 +36,7 @@ class BatchedRunner:
         if rng not in ("native", "replay"):
             raise ValueError(rng)
         self.kind, self.rng, self.seed = kind, rng, int(seed)
+        self.quirks = int(quirks)
         self.plan = GibbsPlan(lmax, nside, nfields, nchains, bl, noise_var, bins, blocks=blocks,
                               proposal_variances=proposal_variances, chain0=chain0, quirks=quirks,
                               n_iter_metropolis=n_iter_metropolis)
@@ -61,7 +63,14 @@ class BatchedRunner:
 
     def init(self, dls_init):
         p = self.plan
-        self.dl = p.dl_tensor(dls_init)
+        if self.dl is None:
+            self.dl = p.dl_tensor(dls_init)
+        else:
+            # keep the buffer a captured graph points at; a re-init drops the graph
+            # (its device iteration counter belongs to the previous run)
+            self.dl.copy_(p.dl_tensor(dls_init))
+        self.graph = None
+        p.iteration_counter(False)
         self.iteration = 0
         if self.kind == "centered":
             # the reference's initial CR (GibbsSampler.py:136-138) -- consumes its draws
@@ -200,7 +209,8 @@ class BatchedRunner:
             return None
         s = self.s.clone()
         if self.kind == "asis" and not self.materialize_recentre and self.iteration > 0:
-            quirk = True
+            # ASIS.py:203 quirk: s <- A(C_new) s; corrected: s <- A(C_new) A(C_tmp)^+ s
+            quirk = bool(self.quirks & C.GS_QUIRK_ASIS_RECENTRE_CENTERED)
             self.plan.recentre(self.dl, s, None if quirk else self.dl_tmp)
         return s
 

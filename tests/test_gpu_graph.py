@@ -85,3 +85,58 @@ def test_multistep_graph_with_sweep_timing(kind, F):
         np.testing.assert_array_equal(tr[(it - 1) % n], want[w + k])
     np.testing.assert_array_equal(g.dl.cpu().numpy(), want[-1])
     assert g.iteration == w + n
+
+
+def test_run_after_capture_restarts_cleanly():
+    """BatchedRunner.init() after a captured graph drops the graph (it points at
+    the previous run's counter) and reuses the D_l buffer: a second run() gives
+    the same history as a fresh runner's run()."""
+    from gibbssampler_amd.problem import synthetic_problem
+    P = synthetic_problem(64, 32, 3, seed=3)
+    g = _runner("noncentered", 3)
+    p = g.plan
+    g.capture_graph()
+    g.step()
+    h1, a1 = g.run(P["dls_init"], 3)
+    fresh = _runner("noncentered", 3)
+    h2, a2 = fresh.run(P["dls_init"], 3)
+    for s in h1:
+        np.testing.assert_array_equal(h1[s], h2[s])
+        np.testing.assert_array_equal(a1[s], a2[s])
+    assert g.graph is None
+
+
+@pytest.mark.parametrize("F", [2, 3])
+def test_asis_skymap_without_quirk(F):
+    """ASIS with reference_quirks off: the lazily re-centred skymap() is
+    A(C_new) A(C_tmp)^+ s, equal to the map re-centred inside the
+    step, and for EB equal to sqrt(C_new / C_tmp) s per l (ASIS.py:185-203)."""
+    import torch
+    from gibbssampler_amd.problem import synthetic_problem
+    from gibbssampler_amd.samplers import BatchedRunner
+    from oracle import harmonic as H
+    P = synthetic_problem(64, 32, F, seed=3)
+    kw = dict(blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=91, quirks=0)
+    lazy = BatchedRunner("asis", P["lmax"], P["nside"], F, 2, P["bl"], P["noise_var"], P["bins"], P["d_alm"], **kw)
+    mat = BatchedRunner("asis", P["lmax"], P["nside"], F, 2, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
+                        materialize_recentre=True, **kw)
+    for r in (lazy, mat):
+        r.init(P["dls_init"])
+        for _ in range(3):
+            r.step()
+    torch.cuda.synchronize()
+    got = lazy.skymap().cpu().numpy()
+    np.testing.assert_array_equal(got, mat.s.cpu().numpy())
+    if F == 2:
+        m = H.Model(P["lmax"], P["nside"], F, P["bl"], P["noise_var"], P["bins"], P["blocks"],
+                    P["proposal_variances"], P["d_alm"])
+        p = lazy.plan
+        sc = lazy.s.cpu().numpy()
+        new, tmp = p.dl_dicts(lazy.dl), p.dl_dicts(lazy.dl_tmp)
+        sl = H.slot_ell(m.L)
+        for c in range(2):
+            for k, sp in enumerate(("EE", "BB")):
+                vn = H.var_from_dl(H.unfold_bins(new[c][sp], P["bins"][sp]))
+                vt = H.var_from_dl(H.unfold_bins(tmp[c][sp], P["bins"][sp]))
+                R = np.sqrt(vn) * np.where(vt != 0, np.sqrt(1.0 / np.where(vt != 0, vt, 1.0)), 0.0)
+                np.testing.assert_allclose(got[c, k], R[sl] * sc[c, k], rtol=1e-13, atol=1e-300)
