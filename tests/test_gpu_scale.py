@@ -1,0 +1,132 @@
+"""GPU parity at scale.
+
+1. Replay mode vs the reference at its OWN default configuration
+   (tests/golden/reference_eb_scale_L512.npz, tools/gen_golden_scale.py:
+   N_side 256, L 512, Planck BB bins, 1 EE + 134 BB blocks, config.py's
+   proposal variances): NonCenteredGibbs / CenteredGibbs / ASIS histories at
+   1e-9 relative, accept flags exact, single CR draws by their per-l spectra.
+2. Native mode vs the oracle at BASELINE sizes: configs[2] (TEB, N_side 512,
+   L 1024, a 32-chain plan; chains 0 and 31 checked: the sky map s, the eight
+   statistic rows, D_l and every accept flag) and configs[1] (centered TEB,
+   N_side 256, L 512, 1 chain).  Tolerance 1e-10 relative (libm ulps).
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import harmonic as H  # noqa: E402
+from tests._golden import GOLDEN, scale_model  # noqa: E402
+from tests._util import stats_rows, rows_to_stats  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gs():
+    return dict(np.load(os.path.join(GOLDEN, "reference_eb_scale_L512.npz")))
+
+
+def _init(gs):
+    return {"EE": gs["init_EE"].copy(), "BB": gs["init_BB"].copy()}
+
+
+@pytest.mark.parametrize("kind,key", [("noncentered", "nc"), ("centered", "c"), ("asis", "asis")])
+def test_scale_replay_driver_matches_reference(gs, kind, key):
+    from gibbssampler_amd.samplers import BatchedRunner
+    m, _ = scale_model(gs)
+    run = BatchedRunner(kind=kind, lmax=m.L, nside=m.nside, nfields=2, nchains=1, bl=m.bl, noise_var=m.noise_var,
+                        bins=m.bins, d_alm=m.d_alm, blocks=m.blocks, proposal_variances=m.proposal_variances,
+                        rng="replay")
+    np.random.seed(int(gs[key + "_seed"]))
+    h, acc = run.run(_init(gs), int(gs[key + "_iters"]))
+    for s in ("EE", "BB"):
+        np.testing.assert_allclose(h[s][:, 0], gs[f"{key}_h_{s}"], rtol=1e-9, err_msg=s)
+        if kind != "centered":
+            np.testing.assert_array_equal(acc[s][:, 0], gs[f"{key}_acc_{s}"], err_msg=s)
+
+
+@pytest.mark.parametrize("key,mode", [("a7", 0), ("a8", 1)])
+def test_scale_replay_cr_matches_reference(gs, key, mode):
+    from gibbssampler_amd.engine import GibbsPlan
+    m, D = scale_model(gs)
+    unb = {"EE": np.arange(m.L + 2), "BB": np.arange(m.L + 2)}
+    p = GibbsPlan(m.L, m.nside, 2, 1, m.bl, m.noise_var, unb)
+    dl = p.dl_tensor({"EE": D["dl_EE"], "BB": D["dl_BB"]})
+    np.random.seed(int(gs[key + "_seed"]))
+    s, st = p.cr_sweep(p.data_tensor(m.d_alm), p.block_params(mode, dl), z=p.replay_cr_normals())
+    s, st = s.cpu().numpy()[0], st.cpu().numpy()[0]
+    np.testing.assert_allclose(s[0, :2048], gs[key + "_head_E"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(s[1, :2048], gs[key + "_head_B"], rtol=1e-12, atol=1e-15)
+    two_l1 = 2 * np.arange(m.L + 1) + 1.0
+    np.testing.assert_allclose(st[0] / two_l1, gs[key + "_cl_E"], rtol=1e-11)
+    np.testing.assert_allclose(st[1] / two_l1, gs[key + "_cl_B"], rtol=1e-11)
+
+
+SEED = 20261015
+
+
+def _check_chain(m, F, s_dev, st_dev, c, chain_id, it, mode, dl_init):
+    un = m.unfold(dl_init)
+    M, Lc = (H.centered_params if mode == 0 else H.noncentered_params)(m, un)
+    z = np.stack([H.cr_normals(SEED, chain_id, it, 0, f, m.L) for f in range(F)])
+    ref = H.cr_apply(m, M, Lc, m.d_alm, z)
+    np.testing.assert_allclose(s_dev[c], ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+    stats = H.sweep_stats(m, ref, m.d_alm)
+    rows = stats_rows(F, stats)
+    np.testing.assert_allclose(st_dev[c], rows, rtol=1e-10, atol=1e-12 * np.abs(rows).max(axis=1, keepdims=True))
+    return stats
+
+
+def test_fullsize_noncentered_matches_oracle_configs2():
+    """BASELINE configs[2]: NC TEB all_sph, N_side 512, L 1024, 32 chains; one
+    iteration; chains 0 and 31 against the oracle (s, statistics, D_l, accepts:
+    the 1,025-l EE/TT/TE blocks and the 468 BB blocks of this layout)."""
+    from gibbssampler_amd.engine import GibbsPlan
+    from gibbssampler_amd.problem import synthetic_problem
+    P = synthetic_problem(1024, 512, 3, seed=0)
+    m = H.Model(P["lmax"], P["nside"], 3, P["bl"], P["noise_var"], P["bins"], P["blocks"],
+                P["proposal_variances"], P["d_alm"])
+    nch, it = 32, 4
+    p = GibbsPlan(m.L, m.nside, 3, nch, m.bl, m.noise_var, m.bins, blocks=m.blocks,
+                  proposal_variances=m.proposal_variances)
+    assert p.nacc > 400
+    d = p.data_tensor(m.d_alm)
+    dl = p.dl_tensor(P["dls_init"])
+    s, st = p.cr_sweep(d, p.block_params(1, dl), seed=SEED, iteration=it)
+    acc = p.nc_mh(st, dl, seed=SEED, iteration=it)
+    torch.cuda.synchronize()
+    out = p.dl_dicts(dl)
+    accs = p.split_accept(acc)
+    for c in (0, nch - 1):
+        s_c = s[c:c + 1].cpu().numpy()
+        st_c = st[c:c + 1].cpu().numpy()
+        _check_chain(m, 3, s_c, st_c, 0, c, it, 1, P["dls_init"])
+        ref, racc = H.nc_mh(m, P["dls_init"], rows_to_stats(3, st_c[0]), seed=SEED, chain=c, iteration=it)
+        for sp in m.spectra:
+            np.testing.assert_allclose(out[c][sp], ref[sp], rtol=1e-10, err_msg=sp)
+            np.testing.assert_array_equal(accs[sp][c], racc[sp], err_msg=sp)
+        del s_c
+
+
+def test_fullsize_centered_matches_oracle_configs1():
+    """BASELINE configs[1]: centered TEB, N_side 256, L 512, 1 chain: s, the
+    statistics and the inverse-Wishart / inverse-Gamma D_l draw."""
+    from gibbssampler_amd.engine import GibbsPlan
+    from gibbssampler_amd.problem import synthetic_problem
+    P = synthetic_problem(512, 256, 3, seed=0)
+    m = H.Model(P["lmax"], P["nside"], 3, P["bl"], P["noise_var"], P["bins"], P["blocks"],
+                P["proposal_variances"], P["d_alm"])
+    it = 9
+    p = GibbsPlan(m.L, m.nside, 3, 1, m.bl, m.noise_var, m.bins)
+    d = p.data_tensor(m.d_alm)
+    dl = p.dl_tensor(P["dls_init"])
+    s, st = p.cr_sweep(d, p.block_params(0, dl), seed=SEED, iteration=it)
+    out = p.dl_dicts(p.cls_draw(st, seed=SEED, iteration=it))
+    st_h = st.cpu().numpy()
+    _check_chain(m, 3, s.cpu().numpy(), st_h, 0, 0, it, 0, P["dls_init"])
+    ref = H.centered_cls_draw(m, rows_to_stats(3, st_h[0]), seed=SEED, chain=0, iteration=it)
+    for sp in m.spectra:
+        np.testing.assert_allclose(out[0][sp], ref[sp], rtol=1e-10, err_msg=sp)
