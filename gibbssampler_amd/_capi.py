@@ -122,6 +122,7 @@ _SIGS = [
                                            c_double_p, _VP]),
     ("gs_masked_center", ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_masked_nc_loglik", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("gs_masked_pixel_mh", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [_VP] * 13),
     ("gs_masked_tt_fullsky", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
                                              ctypes.c_int, _VP, _VP]),
     ("gs_synalm", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, _VP]),

@@ -24,11 +24,17 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <cstdlib>
 
 #include "gibbs_capi.h"
 #include "gs_rng.h"
 #include "gs_common.h"
 #include "gs_block.h"
+
+// library-internal SHT entry points (gs_sht.hip)
+extern "C" long long gs_sht_phi_plane(const gs_sht* p);
+extern "C" int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int* blk, int K,
+                                   const int* blk_lmax, double* phib, double* maps, void* stream);
 
 using namespace gs;
 using gs_detail::set_error;
@@ -598,6 +604,199 @@ __global__ void k_tt_fullsky(int L, const double* __restrict__ dl, const double*
     }
 }
 
+// ---------------------------------------------------------------------------
+// f2, one Metropolis sweep without per-block SHTs (NonCenteredGibbs.py:401-445
+// with the pixel likelihood of :333-355).  The current model map m = A b C^1/2
+// s_nc is linear in the per-l factors C^1/2, and every block k changes one
+// field's factors on its own l-range, so with y_k = A b (C_prop^1/2 -
+// C_cur^1/2) s_nc (restricted to block k) and the residual r = d - m,
+//   lik(accepted set S + k) - lik(S) = <N^-1 (r - sum_{j in S} y_j), y_k> - <N^-1 y_k, y_k> / 2
+//                                    = g_k - sum_{j in S} G_kj - G_kk / 2,
+// g_k = <N^-1 r, y_k>, G_kj = <N^-1 y_k, y_j>.  All y_k come from ONE block
+// synthesis (gs_sht_synth_blocks: the Legendre recurrence shared by every
+// block), G from one weighted Gram pass, and the blocks are then decided in
+// the reference's order by one workgroup -- no host round trip per block.
+// ---------------------------------------------------------------------------
+constexpr int F2_GSUB = 32;          // elements per LDS stage of the Gram pass
+constexpr int F2_RMAX = 176;         // rows (blocks + residual) per Gram pass
+constexpr int F2_BPT = 4;            // 4 x 4 output blocks per thread
+constexpr long long F2_CHUNK = 2048; // elements per Gram workgroup
+
+// delta a (real layout) of blocks [k0, k0 + kn) and their local block table
+template <int F>
+__global__ void k_f2_delta(int L, int k0, int kn, const int* __restrict__ blk, const double* __restrict__ dl_cur,
+                           const double* __restrict__ dl_prop, const double* __restrict__ bl,
+                           const double* __restrict__ s_nc, double* __restrict__ da, int* __restrict__ blk_local) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g <= L) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const int b = blk[f * (L + 1) + g];
+            blk_local[f * (L + 1) + g] = (b >= k0 && b < k0 + kn) ? b - k0 : -1;
+        }
+    }
+    if (g >= NR) return;
+    int l;
+    if (g <= L) l = (int)g;
+    else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+        const int b = blk[f * (L + 1) + l];
+        double v = 0.0;
+        if (b >= k0 && b < k0 + kn) {
+            const double cp = sqrt(var_from_dl(dl_prop[f * (L + 1) + l], l));
+            const double cc = sqrt(var_from_dl(dl_cur[f * (L + 1) + l], l));
+            v = bl[l] * ((cp - cc) * s_nc[f * NR + g]);
+        }
+        da[f * NR + g] = v;
+    }
+}
+
+__global__ void k_f2_resid(long long n, const double* __restrict__ d, const double* __restrict__ m,
+                           double* __restrict__ r) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g < n) r[g] = d[g] - m[g];
+}
+
+// lower triangle of the R x R weighted Gram matrix of rows 0..R-2 = Y, R-1 = r,
+// over one chunk of elements: every row staged once per element (times
+// sqrt(N^-1)) in LDS; thread t owns the 4 x 4 output blocks t, t + 256, ...
+// Per-chunk partials [chunk][nblk4][16], summed in chunk order by k_f2_gram_finish.
+__global__ __launch_bounds__(256) void k_f2_gram(int R, long long n, const double* __restrict__ Y,
+                                                 const double* __restrict__ r, const double* __restrict__ w,
+                                                 double* __restrict__ partial) {
+    __shared__ double S[F2_RMAX + 4][F2_GSUB + 1];
+    const int nb4 = (R + 3) / 4;
+    const int nblk4 = nb4 * (nb4 + 1) / 2;
+    const int tid = threadIdx.x;
+    int bi[F2_BPT], bj[F2_BPT];
+    bool own[F2_BPT];
+#pragma unroll
+    for (int q = 0; q < F2_BPT; ++q) {
+        const int b = tid + q * 256;
+        own[q] = b < nblk4;
+        int i = (int)((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+        while ((i + 1) * (i + 2) / 2 <= b) ++i;
+        while (i * (i + 1) / 2 > b) --i;
+        bi[q] = own[q] ? i : 0;
+        bj[q] = own[q] ? b - i * (i + 1) / 2 : 0;
+    }
+    double acc[F2_BPT][4][4];
+#pragma unroll
+    for (int q = 0; q < F2_BPT; ++q)
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[q][x][y] = 0.0;
+    const long long e0 = blockIdx.x * F2_CHUNK, e1 = min(n, e0 + F2_CHUNK);
+    const int rows = nb4 * 4;
+    for (long long es = e0; es < e1; es += F2_GSUB) {
+        for (int k = tid; k < rows * F2_GSUB; k += 256) {
+            const int row = k / F2_GSUB, c = k % F2_GSUB;
+            const long long e = es + c;
+            double v = 0.0;
+            if (row < R && e < e1) {
+                const double y = row < R - 1 ? Y[(long long)row * n + e] : r[e];
+                v = y * sqrt(w[e]);
+            }
+            S[row][c] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < F2_BPT; ++q) {
+            if (!own[q]) continue;
+            const int ra = 4 * bi[q], rb = 4 * bj[q];
+            for (int c = 0; c < F2_GSUB; ++c) {
+                double a[4], b[4];
+#pragma unroll
+                for (int x = 0; x < 4; ++x) { a[x] = S[ra + x][c]; b[x] = S[rb + x][c]; }
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) acc[q][x][y] = fma(a[x], b[y], acc[q][x][y]);
+            }
+        }
+        __syncthreads();
+    }
+    double* po = partial + (long long)blockIdx.x * nblk4 * 16;
+#pragma unroll
+    for (int q = 0; q < F2_BPT; ++q) {
+        if (!own[q]) continue;
+        const int b = tid + q * 256;
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) po[(long long)b * 16 + x * 4 + y] = acc[q][x][y];
+    }
+}
+
+__global__ void k_f2_gram_finish(int R, int nchunk, const double* __restrict__ partial, double* __restrict__ G) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= R * R) return;
+    const int i = g / R, j = g % R;
+    if (j > i) return;
+    const int nb4 = (R + 3) / 4;
+    const int nblk4 = nb4 * (nb4 + 1) / 2;
+    const int b = (i / 4) * (i / 4 + 1) / 2 + j / 4;
+    const double* pp = partial + (long long)b * 16 + (i % 4) * 4 + (j % 4);
+    double s = 0.0;
+    for (int c = 0; c < nchunk; ++c) s += pp[(long long)c * nblk4 * 16];
+    G[g] = s;
+}
+
+// the decisions of blocks k0 .. k0+kn-1 in order (NonCenteredGibbs.py:427-442):
+// log u < (g_k - sum_{j accepted} G_kj - G_kk / 2) + sum log r; after an
+// acceptance later attempts see delta = 0 (the proposal IS the state).
+// One workgroup; corr[k] = sum over accepted j < k of G_kj, accumulated in
+// decision order.
+__global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* __restrict__ G, int k0, int n_iter,
+                                                   const int* __restrict__ blk_field,
+                                                   const int* __restrict__ blk_bins, int maxbins,
+                                                   const double* __restrict__ logr, const double* __restrict__ u_acc,
+                                                   const double* __restrict__ prop, double* __restrict__ binned,
+                                                   int32_t* __restrict__ accept_out, double* __restrict__ taken_out) {
+    __shared__ double corr[F2_RMAX];
+    __shared__ int taken_s;
+    const int tid = threadIdx.x;
+    for (int k = tid; k < kn; k += blockDim.x) corr[k] = 0.0;
+    __syncthreads();
+    for (int k = 0; k < kn; ++k) {
+        if (tid == 0) {
+            const int kg = k0 + k, f = blk_field[kg];
+            const int lo = blk_bins[2 * kg], hi = blk_bins[2 * kg + 1];
+            double lrs = 0.0;
+            for (int b = lo; b < hi; ++b) lrs += logr[f * maxbins + b];
+            const double delta = (G[(long long)(R - 1) * R + k] - corr[k]) - 0.5 * G[(long long)k * R + k];
+            bool taken = false;
+            for (int att = 0; att < n_iter; ++att) {
+                const bool acc = log(u_acc[(long long)kg * n_iter + att]) < (taken ? 0.0 : delta) + lrs;
+                if (acc && !taken)
+                    for (int b = lo; b < hi; ++b) binned[f * maxbins + b] = prop[f * maxbins + b];
+                taken = taken || acc;
+                accept_out[(long long)kg * n_iter + att] = acc ? 1 : 0;
+            }
+            taken_s = taken ? 1 : 0;
+            taken_out[k] = taken ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        if (taken_s)
+            for (int j = k + 1 + tid; j < kn; j += blockDim.x) corr[j] += G[(long long)j * R + k];
+        __syncthreads();
+    }
+}
+
+// r -= sum over accepted blocks of y_k (before the next group of blocks)
+__global__ void k_f2_update(long long n, int kn, const double* __restrict__ Y, const double* __restrict__ taken,
+                            double* __restrict__ r) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    double v = r[g];
+    for (int k = 0; k < kn; ++k)
+        if (taken[k] != 0.0) v -= Y[(long long)k * n + g];
+    r[g] = v;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -621,6 +820,11 @@ struct gs_masked {
     double *grad0 = nullptr, *grad1 = nullptr, *snew = nullptr, *pix0 = nullptr, *pix1 = nullptr, *vtmp = nullptr;
     double *partial = nullptr, *lr = nullptr;
     double *pr = nullptr, *pz = nullptr, *pp = nullptr, *pq = nullptr, *params_pcg = nullptr, *dots = nullptr;
+    // f2 block MH workspace (allocated on first use, grown as needed)
+    double *f2_da = nullptr, *f2_r = nullptr, *f2_Y = nullptr, *f2_phib = nullptr, *f2_part = nullptr,
+           *f2_G = nullptr, *f2_taken = nullptr;
+    int* f2_blk = nullptr;
+    int f2_cap = 0;                  // blocks the Y / phib buffers hold
 };
 
 namespace {
@@ -629,10 +833,12 @@ void mc_free(gs_masked* c) {
     if (c->sht) gs_sht_destroy(c->sht);
     double* bufs[] = {c->bl, c->dpix, c->ninv, c->g2, c->params, c->params_mala, c->x, c->Abs, c->y, c->r,
                       c->grad0, c->grad1, c->snew, c->pix0, c->pix1, c->vtmp, c->partial, c->lr,
-                      c->pr, c->pz, c->pp, c->pq, c->params_pcg, c->dots};
+                      c->pr, c->pz, c->pp, c->pq, c->params_pcg, c->dots, c->f2_da, c->f2_r, c->f2_Y,
+                      c->f2_phib, c->f2_part, c->f2_G, c->f2_taken};
     for (double* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ell2bin) (void)hipFree(c->ell2bin);
+    if (c->f2_blk) (void)hipFree(c->f2_blk);
     delete c;
 }
 
@@ -977,6 +1183,95 @@ int gs_masked_nc_loglik(gs_masked* c, const double* dl, const double* s_nc, doub
     hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(64), 0, st, nb, c->partial, c->dots);
     hipLaunchKernelGGL(k_mc_halfneg, dim3(1), dim3(64), 0, st, c->dots, lik);
     GS_LAUNCH_CHECK("k_mc_resid");
+    return 0;
+}
+
+// blocks of one group: bounded by the Gram pass (F2_RMAX - 1) and by the
+// workspace budget (GS_F2_GROUP_BYTES, default 6 GiB: the phase planes and
+// maps of every block of a group are resident at once)
+static int f2_group(const gs_masked* c) {
+    const long long nco = c->F == 1 ? 1 : 2;
+    const long long per = nco * (2 * gs_sht_phi_plane(c->sht) * 16 + c->npix * 8);
+    long long budget = 6LL << 30;
+    if (const char* e = getenv("GS_F2_GROUP_BYTES")) budget = std::max(1LL, atoll(e));
+    return (int)std::max(1LL, std::min<long long>(F2_RMAX - 1, budget / std::max(per, 1LL)));
+}
+
+int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* blk, const int* blk_lmax,
+                       const int* blk_field, const int* blk_bins, const double* s_nc, const double* dl_cur,
+                       const double* dl_prop, const double* logr, const double* u_acc, const double* prop_binned,
+                       double* binned, int32_t* accept_out, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (c->F != 1 && c->F != 2)
+        return set_error("gs_masked_pixel_mh: the pixel-domain NC likelihood is defined for T or EB "
+                         "(NonCenteredClsSampler / PolarizationNonCenteredClsSampler)");
+    if (K < 0 || n_iter < 1 || maxbins < 1) return set_error("gs_masked_pixel_mh: K / n_iter / maxbins out of range");
+    if (K == 0) return 0;
+    if (!blk || !blk_lmax || !blk_field || !blk_bins || !s_nc || !dl_cur || !dl_prop || !logr || !u_acc ||
+        !prop_binned || !binned || !accept_out)
+        return set_error("gs_masked_pixel_mh: null argument");
+    const hipStream_t st = S(stream);
+    const int F = c->F, nco = F == 1 ? 1 : 2;
+    const int KG = f2_group(c);
+    const int kcap = std::min(K, KG);
+    const long long n = (long long)F * c->npix;
+    const long long nchunk = (n + F2_CHUNK - 1) / F2_CHUNK;
+    const int nb4max = (kcap + 1 + 3) / 4;
+    if (c->f2_cap < kcap) {
+        double* bufs[] = {c->f2_Y, c->f2_phib, c->f2_part, c->f2_G, c->f2_taken};
+        for (double* b : bufs)
+            if (b) (void)hipFree(b);
+        c->f2_Y = c->f2_phib = c->f2_part = c->f2_G = c->f2_taken = nullptr;
+        c->f2_cap = 0;
+        int rc = 0;
+        rc |= mc_alloc(&c->f2_Y, (size_t)kcap * n);
+        rc |= mc_alloc(&c->f2_phib, (size_t)kcap * nco * 2 * gs_sht_phi_plane(c->sht) * 2);
+        rc |= mc_alloc(&c->f2_part, (size_t)nchunk * (nb4max * (nb4max + 1) / 2) * 16);
+        rc |= mc_alloc(&c->f2_G, (size_t)(kcap + 1) * (kcap + 1));
+        rc |= mc_alloc(&c->f2_taken, (size_t)kcap);
+        if (rc) return -1;
+        c->f2_cap = kcap;
+    }
+    if (!c->f2_da) {
+        int rc = 0;
+        rc |= mc_alloc(&c->f2_da, (size_t)F * c->NR);
+        rc |= mc_alloc(&c->f2_r, (size_t)n);
+        rc |= mc_alloc(&c->f2_blk, (size_t)F * (c->L + 1));
+        if (rc) return -1;
+    }
+    // residual of the current state: r = d - A b C_cur^1/2 s_nc
+    if (gs_masked_center(c, dl_cur, +1, s_nc, c->snew, stream)) return -1;
+    if (mc_synth(c, c->snew, c->pix1, st)) return -1;
+    hipLaunchKernelGGL(k_f2_resid, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->dpix, c->pix1, c->f2_r);
+    GS_LAUNCH_CHECK("k_f2_resid");
+    for (int k0 = 0; k0 < K; k0 += KG) {
+        const int kn = std::min(KG, K - k0);
+        const int R = kn + 1;
+        const dim3 gd(nblocks(std::max<long long>(c->NR, c->L + 1), 256)), bd(256);
+        if (F == 1)
+            hipLaunchKernelGGL(k_f2_delta<1>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
+                               c->f2_blk);
+        else
+            hipLaunchKernelGGL(k_f2_delta<2>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
+                               c->f2_blk);
+        GS_LAUNCH_CHECK("k_f2_delta");
+        if (gs_sht_synth_blocks(c->sht, F, c->f2_da, c->f2_blk, kn, blk_lmax + k0, c->f2_phib, c->f2_Y, stream))
+            return -1;
+        hipLaunchKernelGGL(k_f2_gram, dim3((unsigned)nchunk), dim3(256), 0, st, R, n, c->f2_Y, c->f2_r, c->ninv,
+                           c->f2_part);
+        GS_LAUNCH_CHECK("k_f2_gram");
+        hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256)), dim3(256), 0, st, R, (int)nchunk,
+                           c->f2_part, c->f2_G);
+        GS_LAUNCH_CHECK("k_f2_gram_finish");
+        hipLaunchKernelGGL(k_f2_decide, dim3(1), dim3(256), 0, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
+                           maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken);
+        GS_LAUNCH_CHECK("k_f2_decide");
+        if (k0 + kn < K) {
+            hipLaunchKernelGGL(k_f2_update, dim3(nblocks(n, 256)), dim3(256), 0, st, n, kn, c->f2_Y, c->f2_taken,
+                               c->f2_r);
+            GS_LAUNCH_CHECK("k_f2_update");
+        }
+    }
     return 0;
 }
 

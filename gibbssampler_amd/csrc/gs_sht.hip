@@ -427,6 +427,185 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 }
 
 // ---------------------------------------------------------------------------
+// f2 block synthesis (pixel-domain NC likelihood, NonCenteredGibbs.py:333-355):
+// the maps y_k = A(delta a_k) of K Metropolis blocks at once.  Every (l, field)
+// belongs to at most one block (blk[f][l], -1: none), so one pass of the
+// Legendre recurrence per (m, ring pair) serves every block: the field's
+// accumulator is flushed to block k's phase plane when l leaves block k and
+// reset, i.e. the recurrence is shared and only the outputs multiply.
+// NC = 1: T (spin 0, one output comp per block); 2: E, B -> Q, U (two comps).
+// phib: [K * NCO comps][ns][phi plane]; block k's comps hold only m <= its
+// largest l (the ring stage reads no further, comp_lmax).
+// ---------------------------------------------------------------------------
+struct BlkAcc { double p[4], n[4]; };
+
+template <int NC, bool EVEN>
+__device__ __forceinline__ void blk_accumulate(BlkAcc& A, int f, const LegCoef& c, double v0, double v1, double is2,
+                                               double xis2, double2 a) {
+    if constexpr (NC == 1) {
+        double* t = EVEN ? A.p : A.n;
+        t[0] = fma(a.x, v0, t[0]);
+        t[1] = fma(a.y, v0, t[1]);
+    } else {
+        const double F1 = fma(c.R * xis2, v1, -fma(c.P, is2, c.Q) * v0);
+        const double F2 = fma(c.Rm * is2, v1, -(c.T * xis2) * v0);
+        double* a1 = EVEN ? A.p : A.n;   // F1 carries lambda's parity
+        double* a2 = EVEN ? A.n : A.p;   // F2 the opposite one
+        if (f == 0) {                    // E
+            a1[0] = fma(a.x, F1, a1[0]); a1[1] = fma(a.y, F1, a1[1]);
+            a2[2] = fma(a.y, F2, a2[2]); a2[3] = fma(-a.x, F2, a2[3]);
+        } else {                         // B
+            a2[0] = fma(-a.y, F2, a2[0]); a2[1] = fma(a.x, F2, a2[1]);
+            a1[2] = fma(a.x, F1, a1[2]); a1[3] = fma(a.y, F1, a1[3]);
+        }
+    }
+}
+
+template <int NC>
+__global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const LegCoef* __restrict__ coef,
+                                                                const double2* __restrict__ ain,
+                                                                const int* __restrict__ blk,
+                                                                double2* __restrict__ phib) {
+    constexpr int NF = NC;                      // input fields
+    constexpr int NCO = NC == 1 ? 1 : 2;        // output comps per block
+    const int L = D.L, npair = D.npair, nlm = D.nlm;
+    const int q = blockIdx.x, tile = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g0 = tile * (LTILE / 64) + wave * SR;
+    double x[SR], is2[SR], xis2[SR];
+    int pr[SR];
+    bool act[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        pr[r] = (g0 + r) * 64 + lane;
+        act[r] = pr[r] < npair;
+        x[r] = act[r] ? D.geom[pr[r]].x : 0.0;
+        is2[r] = act[r] ? D.geom[pr[r]].is2 : 0.0;
+        xis2[r] = x[r] * is2[r];
+    }
+    const long long plane = phi_plane(L, npair);
+    for (int h = 0; h < 2; ++h) {
+        const int m = h == 0 ? q : L - q;
+        if (h == 1 && m <= q) break;
+        int ls[SR];
+        int lmin = L + 1;
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+            ls[r] = __builtin_amdgcn_readfirstlane(g0 + r < D.ngroup ? D.lstart[(long long)m * D.ngroup + g0 + r]
+                                                                     : L + 1);
+            lmin = min(lmin, ls[r]);
+        }
+        BlkAcc A[NF][SR];
+        double v0[SR], v1[SR];
+        int kk[SR];
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int r = 0; r < SR; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { A[f][r].p[i] = 0.0; A[f][r].n[i] = 0.0; }
+#pragma unroll
+        for (int r = 0; r < SR; ++r) { v0[r] = 0.0; v1[r] = 0.0; kk[r] = 0; }
+        int cur[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) cur[f] = -1;
+        const long long base = cidx(L, m, m) - m;
+        const LegCoef* cf = coef + base;
+        const double2* a0 = ain + base;
+        // write field f's accumulators to its current block's planes (if any), reset
+        auto flush = [&](int f) {
+            const int k = cur[f];
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                BlkAcc& B = A[f][r];
+                if (k >= 0 && act[r]) {
+                    const long long o = phi_at(m, pr[r], npair);
+                    double2* P = phib + (long long)(k * NCO) * 2 * plane;
+                    if constexpr (NC == 1) {
+                        P[o] = make_double2(B.p[0] + B.n[0], B.p[1] + B.n[1]);
+                        P[plane + o] = make_double2(B.p[0] - B.n[0], B.p[1] - B.n[1]);
+                    } else {
+                        P[o] = make_double2(-(B.p[0] + B.n[0]), -(B.p[1] + B.n[1]));
+                        P[plane + o] = make_double2(-(B.p[0] - B.n[0]), -(B.p[1] - B.n[1]));
+                        P[2 * plane + o] = make_double2(-(B.p[2] + B.n[2]), -(B.p[3] + B.n[3]));
+                        P[3 * plane + o] = make_double2(-(B.p[2] - B.n[2]), -(B.p[3] - B.n[3]));
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { B.p[i] = 0.0; B.n[i] = 0.0; }
+            }
+        };
+        auto track = [&](int l) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int b = blk[f * (L + 1) + l];
+                if (b != cur[f]) { flush(f); cur[f] = b; }
+            }
+        };
+        // blocks wholly below every slot's onset: zero planes (their terms underflow)
+        for (int l = m; l < lmin && l <= L; ++l) track(l);
+        int l = lmin;
+        // ---- slow path: slot activation and scaled lanes ----
+        while (l <= L) {
+            bool live = true;
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (l == ls[r] && act[r]) {
+                    const double2 s0 = D.st[(long long)m * npair + pr[r]];
+                    v1[r] = s0.x; v0[r] = s0.y;
+                    kk[r] = D.stk[(long long)m * npair + pr[r]];
+                }
+                if (ls[r] <= L && (l < ls[r] || __any(kk[r] < 0))) live = false;
+            }
+            if (live) break;
+            track(l);
+            const LegCoef c = cf[l];
+            const LegCoef cn = cf[min(l + 1, L)];
+            const bool even = ((l - m) & 1) == 0;
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (l < ls[r]) continue;
+                const double w0 = kk[r] == 0 ? v0[r] : 0.0, w1 = kk[r] == 0 ? v1[r] : 0.0;
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    const double2 a = a0[(long long)f * nlm + l];
+                    if (even) blk_accumulate<NC, true>(A[f][r], f, c, w0, w1, is2[r], xis2[r], a);
+                    else blk_accumulate<NC, false>(A[f][r], f, c, w0, w1, is2[r], xis2[r], a);
+                }
+                if (l < L) {
+                    rec_step(cn, x[r], v0[r], v1[r]);
+                    if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
+                }
+            }
+            ++l;
+        }
+        // ---- every live slot active and representable ----
+        for (; l <= L; ++l) {
+            track(l);
+            const LegCoef c = cf[l];
+            const LegCoef cn = cf[min(l + 1, L)];
+            const bool even = ((l - m) & 1) == 0;
+            double2 a[NF];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) a[f] = a0[(long long)f * nlm + l];
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                if (ls[r] > L) continue;
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    if (even) blk_accumulate<NC, true>(A[f][r], f, c, v0[r], v1[r], is2[r], xis2[r], a[f]);
+                    else blk_accumulate<NC, false>(A[f][r], f, c, v0[r], v1[r], is2[r], xis2[r], a[f]);
+                }
+                if (l < L) rec_step(cn, x[r], v0[r], v1[r]);
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) flush(f);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // ring FFTs (block-wide, in place, buffer in LDS or global scratch)
 // ---------------------------------------------------------------------------
 // forward (dir = -1): X_k = sum_j x_j e^{-2 pi i jk/M};  dir = +1: conjugate
@@ -655,10 +834,13 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
                                                          const double2* __restrict__ tw, int Mmax,
                                                          const double2* __restrict__ bsk,
                                                          double2* __restrict__ gscratch, double* __restrict__ maps,
-                                                         double2* __restrict__ sscr, int nsplit, int sstride) {
+                                                         double2* __restrict__ sscr, int nsplit, int sstride,
+                                                         const int* __restrict__ comp_lmax, int comp_div) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
+    // block syntheses (f2): comp c holds only m <= comp_lmax[c / comp_div]
+    const int Lc = comp_lmax ? comp_lmax[comp / comp_div] : L;
     const PairGeom g = geom[p];
     const int BD = blockDim.x;
     double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
@@ -682,13 +864,13 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         const int k = sl % K, j0 = sl / K;
         const int nk = (n - k) % n;
         if (sl < K * J) {
-            for (int m = k + j0 * n; m <= L; m += J * n) {
+            for (int m = k + j0 * n; m <= Lc; m += J * n) {
                 const double2 a = H(PN, m);
                 f.nk.x += a.x; f.nk.y += a.y;
                 if (!eq) { const double2 b = H(PS, m); f.sk.x += b.x; f.sk.y += b.y; }
             }
             if (nk != k)
-                for (int m = nk + j0 * n; m <= L; m += J * n) {
+                for (int m = nk + j0 * n; m <= Lc; m += J * n) {
                     const double2 a = H(PN, m);
                     f.nmk.x += a.x; f.nmk.y += a.y;
                     if (!eq) { const double2 b = H(PS, m); f.smk.x += b.x; f.smk.y += b.y; }
@@ -1406,7 +1588,9 @@ int gs_sht_info(const gs_sht* p, int* nside, int* lmax, long long* npix, long lo
 }
 
 static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const double* maps_in, double* maps_out,
-                          hipStream_t st) {
+                          hipStream_t st, const double2* phi = nullptr, const int* comp_lmax = nullptr,
+                          int comp_div = 1) {
+    if (!phi) phi = p->phi;
     const int M = p->cls_M[c];
     const bool glob = M > p->lds_fft_max;
     const int bd = ring_block(M);
@@ -1419,10 +1603,12 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
     if (synth) {
         if (nb8)
             hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n);
+                               p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
+                               comp_lmax, comp_div);
         else
             hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, p->phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n);
+                               p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
+                               comp_lmax, comp_div);
     } else {
         if (nb8)
             hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
@@ -1440,7 +1626,8 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
 // global-scratch class stays on the caller's stream), so the short-ring
 // classes -- a dozen small, latency-bound launches -- run on the plan's side
 // stream while the largest class runs on the caller's.
-static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream) {
+static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
+                     const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1) {
     const size_t ncls = p->cls_M.size();
     size_t big = 0;
     for (size_t c = 1; c < ncls; ++c)
@@ -1452,7 +1639,9 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
     }
     for (size_t c = 0; c < ncls; ++c) {
         const bool on_side = fork && c != big && p->cls_M[c] <= p->lds_fft_max;
-        if (sht_ring_class(p, c, synth, ncomp, maps_in, maps_out, on_side ? p->side : S(stream))) return -1;
+        if (sht_ring_class(p, c, synth, ncomp, maps_in, maps_out, on_side ? p->side : S(stream), phi, comp_lmax,
+                           comp_div))
+            return -1;
     }
     if (fork) {
         GS_CHECK(hipEventRecord(p->ev_join, p->side));
@@ -1492,6 +1681,40 @@ static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, do
     if (ncomp == 1) GS_AF(1); else if (ncomp == 2) GS_AF(2); else GS_AF(3);
 #undef GS_AF
     GS_LAUNCH_CHECK("k_sht_anal_finish");
+    return 0;
+}
+
+long long gs_sht_phi_plane(const gs_sht* p) { return p ? phi_plane(p->L, p->npair) : 0; }
+
+int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int* blk, int K, const int* blk_lmax,
+                        double* phib, double* maps, void* stream) {
+    if (check_sht(p)) return -1;
+    if (nfield != 1 && nfield != 2) return set_error("gs_sht_synth_blocks: nfield must be 1 (T) or 2 (E,B)");
+    if (K < 1 || !alm_real || !blk || !blk_lmax || !phib || !maps) return set_error("gs_sht_synth_blocks: null argument");
+    const long long nin = (long long)nfield * p->nlm;
+    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nfield, alm_real,
+                       GS_ALM_REAL, p->ain);
+    GS_LAUNCH_CHECK("k_sht_alm_in");
+    double2* ph = reinterpret_cast<double2*>(phib);
+    const dim3 grid(p->L / 2 + 1, (p->npair + LTILE - 1) / LTILE);
+    if (nfield == 1)
+        hipLaunchKernelGGL(k_sht_synth_blocks<1>, grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->ain, blk, ph);
+    else
+        hipLaunchKernelGGL(k_sht_synth_blocks<2>, grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->ain, blk, ph);
+    GS_LAUNCH_CHECK("k_sht_synth_blocks");
+    // ring stage: the plan's FFT scratch (global / split rings) holds three comps,
+    // so rings that need it run three comps per launch
+    const int nco = nfield == 1 ? 1 : 2;
+    const int ncomp = K * nco;
+    const bool scratch = p->gscr != nullptr || p->nsplit > 0;
+    const int chunk = scratch ? nco * (3 / nco) : ncomp;    // whole blocks per launch
+    const long long plane = phi_plane(p->L, p->npair);
+    for (int c0 = 0; c0 < ncomp; c0 += chunk) {
+        const int nc = std::min(chunk, ncomp - c0);
+        if (sht_rings(p, true, nc, nullptr, maps + (long long)c0 * p->npix, stream, ph + (long long)c0 * 2 * plane,
+                      blk_lmax + c0 / nco, nco))
+            return -1;
+    }
     return 0;
 }
 

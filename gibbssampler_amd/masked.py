@@ -176,7 +176,8 @@ class MaskedCR:
         s = self._s(s_old)
         grad = torch.empty_like(s)
         pix = torch.empty((self.F, self.Npix), dtype=torch.float64, device=self.device)
-        _capi.check(self.lib.gs_masked_gradient(self.handle, _capi.ptr(self._dl(all_dls)), _capi.ptr(s),
+        dl = self._dl(all_dls)
+        _capi.check(self.lib.gs_masked_gradient(self.handle, _capi.ptr(dl), _capi.ptr(s),
                                                 _capi.ptr(grad), _capi.ptr(pix), _capi.stream_ptr()),
                     "gs_masked_gradient")
         g, p = grad.cpu().numpy(), pix.cpu().numpy()
@@ -335,13 +336,14 @@ class MaskedRunner:
 # ---------------------------------------------------------------------------------------
 class PixelMH:
     """PolarizationNonCenteredClsSampler.sample with all_sph=False
-    (NonCenteredGibbs.py:401-445): truncated-normal proposals for every bin
-    (gs_mh_propose), then per Metropolis block the whole-map likelihood
-    -1/2 sum_pix N^-1 (d - A b C^1/2 s_nc)^2 (compute_log_likelihood,
-    NonCenteredGibbs.py:333-355) evaluated on the device by
-    gs_masked_nc_loglik (one C^1/2 scaling + one SHT synthesis + one
-    reduction).  The accept test needs the scalar on the host (one sync per
-    block, as the reference's own loop); everything else stays resident.
+    (NonCenteredGibbs.py:401-445; TT: NonCenteredClsSampler.sample): truncated-
+    normal proposals for every bin (gs_mh_propose), then the Metropolis blocks
+    scored with the whole-map likelihood -1/2 sum_pix N^-1 (d - A b C^1/2 s_nc)^2
+    (compute_log_likelihood, NonCenteredGibbs.py:333-355) and decided in the
+    reference's order ON THE DEVICE by gs_masked_pixel_mh: the likelihood
+    change of every block comes from one shared-recurrence block synthesis and
+    one weighted Gram pass instead of one SHT and one host round trip per
+    block.  The accept flags are read back once per sweep.
     Replay: numpy draws truncnorm EE, BB then one uniform per block attempt,
     the reference's order (the likelihood draws nothing)."""
 
@@ -370,6 +372,25 @@ class PixelMH:
         self._idx = torch.from_numpy(np.maximum(idx, 0)).to(cr.device)
         self._valid = torch.from_numpy(idx >= 0).to(cr.device)
         self._lik = torch.zeros(1, dtype=torch.float64, device=cr.device)
+        # block tables of gs_masked_pixel_mh, in decision order (spectra in MH order)
+        blk = np.full((F, L + 1), -1, dtype=np.int32)
+        lmax_, field, brange, self._acc_layout = [], [], [], []
+        for s in self.order:
+            k = self.spectra.index(s)
+            edges, nb = self.blocks[s], len(self.bins[s]) - 1
+            for bi in range(len(edges) - 1):
+                lo, hi = int(edges[bi]), min(int(edges[bi + 1]), nb)
+                l0, l1 = (int(self.bins[s][lo]), int(self.bins[s][hi])) if hi > lo else (0, 0)
+                kg = len(field)
+                blk[k, l0:min(l1, L + 1)] = kg
+                lmax_.append(min(l1, L + 1) - 1 if l1 > l0 else -1)
+                field.append(k)
+                brange += [lo, max(hi, lo)]
+            self._acc_layout.append((s, (len(edges) - 1) * self.n_iter))
+        self.K = len(field)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(cr.device)
+        self._blk, self._blk_lmax, self._blk_field, self._blk_bins = dev(blk), dev(lmax_), dev(field), dev(brange)
+        self._acc = torch.zeros(max(self.K * self.n_iter, 1), dtype=torch.int32, device=cr.device)
 
     def unfold(self, binned_t):
         """utils.unfold_bins on the device: [nspec, maxbins] -> [nspec, L+1]."""
@@ -400,41 +421,42 @@ class PixelMH:
         bt = self.plan.dl_tensor(dls)[0]
         return float(self.loglik_t(self.unfold(bt), self.cr._s(s_nonCentered)).item())
 
-    def sample_t(self, s_nc, binned_t, iteration):
-        """one sweep on device tensors: binned_t [2, maxbins] (updated copy
-        returned), s_nc [2, NR]; returns (binned_t, accept dict of lists)."""
+    def sweep_t(self, s_nc, binned_t, iteration):
+        """one sweep on device tensors, no host synchronisation: binned_t
+        [nspec, maxbins] -> (updated copy, accept flags [K * n_iter] int32 in
+        decision order; the flags tensor is reused by the next sweep)."""
         plan, cr = self.plan, self.cr
         dl = binned_t[None].contiguous()
         if cr.rng == "replay":
             up, ua = plan.replay_mh_uniforms()
             prop, logr, _ = plan.mh_propose(dl, up, seed=cr.seed, iteration=iteration)
-            ua_h = ua[0].cpu().numpy()
         else:
             prop, logr, ua = plan.mh_propose(dl, None, seed=cr.seed, iteration=iteration, with_uniforms=True)
-            ua_h = ua[0].cpu().numpy()
-        prop, logr_h = prop[0], logr[0].cpu().numpy()
+        prop0, logr0 = prop[0].contiguous(), logr[0].contiguous()
         cur = binned_t.clone()
-        old_lik = float(self.loglik_t(self.unfold(cur), s_nc).item())
-        accept = {s: [] for s in self.spectra}
-        ui = 0
-        for s in self.order:
-            k = self.spectra.index(s)
-            blocks = self.blocks[s]
-            for bi in range(len(blocks) - 1):
-                lo, hi = int(blocks[bi]), int(blocks[bi + 1])
-                lr_all = float(np.sum(logr_h[k, lo:hi]))
-                for _ in range(self.n_iter):
-                    new = cur.clone()
-                    new[k, lo:hi] = prop[k, lo:hi]
-                    new_lik = float(self.loglik_t(self.unfold(new), s_nc).item())
-                    log_r = (new_lik - old_lik) + lr_all
-                    if np.log(ua_h[ui]) < log_r:
-                        cur, old_lik = new, new_lik
-                        accept[s].append(1)
-                    else:
-                        accept[s].append(0)
-                    ui += 1
-        return cur, accept
+        # every temporary stays referenced until the launch is enqueued (a freed
+        # tensor's block is handed to the next allocation)
+        dl_cur, dl_prop, u0 = self.unfold(cur), self.unfold(prop0), ua[0].contiguous()
+        _capi.check(self.cr.lib.gs_masked_pixel_mh(
+            cr.handle, self.K, self.n_iter, plan.maxbins, _capi.ptr(self._blk), _capi.ptr(self._blk_lmax),
+            _capi.ptr(self._blk_field), _capi.ptr(self._blk_bins), _capi.ptr(s_nc), _capi.ptr(dl_cur),
+            _capi.ptr(dl_prop), _capi.ptr(logr0), _capi.ptr(u0), _capi.ptr(prop0),
+            _capi.ptr(cur), _capi.ptr(self._acc), _capi.stream_ptr()), "gs_masked_pixel_mh")
+        return cur, self._acc
+
+    def split_accept(self, flags):
+        a = flags.cpu().numpy()
+        out, off = {}, 0
+        for s, n in self._acc_layout:
+            out[s] = [int(v) for v in a[off:off + n]]
+            off += n
+        return out
+
+    def sample_t(self, s_nc, binned_t, iteration):
+        """one sweep on device tensors: binned_t [nspec, maxbins] (updated copy
+        returned), s_nc [nspec, NR]; returns (binned_t, accept dict of lists)."""
+        cur, flags = self.sweep_t(s_nc, binned_t, iteration)
+        return cur, self.split_accept(flags)
 
     def sample(self, s_nonCentered, binned_dls_old, iteration=None):
         """reference surface: dict maps / binned dicts in, (binned dict, accept dict) out."""

@@ -284,6 +284,23 @@ int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, dou
  * (EB sqrt(var) / sqrt(inv_var), NonCenteredGibbs.py:236-237; TEB chol(C)). */
 int gs_masked_center(gs_masked* ctx, const double* dl, int dir, const double* in, double* out, void* stream);
 int gs_masked_nc_loglik(gs_masked* ctx, const double* dl, const double* s_nc, double* lik, void* stream);
+/* f2: one Metropolis sweep of the pixel-domain non-centered likelihood over K
+ * blocks (PolarizationNonCenteredClsSampler.sample / NonCenteredClsSampler.sample
+ * with all_sph=False, NonCenteredGibbs.py:401-445 with :333-355), decided on
+ * the device in block order without a host round trip and without one SHT per
+ * block: the per-block map changes come from one shared-recurrence block
+ * synthesis and one weighted Gram pass.  F = 1 (T) or 2 (EB).
+ * blk [F][lmax+1]: block (0..K-1, decision order: spectra in MH order) of each
+ * (field, l), -1 outside every block; blk_lmax [K]: largest l of each block
+ * (-1: empty); blk_field [K]; blk_bins [2K]: bin range [lo, hi) of each block;
+ * s_nc [F][(lmax+1)^2]; dl_cur / dl_prop [F][lmax+1]: unbinned current and
+ * proposed D_l; logr / prop_binned / binned [F][maxbins] (binned in/out:
+ * accepted blocks take the proposal's bins); u_acc [K * n_iter] accept
+ * uniforms in decision order; accept_out [K * n_iter]. */
+int gs_masked_pixel_mh(gs_masked* ctx, int K, int n_iter, int maxbins, const int* blk, const int* blk_lmax,
+                       const int* blk_field, const int* blk_bins, const double* s_nc, const double* dl_cur,
+                       const double* dl_prop, const double* logr, const double* u_acc, const double* prop_binned,
+                       double* binned, int32_t* accept_out, void* stream);
 
 /* Gaussian sky draw for synthetic data (the synalm + smoothalm half of
  * healpy.synfast, main_polarization.py:38): alm[f] = beam[f][l] * (C_l^1/2 z)[f]

@@ -381,3 +381,28 @@ def test_f2_masked_asis_driver_vs_oracle(g, gibbs_cr):
     for sp in ("EE", "BB"):
         np.testing.assert_allclose(h[sp], want[sp], rtol=1e-7)
         np.testing.assert_array_equal(acc[sp], wacc[sp])
+
+
+@pytest.mark.parametrize("n_iter,group_bytes", [(1, None), (2, None), (2, "1"), (1, "50000000")])
+def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes):
+    """gs_masked_pixel_mh decides every block on the device from one block
+    synthesis + one Gram pass; with a small workspace budget the blocks run in
+    groups (one block per group at "1") and the residual is carried between
+    groups.  Native streams, n_iter_metropolis 1 and 2, against the oracle's
+    full-map likelihood per block (oracle/masked.pixel_mh)."""
+    from gibbssampler_amd.masked import PixelMH
+    if group_bytes is not None:
+        monkeypatch.setenv("GS_F2_GROUP_BYTES", group_bytes)
+    bins, blocks, pv = _f2_parts(g)
+    seed, chain, it = 313, 1, 9
+    cr = _cr(g, gibbs_cr=False, ula=False, rng="native", seed=seed, chain=chain)
+    mh = PixelMH(cr, bins, blocks, pv, n_iter_metropolis=n_iter)
+    assert mh.K >= 3
+    snc = np.stack([g["f2_snc_E"], g["f2_snc_B"]])
+    init = {"EE": g["init_EE"].copy(), "BB": g["init_BB"].copy()}
+    new, acc = mh.sample(snc, init, iteration=it)
+    mm, model = _oracle_model(g)
+    want, wacc = MK.pixel_mh(mm, model, init, snc, seed=seed, chain=chain, iteration=it, n_iter=n_iter)
+    _close(new["EE"], want["EE"])
+    _close(new["BB"], want["BB"])
+    assert acc == wacc

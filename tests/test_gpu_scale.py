@@ -76,7 +76,9 @@ def _check_chain(m, F, s_dev, st_dev, c, chain_id, it, mode, dl_init):
     np.testing.assert_allclose(s_dev[c], ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
     stats = H.sweep_stats(m, ref, m.d_alm)
     rows = stats_rows(F, stats)
-    np.testing.assert_allclose(st_dev[c], rows, rtol=1e-10, atol=1e-12 * np.abs(rows).max(axis=1, keepdims=True))
+    for q in range(rows.shape[0]):
+        np.testing.assert_allclose(st_dev[c][q], rows[q], rtol=1e-10, atol=1e-12 * np.abs(rows[q]).max(),
+                                   err_msg=f"statistic row {q}")
     return stats
 
 
