@@ -6,84 +6,152 @@ full sky, N_side = 512, l_max = 1024, 32 chains per GPU, synthetic data
 (SURVEY.md 8d fiducial), native Philox RNG.  One "step" = one Gibbs
 iteration (constrained realisation + C_l draw) of every chain on every GPU.
 
-  python bench.py [--gpus N --steps K --warmup W --workload noncentered|centered|asis]
+  python bench.py [--gpus N --steps K --warmup W --workload NAME]
+
+  noncentered          configs[2] (default line)
+  centered             configs[1] shape (--lmax 512 --nside 256 --nchains 1)
+  asis                 configs[3] per GPU (32 chains / GPU)
+  masked               configs[4]: centered TEB, 80% mask, aux CR n_gibbs 1, N_side 2048 / L 4096
+  masked_centered_ula  HEAD's main_polarization.py run (:113-115,154): masked CenteredGibbs,
+                       gibbs_cr + ula (aux + MALA), EB, N_side 256 / L 512, 1 chain / GPU
+  masked_asis          HEAD's ASIS (:121-124): masked, all_sph=False, gibbs_cr, over-relaxation,
+                       n_gibbs 20, pixel-domain MH (f2), EB, N_side 256 / L 512, 1 chain / GPU
 
 For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL): chains
-are sharded (global chain id = rank * chains_per_gpu + c), no collective runs
-inside an iteration; the D_l traces are all-gathered once after the timed
-region.  value = total chain-iterations / max-over-ranks wall time.
+are sharded (global chain id = rank * chains_per_gpu + c) by
+gibbssampler_amd.distributed.ShardContext, no collective runs inside an
+iteration; the D_l traces are all-gathered once after the timed region.
+value = total chain-iterations / max-over-ranks wall time.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_VALU_PEAK_TFS = 78.6    # MI355X_MICROARCH.md: FP64 vector
+METRIC = "Gibbs iters/sec (constrained-realization + C_l draw), Nside=%d lmax=%d"
+HARMONIC = ("noncentered", "centered", "asis")
+MASKED_HEAD = ("masked_centered_ula", "masked_asis")
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="noncentered", choices=["noncentered", "centered", "asis", "masked"],
-                    help="masked = BASELINE configs[4]: CenteredGibbs TEB with an 80%% mask, aux-variable CR "
-                         "(n_gibbs 1), N_side 2048 / l_max 4096, 1 chain per GPU")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (50; masked modes fewer)")
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--workload", default="noncentered", choices=list(HARMONIC) + ["masked"] + list(MASKED_HEAD))
     ap.add_argument("--nchains", type=int, default=None, help="chains per GPU (32; masked: 1)")
-    ap.add_argument("--lmax", type=int, default=None, help="1024 (masked: 4096)")
-    ap.add_argument("--nside", type=int, default=None, help="512 (masked: 2048)")
+    ap.add_argument("--lmax", type=int, default=None, help="1024 (masked: 4096; HEAD modes: 512)")
+    ap.add_argument("--nside", type=int, default=None, help="512 (masked: 2048; HEAD modes: 256)")
     ap.add_argument("--fields", type=int, default=3, choices=[1, 2, 3])
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU baseline leg")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph of the timed steps")
     ap.add_argument("--time-every", type=int, default=1,
                     help="bracket the CR sweep of every N-th timed step with hipEvents (graph mode)")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
-    masked = a.workload == "masked"
-    a.nchains = a.nchains or (1 if masked else 32)
-    a.lmax = a.lmax or (4096 if masked else 1024)
-    a.nside = a.nside or (2048 if masked else 512)
+    one = a.workload == "masked" or a.workload in MASKED_HEAD
+    a.nchains = a.nchains or (1 if one else 32)
+    if a.workload in MASKED_HEAD:
+        a.lmax, a.nside = a.lmax or 512, a.nside or 256
+        a.steps, a.warmup = a.steps or 5, a.warmup if a.warmup is not None else 1
+    else:
+        a.lmax = a.lmax or (4096 if a.workload == "masked" else 1024)
+        a.nside = a.nside or (2048 if a.workload == "masked" else 512)
+        a.steps = a.steps or 50
+        a.warmup = a.warmup if a.warmup is not None else 5
     return a
 
 
-def sweep_algorithmic_bytes(L, F, nchains, ntask_stats):
+def sweep_algorithmic_bytes(L, F, nchains):
     """Unique HBM bytes one CR-sweep launch must move (DESIGN.md 'Roofline'):
     write s (8 F (L+1)^2 per chain) + read the shared data once (8 F (L+1)^2)
-    + read the per-l operator table (80 B per chain and l) + write the per-task
-    partial statistics."""
+    + read the per-l operator table (80 B per chain and l).  The per-task
+    statistics partials are implementation traffic and are not counted."""
     NR = (L + 1) ** 2
-    return 8 * F * NR * nchains + 8 * F * NR + 80 * (L + 1) * nchains + ntask_stats
+    return 8 * F * NR * nchains + 8 * F * NR + 80 * (L + 1) * nchains
+
+
+def sht_flops(nside, L, c):
+    """N_ringpair * N_lm * c (c = 4 spin-0, 16 spin-2, 20 TEB)."""
+    return 2 * nside * (L + 1) * (L + 2) // 2 * c
+
+
+def load_profile(path, key):
+    try:
+        with open(path) as f:
+            return json.load(f).get(key, {})
+    except (OSError, ValueError):
+        return {}
+
+
+def cpu_baseline_child(args):
+    """The CPU baselines on the host's cores (one chain per core, at most 16:
+    the GPU box's CPU share per GPU), run as a child process before this process
+    touches the GPU: the reference-structured port and the algorithm-matched
+    port (oracle/cpu_baseline.py)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--lmax", str(args.lmax), "--nside", str(args.nside),
+           "--fields", str(args.fields), "--budget", str(args.cpu_budget)]
+    try:
+        out = subprocess.run(cmd, cwd=HERE, env=env, capture_output=True, text=True, timeout=300, check=True)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        print(f"cpu baseline failed: {e}", file=sys.stderr)
+        return None
+    cores = r["cores"]
+    ref, mat = r["reference"], r["matched"]
+    return {"value": round(ref["value"], 5), "unit": "chain-iterations/s", "cores": cores, "kind": "port",
+            "sample": f"{ref['iterations']} NonCentered TEB all_sph iterations, one chain per core on {cores} cores "
+                      f"(of {r['affinity']} in the affinity mask), Nside={args.nside} lmax={args.lmax}, "
+                      f"{ref['seconds']:.1f} s wall: vectorised numpy port with the reference's per-block "
+                      f"full-sky likelihood (oracle/cpu_baseline.py nc_iteration)",
+            "algorithm_matched": {"value": round(mat["value"], 4), "unit": "chain-iterations/s", "cores": cores,
+                                  "sample": f"{mat['iterations']} iterations in {mat['seconds']:.1f} s with the "
+                                            f"GPU's per-l statistics (oracle/cpu_baseline.py nc_iteration_matched)"}}
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from gibbssampler_amd.distributed import ShardContext, dist_env
+    world, rank, local = dist_env()
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    cpu = None
+    if rank == 0 and world == 1 and args.workload == "noncentered" and not args.no_cpu_baseline:
+        cpu = cpu_baseline_child(args)
+    import torch
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
+    ctx = ShardContext(args.nchains, backend="nccl")
     from gibbssampler_amd.build import build
-    if rank == 0 or world == 1:
+    if ctx.rank == 0:
         build()
-    if dist is not None:
-        dist.barrier()
-    if args.workload == "masked":
-        return run_masked(args, rank, world, dist)
+    ctx.barrier()
+    try:
+        if args.workload in HARMONIC:
+            line = run_harmonic(args, ctx, cpu)
+        elif args.workload == "masked":
+            line = run_masked(args, ctx)
+        else:
+            line = run_masked_head(args, ctx)
+        if ctx.rank == 0:
+            print(json.dumps(line))
+    finally:
+        ctx.close()
+
+
+def run_harmonic(args, ctx, cpu):
+    import torch
     from gibbssampler_amd.problem import synthetic_problem
     from gibbssampler_amd.samplers import BatchedRunner
 
@@ -91,10 +159,10 @@ def main():
     runner = BatchedRunner(kind=args.workload, lmax=P["lmax"], nside=P["nside"], nfields=P["nfields"],
                            nchains=args.nchains, bl=P["bl"], noise_var=P["noise_var"], bins=P["bins"],
                            d_alm=P["d_alm"], blocks=P["blocks"], proposal_variances=P["proposal_variances"],
-                           rng="native", seed=args.seed, chain0=rank * args.nchains)
-    plans = (runner.plan,)
+                           rng="native", seed=args.seed, chain0=ctx.chain0)
+    p = runner.plan
     runner.init(P["dls_init"])
-    traces = [p.zeros(args.steps, p.nchains, p.nspec, p.maxbins) for p in plans]
+    trace = p.zeros(args.steps, p.nchains, p.nspec, p.maxbins)
     for _ in range(args.warmup):
         runner.step()
     one_graph = not args.no_graph
@@ -102,15 +170,12 @@ def main():
         # the K timed iterations as ONE hipGraph (D_l trace written on the device);
         # every CR-sweep kernel is bracketed by event-record nodes inside the graph,
         # so its duration is measured on its stream over the timed region itself
-        # (--time-every N brackets only every N-th sweep: an event node costs ~5 us)
-        runner.capture_steps(args.steps, trace=traces[0], trace_capacity=args.steps, time_sweeps=True,
+        runner.capture_steps(args.steps, trace=trace, trace_capacity=args.steps, time_sweeps=True,
                              time_every=args.time_every)
     else:
-        for p in plans:
-            p.sweep_timing(True)        # events around every sweep launch of the timed loop
+        p.sweep_timing(True)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if one_graph:
@@ -118,123 +183,103 @@ def main():
     else:
         for i in range(args.steps):
             runner.step()
-            traces[0][i].copy_(runner.dl)
+            trace[i].copy_(runner.dl)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if dist is not None:
-        dist.barrier()
-    elapsed = t1 - t0
-    timed = [p.sweep_timing(False) for p in plans]
-    timing_mode = ("hipEvents around each sweep inside the timed graph" if one_graph else
-                   "hipEvents around each sweep of the timed loop")
-    trace = torch.cat(traces, 1)
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # the run's only collective: gather every rank's D_l traces (RCCL over xGMI)
-        gathered = [torch.empty_like(trace) for _ in range(world)]
-        dist.all_gather(gathered, trace)
-        torch.cuda.synchronize()
-    total_chain_iters = args.steps * args.nchains * world
-    value = total_chain_iters / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
-
-    if rank == 0:
-        sweep_n = sum(n for _, n in timed)
-        sweep_ms = sum(ms for ms, _ in timed)
-        sweep_avg_ms = sweep_ms / max(sweep_n, 1)
-        per_launch = [sweep_algorithmic_bytes(p.L, p.F, p.nchains, p.nchains * p.ntask * p.nstat * 64 * 8)
-                      for p in plans]
-        alg_bytes = int(round(sum(b * n for b, (_, n) in zip(per_launch, timed)) / max(sweep_n, 1)))
-        achieved = alg_bytes / (sweep_avg_ms * 1e-3) / 1e9
-        plan = plans[0]
-        traffic = None
-        try:
-            with open(args.profile_json) as f:
-                prof = json.load(f)
-            key = f"{args.workload}_L{args.lmax}_F{args.fields}_c{plan.nchains}"
-            if key in prof:
-                traffic = prof[key].get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(P, args)
-        line = {
-            "metric": "Gibbs iters/sec (constrained-realization + C_l draw), Nside=512 lmax=1024",
-            "value": round(value, 3),
-            "unit": "chain-iterations/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (analytic fiducial spectra, d = b s + n in harmonic space, seed 0)",
-            "config": {"workload": f"{args.workload} TEB all_sph full-sky" if args.fields == 3 else args.workload,
-                       "launch": "one hipGraph of all timed iterations" if one_graph else "eager",
-                       "nside": args.nside, "lmax": args.lmax, "nfields": args.fields,
-                       "chains_per_gpu": args.nchains, "global_chains": args.nchains * world,
-                       "rng": "native philox4x32-10", "parallelism": f"chains sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "kernel": "k_cr_sweep", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,
-                         "avg_launch_ms": round(sweep_avg_ms, 5), "launches": sweep_n, "timing": timing_mode},
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line))
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    ctx.barrier()
+    elapsed = ctx.max(t1 - t0)
+    sweep_ms, sweep_n = p.sweep_timing(False)
+    # the run's only collective: every rank's D_l traces, gathered over RCCL / xGMI
+    gathered = ctx.gather(trace)
+    torch.cuda.synchronize()
+    assert gathered.shape[1] == ctx.global_chains
+    if ctx.rank != 0:
+        return None
+    total = args.steps * ctx.global_chains
+    sweep_avg_ms = sweep_ms / max(sweep_n, 1)
+    alg_bytes = sweep_algorithmic_bytes(p.L, p.F, p.nchains)
+    achieved = alg_bytes / (sweep_avg_ms * 1e-3) / 1e9
+    prof = load_profile(args.profile_json, f"{args.workload}_L{args.lmax}_F{args.fields}_c{p.nchains}")
+    return {
+        "metric": METRIC % (512, 1024),
+        "value": round(total / elapsed, 3),
+        "unit": "chain-iterations/s",
+        "n_gpus": ctx.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (analytic fiducial spectra, d = b s + n in harmonic space, seed 0)",
+        "config": {"workload": f"{args.workload} {'TEB' if args.fields == 3 else 'F=%d' % args.fields} all_sph "
+                               f"full-sky" + (" (TEB semantics build-specified; the reference's HEAD is EB, "
+                                              "parity for TT/TE pinned against the oracle only)"
+                                              if args.fields == 3 else ""),
+                   "launch": "one hipGraph of all timed iterations" if one_graph else "eager",
+                   "nside": args.nside, "lmax": args.lmax, "nfields": args.fields,
+                   "chains_per_gpu": args.nchains, "global_chains": ctx.global_chains,
+                   "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
+        "roofline": {"bound": "hbm", "kernel": "k_cr_sweep", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": prof.get("hbm_bytes_per_launch"), "algorithmic_bytes_per_launch": alg_bytes,
+                     "avg_launch_ms": round(sweep_avg_ms, 5), "launches": sweep_n,
+                     "timing": "hipEvents around each sweep inside the timed graph" if one_graph else
+                               "hipEvents around each sweep of the timed loop",
+                     "valu_issue_frac": prof.get("valu_issue_frac"),
+                     "note": "the sweep is issue-bound (Philox + Box-Muller per normal, DESIGN.md 3): "
+                             "valu_issue_frac = SQ_INST_CYCLES_VALU / (SIMDs x cycles) from profiles/"},
+        "cpu_baseline": cpu,
+    }
 
 
-FP64_VALU_PEAK_TFS = 78.6   # MI355X_MICROARCH.md: FP64 vector
+def _masked_data(N, L, nfields, seed=0):
+    """synfast of the fiducial spectra on the device + white noise + the 80%
+    band mask, as host arrays."""
+    import torch
+    from gibbssampler_amd.data import band_mask, synfast
+    from gibbssampler_amd.problem import fiducial_dl
+    dl = fiducial_dl(L, 3)
+    ell = np.arange(L + 1, dtype=np.float64)
+    fac = np.where(ell > 0, 2 * np.pi / np.maximum(ell * (ell + 1), 1), 0.0)
+    cls_ = np.stack([dl[k] * fac for k in ("TT", "EE", "BB", "TE")])
+    if nfields == 2:
+        cls_[0] = 0.0
+        cls_[3] = 0.0
+    np.random.seed(seed)
+    maps = synfast(cls_, N, L, np.radians(0.5))
+    g = torch.Generator(device="cuda").manual_seed(seed + 1)
+    sig = torch.tensor([40.0, 0.2, 0.2], dtype=torch.float64, device="cuda")[:, None]
+    d = maps + sig * torch.randn(maps.shape, dtype=torch.float64, device="cuda", generator=g)
+    mask = band_mask(N)
+    d = (d * torch.from_numpy(mask).cuda()).cpu().numpy()
+    return d, mask, dl
 
 
-def sht_flops(nside, L, ncomp_c=20):
-    """N_ringpair * N_lm * c (c = 4 spin-0 + 16 spin-2 = 20 for TEB)."""
-    return 2 * nside * (L + 1) * (L + 2) // 2 * ncomp_c
-
-
-def run_masked(args, rank, world, dist):
+def run_masked(args, ctx):
     """BASELINE configs[4]: CenteredGibbs TEB, masked (f_sky 0.8), aux-variable CR
     with n_gibbs = 1 (a9, TEB) + inverse-Wishart / inverse-Gamma C_l draw, one
     chain per GPU.  Per iteration: b s -> alm2map (TEB) -> v | s -> map2alm
     (TEB) -> s | v, then the sweep statistics and the C_l draw; all on the device."""
+    import torch
     from gibbssampler_amd import _capi
-    from gibbssampler_amd.data import band_mask, synfast
     from gibbssampler_amd.engine import GibbsPlan
     from gibbssampler_amd.masked import MaskedCR
-    from gibbssampler_amd.problem import fiducial_dl, gauss_beam
+    from gibbssampler_amd.problem import gauss_beam
     from gibbssampler_amd.sht import HealpixSHT
     L, N = args.lmax, args.nside
     Npix = 12 * N * N
     NR = (L + 1) ** 2
     if args.nchains != 1:
         raise SystemExit("masked workload: one chain per GPU (chains shard over GPUs)")
-    dl = fiducial_dl(L, 3)
-    ell = np.arange(L + 1, dtype=np.float64)
-    fac = np.where(ell > 0, 2 * np.pi / np.maximum(ell * (ell + 1), 1), 0.0)
-    cls_ = np.stack([dl[k] * fac for k in ("TT", "EE", "BB", "TE")])
-    np.random.seed(0)
-    fwhm = np.radians(0.5)
-    maps = synfast(cls_, N, L, fwhm)                                   # [3, Npix] device
-    g = torch.Generator(device="cuda").manual_seed(1)
-    sig = torch.tensor([40.0, 0.2, 0.2], dtype=torch.float64, device="cuda")[:, None]
-    d = maps + sig * torch.randn(maps.shape, dtype=torch.float64, device="cuda", generator=g)
-    mask = band_mask(N)
-    mt = torch.from_numpy(mask).cuda()
-    d = (d * mt).cpu().numpy()
-    del maps
-    bl = gauss_beam(fwhm, L)
+    d, mask, dl = _masked_data(N, L, 3)
+    bl = gauss_beam(np.radians(0.5), L)
     cr = MaskedCR({"T": d[0], "Q": d[1], "U": d[2]}, 40.0 ** 2, 0.2 ** 2, bl, L, N, mask=mask, nfields=3,
-                  gibbs_cr=True, n_gibbs=1, rng="native", seed=args.seed, chain=rank)
+                  gibbs_cr=True, n_gibbs=1, rng="native", seed=args.seed, chain=ctx.chain0)
     del d
     bins = {s: np.arange(0, L + 2) for s in ("TT", "EE", "BB", "TE")}
-    plan = GibbsPlan(L, N, 3, 1, bl, [1.0, 1.0, 1.0], bins, chain0=rank)
+    plan = GibbsPlan(L, N, 3, 1, bl, [1.0, 1.0, 1.0], bins, chain0=ctx.chain0)
     d0 = plan.zeros(1, 3, NR)
     dl_t = torch.from_numpy(np.stack([dl[k] for k in ("TT", "EE", "BB", "TE")])).cuda().contiguous()
     s = torch.zeros((3, NR), dtype=torch.float64, device="cuda")
@@ -250,18 +295,13 @@ def run_masked(args, rank, world, dist):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = ctx.max(time.perf_counter() - t0)
     # the transforms the step runs, timed with events on the launch stream
     sht = HealpixSHT(N, L)
     a = torch.zeros((3, NR), dtype=torch.float64, device="cuda")
@@ -278,44 +318,109 @@ def run_masked(args, rank, world, dist):
     torch.cuda.synchronize()
     t_syn = ev[0].elapsed_time(ev[1]) / reps
     t_ana = ev[1].elapsed_time(ev[2]) / reps
-    if rank == 0:
-        fl = sht_flops(N, L)
-        achieved = 2 * fl / ((t_syn + t_ana) * 1e-3) / 1e12
-        line = {
-            "metric": "Gibbs iters/sec (constrained-realization + C_l draw), Nside=%d lmax=%d" % (N, L),
-            "value": round(args.steps * world / elapsed, 4),
-            "unit": "chain-iterations/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (analytic fiducial spectra, synfast on the device + white noise, 80% band mask)",
-            "config": {"workload": "centered TEB masked aux-variable CR (n_gibbs=1)", "nside": N, "lmax": L,
-                       "nfields": 3, "chains_per_gpu": 1, "global_chains": world,
-                       "rng": "native philox4x32-10", "parallelism": f"chains sharded over {world} GPU(s)"},
-            "roofline": {"bound": "fp64", "kernel": "gs_sht alm2map + map2alm (TEB)", "achieved": round(achieved, 2),
-                         "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFS, 4),
-                         "traffic": None, "algorithmic_flops_per_launch": fl,
-                         "avg_launch_ms": {"alm2map": round(t_syn, 3), "map2alm": round(t_ana, 3)}},
-            "cpu_baseline": None,
-            "notes": "healpy is absent, so no CPU SHT baseline at this size; see DESIGN.md",
-        }
-        print(json.dumps(line))
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if ctx.rank != 0:
+        return None
+    fl = sht_flops(N, L, 20)
+    achieved = 2 * fl / ((t_syn + t_ana) * 1e-3) / 1e12
+    return {
+        "metric": METRIC % (N, L),
+        "value": round(args.steps * ctx.world / elapsed, 4),
+        "unit": "chain-iterations/s",
+        "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (analytic fiducial spectra, synfast on the device + white noise, 80% band mask)",
+        "config": {"workload": "centered TEB masked aux-variable CR (n_gibbs=1)", "nside": N, "lmax": L,
+                   "nfields": 3, "chains_per_gpu": 1, "global_chains": ctx.world,
+                   "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
+        "roofline": {"bound": "fp64", "kernel": "gs_sht alm2map + map2alm (TEB)", "achieved": round(achieved, 2),
+                     "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFS, 4),
+                     "traffic": None, "algorithmic_flops_per_launch": fl,
+                     "avg_launch_ms": {"alm2map": round(t_syn, 3), "map2alm": round(t_ana, 3)}},
+        "cpu_baseline": None,
+        "notes": "healpy is absent, so no CPU SHT baseline at this size; see DESIGN.md",
+    }
 
 
-def cpu_baseline(P, args):
-    """Bounded sample of the same workload on one host core (oracle port)."""
-    from oracle import harmonic as H
-    from oracle.cpu_baseline import time_noncentered
-    m = H.Model(P["lmax"], P["nside"], P["nfields"], P["bl"], P["noise_var"], P["bins"], P["blocks"],
-                P["proposal_variances"], P["d_alm"])
-    rate, n, dt = time_noncentered(m, P["dls_init"], budget_s=args.cpu_budget, max_iter=3)
-    return {"value": round(rate, 5), "unit": "chain-iterations/s", "cores": 1, "kind": "port",
-            "sample": f"{n} NonCentered TEB all_sph iteration(s) of 1 chain at Nside={P['nside']} "
-                      f"lmax={P['lmax']} in {dt:.1f} s (vectorised numpy port with the reference's "
-                      f"per-block full-sky likelihood, oracle/cpu_baseline.py)"}
+def run_masked_head(args, ctx):
+    """HEAD's real run modes (main_polarization.py:109-126,154) through the
+    drop-in class surface, EB, one chain per GPU, N_side 256 / L 512 with the
+    reference's Planck BB bins and 1 + 134 Metropolis blocks (config.py:45-55):
+
+      masked_centered_ula  CenteredGibbs(mask, gibbs_cr=True, ula=True): per
+                           iteration the aux-variable CR + MALA composition
+                           (CenteredGibbs.py:831-834) and the C_l draw;
+      masked_asis          ASIS(mask, all_sph=False, gibbs_cr=True, n_gibbs=20,
+                           overrelaxation=True): over-relaxed aux CR (61 SHTs),
+                           centred C_l draw, the pixel-domain MH sweep (f2,
+                           decided on the device), re-centring.
+
+    The reference's init CR (the PCG) runs in the warm-up; the timed region
+    continues the chain for --steps iterations."""
+    import torch
+    from gibbssampler_amd import gibbs as G
+    from gibbssampler_amd.masked import MaskedRunner
+    from gibbssampler_amd.problem import default_bins, default_blocks, proposal_variances, gauss_beam, bin_spectrum
+    L, N = args.lmax, args.nside
+    Npix = 12 * N * N
+    if args.nchains != 1:
+        raise SystemExit("masked run modes: one chain per GPU (chains shard over GPUs)")
+    d, mask, dl = _masked_data(N, L, 2)
+    pix = {"Q": d[1], "U": d[2]}
+    bins = default_bins(L, 2)
+    blocks = default_blocks(L, bins)
+    bl = gauss_beam(np.radians(0.5), L)
+    pv = proposal_variances(L, N, bins, bl, 0.2 ** 2, 40.0 ** 2, fsky=float(np.mean(mask)))
+    init = {s: bin_spectrum(dl[s], bins[s]) for s in ("EE", "BB")}
+    noise_t, noise_p = np.ones(Npix) * 40.0 ** 2, np.ones(Npix) * 0.2 ** 2
+    kw = dict(mask_path=mask, polarization=True, bins=bins, rng="native", seed=args.seed, chain0=ctx.chain0)
+    if args.workload == "masked_centered_ula":
+        smp = G.CenteredGibbs(pix, noise_t, noise_p, 0.5, N, L, Npix, n_iter=args.warmup, gibbs_cr=True, ula=True,
+                              **kw)
+        runner = MaskedRunner(smp.constrained_sampler, smp.bins)
+        n_sht, what = 6, "aux-variable CR (n_gibbs 1) + MALA (CenteredGibbs.py:831-834), EB"
+        h = runner.run(init, max(args.warmup, 1), None)[0]
+        last = {s: h[s][-1] for s in h}
+        go = lambda: runner.run(last, args.steps, runner.s)
+    else:
+        smp = G.ASIS(pix, noise_t, noise_p, 0.5, N, L, Npix, pv, metropolis_blocks=blocks, n_iter=args.warmup,
+                     all_sph=False, gibbs_cr=True, n_gibbs=20, overrelaxation=True, **kw)
+        runner = smp.masked_runner
+        n_sht, what = 61 + 2, ("over-relaxed aux CR n_gibbs 20 (CenteredGibbs.py:733-825), pixel-domain MH "
+                               f"over {runner.mh.K} blocks decided on the device (f2), EB")
+        h = runner.run(init, max(args.warmup, 1))[0]
+        last = {s: h[s][-1] for s in h}
+        go = lambda: runner.run(last, args.steps, s_init=runner.s)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    go()
+    torch.cuda.synchronize()
+    elapsed = ctx.max(time.perf_counter() - t0)
+    if ctx.rank != 0:
+        return None
+    fl = n_sht * sht_flops(N, L, 16)
+    achieved = fl / (elapsed / args.steps) / 1e12
+    return {
+        "metric": METRIC % (N, L),
+        "value": round(args.steps * ctx.world / elapsed, 4),
+        "unit": "chain-iterations/s",
+        "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (analytic fiducial EB spectra, synfast on the device + white noise, 80% band mask)",
+        "config": {"workload": f"{args.workload}: {what}", "surface": "gibbssampler_amd.gibbs (drop-in classes)",
+                   "nside": N, "lmax": L, "nfields": 2, "chains_per_gpu": 1, "global_chains": ctx.world,
+                   "bins": "config.py:45 Planck BB", "blocks": "config.py:51-55",
+                   "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
+        "roofline": {"bound": "fp64", "kernel": f"{n_sht} spin-2 SHT-equivalents per iteration",
+                     "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP64_VALU_PEAK_TFS, 4), "traffic": None,
+                     "algorithmic_flops_per_step": fl},
+        "cpu_baseline": None,
+        "notes": "healpy is absent: no CPU SHT baseline for the masked modes (DESIGN.md 7)",
+    }
 
 
 if __name__ == "__main__":

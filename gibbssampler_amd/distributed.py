@@ -5,7 +5,10 @@ here a node's GPUs each run a contiguous block of chains of one global run:
 rank r owns global chains [r*K, (r+1)*K).  RNG streams are keyed by the
 global chain id, so a chain's trajectory does not depend on the GPU count.
 No collective runs inside an iteration; the D_l traces are gathered once
-(``gather_traces``: one all_gather over RCCL/xGMI, or gloo on CPU).
+(one all_gather over RCCL/xGMI, or gloo on CPU).
+
+One code path for every caller: ``bench.py`` and the ``gibbs.py`` class
+surface (``distributed=True``) both use ``ShardContext``.
 """
 import os
 
@@ -22,6 +25,72 @@ def shard_chains(world_size, rank, chains_per_rank):
         raise ValueError("rank out of range")
     c0 = rank * chains_per_rank
     return list(range(c0, c0 + chains_per_rank))
+
+
+class ShardContext:
+    """The run's place in a torchrun job: world size, rank, local GPU, the
+    first global chain of this rank, and the three host-side collectives the
+    run needs (barrier, max of a scalar, trace gather).  world_size 1 without
+    torch.distributed is the single-process case (every call is local).
+
+    backend: "nccl" (RCCL, one GPU per rank) or "gloo" (CPU; tests)."""
+
+    def __init__(self, chains_per_rank, backend="nccl", init=True):
+        import torch
+        import torch.distributed as dist
+        self.world, self.rank, self.local = dist_env()
+        self.chains_per_rank = int(chains_per_rank)
+        self.chain0 = self.rank * self.chains_per_rank
+        self.backend = backend
+        self.device = torch.device("cuda", self.local) if backend == "nccl" else torch.device("cpu")
+        self._owns_group = False
+        if self.world > 1:
+            if not dist.is_initialized():
+                if not init:
+                    raise RuntimeError("WORLD_SIZE > 1 but torch.distributed is not initialised")
+                kw = {"device_id": self.device} if backend == "nccl" else {}
+                dist.init_process_group(backend, **kw)
+                self._owns_group = True
+            if dist.get_world_size() != self.world:
+                raise RuntimeError("WORLD_SIZE does not match the process group")
+        self.dist = dist if self.world > 1 else None
+
+    @property
+    def global_chains(self):
+        return self.world * self.chains_per_rank
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, value):
+        """max over ranks of a host float (the timed region's wall time)."""
+        if self.dist is None:
+            return float(value)
+        import torch
+        t = torch.tensor([float(value)], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, trace, dim=1):
+        """all_gather a per-rank tensor and concatenate along ``dim`` (the chain
+        axis) in rank order = global chain order."""
+        if self.dist is None:
+            return trace
+        import torch
+        dev = trace.device
+        t = trace.contiguous()
+        if self.backend == "gloo" and t.is_cuda:
+            t = t.cpu()                      # gloo gathers host tensors
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return torch.cat(parts, dim=dim).to(dev)
+
+    def close(self):
+        if self.dist is not None and self._owns_group:
+            self.dist.barrier()
+            self.dist.destroy_process_group()
+            self._owns_group = False
 
 
 def gather_traces(trace, group=None):

@@ -30,7 +30,11 @@ Extra keyword arguments (all optional): ``nchains`` (batched chains on one
 GPU), ``rng`` ("native" Philox or "replay" = numpy's global RNG in the
 reference's draw order), ``seed`` (native streams), ``fields`` ("EB" or
 "TEB" for polarization), ``chain0`` (global id of the first chain),
-``reference_quirks`` (ASIS re-centring of the centered map, ASIS.py:203).
+``reference_quirks`` (ASIS re-centring of the centered map, ASIS.py:203),
+``distributed`` (one process per GPU under torchrun: this rank runs global
+chains [rank * nchains, (rank + 1) * nchains) and ``run()`` returns every
+rank's chains, all-gathered over RCCL -- the reference's SLURM array,
+job-script.sh:6-8), ``dist_backend`` ("nccl" = RCCL, or "gloo").
 """
 import time
 
@@ -135,7 +139,21 @@ class GibbsSampler:
     def __init__(self, pix_map, noise, beam_fwhm_deg, nside, lmax, polarization=False, bins=None, n_iter=10000,
                  gibbs_cr=False, rj_step=False, ula=False, *, nchains=1, rng="native", seed=0, fields=None,
                  chain0=0, reference_quirks=True, noise_pol=None, proposal_variances=None,
-                 metropolis_blocks=None, n_iter_metropolis=1, mask_path=None):
+                 metropolis_blocks=None, n_iter_metropolis=1, mask_path=None, distributed=False,
+                 dist_backend=None):
+        self.shard = None
+        if distributed:
+            # one process per GPU under torchrun: this rank runs global chains
+            # [rank * nchains, (rank + 1) * nchains); run() returns every rank's
+            # chains (histories all-gathered over RCCL) -- the role of the
+            # reference's SLURM array (job-script.sh:6-8)
+            import torch
+            from .distributed import ShardContext
+            backend = dist_backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            self.shard = ShardContext(nchains, backend=backend)
+            if backend == "nccl":
+                torch.cuda.set_device(self.shard.local)
+            chain0 = self.shard.chain0
         self.mask = None
         if mask_path is not None:
             self.mask = _load_mask(mask_path, nside)
@@ -276,12 +294,13 @@ class GibbsSampler:
                               quirk=self.reference_quirks)
 
     def _squeeze(self, a):
-        return a[:, 0] if self.nchains == 1 else a
+        return a[:, 0] if a.shape[1] == 1 else a
 
     def _run_common(self, dls_init):
         runner = self._make_runner()
         init = dls_init if isinstance(dls_init, dict) else {self.spectra[0]: dls_init}
-        h, acc, t = runner.run(init, self.n_iter, timings=True)
+        h, acc, t = runner.run(init, self.n_iter, timings=True,
+                               gather=self.shard.gather if self.shard is not None else None)
         h = {s: self._squeeze(v) for s, v in h.items()}
         if acc is not None:
             acc = {s: self._squeeze(v) for s, v in acc.items()}

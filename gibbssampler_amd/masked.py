@@ -491,7 +491,9 @@ class MaskedMHRunner:
     def _pcg(self, dl, it):
         return self.cr.pcg_solve(dl, self.cr.pcg_rhs(dl, iteration=it))
 
-    def run(self, dls_init, n_iter):
+    def run(self, dls_init, n_iter, s_init=None):
+        """n_iter iterations from dls_init (binned dict).  s_init: continue from
+        this map instead of the reference's PCG start map (ASIS.py:153-156)."""
         cr, mh, plan = self.cr, self.mh, self.plan
         cur = plan.dl_tensor({s: np.asarray(dls_init[s], dtype=np.float64) for s in mh.spectra})[0]
         h = {s: [np.asarray(dls_init[s], dtype=np.float64).copy()] for s in mh.spectra}
@@ -499,7 +501,9 @@ class MaskedMHRunner:
         acc_cr, t_it, t_cr, t_cls, t_nc = [], [], [], [], []
         dl = mh.unfold(cur)
         s = None
-        if self.kind == "asis" and self.cr_kind != KIND_PCG:
+        if s_init is not None:
+            s = cr._s(s_init)
+        elif self.kind == "asis" and self.cr_kind != KIND_PCG:
             s = self._pcg(dl, 0)          # ASIS.py:153-156: the start map from the PCG
         for i in range(n_iter):
             it = i + 1

@@ -110,7 +110,8 @@ class BatchedRunner:
         self.graph_steps = 1
         return g
 
-    def capture_steps(self, nsteps, trace=None, trace_capacity=None, time_sweeps=False, time_every=1):
+    def capture_steps(self, nsteps, trace=None, trace_capacity=None, time_sweeps=False, time_every=1,
+                      accept_trace=None):
         """Native RNG: capture ``nsteps`` whole iterations in ONE hipGraph (one
         replay = nsteps steps).  time_sweeps: bracket the CR-sweep kernel of every
         ``time_every``-th step by event-record nodes (plan.sweep_timing), so the
@@ -128,17 +129,19 @@ class BatchedRunner:
             for i in range(nsteps):
                 if time_sweeps:
                     p.sweep_timing("resume" if i % time_every == 0 else "pause")
+                # accept_trace [nsteps, nchains, nacc]: step i writes its own slot
+                acc = self.accept if accept_trace is None else accept_trace[i]
                 if self.kind == "noncentered":
                     p.nc_prologue(self.dl, seed=self.seed)
                     p.nc_sweep(self.d, self.s, seed=self.seed, finish=False)
                     p.nc_finish()
-                    p.nc_decide_fused(self.dl, seed=self.seed, accept=self.accept, trace=trace,
+                    p.nc_decide_fused(self.dl, seed=self.seed, accept=acc, trace=trace,
                                       capacity=trace_capacity or 0)
                 elif self.kind == "centered":
                     p.step_centered_fused(self.d, self.dl, self.s, seed=self.seed, trace=trace,
                                           capacity=trace_capacity or 0)
                 else:
-                    p.step_asis_fused(self.d, self.dl, self.s, seed=self.seed, accept=self.accept,
+                    p.step_asis_fused(self.d, self.dl, self.s, seed=self.seed, accept=acc,
                                       dl_tmp=self.dl_tmp, recentre=self.materialize_recentre, trace=trace,
                                       capacity=trace_capacity or 0)
         self.graph = g
@@ -170,7 +173,11 @@ class BatchedRunner:
         self.iteration = it
 
     # -- a whole run --------------------------------------------------------------------
-    def run(self, dls_init, n_iter, timings=False):
+    def run(self, dls_init, n_iter, timings=False, gather=None, graph_chunk=32):
+        """n_iter iterations from dls_init; returns (histories, accepts[, step
+        times]).  gather: ShardContext.gather of a torchrun job -- the device
+        histories of every rank are all-gathered along the chain axis (global
+        chain order) before the one copy to the host."""
         p = self.plan
         self.init(dls_init)
         with_start = self.kind != "asis"
@@ -179,6 +186,33 @@ class BatchedRunner:
         if with_start:
             H[0].copy_(self.dl)
         t_steps = []
+        if self.rng == "native" and graph_chunk and n_iter > 0:
+            # the iterations as replays of one captured hipGraph of `chunk` steps
+            # (device-side D_l / accept traces, no host synchronisation inside a
+            # chunk); step times = chunk time / steps from events on the stream
+            chunk = min(int(graph_chunk), n_iter)
+            off = 1 if with_start else 0
+            trace = p.zeros(chunk, p.nchains, p.nspec, p.maxbins)
+            acc_tr = p.zeros(chunk, p.nchains, max(p.nacc, 1), dtype=torch.int32)
+            done, gsteps = 0, 0
+            while done < n_iter:
+                k = min(chunk, n_iter - done)
+                if k != gsteps:
+                    self.capture_steps(k, trace=trace, trace_capacity=chunk, accept_trace=acc_tr)
+                    gsteps = k
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                self.step()
+                e1.record()
+                H[off + done:off + done + k].copy_(trace[:k])
+                A[done:done + k].copy_(acc_tr[:k])
+                if timings:
+                    e1.synchronize()
+                    t_steps += [e0.elapsed_time(e1) * 1e-3 / k] * k
+                done += k
+            self.graph = None
+            p.iteration_counter(False)
+            n_iter = 0
         for i in range(n_iter):
             t0 = time.perf_counter() if timings else 0.0
             self.step()
@@ -188,6 +222,10 @@ class BatchedRunner:
             if timings:
                 torch.cuda.synchronize()
                 t_steps.append(time.perf_counter() - t0)
+        if gather is not None:
+            H = gather(H, dim=1)
+            if self.kind != "centered":
+                A = gather(A, dim=1)
         Hn = H.cpu().numpy()
         hist = {s: Hn[:, :, k, :len(p.bins[s]) - 1] for k, s in enumerate(p.spectra)}
         acc = None

@@ -1,4 +1,4 @@
-"""CPU baseline for bench.py (TEST/MEASUREMENT INFRASTRUCTURE, single core numpy).
+"""CPU baseline for bench.py (TEST/MEASUREMENT INFRASTRUCTURE, numpy, one chain per core).
 
 A vectorised numpy port of the reference's non-centered all_sph Gibbs
 iteration with the reference's per-call work structure
@@ -15,7 +15,19 @@ the build specifies it:
 Pure-Python loops of the reference (generate_var_cl_cython, utils.py:114-135)
 are replaced by numpy indexing, so this baseline is FASTER than the reference
 itself (SURVEY.md 6 measured 374.7 ms per generate_var_cl call at L=1024).
+
+``nc_iteration_matched`` is the algorithm-matched port: the same iteration
+with the GPU's per-l sufficient statistics (one statistics pass after the
+CR; per spectrum the per-l likelihood terms of the current and the proposed
+D_l once, each block summing its own l) -- the CPU figure the GPU's gain is
+attributable against.
+
+``python -m oracle.cpu_baseline --cores N ...`` runs one chain per core
+(worker processes, one numpy thread each) for a fixed wall budget and prints
+one JSON line; bench.py starts it as a child process before it touches the GPU.
 """
+import json
+import os
 import time
 
 import numpy as np
@@ -84,17 +96,105 @@ def nc_iteration(model, dl_binned, sl=None):
     return cur
 
 
-def time_noncentered(model, dl_init, budget_s=20.0, max_iter=5, seed=0):
-    """Run NC iterations until the time budget is spent; returns (iters/s, n)."""
+def nc_iteration_matched(model, dl_binned, sl=None):
+    """One NonCenteredGibbs all_sph iteration with per-l statistics (the GPU's
+    algorithm): CR, the statistics sum_m s s / d s per l, then per spectrum in
+    MH order the per-l terms f_l of the current and of the proposed D_l (blocks
+    of one spectrum cover disjoint l), each block's log ratio a sum over its l."""
+    un = model.unfold(dl_binned)
+    M, Lc = H.noncentered_params(model, un)
+    z = np.stack([np.random.normal(size=H.nreal(model.L)) for _ in range(model.nfields)])
+    s_nc = H.cr_apply(model, M, Lc, model.d_alm, z)
+    stats = H.sweep_stats(model, s_nc, model.d_alm)
+    cur = {s: np.array(v, dtype=np.float64) for s, v in dl_binned.items()}
+    order = list(model.spectra) if model.nfields != 3 else ["EE", "BB", "TT", "TE"]
+    from scipy.special import ndtri
+    prop, logr = {}, {}
+    for s in order:                      # proposals first, the reference's draw order
+        sd = np.sqrt(model.proposal_variances[s])
+        old = cur[s][2:]
+        u = np.random.uniform(size=len(old))
+        if s == "TE":
+            p, lr = old + sd * ndtri(u), np.zeros(len(old))
+        else:
+            p = old + sd * H.truncnorm_ppf_std(u, -old / sd)
+            lr = H.truncnorm_log_ratio(old, p, sd)
+        prop[s] = np.concatenate([cur[s][:2], p])
+        logr[s] = np.concatenate([np.zeros(2), lr])
+    for s in order:
+        alt = {k: v.copy() for k, v in cur.items()}
+        alt[s] = prop[s]
+        un_alt = model.unfold(alt)
+        f_cur = H.nc_loglik_terms(model, model.unfold(cur), stats)
+        f_alt = H.nc_loglik_terms(model, un_alt, stats)
+        edges, nb = model.blocks[s], len(cur[s])
+        bins = model.bins[s]
+        for i in range(len(edges) - 1):
+            lo, hi = int(edges[i]), min(int(edges[i + 1]), nb)
+            ells = np.arange(bins[lo], bins[hi]) if hi > lo else np.arange(0)
+            ok = H._psd_ok(model, un_alt, ells)
+            dlik = float(np.sum(f_alt[ells] - f_cur[ells])) if ok else -np.inf
+            log_r = dlik + float(np.sum(logr[s][lo:hi]))
+            if np.log(np.random.uniform()) < log_r:
+                cur[s][lo:hi] = prop[s][lo:hi]
+    return cur
+
+
+def time_noncentered(model, dl_init, budget_s=20.0, max_iter=5, seed=0, matched=False):
+    """Run NC iterations until the time budget is spent; returns (iters/s, n, seconds)."""
     np.random.seed(seed)
     sl = H.slot_ell(model.L)
+    step = nc_iteration_matched if matched else nc_iteration
     cur = dl_init
     t0 = time.perf_counter()
     n = 0
     while n < max_iter:
-        cur = nc_iteration(model, cur, sl)
+        cur = step(model, cur, sl)
         n += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     return n / dt, n, dt
+
+
+def _worker(args):
+    lmax, nside, fields, budget, max_iter, chain, matched = args
+    from gibbssampler_amd.problem import synthetic_problem
+    P = synthetic_problem(lmax, nside, fields, seed=0)
+    m = H.Model(P["lmax"], P["nside"], P["nfields"], P["bl"], P["noise_var"], P["bins"], P["blocks"],
+                P["proposal_variances"], P["d_alm"])
+    rate, n, dt = time_noncentered(m, P["dls_init"], budget_s=budget, max_iter=max_iter, seed=1000 + chain,
+                                   matched=matched)
+    return rate, n, dt
+
+
+def run_parallel(lmax, nside, fields, budget, cores, matched, max_iter=1000):
+    """One chain per worker process (numpy single-threaded in each), summed rate."""
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_worker, [(lmax, nside, fields, budget, max_iter, c, matched) for c in range(cores)])
+    return sum(r for r, _, _ in res), sum(n for _, n, _ in res), max(d for _, _, d in res)
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lmax", type=int, default=1024)
+    ap.add_argument("--nside", type=int, default=512)
+    ap.add_argument("--fields", type=int, default=3)
+    ap.add_argument("--budget", type=float, default=10.0)
+    ap.add_argument("--cores", type=int, default=0, help="0: the process's CPU affinity, at most 16")
+    a = ap.parse_args()
+    cores = a.cores or min(len(os.sched_getaffinity(0)), 16)
+    out = {"cores": cores, "affinity": len(os.sched_getaffinity(0))}
+    for key, matched in (("reference", False), ("matched", True)):
+        rate, n, dt = run_parallel(a.lmax, a.nside, a.fields, a.budget, cores, matched)
+        out[key] = {"value": rate, "iterations": n, "seconds": dt}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    for v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ[v] = "1"
+    main()

@@ -1,14 +1,16 @@
-"""world_size-2 gloo test of the multi-GPU path's host logic on CPU: each rank
-computes its shard of chains with the (oracle) counter streams and the traces
-are all-gathered; the result equals the single-process computation, i.e. a
-chain's trajectory does not depend on the GPU count."""
+"""world_size-2 gloo test of the multi-GPU path's host logic on CPU, through the
+same functions bench.py and the class surface use (gibbssampler_amd.distributed
+.ShardContext): each rank gets its chain offset from the torchrun environment
+(and the drop-in NonCenteredGibbs(distributed=True) the same offset), computes
+its shard of chains with the (oracle) counter streams, takes the max of its
+wall time and all-gathers the traces; the result equals the single-process
+computation, i.e. a chain's trajectory does not depend on the GPU count."""
 import os
 import socket
 
 import numpy as np
 import pytest
 import torch
-import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
@@ -42,16 +44,28 @@ def _worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from gibbssampler_amd.distributed import shard_chains, gather_traces
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    from gibbssampler_amd.distributed import ShardContext, shard_chains
+    from gibbssampler_amd import gibbs as G
+    from tests._util import make_problem
+    ctx = ShardContext(2, backend="gloo")
+    assert (ctx.world, ctx.rank, ctx.chain0, ctx.global_chains) == (world, rank, 2 * rank, 4)
     mine = shard_chains(world, rank, 2)
+    assert mine == [ctx.chain0, ctx.chain0 + 1]
+    # the drop-in surface takes the same offset from the same context type
+    m, init = make_problem(12, 8, 2, seed=3)
+    smp = G.NonCenteredGibbs({"EE": m.d_alm[0], "BB": m.d_alm[1]}, 40.0 ** 2, 0.2 ** 2, 1.0, 8, 12, 768,
+                             m.proposal_variances, metropolis_blocks=m.blocks, polarization=True, bins=m.bins,
+                             n_iter=3, all_sph=True, nchains=2, distributed=True, dist_backend="gloo")
+    assert smp.chain0 == ctx.chain0 and smp.shard.global_chains == 4
     t = torch.from_numpy(_chain_trace(mine))
-    full = gather_traces(t)
+    full = ctx.gather(t)
+    slowest = ctx.max(float(rank + 1))
     if rank == 0:
-        q.put(full.numpy())
-    dist.barrier()
+        q.put((full.numpy(), slowest))
+    ctx.barrier()
+    import torch.distributed as dist
     dist.destroy_process_group()
 
 
@@ -64,9 +78,10 @@ def test_two_rank_gather_equals_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full = q.get(timeout=240)
+    full, slowest = q.get(timeout=240)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
+    assert slowest == 2.0
     ref = _chain_trace(list(range(4)))
     np.testing.assert_array_equal(full, ref)

@@ -131,3 +131,20 @@ def test_mh_blocks_of_one_spectrum_are_independent():
     changed = np.nonzero(f1 != f0)[0]
     b = m.bins["BB"]
     assert set(changed) <= set(range(b[5], b[6]))
+
+
+def test_cpu_baseline_ports_agree():
+    """The two CPU baselines of bench.py (oracle/cpu_baseline.py) are the same
+    chain: the reference-structured port (full-sky likelihood per block) and the
+    algorithm-matched port (per-l statistics) take the same decisions from the
+    same numpy draws (EB and TEB)."""
+    from oracle import cpu_baseline as CB
+    from tests._util import make_problem
+    for F in (2, 3):
+        m, init = make_problem(24, 16, F, seed=4)
+        np.random.seed(5)
+        a = CB.nc_iteration(m, init)
+        np.random.seed(5)
+        b = CB.nc_iteration_matched(m, init)
+        for s in m.spectra:
+            np.testing.assert_allclose(a[s], b[s], rtol=1e-12)
