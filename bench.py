@@ -201,7 +201,7 @@ def run_harmonic(args, ctx, cpu):
     achieved = alg_bytes / (sweep_avg_ms * 1e-3) / 1e9
     prof = load_profile(args.profile_json, f"{args.workload}_L{args.lmax}_F{args.fields}_c{p.nchains}")
     return {
-        "metric": METRIC % (512, 1024),
+        "metric": METRIC % (args.nside, args.lmax),
         "value": round(total / elapsed, 3),
         "unit": "chain-iterations/s",
         "n_gpus": ctx.world,

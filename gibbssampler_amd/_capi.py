@@ -96,7 +96,7 @@ _SIGS = [
     ("gs_step_noncentered", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
                                            _VP, _VP]),
     ("gs_nc_prologue", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP]),
-    ("gs_nc_sweep", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, _VP]),
+    ("gs_nc_sweep", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, _VP]),
     ("gs_nc_finish", ctypes.c_int, [_VP, _VP]),
     ("gs_nc_decide", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
     ("gs_nc_decide_fused", ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP, ctypes.c_int, _VP]),

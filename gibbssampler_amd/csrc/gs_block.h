@@ -55,18 +55,20 @@ __device__ __forceinline__ CovChol cov_chol_teb(double tt, double ee, double te,
 // MODE 0 centered (CenteredGibbs.py:324-351):   Sigma = (C^+ + diag(b^2 k))^-1, M = Sigma diag(b k)
 // MODE 1 non-centered (NonCenteredGibbs.py:141-174): Sigma = (I + A^T diag(b^2 k) A)^-1,
 //                                                   M = Sigma A^T diag(b k), A = chol(C)
+// the operator of one (chain, l) into registers (the CR sweep computes its own
+// lanes' operators this way; block_params_at stores them)
 template <int F, int MODE>
-__device__ __forceinline__ void block_params_at(int g, int L, int nchains, int maxbins, const double* __restrict__ dl,
-                                                const int* __restrict__ ell2bin, const double* __restrict__ bl,
-                                                double k0, double k1, double k2, double* __restrict__ params) {
+__device__ __forceinline__ void block_params_compute(int chain, int ell, int L, int maxbins,
+                                                     const double* __restrict__ dl, const int* __restrict__ ell2bin,
+                                                     const double* __restrict__ bl, double k0, double k1, double k2,
+                                                     double (&p)[gs_block::NP]) {
     const int Lp1 = L + 1;
-    if (g >= nchains * Lp1) return;
-    const int chain = g / Lp1, ell = g % Lp1;
     constexpr int NS = F == 1 ? 1 : (F == 2 ? 2 : 4);
     const double* dlc = dl + (long long)chain * NS * maxbins;
     const double b = bl[ell];
-    double* p = params + (long long)g * gs_block::NP;
     const double kap[3] = {k0, k1, k2};
+#pragma unroll
+    for (int q = 0; q < gs_block::NP; ++q) p[q] = 0.0;
     if constexpr (F != 3) {
 #pragma unroll
         for (int f = 0; f < F; ++f) {
@@ -130,5 +132,19 @@ __device__ __forceinline__ void block_params_at(int g, int L, int nchains, int m
         p[0] = M00; p[1] = M01; p[2] = M10; p[3] = M11; p[4] = M22;
         p[5] = l00; p[6] = l10; p[7] = l11; p[8] = sqrt(s22); p[9] = 0.0;
     }
+}
+
+template <int F, int MODE>
+__device__ __forceinline__ void block_params_at(int g, int L, int nchains, int maxbins, const double* __restrict__ dl,
+                                                const int* __restrict__ ell2bin, const double* __restrict__ bl,
+                                                double k0, double k1, double k2, double* __restrict__ params) {
+    const int Lp1 = L + 1;
+    if (g >= nchains * Lp1) return;
+    double p[gs_block::NP];
+    block_params_compute<F, MODE>(g / Lp1, g % Lp1, L, maxbins, dl, ell2bin, bl, k0, k1, k2, p);
+    double* o = params + (long long)g * gs_block::NP;
+    constexpr int NW = F == 3 ? gs_block::NP : 2 * F;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) o[q] = p[q];
 }
 

@@ -53,6 +53,11 @@ struct gs_plan {
     int nacc = 0;                    // accept flags per chain
     int mh_order[4] = {0, 1, 2, 3};
     bool has_mh = false;
+    // the CR operator computed per lane inside the sweep (no block-parameter
+    // launch) only for few chains: there a step is launch-bound; with many
+    // chains the per-workgroup recomputation costs more than the table
+    // (measured: 32 TEB chains at L 1024, sweep 271 -> 287 us)
+    bool inkernel_params = false;
     // MH phases: spectra whose blocks are mutually independent run in one launch
     int nphase = 0;
     int phase_n[4] = {0, 0, 0, 0};
@@ -280,6 +285,18 @@ __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const doub
     }
 }
 
+// where the sweep's per-l operator comes from: mode -1 the params table;
+// GS_MODE_CENTERED / GS_MODE_NONCENTERED computed per lane from the chain's
+// binned D_l (saves the block-parameter launch of a step)
+struct SweepOp {
+    int mode;
+    int maxbins;
+    const double* dl;
+    const int* ell2bin;
+    const double* bl;
+    double k0, k1, k2;
+};
+
 // Tiling of the (l, m) triangle: 64-wide l tiles, descending from l = L
 // (tile t holds l in [L-64t-63, L-64t]); a workgroup = 4 waves = 4 adjacent
 // tiles (256 consecutive l) x one chunk of TM rows m, so every row of the
@@ -292,7 +309,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
                                                   const double* __restrict__ params, const double* __restrict__ z,
                                                   double* __restrict__ s, double* __restrict__ partials,
                                                   uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, uint32_t substep,
-                                                  int chain0) {
+                                                  int chain0, SweepOp op) {
     const uint32_t iter = itarg.get();
     constexpr int NS = SweepAcc<F>::NS;
     __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
@@ -325,7 +342,15 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const uint32_t tag = TAG_CR | (substep << 8);
 
     double pm[NP];
-    if (ZM != 2 && lane_ok) {
+    if (ZM != 2 && lane_ok && op.mode >= 0) {
+        // this lane's l: the operator from the chain's D_l (no parameter table)
+        if (op.mode == GS_MODE_CENTERED)
+            block_params_compute<F, GS_MODE_CENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
+                                                      op.k1, op.k2, pm);
+        else
+            block_params_compute<F, GS_MODE_NONCENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
+                                                         op.k1, op.k2, pm);
+    } else if (ZM != 2 && lane_ok) {
         const double* pp = params + ((long long)chain * (L + 1) + ell) * NP;
 #pragma unroll
         for (int q = 0; q < NP; ++q) pm[q] = pp[q];
@@ -409,6 +434,23 @@ __global__ void k_stats_finish(int L, int nchains, int ntile, int nchunk, int tm
 // gamma draws are latency chains: one per thread, not a loop per thread).
 // Optional epilogue of graph-captured centered steps (as MhEpi): the trace
 // record of every bin and the device counter advance by the last workgroup.
+// device iteration counter advance by the last workgroup of a launch (ticket
+// in counter[1]).  Every workgroup read counter[0] at its start and has used
+// the value before the barrier, so the last ticket may advance it; no data is
+// handed between workgroups here, so no release / acquire fence is needed
+// (an agent-scope __threadfence costs ~3.5 us per workgroup,
+// MI355X_MICROARCH.md visibility table); the next launch sees the counter.
+__device__ __forceinline__ void ticket_advance(uint32_t* counter, uint32_t nblk) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(&counter[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == nblk - 1) {
+            __hip_atomic_store(&counter[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&counter[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <int F>
 __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __restrict__ bins,
                                               const int* __restrict__ nbins_arr, const double* __restrict__ stats,
@@ -506,19 +548,7 @@ __global__ __launch_bounds__(64) void k_cls_draw(int L, int nchains, int maxbins
     const uint32_t iter = itarg.get();
     cls_draw_body<F>(L, maxbins, bins, nbins_arr, stats, variates, seed_lo, seed_hi, iter, chain0, dl_out, trace,
                      cap, nchains);
-    if (counter) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            const uint32_t nblk = gridDim.x * gridDim.y * gridDim.z;
-            const uint32_t t = atomicAdd(&counter[1], 1u);
-            if (t == nblk - 1) {
-                counter[1] = 0u;
-                __threadfence();
-                atomicAdd(&counter[0], 1u);
-            }
-        }
-    }
+    if (counter) ticket_advance(counter, gridDim.x * gridDim.y * gridDim.z);
 }
 
 
@@ -966,18 +996,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
         for (int k = tid; k < nrow; k += blockDim.x) tr[k] = Ds[k];
     }
-    if (epi.counter) {
-        __syncthreads();
-        if (tid == 0) {
-            __threadfence();
-            const uint32_t t = atomicAdd(&epi.counter[1], 1u);
-            if (t == gridDim.x - 1) {
-                epi.counter[1] = 0u;
-                __threadfence();
-                atomicAdd(&epi.counter[0], 1u);
-            }
-        }
-    }
+    if (epi.counter) ticket_advance(epi.counter, gridDim.x);
 }
 
 // stats of s_nc = A^+ s, A = chol(C(dl)) (ASIS.py:185-189)
@@ -1304,6 +1323,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_upload(&p->ell2blk, e2k);
     rc |= dev_alloc(&p->gbuf, (size_t)p->nchains * 2 * (L + 1));
     build_tasks(p);
+    p->inkernel_params = p->nchains <= 4;
     const size_t nc = (size_t)p->nchains;
     rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunk * p->nstat * WAVE);
     rc |= dev_alloc(&p->params, nc * (L + 1) * NP);
@@ -1476,9 +1496,11 @@ static int stats_finish(gs_plan* p, double* stats, void* stream) {
 
 static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
                         uint32_t iteration, uint32_t substep, double* s_out, double* stats, bool given,
-                        void* stream, bool finish = true) {
+                        void* stream, bool finish = true, int pmode = -1, const double* dl = nullptr) {
     if (check_plan(p)) return -1;
-    if (!d_alm || !stats || (!given && !params) || (given && !s_out)) return set_error("gs_cr_sweep: null argument");
+    if (!d_alm || !stats || (!given && !params && pmode < 0) || (given && !s_out) || (pmode >= 0 && !dl))
+        return set_error("gs_cr_sweep: null argument");
+    const SweepOp op{pmode, p->maxbins, dl, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2]};
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const dim3 g((unsigned)((long long)p->nchains * p->npair)), b(256);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1486,7 +1508,8 @@ static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, c
     const bool rep = z != nullptr, st = s_out != nullptr;
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunk, p->rows_per_task, p->tasks, d_alm, params, z, s_out,         \
-                                             p->partials, slo, shi, IterArg{iteration, p->itp()}, substep, p->chain0)
+                                             p->partials, slo, shi, IterArg{iteration, p->itp()}, substep, p->chain0, \
+                                             op)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
                         else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
                         else GS_SW(FF, 0, false); } while (0)
@@ -1654,13 +1677,22 @@ int gs_recentre(gs_plan* p, const double* dl_new, const double* dl_old, double* 
     return 0;
 }
 
+// the CR of a step: block parameters of dl (mode) + the sweep, the operator
+// either from the parameter table (many chains) or computed inside the sweep
+static int step_sweep(gs_plan* p, int mode, const double* d_alm, const double* dl, const double* z, uint64_t seed,
+                      uint32_t it, double* s_out, void* stream, bool finish = true) {
+    if (p->inkernel_params)
+        return sweep_launch(p, d_alm, nullptr, z, seed, it, 0, s_out, p->stats, false, stream, finish, mode, dl);
+    if (gs_block_params(p, mode, dl, p->params, stream)) return -1;
+    return sweep_launch(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, false, stream, finish);
+}
+
 // ---- fused iterations ------------------------------------------------------
 int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
                      const double* igvar, uint64_t seed, uint32_t it, void* stream) {
     if (check_plan(p)) return -1;
     if (!d_alm || !dl) return set_error("gs_step_centered: null argument");
-    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
-    if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
+    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, z, seed, it, s_out, stream)) return -1;
     return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
 }
 
@@ -1670,8 +1702,7 @@ int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* 
     if (!p->iter_dev_on) return set_error("gs_step_centered_fused: device iteration counter not enabled");
     if (trace && capacity < 1) return set_error("gs_step_centered_fused: capacity < 1");
     if (!d_alm || !dl) return set_error("gs_step_centered_fused: null argument");
-    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
-    if (gs_cr_sweep(p, d_alm, p->params, nullptr, seed, it, 0, s_out, p->stats, stream)) return -1;
+    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream)) return -1;
     return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->iter_dev, stream);
 }
 
@@ -1681,7 +1712,8 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
     if (!dl) return set_error("gs_nc_prologue: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const int nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
-    const int nbq = nblk((long long)p->nchains * (p->L + 1), 256);
+    // block parameters here (table) unless the sweep computes them per lane
+    const int nbq = p->inkernel_params ? 0 : nblk((long long)p->nchains * (p->L + 1), 256);
     // native mode: the MH accept uniforms are drawn here too (replay draws them on the host)
     p->u_nat_ready = u_prop == nullptr && p->nacc > 0 && !getenv("GS_MH_INKERNEL_UNIFORMS");
     const int nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
@@ -1696,9 +1728,13 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
     return 0;
 }
 
-int gs_nc_sweep(gs_plan* p, const double* d_alm, double* s_out, const double* z, uint64_t seed, uint32_t it,
-                int finish, void* stream) {
+int gs_nc_sweep(gs_plan* p, const double* d_alm, const double* dl, double* s_out, const double* z, uint64_t seed,
+                uint32_t it, int finish, void* stream) {
     if (check_plan(p)) return -1;
+    if (!dl) return set_error("gs_nc_sweep: null argument");
+    if (p->inkernel_params)
+        return sweep_launch(p, d_alm, nullptr, z, seed, it, 0, s_out, p->stats, false, stream, finish != 0,
+                            GS_MODE_NONCENTERED, dl);
     return sweep_launch(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, false, stream, finish != 0);
 }
 
@@ -1734,7 +1770,7 @@ int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_o
     if (!p->has_mh) return set_error("gs_step_noncentered: plan has no MH blocks / proposal variances");
     if (!d_alm || !dl) return set_error("gs_step_noncentered: null argument");
     if (gs_nc_prologue(p, dl, u_prop, seed, it, stream)) return -1;
-    if (gs_nc_sweep(p, d_alm, s_out, z, seed, it, 1, stream)) return -1;
+    if (gs_nc_sweep(p, d_alm, dl, s_out, z, seed, it, 1, stream)) return -1;
     return gs_nc_decide(p, dl, u_acc, seed, it, accept_out, stream);
 }
 
@@ -1746,8 +1782,7 @@ int gs_step_asis(gs_plan* p, const double* d_alm, double* dl, double* s_out, con
     if (!p->has_mh) return set_error("gs_step_asis: plan has no MH blocks / proposal variances");
     if (!d_alm || !dl) return set_error("gs_step_asis: null argument");
     double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
-    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
-    if (gs_cr_sweep(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, stream)) return -1;
+    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, z, seed, it, s_out, stream)) return -1;
     if (gs_cls_draw(p, p->stats, igvar, seed, it, tmp, stream)) return -1;
     if (gs_stats_to_noncentered(p, tmp, p->stats, stream)) return -1;
     const size_t bytes = (size_t)p->nchains * p->nspec * p->maxbins * sizeof(double);
@@ -1772,8 +1807,7 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
     if (!d_alm || !dl) return set_error("gs_step_asis_fused: null argument");
     double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    if (gs_block_params(p, GS_MODE_CENTERED, dl, p->params, stream)) return -1;
-    if (gs_cr_sweep(p, d_alm, p->params, nullptr, seed, it, 0, s_out, p->stats, stream)) return -1;
+    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream)) return -1;
     if (gs_cls_draw(p, p->stats, nullptr, seed, it, tmp, stream)) return -1;
     if (gs_stats_to_noncentered(p, tmp, p->stats, stream)) return -1;
     const size_t bytes = (size_t)p->nchains * p->nspec * p->maxbins * sizeof(double);

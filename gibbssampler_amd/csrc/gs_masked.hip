@@ -281,18 +281,40 @@ __global__ __launch_bounds__(RED_BLOCK) void k_mc_sums(int L, int F, long long n
 }
 
 // accept with log u < log pi(s1) + log q(s0|s1) - log pi(s0) - log q(s1|s0) (577-603)
+// fixed-order sum of N rows of per-block partials over one workgroup of
+// RED_BLOCK threads: thread t sums blocks t, t + RED_BLOCK, ... in order, then
+// a fixed tree in LDS (deterministic; loads spread over the workgroup instead
+// of one thread's dependent chain)
+template <int N>
+__device__ __forceinline__ void block_sums(int nblk, const double* __restrict__ partial, int stride, double (&t)[N]) {
+    __shared__ double red[N][RED_BLOCK];
+    double v[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += RED_BLOCK)
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] += partial[(long long)b * stride + k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) red[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int h = RED_BLOCK / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h)
+#pragma unroll
+            for (int k = 0; k < N; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + h];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) t[k] = red[k][0];
+}
+
 __global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long long nslot, const double* __restrict__ um,
                             uint32_t seed_lo, uint32_t seed_hi, uint32_t chain, uint32_t call, uint32_t iter,
                             const double* __restrict__ s1, double* __restrict__ s0, int32_t* __restrict__ accept,
                             double* __restrict__ log_ratio) {
     __shared__ int acc;
+    double t[NSUM];
+    block_sums<NSUM>(nblk, partial, NSUM, t);
     if (threadIdx.x == 0) {
-        double t[NSUM];
-        for (int k = 0; k < NSUM; ++k) {
-            double v = 0.0;
-            for (int b = 0; b < nblk; ++b) v += partial[b * NSUM + k];
-            t[k] = v;
-        }
         const double lp1 = -0.5 * t[1] + -0.5 * t[7] + t[3];
         const double lp0 = -0.5 * t[0] + -0.5 * t[6] + t[2];
         const double lr = lp1 + (-0.5 * t[4]) - (lp0 + (-0.5 * t[5]));
@@ -472,12 +494,14 @@ __global__ __launch_bounds__(RED_BLOCK) void k_dot2(long long n, const double* _
     if (threadIdx.x == 0) { partial[2 * blockIdx.x] = red[0][0]; partial[2 * blockIdx.x + 1] = red[1][0]; }
 }
 
-__global__ void k_dot2_finish(int nblk, const double* __restrict__ partial, double* __restrict__ out) {
-    if (threadIdx.x != 0) return;
-    double s0 = 0.0, s1 = 0.0;
-    for (int b = 0; b < nblk; ++b) { s0 += partial[2 * b]; s1 += partial[2 * b + 1]; }
-    out[0] = s0;
-    out[1] = s1;
+__global__ __launch_bounds__(RED_BLOCK) void k_dot2_finish(int nblk, const double* __restrict__ partial,
+                                                           double* __restrict__ out) {
+    double t[2];
+    block_sums<2>(nblk, partial, 2, t);
+    if (threadIdx.x == 0) {
+        out[0] = t[0];
+        out[1] = t[1];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1057,7 +1081,7 @@ static int pcg_dots(gs_masked* c, const double* a, const double* b, const double
     const long long n = c->F * c->NR;
     const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
     hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(RED_BLOCK), 0, st, n, a, b, d, e, c->partial);
-    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(64), 0, st, nb, c->partial, c->dots);
+    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(RED_BLOCK), 0, st, nb, c->partial, c->dots);
     GS_LAUNCH_CHECK("k_dot2");
     GS_CHECK(hipMemcpyAsync(host2, c->dots, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
     GS_CHECK(hipStreamSynchronize(st));
@@ -1180,7 +1204,7 @@ int gs_masked_nc_loglik(gs_masked* c, const double* dl, const double* s_nc, doub
     const long long n = c->F * c->npix;
     const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
     hipLaunchKernelGGL(k_mc_resid, dim3(nb), dim3(RED_BLOCK), 0, st, n, c->dpix, c->pix1, c->ninv, c->partial);
-    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(64), 0, st, nb, c->partial, c->dots);
+    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(RED_BLOCK), 0, st, nb, c->partial, c->dots);
     hipLaunchKernelGGL(k_mc_halfneg, dim3(1), dim3(64), 0, st, c->dots, lik);
     GS_LAUNCH_CHECK("k_mc_resid");
     return 0;

@@ -38,6 +38,7 @@
 #include <vector>
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 
 #include "gibbs_capi.h"
 #include "gs_common.h"
@@ -51,12 +52,7 @@ constexpr int LEG_BLOCK = 256;
 #ifndef GS_ANA_C
 #define GS_ANA_C 4
 #endif
-#ifndef GS_ANA_SR
-#define GS_ANA_SR 4
-#endif
 constexpr int ANA_C = GS_ANA_C;             // l per reduction chunk (even)
-constexpr int ASR = GS_ANA_SR;              // ring pairs per lane, analysis
-constexpr int ATILE = ASR * 256;            // ring pairs per analysis workgroup
 constexpr int LDS_FFT_MAX = 8192;           // complex points held in LDS
 constexpr double SC_UP = 0x1p768;
 constexpr double SC_DN = 0x1p-768;
@@ -222,8 +218,9 @@ __global__ __launch_bounds__(256) void k_sht_onset(ShtDev D, const double* __res
 // ---------------------------------------------------------------------------
 // Legendre stages: shared layout
 // ---------------------------------------------------------------------------
-// A workgroup covers LTILE = 1024 consecutive ring pairs for one m pair
-// (m, L - m: balanced work); lane `lane` of wave `w` owns the SR = 4 ring
+// A workgroup covers 4 SR consecutive 64-ring-pair groups for one m pair
+// (m, L - m: balanced work) or one m (paired = 0: small maps, where the m
+// pairs alone do not give ~4 waves per SIMD); lane `lane` of wave `w` owns the SR ring
 // pairs tile*1024 + w*256 + r*64 + lane, so (wave, slot r) is exactly one
 // 64-pair onset group and every per-l coefficient / a_lm value is a
 // wave-uniform scalar load.  Each slot enters at its group's onset l with the
@@ -232,11 +229,6 @@ __global__ __launch_bounds__(256) void k_sht_onset(ShtDev D, const double* __res
 // the parity-unrolled fast path runs the plain recurrence.
 // NC = 1: T (spin 0); 2: E,B <-> Q,U; 3: T,E,B <-> T,Q,U.
 // phi layout: [comp][ns][m][pair] (double2), ns 0 = north, 1 = south
-#ifndef GS_SYN_SR
-#define GS_SYN_SR 2
-#endif
-constexpr int SR = GS_SYN_SR;               // ring pairs per lane, synthesis
-constexpr int LTILE = SR * LEG_BLOCK;
 
 // a_lm in the caller's layout -> ain[comp][nlm] (healpy-ordered complex)
 __global__ void k_sht_alm_in(int L, int nlm, int ncomp, const double* __restrict__ alm, int layout,
@@ -283,15 +275,15 @@ __device__ __forceinline__ void rec_step(const LegCoef& c, double x, double& v0,
     v0 = vn;
 }
 
-template <int NC>
+template <int NC, int SR>
 __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const LegCoef* __restrict__ coef,
                                                              const double2* __restrict__ ain,
-                                                             double2* __restrict__ phi) {
+                                                             double2* __restrict__ phi, int paired) {
     const int L = D.L, npair = D.npair, nlm = D.nlm;
     const int q = blockIdx.x, tile = blockIdx.y;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int g0 = tile * (LTILE / 64) + wave * SR;        // onset group of slot 0
+    const int g0 = tile * (LEG_BLOCK / 64) * SR + wave * SR;   // onset group of slot 0
     double x[SR], is2[SR], xis2[SR];
     int pr[SR];
     bool act[SR];
@@ -306,7 +298,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
     const double2 z2 = make_double2(0.0, 0.0);
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
-        if (h == 1 && m <= q) break;
+        if (h == 1 && (!paired || m <= q)) break;
         int ls[SR];
         int lmin = L + 1;
 #pragma unroll
@@ -461,18 +453,18 @@ __device__ __forceinline__ void blk_accumulate(BlkAcc& A, int f, const LegCoef& 
     }
 }
 
-template <int NC>
+template <int NC, int SR>
 __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const LegCoef* __restrict__ coef,
                                                                 const double2* __restrict__ ain,
                                                                 const int* __restrict__ blk,
-                                                                double2* __restrict__ phib) {
+                                                                double2* __restrict__ phib, int paired) {
     constexpr int NF = NC;                      // input fields
     constexpr int NCO = NC == 1 ? 1 : 2;        // output comps per block
     const int L = D.L, npair = D.npair, nlm = D.nlm;
     const int q = blockIdx.x, tile = blockIdx.y;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int g0 = tile * (LTILE / 64) + wave * SR;
+    const int g0 = tile * (LEG_BLOCK / 64) * SR + wave * SR;
     double x[SR], is2[SR], xis2[SR];
     int pr[SR];
     bool act[SR];
@@ -487,7 +479,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
     const long long plane = phi_plane(L, npair);
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
-        if (h == 1 && m <= q) break;
+        if (h == 1 && (!paired || m <= q)) break;
         int ls[SR];
         int lmin = L + 1;
 #pragma unroll
@@ -1019,7 +1011,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
 }
 
 // ---------------------------------------------------------------------------
-// analysis: Legendre stage.  grid (m pairs, tiles of LTILE ring pairs)
+// analysis: Legendre stage.  grid (m pairs or m, tiles of 4 ASR groups of 64 ring pairs)
 // out: part[tile][comp][nlm] (double2), unweighted sums
 //   T: sum lambda Phi_T ;  E: sum (Q F1 + i U F2) ;  B: sum (U F1 - i Q F2)
 // Per chunk of ANA_C l (aligned to m's parity) every lane sums its 4 ring
@@ -1053,10 +1045,10 @@ __device__ __forceinline__ void ana_term(double* a, const LegCoef& c, double v0,
     }
 }
 
-template <int NC>
+template <int NC, int ASR>
 __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegCoef* __restrict__ coef,
                                                             const double2* __restrict__ phi,
-                                                            double2* __restrict__ part) {
+                                                            double2* __restrict__ part, int paired) {
     constexpr int NO = NC == 1 ? 2 : (NC == 2 ? 4 : 6);   // real outputs per l
     constexpr int NV = NO * ANA_C;
     static_assert(NV <= 32, "chunk too large for the wave reduction");
@@ -1065,7 +1057,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     const int q = blockIdx.x, tile = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g0 = tile * (ATILE / 64) + wave * ASR;
+    const int g0 = tile * (LEG_BLOCK / 64) * ASR + wave * ASR;
     const long long plane = phi_plane(L, npair);
     double x[ASR], is2[ASR], xis2[ASR];
     int pr[ASR];
@@ -1080,7 +1072,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     }
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
-        if (h == 1 && m <= q) break;
+        if (h == 1 && (!paired || m <= q)) break;
         int ls[ASR];
 #pragma unroll
         for (int r = 0; r < ASR; ++r)
@@ -1329,6 +1321,9 @@ inline hipStream_t S(void* s) { return (hipStream_t)s; }
 // ============================================================================
 struct gs_sht {
     int nside = 0, L = 0, npair = 0, ngroup = 0, nlm = 0, ntile = 0, Mmax = 0;
+    // Legendre launch shapes chosen for occupancy (~4 waves per SIMD): ring
+    // pairs per lane (sr) and m pairing, synthesis and analysis
+    int syn_sr = 2, syn_paired = 1, ana_sr = 4, ana_paired = 1;
     long long npix = 0;
     PairGeom* geom = nullptr;
     LegCoef* coef = nullptr;
@@ -1406,7 +1401,30 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     p->nside = N; p->L = L; p->npair = 2 * N; p->ngroup = (p->npair + 63) / 64;
     p->nlm = (L + 1) * (L + 2) / 2;
     p->npix = 12LL * N * N;
-    p->ntile = (p->npair + ATILE - 1) / ATILE;
+    {
+        // the largest ring count per lane (and m pairing) that still gives ~4 waves
+        // per SIMD (1024 SIMDs); small maps fall back to one ring group per lane and
+        // unpaired m.  GS_SHT_SYN / GS_SHT_ANA = "sr,paired" override (tests)
+        auto waves = [&](int sr, int paired) {
+            return (long long)(paired ? L / 2 + 1 : L + 1) * ((p->ngroup + sr - 1) / sr);
+        };
+        auto pick = [&](std::initializer_list<std::pair<int, int>> opts, const char* env, int& sr, int& paired) {
+            sr = 1; paired = 0;
+            for (auto o : opts)
+                if (waves(o.first, o.second) >= 4096) { sr = o.first; paired = o.second; break; }
+            if (const char* e = std::getenv(env)) {
+                int a = 0, b = 0;
+                if (std::sscanf(e, "%d,%d", &a, &b) == 2) { sr = a; paired = b ? 1 : 0; }
+            }
+        };
+        pick({{2, 1}, {1, 1}, {1, 0}}, "GS_SHT_SYN", p->syn_sr, p->syn_paired);
+        pick({{4, 1}, {2, 1}, {1, 1}, {1, 0}}, "GS_SHT_ANA", p->ana_sr, p->ana_paired);
+        if ((p->syn_sr != 1 && p->syn_sr != 2) || (p->ana_sr != 1 && p->ana_sr != 2 && p->ana_sr != 4)) {
+            delete p;
+            return set_error("gs_sht_create: bad GS_SHT_SYN / GS_SHT_ANA override");
+        }
+    }
+    p->ntile = (p->ngroup + 4 * p->ana_sr - 1) / (4 * p->ana_sr);
     // ---- geometry (ring pair r: north ring r+1, south ring 4N-1-r) ----
     std::vector<PairGeom> geom(p->npair);
     int Mmax = 2;
@@ -1659,9 +1677,12 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, ncomp, alm, layout,
                        p->ain);
     GS_LAUNCH_CHECK("k_sht_alm_in");
-    const dim3 grid(p->L / 2 + 1, (p->npair + LTILE - 1) / LTILE);
-#define GS_SL(NC) hipLaunchKernelGGL((k_sht_synth_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->ain, p->phi)
-    if (ncomp == 1) GS_SL(1); else if (ncomp == 2) GS_SL(2); else GS_SL(3);
+    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr));
+#define GS_SL(NC, SR) hipLaunchKernelGGL((k_sht_synth_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
+                                         p->coef, p->ain, p->phi, p->syn_paired)
+#define GS_SL2(NC) do { if (p->syn_sr == 2) GS_SL(NC, 2); else GS_SL(NC, 1); } while (0)
+    if (ncomp == 1) GS_SL2(1); else if (ncomp == 2) GS_SL2(2); else GS_SL2(3);
+#undef GS_SL2
 #undef GS_SL
     GS_LAUNCH_CHECK("k_sht_synth_leg");
     return sht_rings(p, true, ncomp, nullptr, maps, stream);
@@ -1669,9 +1690,13 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
 
 static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream) {
     if (sht_rings(p, false, ncomp, maps, nullptr, stream)) return -1;
-    const dim3 grid(p->L / 2 + 1, p->ntile);
-#define GS_AL(NC) hipLaunchKernelGGL((k_sht_anal_leg<NC>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->phi, p->part)
-    if (ncomp == 1) GS_AL(1); else if (ncomp == 2) GS_AL(2); else GS_AL(3);
+    const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, p->ntile);
+#define GS_AL(NC, SR) hipLaunchKernelGGL((k_sht_anal_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
+                                         p->coef, p->phi, p->part, p->ana_paired)
+#define GS_AL2(NC) do { if (p->ana_sr == 4) GS_AL(NC, 4); else if (p->ana_sr == 2) GS_AL(NC, 2); \
+                        else GS_AL(NC, 1); } while (0)
+    if (ncomp == 1) GS_AL2(1); else if (ncomp == 2) GS_AL2(2); else GS_AL2(3);
+#undef GS_AL2
 #undef GS_AL
     GS_LAUNCH_CHECK("k_sht_anal_leg");
     const double w = 4.0 * PI / (double)p->npix;
@@ -1696,11 +1721,12 @@ int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int
                        GS_ALM_REAL, p->ain);
     GS_LAUNCH_CHECK("k_sht_alm_in");
     double2* ph = reinterpret_cast<double2*>(phib);
-    const dim3 grid(p->L / 2 + 1, (p->npair + LTILE - 1) / LTILE);
-    if (nfield == 1)
-        hipLaunchKernelGGL(k_sht_synth_blocks<1>, grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->ain, blk, ph);
-    else
-        hipLaunchKernelGGL(k_sht_synth_blocks<2>, grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, p->ain, blk, ph);
+    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr));
+#define GS_SB(NF, SR) hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
+                                         p->coef, p->ain, blk, ph, p->syn_paired)
+    if (nfield == 1) { if (p->syn_sr == 2) GS_SB(1, 2); else GS_SB(1, 1); }
+    else { if (p->syn_sr == 2) GS_SB(2, 2); else GS_SB(2, 1); }
+#undef GS_SB
     GS_LAUNCH_CHECK("k_sht_synth_blocks");
     // ring stage: the plan's FFT scratch (global / split rings) holds three comps,
     // so rings that need it run three comps per launch

@@ -253,8 +253,8 @@ class GibbsPlan:
         C.check(self.lib.gs_nc_prologue(self._h, C.ptr(dl), C.ptr(u_prop), int(seed), int(iteration), self._s()),
                 "gs_nc_prologue")
 
-    def nc_sweep(self, d, s_out, z=None, seed=0, iteration=0, finish=True):
-        C.check(self.lib.gs_nc_sweep(self._h, C.ptr(d), C.ptr(s_out), C.ptr(z), int(seed), int(iteration),
+    def nc_sweep(self, d, dl, s_out, z=None, seed=0, iteration=0, finish=True):
+        C.check(self.lib.gs_nc_sweep(self._h, C.ptr(d), C.ptr(dl), C.ptr(s_out), C.ptr(z), int(seed), int(iteration),
                                      int(bool(finish)), self._s()), "gs_nc_sweep")
 
     def nc_finish(self):

@@ -95,7 +95,7 @@ class BatchedRunner:
                 # NC: prologue, sweep (+ statistics), MH decisions with the trace record
                 # and the counter advance fused into the decision launch
                 p.nc_prologue(self.dl, seed=self.seed)
-                p.nc_sweep(self.d, self.s, seed=self.seed)
+                p.nc_sweep(self.d, self.dl, self.s, seed=self.seed)
                 p.nc_decide_fused(self.dl, seed=self.seed, accept=self.accept, trace=trace,
                                   capacity=trace_capacity or 0)
             elif self.kind == "centered":
@@ -133,7 +133,7 @@ class BatchedRunner:
                 acc = self.accept if accept_trace is None else accept_trace[i]
                 if self.kind == "noncentered":
                     p.nc_prologue(self.dl, seed=self.seed)
-                    p.nc_sweep(self.d, self.s, seed=self.seed, finish=False)
+                    p.nc_sweep(self.d, self.dl, self.s, seed=self.seed, finish=False)
                     p.nc_finish()
                     p.nc_decide_fused(self.dl, seed=self.seed, accept=acc, trace=trace,
                                       capacity=trace_capacity or 0)

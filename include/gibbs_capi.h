@@ -152,14 +152,16 @@ int gs_step_noncentered(gs_plan* plan, const double* d_alm, double* dl_binned, d
                         const double* z_replay, const double* u_prop_replay, const double* u_accept_replay,
                         uint64_t seed, uint32_t iteration, int32_t* accept_out, void* stream);
 /* the three stages of gs_step_noncentered, for callers that schedule them:
- *   gs_nc_prologue  NC block parameters of dl and the MH proposals
- *                   (NonCenteredGibbs.py:134-176 operator, 292-330 proposals)
- *   gs_nc_sweep     the CR draw + sufficient statistics into the plan
+ *   gs_nc_prologue  the MH proposals (and native accept uniforms) of dl
+ *                   (NonCenteredGibbs.py:292-330) and, for plans of more than 4
+ *                   chains, the NC block parameters of dl (:134-176)
+ *   gs_nc_sweep     the CR draw + sufficient statistics; plans of <= 4 chains
+ *                   compute the NC operator of dl per l inside the sweep
  *   gs_nc_decide    the Metropolis-within-Gibbs decisions (NonCenteredGibbs.py:401-445) */
 int gs_nc_prologue(gs_plan* plan, const double* dl_binned, const double* u_prop_replay, uint64_t seed,
                    uint32_t iteration, void* stream);
-int gs_nc_sweep(gs_plan* plan, const double* d_alm, double* s_out, const double* z_replay, uint64_t seed,
-                uint32_t iteration, int finish, void* stream);
+int gs_nc_sweep(gs_plan* plan, const double* d_alm, const double* dl_binned, double* s_out, const double* z_replay,
+                uint64_t seed, uint32_t iteration, int finish, void* stream);
 /* finish = 0 leaves the statistics as per-task partials; gs_nc_finish reduces them
  * (fixed order) -- lets a caller bracket the sweep kernel alone with timing events */
 int gs_nc_finish(gs_plan* plan, void* stream);

@@ -205,3 +205,29 @@ def test_large_ring_fft_paths_vs_oracle(thr, ncomp, monkeypatch):
 def test_adjointness_nside2048():
     """exact adjointness at N_side 2048 (split-half Bluestein rings in play)."""
     test_adjointness_fullsize(2048, 4096, 1)
+
+
+SHAPES = [("2,1", "4,1"), ("2,0", "2,1"), ("1,1", "2,0"), ("1,0", "1,1"), ("2,1", "1,0")]
+
+
+@pytest.mark.parametrize("syn,ana", SHAPES)
+@pytest.mark.parametrize("N,L", [(16, 32), (64, 100)])
+def test_legendre_launch_shapes_vs_oracle(monkeypatch, syn, ana, N, L):
+    """Every Legendre launch shape the plan may pick (ring groups per lane 1/2
+    for synthesis, 1/2/4 for analysis; m paired or not) -- chosen by map size
+    for occupancy, forced here with GS_SHT_SYN / GS_SHT_ANA -- against the
+    dense oracle (TEB, both directions; 64/100 with several ring groups)."""
+    torch = _torch()
+    from gibbssampler_amd.sht import HealpixSHT
+    monkeypatch.setenv("GS_SHT_SYN", syn)
+    monkeypatch.setenv("GS_SHT_ANA", ana)
+    sht = HealpixSHT(N, L)
+    rng = np.random.default_rng(N + L)
+    a = _rand_alm(L, 3, rng)
+    want = _oracle_maps(a, N, L, 3)
+    got = sht.alm2map(torch.from_numpy(a).cuda(), ncomp=3, layout="complex").cpu().numpy().reshape(3, -1)
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-11 * np.abs(want).max())
+    maps = rng.standard_normal((3, O.npix(N)))
+    wa = _oracle_alm(maps, N, L, 3, 0)
+    ga = sht.map2alm(torch.from_numpy(maps).cuda(), iter=0, layout="complex", ncomp=3).cpu().numpy().reshape(3, -1)
+    np.testing.assert_allclose(ga, wa, rtol=0, atol=1e-11 * np.abs(wa).max())
