@@ -1,4 +1,15 @@
-"""Build libgibbs_hip.so in-tree for gfx950 (hipcc, no JIT cache)."""
+"""Build libgibbs_hip.so in-tree for gfx950 (hipcc, no JIT cache).
+
+Variants (debug builds):
+  * ``variant="debug"``: -DGS_DEBUG -- device-side bounds assertions (GS_ASSERT)
+    at the kernels' index computations; -> libgibbs_hip_debug.so
+  * ``variant="asan"``: host code under AddressSanitizer (-Xarch_host
+    -fsanitize=address; device code unchanged) for the plan-building and
+    argument-validation paths; -> libgibbs_hip_asan.so, loaded with the clang
+    ASan runtime preloaded (tests/test_capi_asan.py)
+Select a variant at run time with GIBBS_HIP_LIB=<path>.
+"""
+import glob
 import os
 import subprocess
 
@@ -10,6 +21,18 @@ HEADERS = [os.path.join(HERE, "csrc", h) for h in ("gs_rng.h", "gs_common.h", "g
     [os.path.join(ROOT, "include", "gibbs_capi.h")]
 LIB = os.path.join(HERE, "libgibbs_hip.so")
 ARCH = os.environ.get("GIBBS_OFFLOAD_ARCH", "gfx950")
+VARIANTS = {
+    None: (LIB, ["-O3"]),
+    "debug": (os.path.join(HERE, "libgibbs_hip_debug.so"), ["-O3", "-DGS_DEBUG"]),
+    "asan": (os.path.join(HERE, "libgibbs_hip_asan.so"),
+             ["-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", "-fsanitize=address", "-shared-libasan"]),
+}
+
+
+def asan_runtime():
+    """clang's shared ASan runtime that an ASan build needs preloaded."""
+    hits = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    return hits[-1] if hits else None
 
 
 def _stale(target, deps):
@@ -19,18 +42,20 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, variant=None):
+    lib, flags = VARIANTS[variant]
     deps = SOURCES + HEADERS
-    if not force and not _stale(LIB, deps):
-        return LIB
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SOURCES
+    if not force and not _stale(lib, deps):
+        return lib
+    cmd = ["hipcc", f"--offload-arch={ARCH}"] + flags + ["-std=c++17", "-shared", "-fPIC",
+                                                          "-I", os.path.join(ROOT, "include"), "-o", lib + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build(force=True)
+    import sys
+    build(force=True, variant=sys.argv[1] if len(sys.argv) > 1 else None)

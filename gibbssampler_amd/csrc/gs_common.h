@@ -28,3 +28,19 @@ inline int set_error(const std::string& msg) {
         if (_e != hipSuccess)                                                                 \
             return gs_detail::set_error(std::string("launch ") + (name) + ": " + hipGetErrorString(_e)); \
     } while (0)
+
+// device bounds assertions of the debug build (-DGS_DEBUG, build.py variant
+// "debug"): a failed check prints where and traps the kernel; compiled out
+// otherwise
+#if defined(GS_DEBUG)
+#include <cstdio>
+#define GS_ASSERT(cond)                                                                       \
+    do {                                                                                      \
+        if (!(cond)) {                                                                        \
+            printf("GS_ASSERT %s:%d: %s\n", __FILE__, __LINE__, #cond);                      \
+            __builtin_trap();                                                                 \
+        }                                                                                     \
+    } while (0)
+#else
+#define GS_ASSERT(cond) do { } while (0)
+#endif

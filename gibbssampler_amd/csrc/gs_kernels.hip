@@ -78,9 +78,10 @@ struct gs_plan {
     int* meta = nullptr;             // [16]: nbins[4], nblocks[4], acc_off[4], mh_order[4]
     int2* tasks = nullptr;           // [npair] (tile group, row chunk) of the CR sweep
     int npair = 0, ntile = 0, nchunk = 0, rows_per_task = 64;
+    int sweep_tw = 1, nchunkg = 0;   // tiles per sweep workgroup (4 / tw chunks), chunk groups per tile
     int ntask = 0;                   // valid (tile, chunk) waves per chain
     // workspace
-    double* partials = nullptr;      // [nchains][ntile][nchunk][nstat][64]
+    double* partials = nullptr;      // [nchains][ntile][nchunkg][nstat][64]
     double* params = nullptr;        // [nchains][L+1][NP]
     double* stats = nullptr;         // [nchains][nstat][L+1]
     double* prop = nullptr;          // [nchains][nspec][maxbins]
@@ -298,13 +299,14 @@ struct SweepOp {
 };
 
 // Tiling of the (l, m) triangle: 64-wide l tiles, descending from l = L
-// (tile t holds l in [L-64t-63, L-64t]); a workgroup = 4 waves = 4 adjacent
-// tiles (256 consecutive l) x one chunk of TM rows m, so every row of the
-// workgroup is one contiguous 4 KiB run per field and chain; consecutive
-// workgroups are consecutive chains of the same (tiles, rows) block and
-// share the data reads in L2.
+// (tile t holds l in [L-64t-63, L-64t]), rows m in chunks of TM.  A workgroup
+// = 4 waves = TW adjacent tiles x CW = 4 / TW consecutive chunks (plan
+// sweep_tw): with CW > 1 the waves of one tile add their per-l statistic
+// accumulators in LDS in a fixed order, so one partial per (tile, chunk
+// group) goes to HBM instead of one per chunk.  Consecutive workgroups are
+// consecutive chains of the same task and share the data reads in L2.
 template <int F, int ZM, bool STORE>
-__global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunk, int tm,
+__global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
                                                   const double* __restrict__ params, const double* __restrict__ z,
                                                   double* __restrict__ s, double* __restrict__ partials,
@@ -327,13 +329,15 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const int chain = wg % nchains;
     const int lane = threadIdx.x & 63;
     const int2 gc = tasks[pair];
-    if (gc.x < 0) return;                       // padding pair
-    const int t = 4 * gc.x + (threadIdx.x >> 6);
-    if (t >= ntile) return;
+    if (gc.x < 0) return;                       // padding pair (whole workgroup)
+    const int w = threadIdx.x >> 6, cw = 4 / tw;
+    const int t = tw * gc.x + w % tw;
+    const bool tile_ok = t < ntile;
     const int lhi = L - WAVE * t;
-    const int m0 = gc.y * tm;
+    const int m0 = (cw * gc.y + w / tw) * tm;
     const int m1 = min(m0 + tm, lhi + 1);
-    if (m0 >= m1) return;
+    const bool active = tile_ok && m0 < m1;    // no early return: the workgroup meets in LDS below
+    GS_ASSERT(gc.y < nchunkg && gc.x * tw < ntile);
     const int ell_lo = lhi - 63;
     const int ell = ell_lo + lane;
     const bool lane_ok = ell >= 0;
@@ -342,7 +346,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const uint32_t tag = TAG_CR | (substep << 8);
 
     double pm[NP];
-    if (ZM != 2 && lane_ok && op.mode >= 0) {
+    if (ZM != 2 && lane_ok && active && op.mode >= 0) {
         // this lane's l: the operator from the chain's D_l (no parameter table)
         if (op.mode == GS_MODE_CENTERED)
             block_params_compute<F, GS_MODE_CENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
         else
             block_params_compute<F, GS_MODE_NONCENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
                                                          op.k1, op.k2, pm);
-    } else if (ZM != 2 && lane_ok) {
+    } else if (ZM != 2 && lane_ok && active) {
         const double* pp = params + ((long long)chain * (L + 1) + ell) * NP;
 #pragma unroll
         for (int q = 0; q < NP; ++q) pm[q] = pp[q];
@@ -365,9 +369,9 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const double* zc = ZM == 1 ? z + (long long)chain * F * NR : nullptr;
     double* sc = s + (long long)chain * F * NR;
 
-    int m = m0;
+    int m = active ? m0 : m1;
     double dv[F][2];
-    if (m == 0) {
+    if (active && m == 0) {
         if (lane_ok) {
             load_d<F, 1>(d, NR, ell, dv);
             sweep_entry<F, ZM, STORE, 1>(dv, zc, sc, NR, ell, (uint32_t)ell, tag, iter, key, pm, acc, tab);
@@ -382,6 +386,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
         for (; m < m1; ++m) {
             load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
             sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
+            GS_ASSERT(2 * i - (L + 1) + 1 < NR && 2 * i - (L + 1) > L);
             i += L - m;
         }
     } else {
@@ -394,13 +399,30 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
             i += L - m;
         }
     }
-    double* po = partials + (((long long)chain * ntile + t) * nchunk + gc.y) * NS * WAVE;
+    double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
+    if (cw == 1) {
+        if (active)
 #pragma unroll
-    for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
+            for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
+        return;
+    }
+    // the CW waves of a tile: fixed-order sum in LDS, one partial per tile
+    __shared__ double red[4][NS][WAVE];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) red[w][q][lane] = acc[q];
+    __syncthreads();
+    if (w < tw && tile_ok) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            double v = red[w][q][lane];         // ((c0 + c1) + c2) + c3, as k_stats_finish
+            for (int j = 1; j < cw; ++j) v += red[w + j * tw][q][lane];
+            po[q * WAVE + lane] = v;
+        }
+    }
 }
 
 // fixed-order reduction of the sweep partials: stats[chain][q][l]
-__global__ void k_stats_finish(int L, int nchains, int ntile, int nchunk, int tm, int nstat,
+__global__ void k_stats_finish(int L, int nchains, int ntile, int nchunkg, int tm, int cw, int nstat,
                                const double* __restrict__ partials, double* __restrict__ stats) {
     const int Lp1 = L + 1;
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -410,20 +432,35 @@ __global__ void k_stats_finish(int L, int nchains, int ntile, int nchunk, int tm
     const int chain = (int)(g / ((long long)Lp1 * nstat));
     const int t = (L - ell) / WAVE;
     const int lane = ell - (L - WAVE * t - 63);
-    const int cmax = (L - WAVE * t) / tm;
-    const double* pp = partials + ((long long)chain * ntile + t) * nchunk * nstat * WAVE + q * WAVE + lane;
-    // loads issued 8 at a time (latency-bound otherwise), summed in chunk order
+    const int cmax = (L - WAVE * t) / tm;               // last chunk of tile t
+    GS_ASSERT(t < ntile && lane >= 0 && lane < WAVE && cmax / cw < nchunkg);
+    const double* pp = partials + ((long long)chain * ntile + t) * nchunkg * nstat * WAVE + q * WAVE + lane;
     const long long cs = (long long)nstat * WAVE;
+    // the sum is ((c0 + c1) + c2) + c3 per group of 4 chunks, groups in order,
+    // for either workgroup shape (CW = 4: the group sums come from the sweep's
+    // LDS reduction), so the statistics do not depend on the shape -- which
+    // follows the chain count -- and trajectories stay bit-identical for any
+    // batch size or GPU count
     double acc = 0.0;
-    int c = 0;
-    for (; c + 8 <= cmax + 1; c += 8) {
-        double v[8];
+    if (cw == 1) {
+        for (int c0 = 0; c0 <= cmax; c0 += 4) {
+            double v[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = pp[(c + j) * cs];
+            for (int j = 0; j < 4; ++j) v[j] = c0 + j <= cmax ? pp[(c0 + j) * cs] : 0.0;
+            acc += ((v[0] + v[1]) + v[2]) + v[3];
+        }
+    } else {
+        const int gmax = cmax / cw;
+        int c = 0;
+        for (; c + 8 <= gmax + 1; c += 8) {
+            double v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc += v[j];
+            for (int j = 0; j < 8; ++j) v[j] = pp[(c + j) * cs];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc += v[j];
+        }
+        for (; c <= gmax; ++c) acc += pp[c * cs];
     }
-    for (; c <= cmax; ++c) acc += pp[c * cs];
     stats[g] = acc;
 }
 
@@ -931,6 +968,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
             const int4 r = rng[j];
             const int sp = sb.x, blk = sb.y, k = sp == sp0 ? 0 : 1;
             const int lo = r.x, hi = r.y, l0 = r.z, l1 = r.w;
+            GS_ASSERT(lo >= 0 && hi <= maxbins && l0 >= 0 && l1 <= Lp1);
             double diff = 0.0, lrs = 0.0;
             for (int l = l0; l < l1; ++l) diff += g[k * Lp1 + l];
             for (int b = lo; b < hi; ++b) lrs += R[sp * maxbins + b];
@@ -1158,14 +1196,29 @@ void build_tasks(gs_plan* p) {
     p->rows_per_task = tm;
     p->nchunk = L / tm + 1;
     p->ntask = (int)waves(tm);
-    // (tile group, row chunk) pairs, with their work in active lane-rows
+    // workgroup shape: 4 tiles x 1 chunk (each row one 4 KiB run per field).
+    // 1 tile x 4 chunks (the 4 waves' partials summed in LDS: a quarter of the
+    // partial traffic) was measured slower at the bench size (sweep 282-294 vs
+    // 261-281 us, tools/sweep_shape.py, interleaved in one process) and stays
+    // selectable (GS_SWEEP_TW = 1); the statistics' summation order is the same
+    // for both shapes (k_stats_finish)
+    int tw = 4;
+    if (const char* env = getenv("GS_SWEEP_TW")) {
+        const int v = atoi(env);
+        if (v == 1 || v == 4) tw = v;
+    }
+    const int cw = 4 / tw;
+    p->sweep_tw = tw;
+    p->nchunkg = (p->nchunk + cw - 1) / cw;
+    // (tile group, chunk group) pairs, with their work in active lane-rows
     std::vector<std::pair<long long, int2>> work;
-    for (int g = 0; 4 * g < p->ntile; ++g)
-        for (int c = 0; c * tm <= L - WAVE * 4 * g; ++c) {
+    for (int g = 0; tw * g < p->ntile; ++g)
+        for (int c = 0; c * cw * tm <= L - WAVE * tw * g; ++c) {
             long long wl = 0;
-            for (int t = 4 * g; t < std::min(4 * g + 4, p->ntile); ++t) {
+            for (int t = tw * g; t < std::min(tw * g + tw, p->ntile); ++t) {
                 const int lhi = L - WAVE * t, lo = std::max(lhi - 63, 0);
-                for (int m = c * tm; m < std::min(c * tm + tm, lhi + 1); ++m) wl += lhi - std::max(lo, m) + 1;
+                for (int m = c * cw * tm; m < std::min((c + 1) * cw * tm, lhi + 1); ++m)
+                    wl += lhi - std::max(lo, m) + 1;
             }
             work.push_back({wl, make_int2(g, c)});
         }
@@ -1325,7 +1378,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     build_tasks(p);
     p->inkernel_params = p->nchains <= 4;
     const size_t nc = (size_t)p->nchains;
-    rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunk * p->nstat * WAVE);
+    rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunkg * p->nstat * WAVE);
     rc |= dev_alloc(&p->params, nc * (L + 1) * NP);
     rc |= dev_alloc(&p->stats, nc * p->nstat * (L + 1));
     rc |= dev_alloc(&p->prop, nc * p->nspec * maxbins);
@@ -1489,7 +1542,7 @@ static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e
 static int stats_finish(gs_plan* p, double* stats, void* stream) {
     const long long n = (long long)p->nchains * p->nstat * (p->L + 1);
     hipLaunchKernelGGL(k_stats_finish, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
-                       p->nchunk, p->rows_per_task, p->nstat, p->partials, stats);
+                       p->nchunkg, p->rows_per_task, 4 / p->sweep_tw, p->nstat, p->partials, stats);
     GS_LAUNCH_CHECK("k_stats_finish");
     return 0;
 }
@@ -1507,7 +1560,8 @@ static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, c
     if (timing_begin(p, S(stream), &e0, &e1)) return -1;
     const bool rep = z != nullptr, st = s_out != nullptr;
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
-                                             p->nchunk, p->rows_per_task, p->tasks, d_alm, params, z, s_out,         \
+                                             p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,   \
+                                             s_out,                                                                   \
                                              p->partials, slo, shi, IterArg{iteration, p->itp()}, substep, p->chain0, \
                                              op)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \

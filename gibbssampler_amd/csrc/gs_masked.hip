@@ -694,6 +694,7 @@ __global__ __launch_bounds__(256) void k_f2_gram(int R, long long n, const doubl
     const int nb4 = (R + 3) / 4;
     const int nblk4 = nb4 * (nb4 + 1) / 2;
     const int tid = threadIdx.x;
+    GS_ASSERT(R <= F2_RMAX && nblk4 <= 256 * F2_BPT);
     int bi[F2_BPT], bj[F2_BPT];
     bool own[F2_BPT];
 #pragma unroll
@@ -782,6 +783,7 @@ __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* 
                                                    int32_t* __restrict__ accept_out, double* __restrict__ taken_out) {
     __shared__ double corr[F2_RMAX];
     __shared__ int taken_s;
+    GS_ASSERT(kn < F2_RMAX && R == kn + 1);
     const int tid = threadIdx.x;
     for (int k = tid; k < kn; k += blockDim.x) corr[k] = 0.0;
     __syncthreads();
@@ -789,6 +791,7 @@ __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* 
         if (tid == 0) {
             const int kg = k0 + k, f = blk_field[kg];
             const int lo = blk_bins[2 * kg], hi = blk_bins[2 * kg + 1];
+            GS_ASSERT(lo >= 0 && hi <= maxbins && lo <= hi);
             double lrs = 0.0;
             for (int b = lo; b < hi; ++b) lrs += logr[f * maxbins + b];
             const double delta = (G[(long long)(R - 1) * R + k] - corr[k]) - 0.5 * G[(long long)k * R + k];

@@ -508,6 +508,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
         // write field f's accumulators to its current block's planes (if any), reset
         auto flush = [&](int f) {
             const int k = cur[f];
+            GS_ASSERT(k < 0 || m <= L);
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 BlkAcc& B = A[f][r];
@@ -833,6 +834,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     const int comp = blockIdx.y;
     // block syntheses (f2): comp c holds only m <= comp_lmax[c / comp_div]
     const int Lc = comp_lmax ? comp_lmax[comp / comp_div] : L;
+    GS_ASSERT(Lc <= L && p < npair);
     const PairGeom g = geom[p];
     const int BD = blockDim.x;
     double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;

@@ -104,6 +104,26 @@ def alm2cl(alms, alms2=None):
     return o[0] if np.ndim(alms) == 1 else o
 
 
-def adjoint_synthesis_hp(map, bl_map=None):
-    """utils.adjoint_synthesis_hp (utils.py:79-111) -- needs the SHT kernels."""
-    raise NotImplementedError("adjoint_synthesis_hp needs the spherical-harmonic transform (SURVEY.md 8a a17)")
+def adjoint_synthesis_hp(map, bl_map=None, lmax=None):
+    """utils.adjoint_synthesis_hp (utils.py:79-111) on the device SHT: the
+    reference's "adjoint synthesis" Npix/(4 pi) * complex_to_real(map2alm(map,
+    iter=3)) per field (healpy's default iter = 3, so like the reference this is
+    the Jacobi-refined analysis, not the exact adjoint -- SURVEY.md Appendix
+    B.9), times the real-layout beam diagonal ``bl_map`` when given.  One map
+    (T) -> one array; three maps (T, Q, U) -> (alm_T, alm_E, alm_B).  ``lmax``
+    defaults to 2 N_side, the reference's config.L_MAX_SCALARS."""
+    import torch
+    from .sht import HealpixSHT
+    maps = np.asarray(map, dtype=np.float64)
+    pol = maps.ndim == 2 and maps.shape[0] == 3
+    npix = maps.shape[-1]
+    nside = int(round(math.sqrt(npix / 12)))
+    if 12 * nside * nside != npix:
+        raise ValueError("map length is not 12 nside^2")
+    L = 2 * nside if lmax is None else int(lmax)
+    sht = HealpixSHT(nside, L)
+    t = torch.from_numpy(np.ascontiguousarray(maps)).cuda()
+    a = sht.map2alm(t, iter=3, layout="real", ncomp=3 if pol else 1).cpu().numpy() * (npix / (4 * math.pi))
+    if bl_map is not None:
+        a = a * np.asarray(bl_map, dtype=np.float64)
+    return tuple(a) if pol else a

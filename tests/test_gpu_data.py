@@ -127,3 +127,25 @@ def test_fullsky_pixel_maps_input():
         out.append(nc.run({k: v.copy() for k, v in init.items()})[0])
     for s in ("EE", "BB"):
         np.testing.assert_allclose(out[0][s], out[1][s], rtol=1e-9)
+
+
+@pytest.mark.parametrize("pol", [False, True])
+def test_adjoint_synthesis_hp_vs_oracle(pol):
+    """utils.adjoint_synthesis_hp (utils.py:79-111): Npix/4pi complex_to_real(
+    map2alm(map, iter=3)) times the beam diagonal, against the dense oracle."""
+    from gibbssampler_amd import utils as U
+    N, L = 8, 16
+    rng = np.random.default_rng(5)
+    maps = rng.standard_normal((3, O.npix(N))) if pol else rng.standard_normal(O.npix(N))
+    bl = H.gauss_beam(np.radians(5.0), L)[H.slot_ell(L)]
+    got = U.adjoint_synthesis_hp(maps, bl)
+    want = O.map2alm(maps, N, L, iter=3)
+    want = np.atleast_2d(want)
+    resc = O.npix(N) / (4 * np.pi)
+    ref = [H.complex_to_real(w, L) * resc * bl for w in want]
+    if pol:
+        assert len(got) == 3
+        for g, r in zip(got, ref):
+            np.testing.assert_allclose(g, r, rtol=0, atol=1e-10 * np.abs(r).max())
+    else:
+        np.testing.assert_allclose(got, ref[0], rtol=0, atol=1e-10 * np.abs(ref[0]).max())
