@@ -17,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag="r01", key="noncentered_L1024_F3_c32"):
+def main(tag="r02", key="noncentered_L1024_F3_c32"):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -39,6 +39,23 @@ def main(tag="r01", key="noncentered_L1024_F3_c32"):
     prof[key] = {"hbm_bytes_per_launch": int(fetch + write), "read_bytes": int(fetch), "write_bytes": int(write),
                  "correction": "FETCH_SIZE x2, WRITE_SIZE x1 (calibrated: tools/microbench/calib.py)",
                  "source": f"profiles/{tag}_pmc.csv", "kernel": "k_cr_sweep"}
+    # VALU issue fraction of the sweep: SIMD cycles of VALU work / (SIMDs x cycles);
+    # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md DVFS note)
+    valu_csv = os.path.join(src, "valu", "run_counter_collection.csv")
+    if os.path.exists(valu_csv):
+        cnt = {}
+        for x in csv.DictReader(open(valu_csv)):
+            cnt.setdefault((x["Dispatch_Id"], x["Counter_Name"]), 0.0)
+            cnt[(x["Dispatch_Id"], x["Counter_Name"])] += float(x["Counter_Value"])
+        fr = []
+        for d in sorted({k[0] for k in cnt}):
+            cyc = cnt.get((d, "GRBM_GUI_ACTIVE"), 0.0) / 8.0
+            if cyc > 0:
+                fr.append(cnt.get((d, "SQ_INST_CYCLES_VALU"), 0.0) / (1024.0 * cyc))
+        if fr:
+            prof[key]["valu_issue_frac"] = round(statistics.median(fr), 4)
+            prof[key]["valu_source"] = f"profiles/{tag}_valu.csv (SQ_INST_CYCLES_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8))"
+            shutil.copy(valu_csv, os.path.join(dst, f"{tag}_valu.csv"))
     json.dump(prof, open(path, "w"), indent=1)
     # summary table
     st = list(csv.DictReader(open(os.path.join(dst, f"{tag}_kernel_stats.csv"))))
