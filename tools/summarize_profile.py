@@ -51,10 +51,16 @@ def main(tag="r02", key="noncentered_L1024_F3_c32"):
         for d in sorted({k[0] for k in cnt}):
             cyc = cnt.get((d, "GRBM_GUI_ACTIVE"), 0.0) / 8.0
             if cyc > 0:
-                fr.append(cnt.get((d, "SQ_INST_CYCLES_VALU"), 0.0) / (1024.0 * cyc))
+                # VALUBusy (derived_counters.xml) with GRBM_GUI_ACTIVE per XCD:
+                # SQ_ACTIVE_INST_VALU x 4 / (SIMDs x cycles); gfx950 reports no
+                # SQ_INST_CYCLES_VALU
+                fr.append(cnt.get((d, "SQ_ACTIVE_INST_VALU"), 0.0) * 4.0 / (1024.0 * cyc))
         if fr:
             prof[key]["valu_issue_frac"] = round(statistics.median(fr), 4)
-            prof[key]["valu_source"] = f"profiles/{tag}_valu.csv (SQ_INST_CYCLES_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8))"
+            prof[key]["valu_insts_per_launch"] = int(statistics.median(
+                [v for (d, n), v in cnt.items() if n == "SQ_INSTS_VALU"]))
+            prof[key]["valu_source"] = (f"profiles/{tag}_valu.csv: SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x "
+                                        f"GRBM_GUI_ACTIVE / 8 XCDs) (VALUBusy)")
             shutil.copy(valu_csv, os.path.join(dst, f"{tag}_valu.csv"))
     json.dump(prof, open(path, "w"), indent=1)
     # summary table
