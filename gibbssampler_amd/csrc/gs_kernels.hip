@@ -78,7 +78,7 @@ struct gs_plan {
     int* meta = nullptr;             // [16]: nbins[4], nblocks[4], acc_off[4], mh_order[4]
     int2* tasks = nullptr;           // [npair] (tile group, row chunk) of the CR sweep
     int npair = 0, ntile = 0, nchunk = 0, rows_per_task = 64;
-    int sweep_tw = 1, nchunkg = 0;   // tiles per sweep workgroup (4 / tw chunks), chunk groups per tile
+    int sweep_tw = 4, nchunkg = 0;   // tiles per sweep workgroup, chunks per tile
     int ntask = 0;                   // valid (tile, chunk) waves per chain
     // workspace
     double* partials = nullptr;      // [nchains][ntile][nchunkg][nstat][64]
@@ -300,11 +300,11 @@ struct SweepOp {
 
 // Tiling of the (l, m) triangle: 64-wide l tiles, descending from l = L
 // (tile t holds l in [L-64t-63, L-64t]), rows m in chunks of TM.  A workgroup
-// = 4 waves = TW adjacent tiles x CW = 4 / TW consecutive chunks (plan
-// sweep_tw): with CW > 1 the waves of one tile add their per-l statistic
-// accumulators in LDS in a fixed order, so one partial per (tile, chunk
-// group) goes to HBM instead of one per chunk.  Consecutive workgroups are
-// consecutive chains of the same task and share the data reads in L2.
+// = 4 waves = 4 adjacent tiles (256 consecutive l) x one chunk (tw = 4), so
+// every row of the workgroup is one contiguous 4 KiB run per field and chain;
+// consecutive workgroups are consecutive chains of the same task and share the
+// data reads in L2.  Each wave writes its 64 l's statistic partials of its
+// chunk; k_stats_finish sums them in a fixed order.
 template <int F, int ZM, bool STORE>
 __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const int lhi = L - WAVE * t;
     const int m0 = (cw * gc.y + w / tw) * tm;
     const int m1 = min(m0 + tm, lhi + 1);
-    const bool active = tile_ok && m0 < m1;    // no early return: the workgroup meets in LDS below
+    const bool active = tile_ok && m0 < m1;
     GS_ASSERT(gc.y < nchunkg && gc.x * tw < ntile);
     const int ell_lo = lhi - 63;
     const int ell = ell_lo + lane;
@@ -399,69 +399,49 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
             i += L - m;
         }
     }
+    if (!active) return;
     double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
-    if (cw == 1) {
-        if (active)
 #pragma unroll
-            for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
-        return;
-    }
-    // the CW waves of a tile: fixed-order sum in LDS, one partial per tile
-    __shared__ double red[4][NS][WAVE];
-#pragma unroll
-    for (int q = 0; q < NS; ++q) red[w][q][lane] = acc[q];
-    __syncthreads();
-    if (w < tw && tile_ok) {
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            double v = red[w][q][lane];         // ((c0 + c1) + c2) + c3, as k_stats_finish
-            for (int j = 1; j < cw; ++j) v += red[w + j * tw][q][lane];
-            po[q * WAVE + lane] = v;
-        }
-    }
+    for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
 }
 
-// fixed-order reduction of the sweep partials: stats[chain][q][l]
-__global__ void k_stats_finish(int L, int nchains, int ntile, int nchunkg, int tm, int cw, int nstat,
-                               const double* __restrict__ partials, double* __restrict__ stats) {
+// fixed-order reduction of the sweep partials: stats[chain][q][l].  One
+// workgroup per (chain, statistic, tile): wave w sums chunks w, w + 4, ... of
+// the tile's 64 l (lanes; coalesced rows of the partials), four loads in
+// flight, then the four wave sums in wave order -- the same order for any
+// batch size, so every chain's trajectory is bit-identical for any chain
+// count or GPU count
+__global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int ntile, int nchunkg, int tm, int nstat,
+                                                      const double* __restrict__ partials,
+                                                      double* __restrict__ stats) {
+    const int t = blockIdx.x % ntile;
+    const int q = (blockIdx.x / ntile) % nstat;
+    const int chain = blockIdx.x / (ntile * nstat);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int Lp1 = L + 1;
-    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g >= (long long)nchains * nstat * Lp1) return;
-    const int ell = (int)(g % Lp1);
-    const int q = (int)((g / Lp1) % nstat);
-    const int chain = (int)(g / ((long long)Lp1 * nstat));
-    const int t = (L - ell) / WAVE;
-    const int lane = ell - (L - WAVE * t - 63);
     const int cmax = (L - WAVE * t) / tm;               // last chunk of tile t
-    GS_ASSERT(t < ntile && lane >= 0 && lane < WAVE && cmax / cw < nchunkg);
+    GS_ASSERT(chain < nchains && cmax < nchunkg);
     const double* pp = partials + ((long long)chain * ntile + t) * nchunkg * nstat * WAVE + q * WAVE + lane;
     const long long cs = (long long)nstat * WAVE;
-    // the sum is ((c0 + c1) + c2) + c3 per group of 4 chunks, groups in order,
-    // for either workgroup shape (CW = 4: the group sums come from the sweep's
-    // LDS reduction), so the statistics do not depend on the shape -- which
-    // follows the chain count -- and trajectories stay bit-identical for any
-    // batch size or GPU count
     double acc = 0.0;
-    if (cw == 1) {
-        for (int c0 = 0; c0 <= cmax; c0 += 4) {
-            double v[4];
+    int c = w;
+    for (; c + 12 <= cmax; c += 16) {
+        double v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = c0 + j <= cmax ? pp[(c0 + j) * cs] : 0.0;
-            acc += ((v[0] + v[1]) + v[2]) + v[3];
-        }
-    } else {
-        const int gmax = cmax / cw;
-        int c = 0;
-        for (; c + 8 <= gmax + 1; c += 8) {
-            double v[8];
+        for (int j = 0; j < 4; ++j) v[j] = pp[(c + 4 * j) * cs];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = pp[(c + j) * cs];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc += v[j];
-        }
-        for (; c <= gmax; ++c) acc += pp[c * cs];
+        for (int j = 0; j < 4; ++j) acc += v[j];
     }
-    stats[g] = acc;
+    for (; c <= cmax; c += 4) acc += pp[c * cs];
+    __shared__ double red[4][WAVE];
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w == 0) {
+        const int ell = L - WAVE * t - 63 + lane;
+        if (ell >= 0)
+            stats[((long long)chain * nstat + q) * Lp1 + ell] = ((red[0][lane] + red[1][lane]) + red[2][lane]) +
+                                                                 red[3][lane];
+    }
 }
 
 // ============================================================================
@@ -1182,13 +1162,12 @@ void build_tasks(gs_plan* p) {
     };
     // rows per chunk: fixed (independent of the chain count), so the fixed-order
     // statistic sums -- and therefore every chain's trajectory -- are bit-identical
-    // whatever the batch size or GPU count.  20-24 rows measured best at the
-    // BASELINE size (tools/sweep_rows.py, interleaved in one process: sweep +
-    // finish 264-267 us against 280-284 us at 32 rows, 271 us at 16)
-    // smaller l_max: fewer tasks per chain, so shorter ones keep the chip busy
-    // (single-chain configs[1], L = 512: 8 rows 42 us per step vs 57 us at 24);
-    // a function of L only, never of the chain count
-    int tm = L >= 1024 ? 24 : (L > 512 ? 16 : 8);
+    // whatever the batch size or GPU count; a function of L only.  Measured with
+    // tools/step_ab.py (whole graph-captured steps, interleaved in one process),
+    // r02 with the workgroup-per-tile statistics finish: NC TEB 32 chains at
+    // L 1024: 12 / 16 / 20 / 24 rows 308.5 / 308.5 / 312.0 / 319.3 us per step;
+    // centered 1 chain at L 512: 2 / 4 / 8 rows 25.7 / 22.4 / 26.0 us
+    int tm = L > 512 ? 16 : (L > 256 ? 4 : 8);
     if (const char* env = getenv("GS_SWEEP_ROWS")) {
         const int v = atoi(env);
         if (v >= 1 && v <= 1024) tm = v;
@@ -1197,16 +1176,10 @@ void build_tasks(gs_plan* p) {
     p->nchunk = L / tm + 1;
     p->ntask = (int)waves(tm);
     // workgroup shape: 4 tiles x 1 chunk (each row one 4 KiB run per field).
-    // 1 tile x 4 chunks (the 4 waves' partials summed in LDS: a quarter of the
-    // partial traffic) was measured slower at the bench size (sweep 282-294 vs
-    // 261-281 us, tools/sweep_shape.py, interleaved in one process) and stays
-    // selectable (GS_SWEEP_TW = 1); the statistics' summation order is the same
-    // for both shapes (k_stats_finish)
-    int tw = 4;
-    if (const char* env = getenv("GS_SWEEP_TW")) {
-        const int v = atoi(env);
-        if (v == 1 || v == 4) tw = v;
-    }
+    // 1 tile x 4 chunks with the 4 waves' partials summed in LDS (a quarter of
+    // the partial traffic) was measured slower at the bench size (sweep
+    // 282-294 vs 261-281 us, interleaved in one process) and removed (r02)
+    const int tw = 4;
     const int cw = 4 / tw;
     p->sweep_tw = tw;
     p->nchunkg = (p->nchunk + cw - 1) / cw;
@@ -1540,9 +1513,9 @@ static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e
 }
 
 static int stats_finish(gs_plan* p, double* stats, void* stream) {
-    const long long n = (long long)p->nchains * p->nstat * (p->L + 1);
-    hipLaunchKernelGGL(k_stats_finish, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
-                       p->nchunkg, p->rows_per_task, 4 / p->sweep_tw, p->nstat, p->partials, stats);
+    const long long n = (long long)p->nchains * p->nstat * p->ntile;
+    hipLaunchKernelGGL(k_stats_finish, dim3((unsigned)n), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
+                       p->nchunkg, p->rows_per_task, p->nstat, p->partials, stats);
     GS_LAUNCH_CHECK("k_stats_finish");
     return 0;
 }
