@@ -103,6 +103,7 @@ _SIGS = [
     ("gs_step_asis", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
                                     _VP, _VP, ctypes.c_int, _VP]),
     ("gs_iteration_counter", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_uint32]),
+    ("gs_graph_step", ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32]),
     ("gs_advance_iteration", ctypes.c_int, [_VP, _VP]),
     ("gs_record_trace", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_uint32, _VP]),
     ("gs_sweep_timing", ctypes.c_int, [_VP, ctypes.c_int, c_double_p, c_int_p]),

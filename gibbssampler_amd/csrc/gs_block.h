@@ -26,11 +26,13 @@ __device__ __forceinline__ double dl_at(const double* __restrict__ dl_chain, con
 }
 
 // iteration counter of the counter-based streams: a host value, or (for
-// hipGraph replay) a device word advanced by k_iter_advance once per step
+// hipGraph replay) a device base word plus the step's offset within the
+// captured graph (host); the graph's last step advances the base by the
+// number of steps it holds, so only one launch per replay takes a ticket
 struct IterArg {
     uint32_t host;
     const uint32_t* dev;
-    __device__ __forceinline__ uint32_t get() const { return dev ? *dev : host; }
+    __device__ __forceinline__ uint32_t get() const { return dev ? *dev + host : host; }
 };
 
 // lower Cholesky of the TE block of C and the B entry, zero-variance rule
@@ -55,24 +57,36 @@ __device__ __forceinline__ CovChol cov_chol_teb(double tt, double ee, double te,
 // MODE 0 centered (CenteredGibbs.py:324-351):   Sigma = (C^+ + diag(b^2 k))^-1, M = Sigma diag(b k)
 // MODE 1 non-centered (NonCenteredGibbs.py:141-174): Sigma = (I + A^T diag(b^2 k) A)^-1,
 //                                                   M = Sigma A^T diag(b k), A = chol(C)
-// the operator of one (chain, l) into registers (the CR sweep computes its own
-// lanes' operators this way; block_params_at stores them)
-template <int F, int MODE>
-__device__ __forceinline__ void block_params_compute(int chain, int ell, int L, int maxbins,
-                                                     const double* __restrict__ dl, const int* __restrict__ ell2bin,
-                                                     const double* __restrict__ bl, double k0, double k1, double k2,
-                                                     double (&p)[gs_block::NP]) {
+// the D_l of every spectrum at this l (for the operator below): the bin
+// indices, then the values, each group issued together and unconditionally (an
+// unbinned l reads bin 0 and drops it) -- two memory latencies in all
+template <int F>
+__device__ __forceinline__ void block_params_load(int chain, int ell, int L, int maxbins, const double* __restrict__ dl,
+                                                  const int* __restrict__ ell2bin,
+                                                  double (&dq)[F == 1 ? 1 : (F == 2 ? 2 : 4)]) {
     const int Lp1 = L + 1;
     constexpr int NS = F == 1 ? 1 : (F == 2 ? 2 : 4);
     const double* dlc = dl + (long long)chain * NS * maxbins;
-    const double b = bl[ell];
+    int bq[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) bq[q] = ell2bin[q * Lp1 + ell];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) dq[q] = dlc[q * maxbins + max(bq[q], 0)];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) dq[q] = bq[q] < 0 ? 0.0 : dq[q];
+}
+
+// the operator from this l's binned D_l (dq) and beam b
+template <int F, int MODE>
+__device__ __forceinline__ void block_params_from(int ell, double b, const double (&dq)[F == 1 ? 1 : (F == 2 ? 2 : 4)],
+                                                  double k0, double k1, double k2, double (&p)[gs_block::NP]) {
     const double kap[3] = {k0, k1, k2};
 #pragma unroll
     for (int q = 0; q < gs_block::NP; ++q) p[q] = 0.0;
     if constexpr (F != 3) {
 #pragma unroll
         for (int f = 0; f < F; ++f) {
-            const double v = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, f, ell), ell);
+            const double v = var_from_dl(dq[f], ell);
             double sig, M;
             if constexpr (MODE == 0) {
                 const double iv = v != 0.0 ? 1.0 / v : 0.0;
@@ -86,10 +100,10 @@ __device__ __forceinline__ void block_params_compute(int chain, int ell, int L, 
             p[F + f] = sqrt(sig);
         }
     } else {
-        const double tt = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 0, ell), ell);
-        const double ee = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 1, ell), ell);
-        const double bb = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 2, ell), ell);
-        const double te = var_from_dl(dl_at(dlc, ell2bin, maxbins, Lp1, 3, ell), ell);
+        const double tt = var_from_dl(dq[0], ell);
+        const double ee = var_from_dl(dq[1], ell);
+        const double bb = var_from_dl(dq[2], ell);
+        const double te = var_from_dl(dq[3], ell);
         const double p0 = b * b * k0, p1 = b * b * k1, p2 = b * b * k2;
         double s00, s11, s01, s22, M00, M01, M10, M11, M22;
         if constexpr (MODE == 0) {
@@ -132,6 +146,18 @@ __device__ __forceinline__ void block_params_compute(int chain, int ell, int L, 
         p[0] = M00; p[1] = M01; p[2] = M10; p[3] = M11; p[4] = M22;
         p[5] = l00; p[6] = l10; p[7] = l11; p[8] = sqrt(s22); p[9] = 0.0;
     }
+}
+
+// the operator of one (chain, l) into registers (the CR sweep computes its own
+// lanes' operators this way; block_params_at stores them)
+template <int F, int MODE>
+__device__ __forceinline__ void block_params_compute(int chain, int ell, int L, int maxbins,
+                                                     const double* __restrict__ dl, const int* __restrict__ ell2bin,
+                                                     const double* __restrict__ bl, double k0, double k1, double k2,
+                                                     double (&p)[gs_block::NP]) {
+    double dq[F == 1 ? 1 : (F == 2 ? 2 : 4)];
+    block_params_load<F>(chain, ell, L, maxbins, dl, ell2bin, dq);
+    block_params_from<F, MODE>(ell, bl[ell], dq, k0, k1, k2, p);
 }
 
 template <int F, int MODE>

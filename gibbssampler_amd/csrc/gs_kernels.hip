@@ -58,6 +58,9 @@ struct gs_plan {
     // chains the per-workgroup recomputation costs more than the table
     // (measured: 32 TEB chains at L 1024, sweep 271 -> 287 us)
     bool inkernel_params = false;
+    // the latency form of the sweep (all loads first) may be used for short tasks;
+    // GS_SWEEP_THROUGHPUT at plan creation forces the throughput form (A/B timing)
+    bool sweep_latency = true;
     // MH phases: spectra whose blocks are mutually independent run in one launch
     int nphase = 0;
     int phase_n[4] = {0, 0, 0, 0};
@@ -93,6 +96,11 @@ struct gs_plan {
     uint32_t* iter_dev = nullptr;
     bool iter_dev_on = false;
     const uint32_t* itp() const { return iter_dev_on ? iter_dev : nullptr; }
+    // graph-captured steps (gs_graph_step): this step's offset from the device
+    // base, and how far its last launch advances the base (0: not at all)
+    uint32_t graph_off = 0, graph_adv = 1;
+    IterArg ita(uint32_t host_it) const { return IterArg{iter_dev_on ? graph_off : host_it, itp()}; }
+    uint32_t* adv_counter() const { return iter_dev_on && graph_adv ? iter_dev : nullptr; }
     // dominant-kernel timing
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -305,7 +313,138 @@ struct SweepOp {
 // consecutive workgroups are consecutive chains of the same task and share the
 // data reads in L2.  Each wave writes its 64 l's statistic partials of its
 // chunk; k_stats_finish sums them in a fixed order.
-template <int F, int ZM, bool STORE>
+// the operator of this lane's l: from the chain's D_l (op.mode >= 0) or the table
+template <int F>
+__device__ __forceinline__ void sweep_operator(bool ok, int chain, int ell, int L, const double* __restrict__ params,
+                                               const SweepOp& op, double (&pm)[NP]) {
+    if (ok && op.mode >= 0) {
+        if (op.mode == GS_MODE_CENTERED)
+            block_params_compute<F, GS_MODE_CENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
+                                                      op.k1, op.k2, pm);
+        else
+            block_params_compute<F, GS_MODE_NONCENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
+                                                         op.k1, op.k2, pm);
+    } else if (ok) {
+        const double* pp = params + ((long long)chain * (L + 1) + ell) * NP;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) pm[q] = pp[q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) pm[q] = 0.0;
+    }
+}
+
+// Latency form of the sweep for few chains (PRE = the most rows a task holds):
+// there the launch has ~one wave per SIMD and each wave's time is its chain of
+// memory latencies, so every global load of the wave -- its PRE data rows, the
+// Box-Muller tables, the operator's D_l -- is issued before any of them is
+// used (one memory round trip instead of one per row plus two for the
+// prologue).  Same arithmetic in the same order as the throughput form below.
+template <int F, bool STORE, int PRE>
+__device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
+                                                 const int2* __restrict__ tasks, const double* __restrict__ d,
+                                                 double* __restrict__ s,
+                                                 double* __restrict__ partials, uint32_t seed_lo, uint32_t seed_hi,
+                                                 uint32_t iter, uint32_t substep, int chain0, const SweepOp& op,
+                                                 double* tab) {
+    constexpr int NS = SweepAcc<F>::NS;
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int pair = wg / nchains;
+    const int chain = wg % nchains;
+    const int lane = threadIdx.x & 63;
+    const int2 gc = tasks[pair];
+    if (gc.x < 0) return;                       // padding pair (whole workgroup, before any barrier)
+    const int w = threadIdx.x >> 6, cw = 4 / tw;
+    const int t = tw * gc.x + w % tw;
+    const int lhi = L - WAVE * t;
+    const int m0 = (cw * gc.y + w / tw) * tm;
+    const int m1 = min(m0 + tm, lhi + 1);
+    const bool active = t < ntile && m0 < m1;
+    GS_ASSERT(m1 - m0 <= PRE || !active);
+    const int ell_lo = lhi - 63;
+    const int ell = ell_lo + lane;
+    const bool lane_ok = ell >= 0;
+    const long long NR = (long long)(L + 1) * (L + 1);
+    // 1. the data rows: lanes outside the triangle (l < m, l < 0) read the
+    //    row's diagonal entry instead (in bounds, never used); row m = 0 is one
+    //    slot per l (its second load, slot l + 1 <= L + 1, is never used).  No
+    //    load sits behind a condition, so they all issue back to back.
+    // 0. the l -> bin indices of the operator's D_l (first: the D_l loads that
+    //    depend on them then wait for these alone, not for the rows below)
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    const int lc = max(ell, 0);
+    int bidx[NSP];
+#pragma unroll
+    for (int q = 0; q < NSP; ++q) bidx[q] = op.ell2bin[q * (L + 1) + lc];
+    double dq[PRE][F][2];
+    {
+        const int mlast = max(m1 - 1, m0);
+#pragma unroll
+        for (int k = 0; k < PRE; ++k) {
+            const int mk = min(m0 + k, mlast);
+            const int le = min(max(ell, mk), L);
+            const long long i = (long long)mk * (2 * L + 1 - mk) / 2 + le;
+            const long long r = mk == 0 ? (long long)le : 2 * i - (L + 1);
+            load_d<F, 2>(d, NR, r, dq[k]);
+        }
+    }
+    // 2. the Box-Muller tables into registers (staged in LDS below), the beam
+    double tv[(BM_TAB_DOUBLES + 255) / 256];
+#pragma unroll
+    for (int k = 0; k < (BM_TAB_DOUBLES + 255) / 256; ++k) {
+        const int j = threadIdx.x + 256 * k;
+        tv[k] = j < 256 ? BM_LOG_TAB[j] : BM_TRIG_TAB[min(j - 256, 511)];
+    }
+    const double bq = op.bl[lc];
+    // 3. this l's D_l (the latency form always computes the operator in-kernel,
+    //    op.mode >= 0; an unbinned l reads bin 0 and drops it)
+    double dlq[NSP];
+    {
+        const double* dlc = op.dl + (long long)chain * NSP * op.maxbins;
+#pragma unroll
+        for (int q = 0; q < NSP; ++q) dlq[q] = dlc[q * op.maxbins + max(bidx[q], 0)];
+#pragma unroll
+        for (int q = 0; q < NSP; ++q) dlq[q] = bidx[q] < 0 ? 0.0 : dlq[q];
+    }
+    // 4. the operator
+    double pm[NP];
+    if (op.mode == GS_MODE_CENTERED)
+        block_params_from<F, GS_MODE_CENTERED>(lc, bq, dlq, op.k0, op.k1, op.k2, pm);
+    else
+        block_params_from<F, GS_MODE_NONCENTERED>(lc, bq, dlq, op.k0, op.k1, op.k2, pm);
+#pragma unroll
+    for (int k = 0; k < (BM_TAB_DOUBLES + 255) / 256; ++k) {
+        const int j = threadIdx.x + 256 * k;
+        if (j < BM_TAB_DOUBLES) tab[j] = tv[k];
+    }
+    __syncthreads();
+    if (!active) return;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    const uint32_t tag = TAG_CR | (substep << 8);
+    double acc[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) acc[q] = 0.0;
+    double* sc = s + (long long)chain * F * NR;
+#pragma unroll
+    for (int k = 0; k < PRE; ++k) {
+        const int m = m0 + k;
+        if (m < m1 && lane_ok && ell >= m) {
+            if (m == 0) {
+                sweep_entry<F, 0, STORE, 1>(dq[k], nullptr, sc, NR, ell, (uint32_t)ell, tag, iter, key, pm, acc, tab);
+            } else {
+                const long long i = (long long)m * (2 * L + 1 - m) / 2 + ell;
+                sweep_entry<F, 0, STORE, 2>(dq[k], nullptr, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm,
+                                            acc, tab);
+            }
+        }
+    }
+    double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
+}
+
+template <int F, int ZM, bool STORE, int PRE = 0>
 __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
                                                   const double* __restrict__ params, const double* __restrict__ z,
@@ -315,6 +454,12 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const uint32_t iter = itarg.get();
     constexpr int NS = SweepAcc<F>::NS;
     __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
+    if constexpr (PRE > 0) {
+        static_assert(ZM == 0, "latency form: native draws only");
+        cr_sweep_latency<F, STORE, PRE>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo,
+                                        seed_hi, iter, substep, chain0, op, tab);
+        return;
+    }
     if constexpr (ZM == 0) {
         bm_stage_tables(tab);
         __syncthreads();
@@ -346,22 +491,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const uint32_t tag = TAG_CR | (substep << 8);
 
     double pm[NP];
-    if (ZM != 2 && lane_ok && active && op.mode >= 0) {
-        // this lane's l: the operator from the chain's D_l (no parameter table)
-        if (op.mode == GS_MODE_CENTERED)
-            block_params_compute<F, GS_MODE_CENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
-                                                      op.k1, op.k2, pm);
-        else
-            block_params_compute<F, GS_MODE_NONCENTERED>(chain, ell, L, op.maxbins, op.dl, op.ell2bin, op.bl, op.k0,
-                                                         op.k1, op.k2, pm);
-    } else if (ZM != 2 && lane_ok && active) {
-        const double* pp = params + ((long long)chain * (L + 1) + ell) * NP;
-#pragma unroll
-        for (int q = 0; q < NP; ++q) pm[q] = pp[q];
-    } else {
-#pragma unroll
-        for (int q = 0; q < NP; ++q) pm[q] = 0.0;
-    }
+    sweep_operator<F>(ZM != 2 && lane_ok && active, chain, ell, L, params, op, pm);
     double acc[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) acc[q] = 0.0;
@@ -423,16 +553,20 @@ __global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int nt
     GS_ASSERT(chain < nchains && cmax < nchunkg);
     const double* pp = partials + ((long long)chain * ntile + t) * nchunkg * nstat * WAVE + q * WAVE + lane;
     const long long cs = (long long)nstat * WAVE;
+    // groups of G of this wave's chunks, every load of a group issued before
+    // the sums (the last group's loads clamped to a valid chunk, its extra
+    // values dropped): with few chains the finish is a chain of memory
+    // latencies, one per group; the sums keep the chunk order
+    constexpr int G = 16;
     double acc = 0.0;
-    int c = w;
-    for (; c + 12 <= cmax; c += 16) {
-        double v[4];
+    for (int c = w; c <= cmax; c += 4 * G) {
+        double v[G];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = pp[(c + 4 * j) * cs];
+        for (int j = 0; j < G; ++j) v[j] = pp[min(c + 4 * j, cmax) * cs];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc += v[j];
+        for (int j = 0; j < G; ++j)
+            if (c + 4 * j <= cmax) acc += v[j];
     }
-    for (; c <= cmax; c += 4) acc += pp[c * cs];
     __shared__ double red[4][WAVE];
     red[w][lane] = acc;
     __syncthreads();
@@ -457,13 +591,13 @@ __global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int nt
 // handed between workgroups here, so no release / acquire fence is needed
 // (an agent-scope __threadfence costs ~3.5 us per workgroup,
 // MI355X_MICROARCH.md visibility table); the next launch sees the counter.
-__device__ __forceinline__ void ticket_advance(uint32_t* counter, uint32_t nblk) {
+__device__ __forceinline__ void ticket_advance(uint32_t* counter, uint32_t nblk, uint32_t adv) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t t = __hip_atomic_fetch_add(&counter[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == nblk - 1) {
             __hip_atomic_store(&counter[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&counter[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&counter[0], adv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -502,12 +636,28 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
         }
         {
             double nu = 0.0, a = 0.0, dd = 0.0, c = 0.0;
-            for (int l = be[b]; l < be[b + 1]; ++l) {
-                const double w = (double)l * (l + 1) / (2.0 * PI);
-                nu += 2.0 * l + 1.0;
-                a += w * st[0 * Lp1 + l];
-                dd += w * st[1 * Lp1 + l];
-                c += w * st[3 * Lp1 + l];
+            // the bin's statistics in groups of 8 l with every load issued before
+            // the sums (clamped indices, no load behind a condition): one memory
+            // latency per 8 l instead of one per l; the sums keep the l order
+            const int l0 = be[b], l1 = be[b + 1];
+            for (int lg = l0; lg < l1; lg += 8) {
+                double va[8], vd[8], vc[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int l = min(lg + j, l1 - 1);
+                    va[j] = st[0 * Lp1 + l]; vd[j] = st[1 * Lp1 + l]; vc[j] = st[3 * Lp1 + l];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int l = lg + j;
+                    if (l < l1) {
+                        const double w = (double)l * (l + 1) / (2.0 * PI);
+                        nu += 2.0 * l + 1.0;
+                        a += w * va[j];
+                        dd += w * vd[j];
+                        c += w * vc[j];
+                    }
+                }
             }
             nu -= 3.0;
             double tt = 0.0, ee = 0.0, te = 0.0;
@@ -517,8 +667,10 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
                 const double l00 = sqrt(s00);
                 const double l10 = s01 / l00;
                 const double l11 = sqrt(s11 - l10 * l10);
-                const double c1 = sqrt(2.0 * gamma_mt(0.5 * nu, key, b, 16, iter, 0));
-                const double c2 = sqrt(2.0 * gamma_mt(0.5 * (nu - 1.0), key, b, 17, iter, 0));
+                double g1, g2;
+                gamma_mt_pair(0.5 * nu, 0.5 * (nu - 1.0), key, b, 16, 17, iter, 0, g1, g2);
+                const double c1 = sqrt(2.0 * g1);
+                const double c2 = sqrt(2.0 * g2);
                 const double n = normal1(key, b, 0, TAG_IW_N, iter);
                 const double b00 = l00 * c1;
                 const double b10 = l10 * c1 + l11 * n;
@@ -541,10 +693,20 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
     }
     {
         double beta = 0.0, expo = 0.0;
-        for (int l = be[b]; l < be[b + 1]; ++l) {
-            const double chat = st[ssrow * Lp1 + l] / (2.0 * l + 1.0);
-            beta += (2.0 * l + 1.0) * l * (l + 1.0) * (chat / (4.0 * PI));
-            expo += (2.0 * l + 1.0) / 2.0;
+        const int l0 = be[b], l1 = be[b + 1];
+        for (int lg = l0; lg < l1; lg += 8) {          // loads first, as in the TEB block above
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = st[ssrow * Lp1 + min(lg + j, l1 - 1)];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int l = lg + j;
+                if (l < l1) {
+                    const double chat = v[j] / (2.0 * l + 1.0);
+                    beta += (2.0 * l + 1.0) * l * (l + 1.0) * (chat / (4.0 * PI));
+                    expo += (2.0 * l + 1.0) / 2.0;
+                }
+            }
         }
         const double alpha = b == 0 ? 1.0 : expo - 1.0;
         double X;
@@ -561,11 +723,11 @@ __global__ __launch_bounds__(64) void k_cls_draw(int L, int nchains, int maxbins
                                                  const double* __restrict__ variates, uint32_t seed_lo,
                                                  uint32_t seed_hi, IterArg itarg, int chain0,
                                                  double* __restrict__ dl_out, double* __restrict__ trace, int cap,
-                                                 uint32_t* __restrict__ counter) {
+                                                 uint32_t* __restrict__ counter, uint32_t adv) {
     const uint32_t iter = itarg.get();
     cls_draw_body<F>(L, maxbins, bins, nbins_arr, stats, variates, seed_lo, seed_hi, iter, chain0, dl_out, trace,
                      cap, nchains);
-    if (counter) ticket_advance(counter, gridDim.x * gridDim.y * gridDim.z);
+    if (counter) ticket_advance(counter, gridDim.x * gridDim.y * gridDim.z, adv);
 }
 
 
@@ -839,8 +1001,9 @@ struct MhPhases {
 struct MhEpi {
     double* trace;          // nullable: trace[(it-1) % cap][chain][nspec][maxbins]
     int cap;
-    uint32_t* counter;      // nullable: [0] iteration (advanced), [1] finished-workgroup ticket
+    uint32_t* counter;      // nullable: [0] iteration base (advanced by adv), [1] finished-workgroup ticket
     int nchains;
+    uint32_t adv;
 };
 
 // SC: this chain's per-l statistics cached in LDS for the whole kernel (every
@@ -1014,7 +1177,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
         double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
         for (int k = tid; k < nrow; k += blockDim.x) tr[k] = Ds[k];
     }
-    if (epi.counter) ticket_advance(epi.counter, gridDim.x);
+    if (epi.counter) ticket_advance(epi.counter, gridDim.x, epi.adv);
 }
 
 // stats of s_nc = A^+ s, A = chol(C(dl)) (ASIS.py:185-189)
@@ -1350,6 +1513,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->gbuf, (size_t)p->nchains * 2 * (L + 1));
     build_tasks(p);
     p->inkernel_params = p->nchains <= 4;
+    p->sweep_latency = getenv("GS_SWEEP_THROUGHPUT") == nullptr;
     const size_t nc = (size_t)p->nchains;
     rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunkg * p->nstat * WAVE);
     rc |= dev_alloc(&p->params, nc * (L + 1) * NP);
@@ -1520,7 +1684,7 @@ static int stats_finish(gs_plan* p, double* stats, void* stream) {
     return 0;
 }
 
-static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, const double* z, uint64_t seed,
+static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, const double* z, uint64_t seed,
                         uint32_t iteration, uint32_t substep, double* s_out, double* stats, bool given,
                         void* stream, bool finish = true, int pmode = -1, const double* dl = nullptr) {
     if (check_plan(p)) return -1;
@@ -1532,10 +1696,24 @@ static int sweep_launch(gs_plan* p, const double* d_alm, const double* params, c
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing_begin(p, S(stream), &e0, &e1)) return -1;
     const bool rep = z != nullptr, st = s_out != nullptr;
+    // latency form (all loads first) for few chains with short tasks; the
+    // throughput form otherwise (more chains: its registers buy occupancy)
+    const bool lat = pmode >= 0 && p->rows_per_task <= 4 && !given && !rep && st &&
+                     p->sweep_latency;
+    if (lat) {
+#define GS_SWL(FF) hipLaunchKernelGGL((k_cr_sweep<FF, 0, true, 4>), g, b, 0, S(stream), p->L, p->nchains, p->ntile,   \
+                                      p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z, s_out,     \
+                                      p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op)
+        if (p->F == 1) GS_SWL(1); else if (p->F == 2) GS_SWL(2); else GS_SWL(3);
+#undef GS_SWL
+        GS_LAUNCH_CHECK("k_cr_sweep");
+        if (p->timing && record_ev(e1, S(stream))) return -1;
+        return finish ? stats_finish(p, stats, stream) : 0;
+    }
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,   \
                                              s_out,                                                                   \
-                                             p->partials, slo, shi, IterArg{iteration, p->itp()}, substep, p->chain0, \
+                                             p->partials, slo, shi, p->ita(iteration), substep, p->chain0, \
                                              op)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
                         else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
@@ -1565,8 +1743,8 @@ static int cls_draw_launch(gs_plan* p, const double* stats, const double* variat
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const dim3 g(p->nchains, p->nspec, (p->maxbins + 63) / 64), b(64);
 #define GS_CD(FF) hipLaunchKernelGGL((k_cls_draw<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
-                                     stats, variates, slo, shi, IterArg{iteration, p->itp()}, p->chain0, dl_out, trace, \
-                                     cap, counter)
+                                     stats, variates, slo, shi, p->ita(iteration), p->chain0, dl_out, trace, \
+                                     cap, counter, p->graph_adv)
     if (p->F == 1) GS_CD(1); else if (p->F == 2) GS_CD(2); else GS_CD(3);
 #undef GS_CD
     GS_LAUNCH_CHECK("k_cls_draw");
@@ -1592,14 +1770,14 @@ int gs_mh_propose(gs_plan* p, const double* dl, const double* u_prop, uint64_t s
     GS_CHECK(hipMemsetAsync(logr_out, 0, nprop * sizeof(double), S(stream)));
 #define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
                                      p->maxbins, p->meta, p->prop_sd, dl, prop_out, logr_out, u_prop, slo, shi,     \
-                                     IterArg{iteration, p->itp()}, p->chain0)
+                                     p->ita(iteration), p->chain0)
     if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
 #undef GS_MP
     GS_LAUNCH_CHECK("k_mh_propose");
     if (u_acc_out) {
         const long long n = (long long)p->nchains * p->nacc;
         hipLaunchKernelGGL(k_mh_uniforms, dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->nchains, p->nspec,
-                           p->maxbins, p->meta, p->nacc, p->n_iter_mh, slo, shi, IterArg{iteration, p->itp()},
+                           p->maxbins, p->meta, p->nacc, p->n_iter_mh, slo, shi, p->ita(iteration),
                            p->chain0, u_acc_out);
         GS_LAUNCH_CHECK("k_mh_uniforms");
     }
@@ -1614,7 +1792,7 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
 #define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
-                                     p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi, IterArg{iteration, p->itp()}, \
+                                     p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi, p->ita(iteration), \
                                      p->chain0)
     if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
 #undef GS_MP
@@ -1626,7 +1804,7 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
                      uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi) {
     int maxnb = 0;
-    const MhEpi none{nullptr, 1, nullptr, p->nchains};
+    const MhEpi none{nullptr, 1, nullptr, p->nchains, 0};
     const MhEpi E = epi ? *epi : none;
     MhPhases ph{};
     ph.nphase = p->nphase;
@@ -1648,7 +1826,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
 #define GS_MF2(FF, SCV, LDSV) hipLaunchKernelGGL((k_mh_fused<FF, SCV>), dim3(p->nchains), dim3(1024), LDSV, S(stream), p->L, p->maxbins, ph, \
                                      p->phase_tab, p->phase_rng, p->bins, p->blocks, p->meta + 8, p->nacc, p->n_iter_mh, p->ell2blk,    \
                                      p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop,       \
-                                     p->logr, u_acc, slo, shi, IterArg{iteration, p->itp()}, p->chain0, accept_out, E)
+                                     p->logr, u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out, E)
         if (p->F == 1) { GS_MF(1); } else if (p->F == 2) { GS_MF(2); } else { GS_MF(3); }
 #undef GS_MF2
 #undef GS_MF
@@ -1672,7 +1850,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
         const int2* tab = p->phase_tab + p->phase_off[ph];
 #define GS_MA(FF) hipLaunchKernelGGL((k_mh_accept<FF>), dim3(nblk(waves, 4)), dim3(256), 0, S(stream), p->L, p->nchains, \
                                      p->maxbins, sp0, p->bins, p->blocks, tab, nb, p->meta + 8, p->nacc, p->n_iter_mh, \
-                                     p->gbuf, dl, p->prop, p->logr, u_acc, slo, shi, IterArg{iteration, p->itp()}, p->chain0, accept_out)
+                                     p->gbuf, dl, p->prop, p->logr, u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out)
         if (p->F == 1) GS_MA(1); else if (p->F == 2) GS_MA(2); else GS_MA(3);
 #undef GS_MA
         GS_LAUNCH_CHECK("k_mh_accept");
@@ -1730,7 +1908,7 @@ int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* 
     if (trace && capacity < 1) return set_error("gs_step_centered_fused: capacity < 1");
     if (!d_alm || !dl) return set_error("gs_step_centered_fused: null argument");
     if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream)) return -1;
-    return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->iter_dev, stream);
+    return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->adv_counter(), stream);
 }
 
 int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t it, void* stream) {
@@ -1748,7 +1926,7 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
                                       p->u_nat, p->nspec, p->nacc, p->n_iter_mh, p->L,                                  \
                                       p->nchains, p->maxbins, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], \
                                       p->params, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi,            \
-                                      IterArg{it, p->itp()}, p->chain0)
+                                      p->ita(it), p->chain0)
     if (p->F == 1) GS_PRO(1); else if (p->F == 2) GS_PRO(2); else GS_PRO(3);
 #undef GS_PRO
     GS_LAUNCH_CHECK("k_nc_prologue");
@@ -1786,7 +1964,7 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
     if (!dl) return set_error("gs_nc_decide_fused: null argument");
     if (trace && capacity < 1) return set_error("gs_nc_decide_fused: capacity < 1");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    const MhEpi epi{trace, std::max(capacity, 1), p->iter_dev_on ? p->iter_dev : nullptr, p->nchains};
+    const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv};
     return mh_decide(p, p->stats, dl, p->u_nat_ready ? p->u_nat : nullptr, slo, shi, it, accept_out, stream, &epi);
 }
 
@@ -1842,13 +2020,13 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
     const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
 #define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
                                      p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, nullptr, slo, shi,        \
-                                     IterArg{it, p->itp()}, p->chain0)
+                                     p->ita(it), p->chain0)
     if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
 #undef GS_MP
     GS_LAUNCH_CHECK("k_mh_propose");
     // the trace record and the counter advance ride in the MH launch (no kernel
     // after it reads the counter: the re-centring uses D_l only)
-    const MhEpi epi{trace, trace ? capacity : 1, p->iter_dev, p->nchains};
+    const MhEpi epi{trace, trace ? capacity : 1, p->adv_counter(), p->nchains, p->graph_adv};
     if (mh_decide(p, p->stats, dl, nullptr, slo, shi, it, accept_out, stream, &epi)) return -1;
     if (recentre && s_out) {
         const bool quirk = (p->quirks & GS_QUIRK_ASIS_RECENTRE_CENTERED) != 0;
@@ -1860,7 +2038,17 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
 int gs_iteration_counter(gs_plan* p, int enable, uint32_t start) {
     if (check_plan(p)) return -1;
     p->iter_dev_on = enable != 0;
+    p->graph_off = 0;
+    p->graph_adv = 1;
     if (enable) GS_CHECK(hipMemcpy(p->iter_dev, &start, sizeof(uint32_t), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int gs_graph_step(gs_plan* p, uint32_t offset, uint32_t advance) {
+    if (check_plan(p)) return -1;
+    if (!p->iter_dev_on) return set_error("gs_graph_step: device counter not enabled");
+    p->graph_off = offset;
+    p->graph_adv = advance;
     return 0;
 }
 
@@ -1878,7 +2066,7 @@ int gs_record_trace(gs_plan* p, const double* dl, double* trace, int capacity, u
     if (!dl || !trace) return set_error("gs_record_trace: null argument");
     const long long n = (long long)p->nchains * p->nspec * p->maxbins;
     hipLaunchKernelGGL(k_record_trace, dim3(nblk(n, 256)), dim3(256), 0, S(stream), n, dl, trace, capacity,
-                       IterArg{iteration, p->itp()});
+                       p->ita(iteration));
     GS_LAUNCH_CHECK("k_record_trace");
     return 0;
 }

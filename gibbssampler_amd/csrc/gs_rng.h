@@ -163,6 +163,56 @@ __device__ inline double gamma_mt(double alpha, Key k, uint32_t b, uint32_t spec
     return g;
 }
 
+// Two independent Gamma draws with the streams of gamma_mt(alpha0, k, b, spec0,
+// it, sub) and gamma_mt(alpha1, k, b, spec1, it, sub), bit-identical to those
+// two calls, run in lockstep: attempt j of both in one loop iteration, so the
+// two rejection chains overlap instead of following one another (the
+// inverse-Wishart's two Bartlett factors).
+__device__ inline void gamma_mt_pair(double alpha0, double alpha1, Key k, uint32_t b, uint32_t spec0, uint32_t spec1,
+                                     uint32_t it, uint32_t sub, double& g0, double& g1) {
+    const double al[2] = {alpha0, alpha1};
+    const double a[2] = {alpha0 >= 1.0 ? alpha0 : alpha0 + 1.0, alpha1 >= 1.0 ? alpha1 : alpha1 + 1.0};
+    const uint32_t sp[2] = {spec0, spec1};
+    double d[2], c[2], g[2] = {0.0, 0.0};
+    bool done[2] = {false, false};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        d[q] = a[q] - 1.0 / 3.0;
+        c[q] = 1.0 / sqrt(9.0 * d[q]);
+    }
+    for (uint32_t j = 0; j < (1u << 20) && !(done[0] && done[1]); ++j) {
+        // both attempts unconditionally (pure functions of the counters), so
+        // their Philox / Box-Muller chains interleave; a finished draw ignores its
+        // later attempts
+        double x[2], u[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t cc = sp[q] | (j << 8);
+            x[q] = normal1(k, b, cc, TAG_GAMMA_N | (sub << 8), it);
+            u[q] = uniform1(k, b, cc, TAG_GAMMA_U | (sub << 8), it);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const double t = 1.0 + c[q] * x[q];
+            const double v = t * t * t;
+            const bool acc = t > 0.0 && (u[q] < 1.0 - 0.0331 * (x[q] * x[q]) * (x[q] * x[q]) ||
+                                         log(u[q]) < 0.5 * x[q] * x[q] + d[q] * (1.0 - v + log(v)));
+            if (acc && !done[q]) {
+                g[q] = d[q] * v;
+                done[q] = true;
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (al[q] < 1.0) {
+            const double ub = uniform1(k, b, sp[q], TAG_GAMMA_BOOST | (sub << 8), it);
+            g[q] = g[q] * exp(log(ub) / al[q]);
+        }
+    g0 = g[0];
+    g1 = g[1];
+}
+
 // ---- table-driven fp64 Box-Muller for the CR sweep ------------------------
 // The tables (gs_bm_tables.h, correctly rounded) are staged in LDS once per
 // workgroup: tab[0..255] = {c_k, -ln c_k} (128 cells of [sqrt(1/2), sqrt(2))),

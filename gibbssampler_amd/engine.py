@@ -278,6 +278,11 @@ class GibbsPlan:
     def iteration_counter(self, enable, start=1):
         C.check(self.lib.gs_iteration_counter(self._h, 1 if enable else 0, int(start)), "gs_iteration_counter")
 
+    def graph_step(self, offset, advance):
+        """Offset of the next captured step from the device base, and the advance
+        its last launch applies (gs_graph_step)."""
+        C.check(self.lib.gs_graph_step(self._h, int(offset), int(advance)), "gs_graph_step")
+
     def advance_iteration(self):
         C.check(self.lib.gs_advance_iteration(self._h, self._s()), "gs_advance_iteration")
 

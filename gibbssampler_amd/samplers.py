@@ -127,6 +127,9 @@ class BatchedRunner:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for i in range(nsteps):
+                # step i reads base + i; only the last step's last launch advances
+                # the base (by nsteps): one counter ticket per replay
+                p.graph_step(i, nsteps if i == nsteps - 1 else 0)
                 if time_sweeps:
                     p.sweep_timing("resume" if i % time_every == 0 else "pause")
                 # accept_trace [nsteps, nchains, nacc]: step i writes its own slot
@@ -144,6 +147,7 @@ class BatchedRunner:
                     p.step_asis_fused(self.d, self.dl, self.s, seed=self.seed, accept=acc,
                                       dl_tmp=self.dl_tmp, recentre=self.materialize_recentre, trace=trace,
                                       capacity=trace_capacity or 0)
+        p.graph_step(0, 1)
         self.graph = g
         self.graph_steps = nsteps
         return g

@@ -183,10 +183,16 @@ int gs_step_asis(gs_plan* plan, const double* d_alm, double* dl_binned, double* 
                  int recentre, void* stream);
 
 /* hipGraph support: with the device counter enabled every RNG-consuming
- * kernel reads the iteration from a device word (the host value is ignored)
- * and gs_advance_iteration increments it, so one captured step replays as the
- * next iteration */
+ * kernel reads the iteration as a device base word plus the step's offset
+ * (the host iteration argument is ignored), so a captured graph replays as
+ * the next iterations.  gs_graph_step(offset, advance) sets the offset of the
+ * steps launched next (0 after gs_iteration_counter) and how far the fused
+ * entry points' last launch advances the base (1 after gs_iteration_counter:
+ * one captured step per replay; a graph of K steps passes offsets 0..K-1 and
+ * advance K on its last step, 0 on the others -- one ticket per replay).
+ * gs_advance_iteration increments the base by one from the stream. */
 int gs_iteration_counter(gs_plan* plan, int enable, uint32_t start);
+int gs_graph_step(gs_plan* plan, uint32_t offset, uint32_t advance);
 int gs_advance_iteration(gs_plan* plan, void* stream);
 /* trace[(it-1) % capacity][nchains][nspec][maxbins] <- dl_binned (history of GibbsSampler.py:172-173) */
 int gs_record_trace(gs_plan* plan, const double* dl_binned, double* trace, int capacity, uint32_t iteration,
