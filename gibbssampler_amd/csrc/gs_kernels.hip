@@ -557,7 +557,7 @@ __global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int nt
     // the sums (the last group's loads clamped to a valid chunk, its extra
     // values dropped): with few chains the finish is a chain of memory
     // latencies, one per group; the sums keep the chunk order
-    constexpr int G = 16;
+    constexpr int G = 16;             // 32 measured slower (4.7 -> 5.4 us at configs[1])
     double acc = 0.0;
     for (int c = w; c <= cmax; c += 4 * G) {
         double v[G];
@@ -635,31 +635,45 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
             return;
         }
         {
-            double nu = 0.0, a = 0.0, dd = 0.0, c = 0.0;
             // the bin's statistics in groups of 8 l with every load issued before
-            // the sums (clamped indices, no load behind a condition): one memory
-            // latency per 8 l instead of one per l; the sums keep the l order
+            // the sums (clamped indices, no load behind a condition); the first
+            // group is issued before the Gamma draws, which need only the bin's
+            // degrees of freedom, nu = sum (2l + 1) - 3 = l1^2 - l0^2 - 3 (exact,
+            // as the reference's running sum is), so the loads and the draws
+            // overlap.  The sums keep the l order.
             const int l0 = be[b], l1 = be[b + 1];
-            for (int lg = l0; lg < l1; lg += 8) {
-                double va[8], vd[8], vc[8];
+            double va[8], vd[8], vc[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int l = min(lg + j, l1 - 1);
-                    va[j] = st[0 * Lp1 + l]; vd[j] = st[1 * Lp1 + l]; vc[j] = st[3 * Lp1 + l];
+            for (int j = 0; j < 8; ++j) {
+                const int l = max(min(l0 + j, l1 - 1), 0);
+                va[j] = st[0 * Lp1 + l]; vd[j] = st[1 * Lp1 + l]; vc[j] = st[3 * Lp1 + l];
+            }
+            const double nu = (double)(l1 * l1 - l0 * l0) - 3.0;
+            double g1 = 0.0, g2 = 0.0, n = 0.0;
+            if (b >= 2) {
+                gamma_mt_pair(0.5 * nu, 0.5 * (nu - 1.0), key, b, 16, 17, iter, 0, g1, g2);
+                n = normal1(key, b, 0, TAG_IW_N, iter);
+            }
+            double a = 0.0, dd = 0.0, c = 0.0;
+            for (int lg = l0; lg < l1; lg += 8) {
+                if (lg > l0) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int l = min(lg + j, l1 - 1);
+                        va[j] = st[0 * Lp1 + l]; vd[j] = st[1 * Lp1 + l]; vc[j] = st[3 * Lp1 + l];
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int l = lg + j;
                     if (l < l1) {
                         const double w = (double)l * (l + 1) / (2.0 * PI);
-                        nu += 2.0 * l + 1.0;
                         a += w * va[j];
                         dd += w * vd[j];
                         c += w * vc[j];
                     }
                 }
             }
-            nu -= 3.0;
             double tt = 0.0, ee = 0.0, te = 0.0;
             if (b >= 2) {
                 const double det = a * dd - c * c;
@@ -667,11 +681,8 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
                 const double l00 = sqrt(s00);
                 const double l10 = s01 / l00;
                 const double l11 = sqrt(s11 - l10 * l10);
-                double g1, g2;
-                gamma_mt_pair(0.5 * nu, 0.5 * (nu - 1.0), key, b, 16, 17, iter, 0, g1, g2);
                 const double c1 = sqrt(2.0 * g1);
                 const double c2 = sqrt(2.0 * g2);
-                const double n = normal1(key, b, 0, TAG_IW_N, iter);
                 const double b00 = l00 * c1;
                 const double b10 = l10 * c1 + l11 * n;
                 const double b11 = l11 * c2;
@@ -692,26 +703,33 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
         return;
     }
     {
-        double beta = 0.0, expo = 0.0;
+        // as the TEB block above: the first 24 statistics issued before the
+        // Gamma draw, whose shape needs only sum (2l + 1) / 2 = (l1^2 - l0^2) / 2
         const int l0 = be[b], l1 = be[b + 1];
-        for (int lg = l0; lg < l1; lg += 8) {          // loads first, as in the TEB block above
-            double v[8];
+        constexpr int G = 24;
+        double v[G];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = st[ssrow * Lp1 + min(lg + j, l1 - 1)];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int l = lg + j;
-                if (l < l1) {
-                    const double chat = v[j] / (2.0 * l + 1.0);
-                    beta += (2.0 * l + 1.0) * l * (l + 1.0) * (chat / (4.0 * PI));
-                    expo += (2.0 * l + 1.0) / 2.0;
-                }
-            }
-        }
+        for (int j = 0; j < G; ++j) v[j] = st[ssrow * Lp1 + max(min(l0 + j, l1 - 1), 0)];
+        const double expo = (double)(l1 * l1 - l0 * l0) / 2.0;
         const double alpha = b == 0 ? 1.0 : expo - 1.0;
         double X;
         if (variates) X = variates[((long long)chain * NSP + sp) * maxbins + b];
         else X = b < 2 ? 0.0 : 1.0 / gamma_mt(alpha, key, b, sp, iter, 0);
+        double beta = 0.0;
+        for (int lg = l0; lg < l1; lg += G) {
+            if (lg > l0) {
+#pragma unroll
+                for (int j = 0; j < G; ++j) v[j] = st[ssrow * Lp1 + min(lg + j, l1 - 1)];
+            }
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const int l = lg + j;
+                if (l < l1) {
+                    const double chat = v[j] / (2.0 * l + 1.0);
+                    beta += (2.0 * l + 1.0) * l * (l + 1.0) * (chat / (4.0 * PI));
+                }
+            }
+        }
         out[b] = b < 2 ? 0.0 : beta * X;
         if (tr) tr[sp * maxbins + b] = out[b];
     }
