@@ -90,6 +90,13 @@ struct ShtDev {
     const int* lstart;       // [L+1][ngroup]
     const double2* st;       // [L+1][npair] (lambda_{ls-1}, lambda_ls), scaled
     const int* stk;          // [L+1][npair] scale exponent at ls
+    // l-segmented analysis (small maps): segment s of m covers l in
+    // [m + s seg, m + (s + 1) seg); the recurrence state at each segment start
+    // s >= 1 is a plan-time table (0: no segments, one walk from m to L)
+    int seg;
+    const int* segoff;       // [L+1] first table row of m's segments s >= 1
+    const double2* sst;      // [rows][npair] (lambda_{lA-1}, lambda_lA), scaled
+    const int* sstk;         // [rows][npair] scale exponent at lA
 };
 
 __device__ __forceinline__ long long cidx(int L, int l, int m) { return (long long)m * (2 * L + 1 - m) / 2 + l; }
@@ -212,6 +219,43 @@ __global__ __launch_bounds__(256) void k_sht_onset(ShtDev D, const double* __res
     if (act) {
         st[(long long)m * npair + p] = make_double2(v1, v0);
         stk[(long long)m * npair + p] = k;
+    }
+}
+
+// per (m, pair): the analysis recurrence's state at every segment start
+// lA = m + s seg (s >= 1) past the group's onset, walked from the onset state
+// with exactly the transform's step and rescaling (rec_step below), so a
+// segment entered at lA continues the same sequence a single walk would hold
+__device__ __forceinline__ void rec_step(const LegCoef& c, double x, double& v0, double& v1);
+__global__ __launch_bounds__(256) void k_sht_segstate(ShtDev D) {
+    const int L = D.L, npair = D.npair, S = D.seg;
+    const int m = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npair || S <= 0) return;
+    const int ls = D.lstart[(long long)m * D.ngroup + (p >> 6)];
+    const long long row0 = D.segoff[m];
+    const double x = D.geom[p].x;
+    const LegCoef* cf = D.coef + (cidx(L, m, m) - m);
+    double v1 = 0.0, v0 = 0.0;
+    int k = 0;
+    if (ls <= L) {
+        const double2 s0 = D.st[(long long)m * npair + p];
+        v1 = s0.x; v0 = s0.y;
+        k = D.stk[(long long)m * npair + p];
+    }
+    int l = ls;                                   // the state holds lambda_l
+    for (int s = 1; m + s * S <= L; ++s) {
+        const int lA = m + s * S;
+        if (ls <= L && lA > ls) {
+            for (; l < lA; ++l) {
+                rec_step(cf[l + 1], x, v0, v1);
+                if (k < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
+            }
+        }
+        const long long o = (row0 + s - 1) * npair + p;
+        const bool live = ls <= L && lA > ls;
+        const_cast<double2*>(D.sst)[o] = live ? make_double2(v1, v0) : make_double2(0.0, 0.0);
+        const_cast<int*>(D.sstk)[o] = live ? k : 0;
     }
 }
 
@@ -1075,11 +1119,23 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
         if (h == 1 && (!paired || m <= q)) break;
+        // l-segment of this launch (D.seg > 0, unpaired m): [lA, lend]; else m..L
+        const int sg = blockIdx.z;
+        const int lA = D.seg > 0 ? m + sg * D.seg : m;
+        if (lA > L) break;
+        const int lend = D.seg > 0 ? min(lA + D.seg - 1, L) : L;
         int ls[ASR];
+        bool tab[ASR];
 #pragma unroll
-        for (int r = 0; r < ASR; ++r)
+        for (int r = 0; r < ASR; ++r) {
             ls[r] = __builtin_amdgcn_readfirstlane(g0 + r < D.ngroup ? D.lstart[(long long)m * D.ngroup + g0 + r]
                                                                      : L + 1);
+            // a slot already past its onset at the segment start enters at lA with
+            // the tabulated state (loaded below); otherwise at its onset, as before
+            tab[r] = ls[r] <= L && ls[r] < lA;
+            if (tab[r]) ls[r] = lA;
+            if (ls[r] > lend) ls[r] = L + 1;          // nothing of this slot in the segment
+        }
         // each wave walks l from its own slots' first onset (no workgroup sync)
         int lmin = L + 1;
 #pragma unroll
@@ -1091,6 +1147,12 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
 #pragma unroll
         for (int r = 0; r < ASR; ++r) {
             v0[r] = 0.0; v1[r] = 0.0; kk[r] = 0;
+            if (tab[r] && ls[r] <= L && act[r]) {
+                const long long o = (long long)(D.segoff[m] + sg - 1) * npair + pr[r];
+                const double2 s0 = D.sst[o];
+                v1[r] = s0.x; v0[r] = s0.y;
+                kk[r] = D.sstk[o];
+            }
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 double2 a = make_double2(0.0, 0.0), b = a;
@@ -1158,7 +1220,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
             if (hh == 0 && o < NV) {
                 const int cc = o / NO, oo = o % NO;
                 const int l = l0 + cc;
-                if (l >= m && l <= L) {
+                if (l >= lA && l <= lend) {
                     const int comp = oo >> 1;
                     double* dst = reinterpret_cast<double*>(
                         part + (((long long)tile * 4 + wave) * NC + comp) * D.nlm + obase + l);
@@ -1178,13 +1240,13 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
 #pragma unroll
             for (int cc = 0; cc < ANA_C; ++cc) {
                 const int l = l0 + cc;
-                if (l > L) break;
+                if (l > lend) break;
                 const LegCoef c = cf[l];
                 const LegCoef cn = cf[min(l + 1, L)];
 #pragma unroll
                 for (int r = 0; r < ASR; ++r) {
                     if (l < ls[r]) continue;                 // uniform per wave
-                    if (l == ls[r] && act[r]) {
+                    if (l == ls[r] && act[r] && !tab[r]) {
                         const double2 s0 = D.st[(long long)m * npair + pr[r]];
                         v1[r] = s0.x; v0[r] = s0.y;
                         kk[r] = D.stk[(long long)m * npair + pr[r]];
@@ -1200,7 +1262,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         };
         int l0 = lstart0;
         // phase 1: guarded chunks until every live slot is active and representable
-        for (; l0 <= L; l0 += ANA_C) {
+        for (; l0 <= lend; l0 += ANA_C) {
             double acc[NV];
 #pragma unroll
             for (int i = 0; i < NV; ++i) acc[i] = 0.0;
@@ -1221,7 +1283,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         {
             bool pend = false;
             int pl0 = 0, cur = 0;
-            for (; l0 + ANA_C - 1 <= L; l0 += ANA_C) {
+            for (; l0 + ANA_C - 1 <= lend; l0 += ANA_C) {
                 double rv[8];
                 if (pend) get_chunk(cur ^ 1, rv);
                 double acc[NV];
@@ -1255,7 +1317,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         asm volatile("; ANA_CHUNK_END");
 #endif
         // phase 3: the partial last chunk
-        if (l0 <= L) {
+        if (l0 <= lend) {
             double acc[NV];
 #pragma unroll
             for (int i = 0; i < NV; ++i) acc[i] = 0.0;
@@ -1263,7 +1325,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
             reduce_store(acc, l0);
         }
         // l below the wave's first chunk: exact zeros
-        for (int l = m + lane; l < min(lstart0, L + 1); l += 64)
+        for (int l = lA + lane; l < min(lstart0, lend + 1); l += 64)
             for (int c = 0; c < NC; ++c)
                 part[(((long long)tile * 4 + wave) * NC + c) * D.nlm + obase + l] = make_double2(0.0, 0.0);
     }
@@ -1326,6 +1388,11 @@ struct gs_sht {
     // Legendre launch shapes chosen for occupancy (~4 waves per SIMD): ring
     // pairs per lane (sr) and m pairing, synthesis and analysis
     int syn_sr = 2, syn_paired = 1, ana_sr = 4, ana_paired = 1;
+    // l-segments of the analysis (0: none) and their state table
+    int seg = 0, nseg = 1;
+    int* segoff = nullptr;
+    double2* sst = nullptr;
+    int* sstk = nullptr;
     long long npix = 0;
     PairGeom* geom = nullptr;
     LegCoef* coef = nullptr;
@@ -1346,6 +1413,11 @@ struct gs_sht {
     std::vector<int> cls_M;      // M of each class
     std::vector<int> cls_n;      // pairs in the class
     std::vector<int*> cls_pairs; // device lists
+    // small maps: every ring pair in ONE ring-stage launch (FFT lengths up to
+    // merged_M, all in LDS; largest rings first) instead of one latency-bound
+    // launch per length class; 0 pairs = per-class launches
+    int* merged_pairs = nullptr;
+    int merged_n = 0, merged_M = 0;
     // the short-ring classes run on a side stream beside the largest class
     // (fork / join by events, graph-capturable); 0 = all on the caller's stream
     hipStream_t side = nullptr;
@@ -1355,6 +1427,7 @@ struct gs_sht {
         ShtDev D;
         D.L = L; D.npair = npair; D.ngroup = ngroup; D.nlm = nlm;
         D.geom = geom; D.coef = coef; D.lstart = lstart; D.st = st; D.stk = stk;
+        D.seg = seg; D.segoff = segoff; D.sst = sst; D.sstk = sstk;
         return D;
     }
 };
@@ -1370,7 +1443,7 @@ int sht_alloc(gs_sht* p, T** dst, size_t n) {
 
 void sht_free(gs_sht* p) {
     void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->sscr,
-                    p->mapw, p->ain};
+                    p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (int* b : p->cls_pairs)
@@ -1427,6 +1500,22 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         }
     }
     p->ntile = (p->ngroup + 4 * p->ana_sr - 1) / (4 * p->ana_sr);
+    // small maps (one ring group per lane, unpaired m: still few waves per SIMD,
+    // each walking up to L + 1 recurrence steps in a latency-bound chain): split
+    // every m's l range into segments of GS_SHT_SEG (default 64) l, entered with
+    // a plan-time recurrence state -- independent waves with short chains.
+    // GS_SHT_SEG=0 turns it off; an explicit value applies to any shape (tests)
+    {
+        const char* e = std::getenv("GS_SHT_SEG");
+        int sg = (p->ana_sr == 1 && !p->ana_paired) ? 64 : 0;
+        if (e) sg = std::atoi(e);
+        if (sg < 0 || (sg & 1) || (sg > 0 && sg % ANA_C != 0)) {
+            delete p;
+            return set_error("gs_sht_create: GS_SHT_SEG must be 0 or a positive multiple of 4");
+        }
+        p->seg = sg >= L + 1 ? 0 : sg;
+        p->nseg = p->seg ? (L + p->seg) / p->seg : 1;
+    }
     // ---- geometry (ring pair r: north ring r+1, south ring 4N-1-r) ----
     std::vector<PairGeom> geom(p->npair);
     int Mmax = 2;
@@ -1509,7 +1598,22 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     rc |= sht_alloc(p, &p->part, (size_t)p->ntile * 4 * 3 * p->nlm);   // one partial per analysis wave
     rc |= sht_alloc(p, &p->mapw, (size_t)3 * p->npix);
     rc |= sht_alloc(p, &p->ain, (size_t)3 * p->nlm);
+    std::vector<int> segoff(L + 1, 0);
+    long long segrows = 0;
+    if (p->seg) {
+        for (int m = 0; m <= L; ++m) {
+            segoff[m] = (int)segrows;
+            segrows += (L - m) / p->seg;                // segments s >= 1 of m: m + s seg <= L
+        }
+        rc |= sht_alloc(p, &p->segoff, (size_t)L + 1);
+        rc |= sht_alloc(p, &p->sst, (size_t)std::max<long long>(segrows, 1) * p->npair);
+        rc |= sht_alloc(p, &p->sstk, (size_t)std::max<long long>(segrows, 1) * p->npair);
+    }
     if (rc) { sht_free(p); return -1; }
+    if (p->seg && hipMemcpy(p->segoff, segoff.data(), segoff.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        sht_free(p);
+        return set_error("gs_sht_create: segment table upload failed");
+    }
     // ring classes by M
     std::vector<int> Ms;
     for (auto& g : geom) Ms.push_back(g.M);
@@ -1532,6 +1636,25 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         if (M > p->lds_fft_max) gscr_need = std::max<long long>(gscr_need, 3LL * (long long)lst.size() * Mmax);
     }
     if (gscr_need && sht_alloc(p, &p->gscr, (size_t)gscr_need)) { sht_free(p); return -1; }
+    {
+        // one merged ring launch when every length fits a small LDS buffer
+        // (GS_SHT_MERGE_RINGS=0/1 forces it off/on where legal)
+        const int mmax = Ms.empty() ? 0 : Ms.back();
+        bool merge = mmax <= 2048 && mmax <= p->lds_fft_max && p->nsplit == 0;
+        if (const char* e = std::getenv("GS_SHT_MERGE_RINGS")) merge = std::atoi(e) != 0 && mmax <= p->lds_fft_max && p->nsplit == 0;
+        if (merge && Ms.size() > 1) {
+            std::vector<int> all(p->npair);
+            for (int r = 0; r < p->npair; ++r) all[r] = r;
+            std::stable_sort(all.begin(), all.end(), [&](int a, int b) { return geom[a].M > geom[b].M; });
+            if (sht_alloc(p, &p->merged_pairs, all.size()) ||
+                hipMemcpy(p->merged_pairs, all.data(), all.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+                sht_free(p);
+                return set_error("gs_sht_create: merged ring list upload failed");
+            }
+            p->merged_n = p->npair;
+            p->merged_M = mmax;
+        }
+    }
     if (p->nsplit) {
         int nmax = 0;
         for (auto& g : geom) if (g.split) nmax = std::max(nmax, g.nphi);
@@ -1565,6 +1688,8 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     hipLaunchKernelGGL(k_sht_lmm, dim3(nblocks(p->npair, 64)), dim3(64), 0, 0, L, p->npair, p->geom, lmm, lmk);
     hipLaunchKernelGGL(k_sht_onset, dim3(nblocks(p->npair, 256), L + 1), dim3(256), 0, 0, p->dev(), lmm, lmk,
                        p->lstart, p->st, p->stk);
+    if (p->seg)
+        hipLaunchKernelGGL(k_sht_segstate, dim3(nblocks(p->npair, 256), L + 1), dim3(256), 0, 0, p->dev());
     if (!bs_pairs.empty()) {
         int* dp = nullptr;
         if (hipMalloc((void**)&dp, bs_pairs.size() * sizeof(int)) == hipSuccess &&
@@ -1648,6 +1773,37 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
 // stream while the largest class runs on the caller's.
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
                      const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1) {
+    if (p->merged_n > 0) {
+        // all ring pairs in one launch: the block size and LDS of the longest FFT
+        // (shorter rings leave threads idle; their fold reduction uses the
+        // J = block / K aliases per bin pair, as a short-ring class does)
+        const int M = p->merged_M, bd = ring_block(M);
+        const bool nb8 = M / 2 > 4 * bd;
+        const size_t lds = (size_t)M * sizeof(double2) + (size_t)bd * 4 * sizeof(double2);
+        const dim3 grid(p->merged_n, ncomp);
+        const double2* ph = phi ? phi : p->phi;
+        if (synth) {
+            if (nb8)
+                hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
+                                   p->nsplit, p->split_n, comp_lmax, comp_div);
+            else
+                hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
+                                   p->nsplit, p->split_n, comp_lmax, comp_div);
+        } else {
+            if (nb8)
+                hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
+                                   p->nsplit, p->split_n);
+            else
+                hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
+                                   p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
+                                   p->nsplit, p->split_n);
+        }
+        GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring (merged)" : "k_sht_anal_ring (merged)");
+        return 0;
+    }
     const size_t ncls = p->cls_M.size();
     size_t big = 0;
     for (size_t c = 1; c < ncls; ++c)
@@ -1692,7 +1848,7 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
 
 static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream) {
     if (sht_rings(p, false, ncomp, maps, nullptr, stream)) return -1;
-    const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, p->ntile);
+    const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, p->ntile, p->nseg);
 #define GS_AL(NC, SR) hipLaunchKernelGGL((k_sht_anal_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
                                          p->coef, p->phi, p->part, p->ana_paired)
 #define GS_AL2(NC) do { if (p->ana_sr == 4) GS_AL(NC, 4); else if (p->ana_sr == 2) GS_AL(NC, 2); \
