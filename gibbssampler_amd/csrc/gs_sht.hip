@@ -462,6 +462,163 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
     }
 }
 
+// l-segmented synthesis for small maps (D.seg > 0, one ring group per lane):
+// workgroup = (m, 64-pair group), wave w = segment w of m's l range, entered
+// at lA = m + w seg with the plan-time recurrence state (or at the group's
+// onset, if later); the segments' partial sums meet in LDS and wave 0 adds
+// them in segment order.  The chain of one wave is <= seg l steps instead of
+// L + 1 - m.  Waves whose segment starts past L end at once (before the
+// barrier; an ended wave no longer counts at it).
+template <int NC>
+__global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegCoef* __restrict__ coef,
+                                                           const double2* __restrict__ ain,
+                                                           double2* __restrict__ phi) {
+    // per wave a slice of SEG_SLICE doubles: the segment's recurrence / spin-2
+    // coefficients (66 l: the loop reads up to l + 2) and a_lm (64 l per comp),
+    // staged once with coalesced vector loads (the single-walk kernel reads them
+    // as scalar loads per l, a memory latency per step); after the walk the
+    // slice holds the wave's 12 x 64 partial sums
+    constexpr int SEG_SLICE = 66 * 8 + 3 * 64 * 2;
+    extern __shared__ __attribute__((aligned(16))) double sred[];   // [waves][SEG_SLICE]
+    const int L = D.L, npair = D.npair, nlm = D.nlm;
+    const int m = blockIdx.x, grp = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int sg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lA = m + sg * D.seg;
+    if (lA > L) return;
+    const int nact = (L - m) / D.seg + 1;                 // segments of this m
+    const int lend = min(lA + D.seg - 1, L);
+    const int pr = grp * 64 + lane;
+    const bool act = pr < npair;
+    const double x = act ? D.geom[pr].x : 0.0;
+    const double is2 = act ? D.geom[pr].is2 : 0.0;
+    const double xis2 = x * is2;
+    int ls = __builtin_amdgcn_readfirstlane(D.lstart[(long long)m * D.ngroup + grp]);
+    const bool tab = ls <= L && ls < lA;
+    if (tab) ls = lA;
+    if (ls > lend) ls = L + 1;
+    const double2 z2 = make_double2(0.0, 0.0);
+    SynAcc A;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { A.tp[i] = 0.0; A.tn[i] = 0.0; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { A.sp[i] = 0.0; A.sn[i] = 0.0; }
+    double v0 = 0.0, v1 = 0.0;
+    int kk = 0;
+    if (tab && ls <= L && act) {
+        const long long o = (long long)(D.segoff[m] + sg - 1) * npair + pr;
+        const double2 s0 = D.sst[o];
+        v1 = s0.x; v0 = s0.y;
+        kk = D.sstk[o];
+    }
+    const long long base = cidx(L, m, m) - m;
+    double* slice = sred + (long long)sg * SEG_SLICE;
+    {
+        const LegCoef* cfg = coef + base;
+        auto put = [&](int slot, int l) {
+            const double2* src = reinterpret_cast<const double2*>(cfg + l);
+            double2* dst = reinterpret_cast<double2*>(slice + slot * 8);
+            const double2 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
+            dst[0] = q0; dst[1] = q1; dst[2] = q2; dst[3] = q3;
+        };
+        put(lane, min(lA + lane, L));
+        if (lane < 2) put(64 + lane, min(lA + 64 + lane, L));
+        const int la = min(lA + lane, L);
+        double2* as = reinterpret_cast<double2*>(slice + 66 * 8);
+        if constexpr (NC != 2) as[lane] = ain[base + la];
+        if constexpr (NC != 1) {
+            const double2* aEg = ain + (NC == 3 ? nlm : 0) + base;
+            as[(NC == 3 ? 64 : 0) + lane] = aEg[la];
+            as[(NC == 3 ? 128 : 64) + lane] = aEg[nlm + la];
+        }
+    }
+    __syncthreads();            // every wave still running reaches it (ended waves do not count)
+    const LegCoef* cfs = reinterpret_cast<const LegCoef*>(slice);
+    const double2* as = reinterpret_cast<const double2*>(slice + 66 * 8);
+    auto cf = [&](int l) { return cfs[l - lA]; };
+    auto aT = [&](int l) { return as[l - lA]; };
+    auto aE = [&](int l) { return as[(NC == 3 ? 64 : 0) + l - lA]; };
+    auto aB = [&](int l) { return as[(NC == 3 ? 128 : 64) + l - lA]; };
+    if (ls <= L) {
+        int l = ls;
+        // slow path: activation at the onset, scaled lanes
+        while (l <= lend) {
+            if (l == ls && act && !tab) {
+                const double2 s0 = D.st[(long long)m * npair + pr];
+                v1 = s0.x; v0 = s0.y;
+                kk = D.stk[(long long)m * npair + pr];
+            }
+            if (!__any(kk < 0)) break;
+            const LegCoef c = cf(l);
+            const double2 t = NC != 2 ? aT(l) : z2;
+            const double2 e = NC != 1 ? aE(l) : z2;
+            const double2 b = NC != 1 ? aB(l) : z2;
+            const LegCoef cn = cf(min(l + 1, L));
+            const double w0 = kk == 0 ? v0 : 0.0, w1 = kk == 0 ? v1 : 0.0;
+            if (((l - m) & 1) == 0) syn_accumulate<NC, true>(A, c, w0, w1, is2, xis2, t, e, b);
+            else syn_accumulate<NC, false>(A, c, w0, w1, is2, xis2, t, e, b);
+            if (l < L) {
+                rec_step(cn, x, v0, v1);
+                if (kk < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++kk; }
+            }
+            ++l;
+        }
+        // fast path (onset state loaded above when the onset is the first l)
+        if (l <= lend && ((l - m) & 1)) {
+            const LegCoef c = cf(l);
+            const LegCoef cn = cf(min(l + 1, L));
+            const double2 t = NC != 2 ? aT(l) : z2, e = NC != 1 ? aE(l) : z2, b = NC != 1 ? aB(l) : z2;
+            syn_accumulate<NC, false>(A, c, v0, v1, is2, xis2, t, e, b);
+            if (l < L) rec_step(cn, x, v0, v1);
+            ++l;
+        }
+        for (; l + 1 <= lend; l += 2) {
+            const LegCoef c0 = cf(l), c1 = cf(l + 1), c2 = cf(min(l + 2, L));
+            const double2 t0 = NC != 2 ? aT(l) : z2, e0 = NC != 1 ? aE(l) : z2, b0 = NC != 1 ? aB(l) : z2;
+            const double2 t1 = NC != 2 ? aT(l + 1) : z2, e1 = NC != 1 ? aE(l + 1) : z2, b1 = NC != 1 ? aB(l + 1) : z2;
+            syn_accumulate<NC, true>(A, c0, v0, v1, is2, xis2, t0, e0, b0);
+            rec_step(c1, x, v0, v1);
+            syn_accumulate<NC, false>(A, c1, v0, v1, is2, xis2, t1, e1, b1);
+            rec_step(c2, x, v0, v1);
+        }
+        if (l <= lend) {
+            const LegCoef c = cf(l);
+            const double2 t = NC != 2 ? aT(l) : z2, e = NC != 1 ? aE(l) : z2, b = NC != 1 ? aB(l) : z2;
+            syn_accumulate<NC, true>(A, c, v0, v1, is2, xis2, t, e, b);
+        }
+    }
+    // segment partial sums -> LDS; wave 0 adds them in segment order
+    double* my = slice + lane;      // this wave's own slice (its staging is no longer read)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { my[i * 64] = A.tp[i]; my[(2 + i) * 64] = A.tn[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { my[(4 + i) * 64] = A.sp[i]; my[(8 + i) * 64] = A.sn[i]; }
+    __syncthreads();
+    if (sg != 0 || !act) return;
+    for (int w = 1; w < nact; ++w) {
+        const double* o = sred + (long long)w * SEG_SLICE + lane;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) { A.tp[i] += o[i * 64]; A.tn[i] += o[(2 + i) * 64]; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { A.sp[i] += o[(4 + i) * 64]; A.sn[i] += o[(8 + i) * 64]; }
+    }
+    const long long plane = phi_plane(L, npair);
+    const long long o = phi_at(m, pr, npair);
+    int comp = 0;
+    if constexpr (NC != 2) {
+        phi[(2 * comp + 0) * plane + o] = make_double2(A.tp[0] + A.tn[0], A.tp[1] + A.tn[1]);
+        phi[(2 * comp + 1) * plane + o] = make_double2(A.tp[0] - A.tn[0], A.tp[1] - A.tn[1]);
+        ++comp;
+    }
+    if constexpr (NC != 1) {
+        phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[0] + A.sn[0]), -(A.sp[1] + A.sn[1]));
+        phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[0] - A.sn[0]), -(A.sp[1] - A.sn[1]));
+        ++comp;
+        phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[2] + A.sn[2]), -(A.sp[3] + A.sn[3]));
+        phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[2] - A.sn[2]), -(A.sp[3] - A.sn[3]));
+    }
+}
+
 // ---------------------------------------------------------------------------
 // f2 block synthesis (pixel-domain NC likelihood, NonCenteredGibbs.py:333-355):
 // the maps y_k = A(delta a_k) of K Metropolis blocks at once.  Every (l, field)
@@ -1091,10 +1248,14 @@ __device__ __forceinline__ void ana_term(double* a, const LegCoef& c, double v0,
     }
 }
 
-template <int NC, int ASR>
+template <int NC, int ASR, bool SEGL>
 __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegCoef* __restrict__ coef,
                                                             const double2* __restrict__ phi,
                                                             double2* __restrict__ part, int paired) {
+    // SEGL (l-segmented launches): the segment's coefficients (<= seg + 2 l) are
+    // staged once per workgroup in LDS with coalesced loads instead of one
+    // scalar load (a memory latency) per l step and wave
+    __shared__ __attribute__((aligned(16))) LegCoef cstage[SEGL ? 68 : 1];
     constexpr int NO = NC == 1 ? 2 : (NC == 2 ? 4 : 6);   // real outputs per l
     constexpr int NV = NO * ANA_C;
     static_assert(NV <= 32, "chunk too large for the wave reduction");
@@ -1166,6 +1327,15 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         }
         const long long obase = cidx(L, m, m) - m;
         const LegCoef* cf = coef + obase;
+        if constexpr (SEGL) {
+            __syncthreads();                        // the previous m's readers are done
+            const double2* src = reinterpret_cast<const double2*>(coef);
+            double2* dst = reinterpret_cast<double2*>(cstage);
+            for (int i = tid; i < (D.seg + 2) * 4; i += LEG_BLOCK)
+                dst[i] = src[(obase + min(lA + i / 4, L)) * 4 + (i & 3)];
+            __syncthreads();
+            cf = cstage - lA;                       // cf[l], lA <= l <= lA + seg + 1
+        }
         // chunks start on m's parity so positions 0, 2 of a chunk are even
         const int lstart0 = lmin - ((lmin - m) & 1);
         double* red = red_all[wave];
@@ -1835,6 +2005,16 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, ncomp, alm, layout,
                        p->ain);
     GS_LAUNCH_CHECK("k_sht_alm_in");
+    if (p->seg > 0 && p->syn_sr == 1 && !p->syn_paired && p->nseg <= 16) {
+        // small maps: l-segmented synthesis, one wave per segment
+        const dim3 g2(p->L + 1, p->ngroup), b2(64 * p->nseg);
+        const size_t lds = (size_t)p->nseg * (66 * 8 + 3 * 64 * 2) * sizeof(double);
+#define GS_SS(NC) hipLaunchKernelGGL((k_sht_synth_leg_seg<NC>), g2, b2, lds, S(stream), p->dev(), p->coef, p->ain, p->phi)
+        if (ncomp == 1) GS_SS(1); else if (ncomp == 2) GS_SS(2); else GS_SS(3);
+#undef GS_SS
+        GS_LAUNCH_CHECK("k_sht_synth_leg_seg");
+        return sht_rings(p, true, ncomp, nullptr, maps, stream);
+    }
     const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr));
 #define GS_SL(NC, SR) hipLaunchKernelGGL((k_sht_synth_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
                                          p->coef, p->ain, p->phi, p->syn_paired)
@@ -1849,8 +2029,11 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
 static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream) {
     if (sht_rings(p, false, ncomp, maps, nullptr, stream)) return -1;
     const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, p->ntile, p->nseg);
-#define GS_AL(NC, SR) hipLaunchKernelGGL((k_sht_anal_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
-                                         p->coef, p->phi, p->part, p->ana_paired)
+#define GS_AL(NC, SR) do { if (p->seg > 0 && p->seg <= 64) \
+        hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, true>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, \
+                           p->phi, p->part, p->ana_paired); \
+    else hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, \
+                            p->phi, p->part, p->ana_paired); } while (0)
 #define GS_AL2(NC) do { if (p->ana_sr == 4) GS_AL(NC, 4); else if (p->ana_sr == 2) GS_AL(NC, 2); \
                         else GS_AL(NC, 1); } while (0)
     if (ncomp == 1) GS_AL2(1); else if (ncomp == 2) GS_AL2(2); else GS_AL2(3);

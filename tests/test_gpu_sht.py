@@ -237,17 +237,22 @@ def test_legendre_launch_shapes_vs_oracle(monkeypatch, syn, ana, N, L):
 @pytest.mark.parametrize("ana", ["1,0", "2,1", "4,1"])
 @pytest.mark.parametrize("N,L", [(16, 32), (64, 100)])
 def test_segmented_analysis_vs_oracle(monkeypatch, seg, ana, N, L):
-    """l-segmented analysis (GS_SHT_SEG: every m's l range split into segments
-    entered with the plan-time recurrence state; the default for small maps)
-    against the dense oracle, for every analysis launch shape, with segment
-    starts before, inside and after the polar onsets."""
+    """l-segmented analysis and synthesis (GS_SHT_SEG: every m's l range split
+    into segments entered with the plan-time recurrence state; the default for
+    small maps) against the dense oracle, for every analysis launch shape, with
+    segment starts before, inside and after the polar onsets."""
     torch = _torch()
     from gibbssampler_amd.sht import HealpixSHT
     monkeypatch.setenv("GS_SHT_SEG", str(seg))
     monkeypatch.setenv("GS_SHT_ANA", ana)
+    monkeypatch.setenv("GS_SHT_SYN", "1,0")        # the segmented synthesis's shape
     sht = HealpixSHT(N, L)
     rng = np.random.default_rng(seg + N + L)
     for ncomp in (1, 2, 3):
+        a = _rand_alm(L, ncomp, rng)
+        want = _oracle_maps(a, N, L, ncomp)
+        got = sht.alm2map(torch.from_numpy(a).cuda(), ncomp=ncomp, layout="complex").cpu().numpy()
+        np.testing.assert_allclose(got.reshape(ncomp, -1), want, rtol=0, atol=1e-11 * np.abs(want).max())
         maps = rng.standard_normal((ncomp, O.npix(N)))
         wa = _oracle_alm(maps, N, L, ncomp, 0)
         ga = sht.map2alm(torch.from_numpy(maps).cuda(), iter=0, layout="complex",
@@ -258,19 +263,22 @@ def test_segmented_analysis_vs_oracle(monkeypatch, seg, ana, N, L):
 @pytest.mark.parametrize("N,L,seg", [(256, 512, 64), (256, 512, 16), (512, 1024, 64)])
 def test_segmented_analysis_matches_single_walk(monkeypatch, N, L, seg):
     """At the HEAD masked modes' size (and N_side 512): segmented and
-    single-walk analysis agree to rounding (the segment states continue the
+    single-walk analysis and synthesis agree to rounding (the segment states continue the
     same recurrence; only the reduction grouping of a few l differs), iter 0
     and the Jacobi iter 3, TEB."""
     torch = _torch()
     from gibbssampler_amd.sht import HealpixSHT
     rng = np.random.default_rng(N + seg)
     maps = torch.from_numpy(rng.standard_normal((3, 12 * N * N))).cuda()
+    alm = torch.from_numpy(_rand_alm(L, 3, rng)).cuda()
     out = {}
     for sg in (0, seg):
         monkeypatch.setenv("GS_SHT_SEG", str(sg))
         monkeypatch.setenv("GS_SHT_ANA", "1,0")
+        monkeypatch.setenv("GS_SHT_SYN", "1,0")
         sht = HealpixSHT(N, L)
         out[sg] = [sht.map2alm(maps, iter=it, layout="complex", ncomp=3).cpu().numpy() for it in (0, 3)]
+        out[sg].append(sht.alm2map(alm, ncomp=3, layout="complex").cpu().numpy())
         del sht
     for a, b in zip(out[0], out[seg]):
         np.testing.assert_allclose(b, a, rtol=0, atol=1e-12 * np.abs(a).max())
