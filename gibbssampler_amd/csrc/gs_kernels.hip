@@ -541,6 +541,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
 // flight, then the four wave sums in wave order -- the same order for any
 // batch size, so every chain's trajectory is bit-identical for any chain
 // count or GPU count
+template <int G>
 __global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int ntile, int nchunkg, int tm, int nstat,
                                                       const double* __restrict__ partials,
                                                       double* __restrict__ stats) {
@@ -556,8 +557,10 @@ __global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int nt
     // groups of G of this wave's chunks, every load of a group issued before
     // the sums (the last group's loads clamped to a valid chunk, its extra
     // values dropped): with few chains the finish is a chain of memory
-    // latencies, one per group; the sums keep the chunk order
-    constexpr int G = 16;             // 32 measured slower (4.7 -> 5.4 us at configs[1])
+    // latencies, one per group (G = 16; 32 measured slower, 4.7 -> 5.4 us at
+    // configs[1]); with many it is bound by the partials' bytes and G = 4
+    // wastes least on clamped loads (32 chains: 11.2 us against 13.9 at 16).
+    // The sums keep the chunk order for any G.
     double acc = 0.0;
     for (int c = w; c <= cmax; c += 4 * G) {
         double v[G];
@@ -1696,8 +1699,12 @@ static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e
 
 static int stats_finish(gs_plan* p, double* stats, void* stream) {
     const long long n = (long long)p->nchains * p->nstat * p->ntile;
-    hipLaunchKernelGGL(k_stats_finish, dim3((unsigned)n), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
-                       p->nchunkg, p->rows_per_task, p->nstat, p->partials, stats);
+    if (p->nchains <= 4)
+        hipLaunchKernelGGL(k_stats_finish<16>, dim3((unsigned)n), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
+                           p->nchunkg, p->rows_per_task, p->nstat, p->partials, stats);
+    else
+        hipLaunchKernelGGL(k_stats_finish<4>, dim3((unsigned)n), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
+                           p->nchunkg, p->rows_per_task, p->nstat, p->partials, stats);
     GS_LAUNCH_CHECK("k_stats_finish");
     return 0;
 }
