@@ -558,17 +558,31 @@ __global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int nt
     // the sums (the last group's loads clamped to a valid chunk, its extra
     // values dropped): with few chains the finish is a chain of memory
     // latencies, one per group (G = 16; 32 measured slower, 4.7 -> 5.4 us at
-    // configs[1]); with many it is bound by the partials' bytes and G = 4
-    // wastes least on clamped loads (32 chains: 11.2 us against 13.9 at 16).
-    // The sums keep the chunk order for any G.
+    // configs[1]); with many it is bound by the partials' bytes, and the
+    // unclamped four-in-flight form reads nothing twice (32 chains: 11.2 us,
+    // 13.2-13.9 with clamped groups of 4 or 16).  The sums keep the chunk
+    // order in both forms.
     double acc = 0.0;
-    for (int c = w; c <= cmax; c += 4 * G) {
-        double v[G];
+    if constexpr (G <= 4) {
+        // bandwidth-bound form (many chains): four loads in flight, no clamped extras
+        int c = w;
+        for (; c + 12 <= cmax; c += 16) {
+            double v[4];
 #pragma unroll
-        for (int j = 0; j < G; ++j) v[j] = pp[min(c + 4 * j, cmax) * cs];
+            for (int j = 0; j < 4; ++j) v[j] = pp[(c + 4 * j) * cs];
 #pragma unroll
-        for (int j = 0; j < G; ++j)
-            if (c + 4 * j <= cmax) acc += v[j];
+            for (int j = 0; j < 4; ++j) acc += v[j];
+        }
+        for (; c <= cmax; c += 4) acc += pp[c * cs];
+    } else {
+        for (int c = w; c <= cmax; c += 4 * G) {
+            double v[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) v[j] = pp[min(c + 4 * j, cmax) * cs];
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+                if (c + 4 * j <= cmax) acc += v[j];
+        }
     }
     __shared__ double red[4][WAVE];
     red[w][lane] = acc;
