@@ -654,11 +654,15 @@ __device__ __forceinline__ void blk_accumulate(BlkAcc& A, int f, const LegCoef& 
     }
 }
 
-template <int NC, int SR>
+// STG: the m's recurrence coefficients, a_lm and block indices (l = m..L) are
+// staged in LDS by coalesced loads once per m (small l_max: <= 64 KB), instead
+// of wave-uniform scalar loads -- one memory latency -- per l step
+template <int NC, int SR, bool STG>
 __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const LegCoef* __restrict__ coef,
                                                                 const double2* __restrict__ ain,
                                                                 const int* __restrict__ blk,
                                                                 double2* __restrict__ phib, int paired) {
+    extern __shared__ __attribute__((aligned(16))) double2 bstage[];
     constexpr int NF = NC;                      // input fields
     constexpr int NCO = NC == 1 ? 1 : 2;        // output comps per block
     const int L = D.L, npair = D.npair, nlm = D.nlm;
@@ -706,6 +710,32 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
         const long long base = cidx(L, m, m) - m;
         const LegCoef* cf = coef + base;
         const double2* a0 = ain + base;
+        const int nl = L + 1 - m;                  // l = m .. L
+        const LegCoef* cfs = nullptr;
+        const double2* as = nullptr;
+        const int* bs = nullptr;
+        if constexpr (STG) {
+            __syncthreads();                       // the previous m's readers are done
+            double2* c2 = bstage;                                  // [nl][4] (LegCoef)
+            double2* a2 = bstage + 4 * nl;                         // [NF][nl]
+            int* b2 = reinterpret_cast<int*>(a2 + NF * nl);        // [NF][nl]
+            const double2* src = reinterpret_cast<const double2*>(coef + base + m);
+            for (int i = threadIdx.x; i < 4 * nl; i += LEG_BLOCK) c2[i] = src[i];
+            for (int i = threadIdx.x; i < NF * nl; i += LEG_BLOCK) {
+                const int f = i / nl, j = i - f * nl;
+                a2[i] = a0[(long long)f * nlm + m + j];
+                b2[i] = blk[f * (L + 1) + m + j];
+            }
+            __syncthreads();
+            cfs = reinterpret_cast<const LegCoef*>(c2);
+            as = a2;
+            bs = b2;
+        }
+        auto CF = [&](int l) -> LegCoef { if constexpr (STG) return cfs[l - m]; else return cf[l]; };
+        auto AL = [&](int f, int l) -> double2 {
+            if constexpr (STG) return as[f * nl + l - m]; else return a0[(long long)f * nlm + l];
+        };
+        auto BK = [&](int f, int l) -> int { if constexpr (STG) return bs[f * nl + l - m]; else return blk[f * (L + 1) + l]; };
         // write field f's accumulators to its current block's planes (if any), reset
         auto flush = [&](int f) {
             const int k = cur[f];
@@ -733,7 +763,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
         auto track = [&](int l) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
-                const int b = blk[f * (L + 1) + l];
+                const int b = BK(f, l);
                 if (b != cur[f]) { flush(f); cur[f] = b; }
             }
         };
@@ -754,8 +784,8 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
             }
             if (live) break;
             track(l);
-            const LegCoef c = cf[l];
-            const LegCoef cn = cf[min(l + 1, L)];
+            const LegCoef c = CF(l);
+            const LegCoef cn = CF(min(l + 1, L));
             const bool even = ((l - m) & 1) == 0;
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
@@ -763,7 +793,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
                 const double w0 = kk[r] == 0 ? v0[r] : 0.0, w1 = kk[r] == 0 ? v1[r] : 0.0;
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
-                    const double2 a = a0[(long long)f * nlm + l];
+                    const double2 a = AL(f, l);
                     if (even) blk_accumulate<NC, true>(A[f][r], f, c, w0, w1, is2[r], xis2[r], a);
                     else blk_accumulate<NC, false>(A[f][r], f, c, w0, w1, is2[r], xis2[r], a);
                 }
@@ -777,12 +807,12 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
         // ---- every live slot active and representable ----
         for (; l <= L; ++l) {
             track(l);
-            const LegCoef c = cf[l];
-            const LegCoef cn = cf[min(l + 1, L)];
+            const LegCoef c = CF(l);
+            const LegCoef cn = CF(min(l + 1, L));
             const bool even = ((l - m) & 1) == 0;
             double2 a[NF];
 #pragma unroll
-            for (int f = 0; f < NF; ++f) a[f] = a0[(long long)f * nlm + l];
+            for (int f = 0; f < NF; ++f) a[f] = AL(f, l);
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 if (ls[r] > L) continue;
@@ -2063,8 +2093,16 @@ int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int
     GS_LAUNCH_CHECK("k_sht_alm_in");
     double2* ph = reinterpret_cast<double2*>(phib);
     const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr));
-#define GS_SB(NF, SR) hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
-                                         p->coef, p->ain, blk, ph, p->syn_paired)
+    // staged variant when m = 0's coefficients, a_lm and block indices fit 64 KB
+    // of LDS (GS_SHT_BLK_STAGE=0 turns it off: tests)
+    const size_t stg = (size_t)(p->L + 1) * (4 * sizeof(double2) + nfield * (sizeof(double2) + sizeof(int)));
+    const char* stg_env = getenv("GS_SHT_BLK_STAGE");
+    const bool stage_off = stg_env && atoi(stg_env) == 0;
+    const bool use_stg = stg <= 64 * 1024 && !stage_off;
+#define GS_SB(NF, SR) do { if (use_stg) hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR, true>), grid, dim3(LEG_BLOCK), \
+                                         stg, S(stream), p->dev(), p->coef, p->ain, blk, ph, p->syn_paired); \
+    else hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
+                            p->coef, p->ain, blk, ph, p->syn_paired); } while (0)
     if (nfield == 1) { if (p->syn_sr == 2) GS_SB(1, 2); else GS_SB(1, 1); }
     else { if (p->syn_sr == 2) GS_SB(2, 2); else GS_SB(2, 1); }
 #undef GS_SB

@@ -383,14 +383,17 @@ def test_f2_masked_asis_driver_vs_oracle(g, gibbs_cr):
         np.testing.assert_array_equal(acc[sp], wacc[sp])
 
 
-@pytest.mark.parametrize("n_iter,group_bytes", [(1, None), (2, None), (2, "1"), (1, "50000000")])
-def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes):
+@pytest.mark.parametrize("n_iter,group_bytes,stage", [(1, None, "1"), (2, None, "1"), (2, "1", "1"),
+                                                     (1, "50000000", "1"), (1, None, "0"), (2, "1", "0")])
+def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes, stage):
     """gs_masked_pixel_mh decides every block on the device from one block
     synthesis + one Gram pass; with a small workspace budget the blocks run in
     groups (one block per group at "1") and the residual is carried between
     groups.  Native streams, n_iter_metropolis 1 and 2, against the oracle's
-    full-map likelihood per block (oracle/masked.pixel_mh)."""
+    full-map likelihood per block (oracle/masked.pixel_mh).  stage "0": the
+    block synthesis without the LDS-staged inputs (the large-l_max form)."""
     from gibbssampler_amd.masked import PixelMH
+    monkeypatch.setenv("GS_SHT_BLK_STAGE", stage)
     if group_bytes is not None:
         monkeypatch.setenv("GS_F2_GROUP_BYTES", group_bytes)
     bins, blocks, pv = _f2_parts(g)
