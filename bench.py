@@ -39,6 +39,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VALU_PEAK_TFS = 78.6    # MI355X_MICROARCH.md: FP64 vector
 METRIC = "Gibbs iters/sec (constrained-realization + C_l draw), Nside=%d lmax=%d"
 HARMONIC = ("noncentered", "centered", "asis")
+SURFACE = ("surface_noncentered",)
 MASKED_HEAD = ("masked_centered_ula", "masked_asis")
 
 
@@ -47,7 +48,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (50; masked modes fewer)")
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--workload", default="noncentered", choices=list(HARMONIC) + ["masked"] + list(MASKED_HEAD))
+    ap.add_argument("--workload", default="noncentered",
+                    choices=list(HARMONIC) + ["masked"] + list(MASKED_HEAD) + list(SURFACE))
     ap.add_argument("--nchains", type=int, default=None, help="chains per GPU (32; masked: 1)")
     ap.add_argument("--lmax", type=int, default=None, help="1024 (masked: 4096; HEAD modes: 512)")
     ap.add_argument("--nside", type=int, default=None, help="512 (masked: 2048; HEAD modes: 256)")
@@ -142,6 +144,8 @@ def main():
     try:
         if args.workload in HARMONIC:
             line = run_harmonic(args, ctx, cpu)
+        elif args.workload in SURFACE:
+            line = run_surface(args, ctx)
         elif args.workload == "masked":
             line = run_masked(args, ctx)
         else:
@@ -241,6 +245,56 @@ def run_harmonic(args, ctx, cpu):
                      "note": "the sweep is issue-bound (Philox + Box-Muller per normal, DESIGN.md 3): "
                              "valu_issue_frac = SQ_INST_CYCLES_VALU / (SIMDs x cycles) from profiles/"},
         "cpu_baseline": cpu,
+    }
+
+
+def run_surface(args, ctx):
+    """BASELINE configs[2] through the drop-in class surface a
+    main_polarization.py caller uses (gibbs.NonCenteredGibbs, all_sph, TEB,
+    native streams): wall time of ``run(dls_init)`` for --steps iterations --
+    the runner's replays of captured hipGraph chunks (32 steps each), the
+    per-chunk trace copies and the histories' one transfer to the host
+    included.  A warmup run of --warmup iterations builds the plan first."""
+    import torch
+    from gibbssampler_amd.gibbs import NonCenteredGibbs
+    from gibbssampler_amd.problem import synthetic_problem
+    L, N = args.lmax, args.nside
+    P = synthetic_problem(L, N, 3, seed=0)
+    d = P["d_alm"]
+    pix = {"TT": d[0], "EE": d[1], "BB": d[2]}
+    nv = P["noise_var"]
+    ncg = NonCenteredGibbs(pix, float(nv[0]), float(nv[1]), 0.5, N, L, 12 * N * N, P["proposal_variances"],
+                           metropolis_blocks=P["blocks"], polarization=True, bins=P["bins"], all_sph=True,
+                           n_iter=max(args.warmup, 1), rng="native", seed=args.seed, nchains=args.nchains,
+                           fields="TEB", chain0=ctx.chain0)
+    ncg.run(P["dls_init"])
+    ncg.n_iter = args.steps
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    out = ncg.run(P["dls_init"])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ctx.barrier()
+    elapsed = ctx.max(t1 - t0)
+    if ctx.rank != 0:
+        return None
+    hist = out[0]
+    assert np.asarray(hist["EE"]).shape[0] == args.steps + 1
+    total = args.steps * ctx.global_chains
+    return {
+        "metric": METRIC % (N, L), "value": round(total / elapsed, 3), "unit": "chain-iterations/s",
+        "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (analytic fiducial spectra, d = b s + n in harmonic space, seed 0)",
+        "config": {"workload": "noncentered TEB all_sph full-sky through gibbs.NonCenteredGibbs.run (drop-in surface)",
+                   "launch": "run(): replays of captured 32-step hipGraph chunks, histories to the host once",
+                   "nside": N, "lmax": L, "nfields": 3, "chains_per_gpu": args.nchains,
+                   "global_chains": ctx.global_chains, "rng": "native philox4x32-10",
+                   "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
+        "roofline": None, "cpu_baseline": None,
+        "notes": "the surface's own throughput (VERDICT r01 item 10); the roofline of its sweep is the default line's",
     }
 
 
