@@ -21,11 +21,18 @@ HEADERS = [os.path.join(HERE, "csrc", h) for h in ("gs_rng.h", "gs_common.h", "g
     [os.path.join(ROOT, "include", "gibbs_capi.h")]
 LIB = os.path.join(HERE, "libgibbs_hip.so")
 ARCH = os.environ.get("GIBBS_OFFLOAD_ARCH", "gfx950")
+# -ffp-contract=on: a*b+c is fused only within one expression (decided by the
+# source), never across statements (hipcc's default "fast-honor-pragmas" lets
+# the backend fuse depending on the inlining context), so the same device
+# function gives the same bits in every kernel that inlines it -- e.g. the
+# sweep's latency and throughput forms, the in-sweep and tabulated CR operator
+# (tests/test_gpu_graph.py::test_sweep_latency_form_bit_identical)
+COMMON = ["-ffp-contract=on"]
 VARIANTS = {
-    None: (LIB, ["-O3"]),
-    "debug": (os.path.join(HERE, "libgibbs_hip_debug.so"), ["-O3", "-DGS_DEBUG"]),
+    None: (LIB, ["-O3"] + COMMON),
+    "debug": (os.path.join(HERE, "libgibbs_hip_debug.so"), ["-O3", "-DGS_DEBUG"] + COMMON),
     "asan": (os.path.join(HERE, "libgibbs_hip_asan.so"),
-             ["-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", "-fsanitize=address", "-shared-libasan"]),
+             ["-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", "-fsanitize=address", "-shared-libasan"] + COMMON),
 }
 
 
@@ -44,7 +51,7 @@ def _stale(target, deps):
 
 def build(force=False, verbose=True, variant=None):
     lib, flags = VARIANTS[variant]
-    deps = SOURCES + HEADERS
+    deps = SOURCES + HEADERS + [os.path.abspath(__file__)]
     if not force and not _stale(lib, deps):
         return lib
     cmd = ["hipcc", f"--offload-arch={ARCH}"] + flags + ["-std=c++17", "-shared", "-fPIC",

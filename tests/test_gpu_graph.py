@@ -140,3 +140,38 @@ def test_asis_skymap_without_quirk(F):
                 vt = H.var_from_dl(H.unfold_bins(tmp[c][sp], P["bins"][sp]))
                 R = np.sqrt(vn) * np.where(vt != 0, np.sqrt(1.0 / np.where(vt != 0, vt, 1.0)), 0.0)
                 np.testing.assert_allclose(got[c, k], R[sl] * sc[c, k], rtol=1e-13, atol=1e-300)
+
+
+@pytest.mark.parametrize("kind,F", [("centered", 1), ("centered", 2), ("centered", 3), ("noncentered", 2),
+                                    ("noncentered", 3), ("asis", 3)])
+def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
+    """Plans of <= 4 chains with <= 4 rows per task (257 <= L <= 512) run the
+    latency form of the sweep (every load issued first); it must give the same
+    bits as the throughput form (GS_SWEEP_THROUGHPUT=1 at plan creation): same
+    arithmetic, same row order -- maps, D_l and accept flags over 3 native steps,
+    eager and as one captured 3-step graph (gs_graph_step offsets)."""
+    from gibbssampler_amd.problem import synthetic_problem
+    from gibbssampler_amd.samplers import BatchedRunner
+    P = synthetic_problem(300, 128, F, seed=5)
+
+    def run(env, graph):
+        if env:
+            monkeypatch.setenv("GS_SWEEP_THROUGHPUT", "1")
+        else:
+            monkeypatch.delenv("GS_SWEEP_THROUGHPUT", raising=False)
+        r = BatchedRunner(kind, P["lmax"], P["nside"], F, 2, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
+                          blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=17)
+        assert r.plan.rows_per_task == 4
+        r.init(P["dls_init"])
+        if graph:
+            r.capture_steps(3)
+            r.step()
+        else:
+            for _ in range(3):
+                r.step()
+        return r.dl.cpu().numpy(), r.s.cpu().numpy(), r.accept.cpu().numpy()
+
+    for graph in (False, True):
+        a, b = run(False, graph), run(True, graph)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
