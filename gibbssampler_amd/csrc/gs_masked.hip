@@ -765,8 +765,19 @@ __global__ void k_f2_gram_finish(int R, int nchunk, const double* __restrict__ p
     const int nblk4 = nb4 * (nb4 + 1) / 2;
     const int b = (i / 4) * (i / 4 + 1) / 2 + j / 4;
     const double* pp = partial + (long long)b * 16 + (i % 4) * 4 + (j % 4);
+    const long long cs = (long long)nblk4 * 16;
+    // chunks in order, 16 loads issued before their sums (the last group's
+    // extra loads clamped and dropped): one memory latency per 16 chunks
+    // instead of one per chunk (768 chunks at N_side 256: 284 us before)
     double s = 0.0;
-    for (int c = 0; c < nchunk; ++c) s += pp[(long long)c * nblk4 * 16];
+    for (int c0 = 0; c0 < nchunk; c0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) v[t] = pp[(long long)min(c0 + t, nchunk - 1) * cs];
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            if (c0 + t < nchunk) s += v[t];
+    }
     G[g] = s;
 }
 
@@ -774,42 +785,73 @@ __global__ void k_f2_gram_finish(int R, int nchunk, const double* __restrict__ p
 // log u < (g_k - sum_{j accepted} G_kj - G_kk / 2) + sum log r; after an
 // acceptance later attempts see delta = 0 (the proposal IS the state).
 // One workgroup; corr[k] = sum over accepted j < k of G_kj, accumulated in
-// decision order.
+// decision order.  Everything that does not depend on earlier decisions --
+// the lower triangle of G, each block's sum of log proposal ratios and the
+// log accept uniforms -- is staged in LDS in parallel first, so the serial
+// chain of decisions touches LDS only (it was a chain of global-memory
+// latencies per block: 236 us for 135 blocks at N_side 256).
 __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* __restrict__ G, int k0, int n_iter,
                                                    const int* __restrict__ blk_field,
                                                    const int* __restrict__ blk_bins, int maxbins,
                                                    const double* __restrict__ logr, const double* __restrict__ u_acc,
                                                    const double* __restrict__ prop, double* __restrict__ binned,
                                                    int32_t* __restrict__ accept_out, double* __restrict__ taken_out) {
+    extern __shared__ __attribute__((aligned(16))) double Gl[];      // [R (R + 1) / 2] lower triangle,
+                                                                     // then [kn][n_iter] log u
     __shared__ double corr[F2_RMAX];
+    __shared__ double lrs[F2_RMAX];
+    __shared__ int bfield[F2_RMAX], blo[F2_RMAX], bhi[F2_RMAX];
     __shared__ int taken_s;
     GS_ASSERT(kn < F2_RMAX && R == kn + 1);
     const int tid = threadIdx.x;
-    for (int k = tid; k < kn; k += blockDim.x) corr[k] = 0.0;
+    const int ntri = R * (R + 1) / 2;
+    double* lu = Gl + ntri;
+    for (int t = tid; t < kn * n_iter; t += blockDim.x) lu[t] = log(u_acc[(long long)k0 * n_iter + t]);
+    for (int t = tid; t < ntri; t += blockDim.x) {
+        int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while ((i + 1) * (i + 2) / 2 <= t) ++i;
+        while (i * (i + 1) / 2 > t) --i;
+        Gl[t] = G[(long long)i * R + (t - i * (i + 1) / 2)];
+    }
+    for (int k = tid; k < kn; k += blockDim.x) {
+        corr[k] = 0.0;
+        const int kg = k0 + k, f = blk_field[kg];
+        const int lo = blk_bins[2 * kg], hi = blk_bins[2 * kg + 1];
+        GS_ASSERT(lo >= 0 && hi <= maxbins && lo <= hi);
+        bfield[k] = f; blo[k] = lo; bhi[k] = hi;
+        double sl = 0.0;
+        for (int b = lo; b < hi; ++b) sl += logr[f * maxbins + b];
+        lrs[k] = sl;
+    }
     __syncthreads();
+    const int rl = (R - 1) * R / 2;                        // row R - 1 (the residual) of the triangle
     for (int k = 0; k < kn; ++k) {
         if (tid == 0) {
-            const int kg = k0 + k, f = blk_field[kg];
-            const int lo = blk_bins[2 * kg], hi = blk_bins[2 * kg + 1];
-            GS_ASSERT(lo >= 0 && hi <= maxbins && lo <= hi);
-            double lrs = 0.0;
-            for (int b = lo; b < hi; ++b) lrs += logr[f * maxbins + b];
-            const double delta = (G[(long long)(R - 1) * R + k] - corr[k]) - 0.5 * G[(long long)k * R + k];
+            const int kg = k0 + k, f = bfield[k];
+            const double delta = (Gl[rl + k] - corr[k]) - 0.5 * Gl[k * (k + 1) / 2 + k];
             bool taken = false;
             for (int att = 0; att < n_iter; ++att) {
-                const bool acc = log(u_acc[(long long)kg * n_iter + att]) < (taken ? 0.0 : delta) + lrs;
-                if (acc && !taken)
-                    for (int b = lo; b < hi; ++b) binned[f * maxbins + b] = prop[f * maxbins + b];
+                const bool acc = lu[k * n_iter + att] < (taken ? 0.0 : delta) + lrs[k];
                 taken = taken || acc;
                 accept_out[(long long)kg * n_iter + att] = acc ? 1 : 0;
             }
             taken_s = taken ? 1 : 0;
             taken_out[k] = taken ? 1.0 : 0.0;
+            (void)f;
         }
         __syncthreads();
-        if (taken_s)
-            for (int j = k + 1 + tid; j < kn; j += blockDim.x) corr[j] += G[(long long)j * R + k];
+        if (taken_s) {
+            for (int j = k + 1 + tid; j < kn; j += blockDim.x) corr[j] += Gl[j * (j + 1) / 2 + k];
+            if (tid == 0) bfield[k] = -1 - bfield[k];          // mark taken (field kept, encoded)
+        }
         __syncthreads();
+    }
+    // the accepted blocks' proposals into the binned spectra, all blocks in
+    // parallel (their bins are disjoint), off the serial decision chain
+    for (int k = 0; k < kn; ++k) {
+        if (bfield[k] >= 0) continue;
+        const int f = -1 - bfield[k];
+        for (int b = blo[k] + tid; b < bhi[k]; b += blockDim.x) binned[f * maxbins + b] = prop[f * maxbins + b];
     }
 }
 
@@ -1290,7 +1332,12 @@ int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* 
         hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256)), dim3(256), 0, st, R, (int)nchunk,
                            c->f2_part, c->f2_G);
         GS_LAUNCH_CHECK("k_f2_gram_finish");
-        hipLaunchKernelGGL(k_f2_decide, dim3(1), dim3(256), 0, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
+        const size_t dlds = ((size_t)R * (R + 1) / 2 + (size_t)kn * n_iter) * sizeof(double);
+        if (dlds > 64 * 1024) {                 // the triangle of G beyond 64 KB of dynamic LDS
+            (void)hipFuncSetAttribute((const void*)k_f2_decide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds);
+            (void)hipGetLastError();
+        }
+        hipLaunchKernelGGL(k_f2_decide, dim3(1), dim3(256), dlds, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
                            maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken);
         GS_LAUNCH_CHECK("k_f2_decide");
         if (k0 + kn < K) {
