@@ -14,6 +14,15 @@ import numpy as np
 from .problem import BINS_BB_512, gauss_beam, default_blocks, proposal_variances
 
 
+# cosmological parameter prior (config.py:10-12); the theory spectra they feed
+# (utils.generate_cls through CLASS) are out of scope
+COSMO_PARAMS_NAMES = ["n_s", "omega_b", "omega_cdm", "100*theta_s", "ln10^{10}A_s", "tau_reio"]
+COSMO_PARAMS_MEAN_PRIOR = np.array([0.9665, 0.02242, 0.11933, 1.04101, 3.047, 0.0561])
+COSMO_PARAMS_SIGMA_PRIOR = np.array([0.0038, 0.00014, 0.00091, 0.00029, 0.014, 0.0071])
+# config.py:205-207 sets it from preliminary chains (non-preliminary runs only)
+starting_point = None
+
+
 @dataclass
 class GibbsConfig:
     NSIDE: int = 256
@@ -42,10 +51,8 @@ class GibbsConfig:
         self.bl_gauss = gauss_beam(self.fwhm_radians, L)
         self.bl_map = np.concatenate([self.bl_gauss, np.array(
             [cl for m in range(1, L + 1) for cl in self.bl_gauss[m:] for _ in range(2)])])
-        mask = np.ones(L + 1)
         self.mask_inversion = np.ones((L + 1) ** 2, dtype=bool)      # cp38 config, src line 56-58
         self.mask_inversion[[0, 1, L + 1, L + 2]] = False
-        del mask
         self.proposal_variances_nc_polarized = proposal_variances(L, self.NSIDE, self.bins, self.bl_gauss,
                                                                   self.noise_covar_pol, self.noise_covar_temp)
 

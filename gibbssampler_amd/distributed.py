@@ -92,15 +92,3 @@ class ShardContext:
             self.dist.destroy_process_group()
             self._owns_group = False
 
-
-def gather_traces(trace, group=None):
-    """All-gather a per-rank trace tensor [n_iter, chains_per_rank, ...] into
-    [n_iter, world * chains_per_rank, ...] ordered by global chain id."""
-    import torch
-    import torch.distributed as dist
-    if not dist.is_available() or not dist.is_initialized():
-        return trace
-    world = dist.get_world_size(group)
-    parts = [torch.empty_like(trace) for _ in range(world)]
-    dist.all_gather(parts, trace.contiguous(), group=group)
-    return torch.cat(parts, dim=1)
