@@ -643,6 +643,8 @@ __global__ void k_tt_fullsky(int L, const double* __restrict__ dl, const double*
 // ---------------------------------------------------------------------------
 constexpr int F2_GSUB = 32;          // elements per LDS stage of the Gram pass
 constexpr int F2_RMAX = 176;         // rows (blocks + residual) per Gram pass
+// dynamic LDS k_f2_decide may use: 160 KB less its static arrays (5 x F2_RMAX words + 1)
+constexpr size_t F2_DECIDE_LDS = 160 * 1024 - (2 * sizeof(double) + 3 * sizeof(int)) * F2_RMAX - 64;
 constexpr int F2_BPT = 4;            // 4 x 4 output blocks per thread
 constexpr long long F2_CHUNK = 2048; // elements per Gram workgroup
 
@@ -795,9 +797,10 @@ __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* 
                                                    const int* __restrict__ blk_bins, int maxbins,
                                                    const double* __restrict__ logr, const double* __restrict__ u_acc,
                                                    const double* __restrict__ prop, double* __restrict__ binned,
-                                                   int32_t* __restrict__ accept_out, double* __restrict__ taken_out) {
+                                                   int32_t* __restrict__ accept_out, double* __restrict__ taken_out,
+                                                   int lu_lds) {
     extern __shared__ __attribute__((aligned(16))) double Gl[];      // [R (R + 1) / 2] lower triangle,
-                                                                     // then [kn][n_iter] log u
+                                                                     // then (lu_lds) [kn][n_iter] log u
     __shared__ double corr[F2_RMAX];
     __shared__ double lrs[F2_RMAX];
     __shared__ int bfield[F2_RMAX], blo[F2_RMAX], bhi[F2_RMAX];
@@ -806,7 +809,10 @@ __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* 
     const int tid = threadIdx.x;
     const int ntri = R * (R + 1) / 2;
     double* lu = Gl + ntri;
-    for (int t = tid; t < kn * n_iter; t += blockDim.x) lu[t] = log(u_acc[(long long)k0 * n_iter + t]);
+    // the log uniforms go to LDS when they fit beside the triangle (the host
+    // decides); otherwise the serial chain takes them from global memory
+    if (lu_lds)
+        for (int t = tid; t < kn * n_iter; t += blockDim.x) lu[t] = log(u_acc[(long long)k0 * n_iter + t]);
     for (int t = tid; t < ntri; t += blockDim.x) {
         int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
         while ((i + 1) * (i + 2) / 2 <= t) ++i;
@@ -831,7 +837,8 @@ __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* 
             const double delta = (Gl[rl + k] - corr[k]) - 0.5 * Gl[k * (k + 1) / 2 + k];
             bool taken = false;
             for (int att = 0; att < n_iter; ++att) {
-                const bool acc = lu[k * n_iter + att] < (taken ? 0.0 : delta) + lrs[k];
+                const double l_u = lu_lds ? lu[k * n_iter + att] : log(u_acc[(long long)kg * n_iter + att]);
+                const bool acc = l_u < (taken ? 0.0 : delta) + lrs[k];
                 taken = taken || acc;
                 accept_out[(long long)kg * n_iter + att] = acc ? 1 : 0;
             }
@@ -1332,13 +1339,21 @@ int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* 
         hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256)), dim3(256), 0, st, R, (int)nchunk,
                            c->f2_part, c->f2_G);
         GS_LAUNCH_CHECK("k_f2_gram_finish");
-        const size_t dlds = ((size_t)R * (R + 1) / 2 + (size_t)kn * n_iter) * sizeof(double);
-        if (dlds > 64 * 1024) {                 // the triangle of G beyond 64 KB of dynamic LDS
-            (void)hipFuncSetAttribute((const void*)k_f2_decide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds);
+        // dynamic LDS: G's lower triangle (<= 124.6 KB at F2_RMAX rows), plus the
+        // log uniforms when they fit in what the static arrays leave of 160 KB
+        const size_t tri = (size_t)R * (R + 1) / 2 * sizeof(double);
+        const size_t lus = (size_t)kn * n_iter * sizeof(double);
+        const int lu_lds = tri + lus <= F2_DECIDE_LDS ? 1 : 0;
+        const size_t dlds = tri + (lu_lds ? lus : 0);
+        if (dlds > F2_DECIDE_LDS) return set_error("gs_masked_pixel_mh: Gram triangle exceeds the decision LDS");
+        if (dlds > 64 * 1024 &&                 // the triangle of G beyond 64 KB of dynamic LDS
+            hipFuncSetAttribute((const void*)k_f2_decide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds) !=
+                hipSuccess) {
             (void)hipGetLastError();
+            return set_error("gs_masked_pixel_mh: cannot raise k_f2_decide's dynamic LDS limit");
         }
         hipLaunchKernelGGL(k_f2_decide, dim3(1), dim3(256), dlds, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
-                           maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken);
+                           maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken, lu_lds);
         GS_LAUNCH_CHECK("k_f2_decide");
         if (k0 + kn < K) {
             hipLaunchKernelGGL(k_f2_update, dim3(nblocks(n, 256)), dim3(256), 0, st, n, kn, c->f2_Y, c->f2_taken,

@@ -125,29 +125,32 @@ class BatchedRunner:
         if time_sweeps:
             p.sweep_timing(True)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for i in range(nsteps):
-                # step i reads base + i; only the last step's last launch advances
-                # the base (by nsteps): one counter ticket per replay
-                p.graph_step(i, nsteps if i == nsteps - 1 else 0)
-                if time_sweeps:
-                    p.sweep_timing("resume" if i % time_every == 0 else "pause")
-                # accept_trace [nsteps, nchains, nacc]: step i writes its own slot
-                acc = self.accept if accept_trace is None else accept_trace[i]
-                if self.kind == "noncentered":
-                    p.nc_prologue(self.dl, seed=self.seed)
-                    p.nc_sweep(self.d, self.dl, self.s, seed=self.seed, finish=False)
-                    p.nc_finish()
-                    p.nc_decide_fused(self.dl, seed=self.seed, accept=acc, trace=trace,
-                                      capacity=trace_capacity or 0)
-                elif self.kind == "centered":
-                    p.step_centered_fused(self.d, self.dl, self.s, seed=self.seed, trace=trace,
+        try:
+            with torch.cuda.graph(g):
+                for i in range(nsteps):
+                    # step i reads base + i; only the last step's last launch advances
+                    # the base (by nsteps): one counter ticket per replay
+                    p.graph_step(i, nsteps if i == nsteps - 1 else 0)
+                    if time_sweeps:
+                        p.sweep_timing("resume" if i % time_every == 0 else "pause")
+                    # accept_trace [nsteps, nchains, nacc]: step i writes its own slot
+                    acc = self.accept if accept_trace is None else accept_trace[i]
+                    if self.kind == "noncentered":
+                        p.nc_prologue(self.dl, seed=self.seed)
+                        p.nc_sweep(self.d, self.dl, self.s, seed=self.seed, finish=False)
+                        p.nc_finish()
+                        p.nc_decide_fused(self.dl, seed=self.seed, accept=acc, trace=trace,
                                           capacity=trace_capacity or 0)
-                else:
-                    p.step_asis_fused(self.d, self.dl, self.s, seed=self.seed, accept=acc,
-                                      dl_tmp=self.dl_tmp, recentre=self.materialize_recentre, trace=trace,
-                                      capacity=trace_capacity or 0)
-        p.graph_step(0, 1)
+                    elif self.kind == "centered":
+                        p.step_centered_fused(self.d, self.dl, self.s, seed=self.seed, trace=trace,
+                                              capacity=trace_capacity or 0)
+                    else:
+                        p.step_asis_fused(self.d, self.dl, self.s, seed=self.seed, accept=acc,
+                                          dl_tmp=self.dl_tmp, recentre=self.materialize_recentre, trace=trace,
+                                          capacity=trace_capacity or 0)
+        finally:
+            # back to one step per replay even when a launch raised inside the capture
+            p.graph_step(0, 1)
         self.graph = g
         self.graph_steps = nsteps
         return g
@@ -214,6 +217,9 @@ class BatchedRunner:
                     e1.synchronize()
                     t_steps += [e0.elapsed_time(e1) * 1e-3 / k] * k
                 done += k
+            # the last step's flags, as the eager path leaves them in runner.accept
+            if self.kind != "centered":
+                self.accept.copy_(acc_tr[k - 1][:, :self.accept.shape[1]])
             self.graph = None
             p.iteration_counter(False)
             n_iter = 0

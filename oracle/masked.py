@@ -108,8 +108,10 @@ class MaskedModel:
 
     def synth(self, s_real):
         """maps of b * s (s real layout [F, NR]) -> [F, Npix] for the field rows."""
-        a = np.zeros((3, O._cidx(self.L)[0].shape[0]), dtype=np.complex128)
         ls = O._cidx(self.L)[0]
+        if self.F == 1:          # temperature only: the spin-0 transform alone
+            return O.alm2map(H.real_to_complex(s_real[0], self.L) * self.bl[ls], self.nside, self.L)[None]
+        a = np.zeros((3, ls.shape[0]), dtype=np.complex128)
         for k, r in enumerate(self.rows):
             a[r] = H.real_to_complex(s_real[k], self.L) * self.bl[ls]
         m = O.alm2map(a, self.nside, self.L)
@@ -117,6 +119,8 @@ class MaskedModel:
 
     def analysis(self, mp, iter=0):
         """complex_to_real(map2alm(maps, iter)) for the field rows: [F, NR]."""
+        if self.F == 1:          # temperature only: the spin-0 transform alone
+            return H.complex_to_real(O.map2alm(np.asarray(mp)[0], self.nside, self.L, iter=iter), self.L)[None]
         full = np.zeros((3, self.Npix))
         for k, r in enumerate(self.rows):
             full[r] = mp[k]

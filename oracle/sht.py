@@ -44,6 +44,7 @@ the FFT, the aliasing fold nor the scaled Legendre recurrence of the device
 code.  Sizes: intended for N_side <= 64, l_max <= 128 (dense [ring, l, m]
 tables; the unscaled recurrence is asserted not to underflow).
 """
+import functools
 import math
 
 import numpy as np
@@ -178,6 +179,30 @@ def _from_lm(A, L):
     return A[ls, ms].copy()
 
 
+@functools.lru_cache(maxsize=2)
+def _ring_exp(nside, L):
+    """per ring the [nphi, L+1] table e^{i m phi_j} (cached per geometry: the
+    oracle's transforms are direct sums, this only avoids recomputing them)."""
+    z, nphi, phi0, start = ring_info(nside)
+    m = np.arange(L + 1)
+    out = []
+    for r in range(len(z)):
+        phi = phi0[r] + 2.0 * math.pi * np.arange(nphi[r]) / nphi[r]
+        out.append(np.exp(1j * np.outer(phi, m)))
+    return out
+
+
+@functools.lru_cache(maxsize=2)
+def _ring_legendre(nside, L):
+    """(lambda, F1, F2)[ring, l, m] at the ring colatitudes (cached per geometry)."""
+    z = ring_info(nside)[0]
+    lam = lambda_lm(L, z)
+    F1, F2 = spin2_F(L, z, lam)
+    for a in (lam, F1, F2):
+        a.flags.writeable = False
+    return lam, F1, F2
+
+
 def _ring_sum(F, nside):
     """map pixels from per-ring F[ring, m]: sum_m c_m Re[F_m e^{i m phi_j}]."""
     z, nphi, phi0, start = ring_info(nside)
@@ -185,11 +210,9 @@ def _ring_sum(F, nside):
     out = np.empty(npix(nside))
     cm = np.full(L + 1, 2.0)
     cm[0] = 1.0
-    m = np.arange(L + 1)
+    E = _ring_exp(nside, L)
     for r in range(len(z)):
-        phi = phi0[r] + 2.0 * math.pi * np.arange(nphi[r]) / nphi[r]
-        E = np.exp(1j * np.outer(phi, m))
-        out[start[r]:start[r] + nphi[r]] = (E @ (cm * F[r])).real
+        out[start[r]:start[r] + nphi[r]] = (E[r] @ (cm * F[r])).real
     return out
 
 
@@ -197,11 +220,9 @@ def _ring_phase(mp, nside, L):
     """Phi[ring, m] = sum_j map_j e^{-i m phi_j}."""
     z, nphi, phi0, start = ring_info(nside)
     P = np.empty((len(z), L + 1), dtype=np.complex128)
-    m = np.arange(L + 1)
+    E = _ring_exp(nside, L)
     for r in range(len(z)):
-        phi = phi0[r] + 2.0 * math.pi * np.arange(nphi[r]) / nphi[r]
-        E = np.exp(-1j * np.outer(m, phi))
-        P[r] = E @ mp[start[r]:start[r] + nphi[r]]
+        P[r] = E[r].conj().T @ mp[start[r]:start[r] + nphi[r]]
     return P
 
 
@@ -209,13 +230,11 @@ def alm2map(alms, nside, lmax):
     """alms: complex [L lm] (spin 0, T only) or [3, nlm] (T, E, B -> T, Q, U)."""
     alms = np.asarray(alms)
     L = lmax
-    z = ring_info(nside)[0]
-    lam = lambda_lm(L, z)
+    lam, F1, F2 = _ring_legendre(nside, L)
     if alms.ndim == 1:
         A = _to_lm(alms, L)
         F = np.einsum("rlm,lm->rm", lam, A)
         return _ring_sum(F, nside)
-    F1, F2 = spin2_F(L, z, lam)
     AT, AE, AB = (_to_lm(a, L) for a in alms)
     T = _ring_sum(np.einsum("rlm,lm->rm", lam, AT), nside)
     Q = _ring_sum(-(np.einsum("rlm,lm->rm", F1, AE) + 1j * np.einsum("rlm,lm->rm", F2, AB)), nside)
@@ -228,11 +247,7 @@ def map2alm(maps, nside, lmax, iter=0):
     maps = np.asarray(maps, dtype=np.float64)
     L = lmax
     w = FOURPI / npix(nside)
-    z = ring_info(nside)[0]
-    lam = lambda_lm(L, z)
-    F1 = F2 = None
-    if maps.ndim == 2:
-        F1, F2 = spin2_F(L, z, lam)
+    lam, F1, F2 = _ring_legendre(nside, L)
 
     def adj(mp):
         if mp.ndim == 1:

@@ -409,3 +409,54 @@ def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes, s
     _close(new["EE"], want["EE"])
     _close(new["BB"], want["BB"])
     assert acc == wacc
+
+
+@pytest.fixture(scope="module")
+def f2_large():
+    """N_side 32, l_max 70, unbinned EE and BB with one Metropolis block per bin
+    from bin 2: 69 + 69 = 138 blocks, so one Gram group has R = 139 rows (G's
+    triangle 77.8 KB: the > 64 KB dynamic-LDS decision path) and the Gram pass
+    an uneven number of chunks."""
+    from gibbssampler_amd.problem import gauss_beam
+    N, L = 32, 70
+    npix = 12 * N * N
+    rng = np.random.default_rng(4242)
+    theta, _ = O.pixel_angles(N)
+    mask = (np.abs(np.cos(theta)) > 0.2).astype(np.float64)
+    bins = {"EE": np.arange(0, L + 2), "BB": np.arange(0, L + 2)}
+    blocks = {"EE": np.arange(2, L + 2), "BB": np.arange(2, L + 2)}
+    dl = {"EE": np.r_[0.0, 0.0, 10.0 * (np.arange(2, L + 1) / 100.0) ** 0.5], "BB": np.r_[0.0, 0.0, np.full(L - 1, 0.05)]}
+    pv = {"EE": (0.02 * dl["EE"][2:]) ** 2, "BB": np.full(L - 1, 0.01) ** 2}     # bins >= 2
+    pix = {"Q": rng.normal(0, 0.5, npix), "U": rng.normal(0, 0.5, npix)}
+    snc = rng.normal(size=(2, (L + 1) ** 2))
+    return dict(N=N, L=L, mask=mask, bins=bins, blocks=blocks, dl=dl, pv=pv, pix=pix, snc=snc,
+                bl=gauss_beam(np.radians(0.5), L))
+
+
+@pytest.mark.parametrize("n_iter", [1, 20, 90])
+def test_f2_large_group_decisions_equal_one_block_groups(f2_large, monkeypatch, n_iter):
+    """the large-R decision path (138 blocks in one group, G's
+    triangle beyond 64 KB of LDS) and n_iter_metropolis up to 90 (the log
+    uniforms then no longer fit in LDS beside the triangle and are read from
+    global memory) decide exactly as one block per group, whose path the
+    small-fixture tests pin against the oracle's full-map likelihood."""
+    from gibbssampler_amd.masked import MaskedCR, PixelMH
+    q = f2_large
+    out = []
+    for group_bytes in (None, "1"):
+        if group_bytes is None:
+            monkeypatch.delenv("GS_F2_GROUP_BYTES", raising=False)
+        else:
+            monkeypatch.setenv("GS_F2_GROUP_BYTES", group_bytes)
+        cr = MaskedCR(q["pix"], 40.0 ** 2, np.full(12 * q["N"] ** 2, 0.2 ** 2), q["bl"], q["L"], q["N"],
+                      mask=q["mask"], gibbs_cr=False, ula=False, rng="native", seed=515, chain=2)
+        mh = PixelMH(cr, q["bins"], q["blocks"], q["pv"], n_iter_metropolis=n_iter)
+        assert mh.K == 138
+        new, acc = mh.sample(q["snc"], {k: v.copy() for k, v in q["dl"].items()}, iteration=3)
+        out.append((new, acc))
+    (n0, a0), (n1, a1) = out
+    assert a0 == a1
+    nacc = sum(int(np.sum(v)) for v in a0.values())
+    assert 0 < nacc < 138 * n_iter, nacc              # both branches of the decision exercised
+    for sp in ("EE", "BB"):
+        np.testing.assert_array_equal(n0[sp], n1[sp])
