@@ -16,6 +16,10 @@ iteration (constrained realisation + C_l draw) of every chain on every GPU.
                        gibbs_cr + ula (aux + MALA), EB, N_side 256 / L 512, 1 chain / GPU
   masked_asis          HEAD's ASIS (:121-124): masked, all_sph=False, gibbs_cr, over-relaxation,
                        n_gibbs 20, pixel-domain MH (f2), EB, N_side 256 / L 512, 1 chain / GPU
+  masked_centered_pcg  HEAD's centered_gibbs (:109-111): masked, gibbs_cr=False, ula=False -> the
+                       PCG CR (f1, device-resident CG) every iteration + C_l draw, EB, N256 / L512
+  masked_noncentered   HEAD's non_centered_gibbs (:117-120) with the mask: PCG CR, C^-1/2, the
+                       pixel-domain MH sweep (f2), EB, N_side 256 / L 512, 1 chain / GPU
 
 For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL): chains
 are sharded (global chain id = rank * chains_per_gpu + c) by
@@ -40,7 +44,7 @@ FP64_VALU_PEAK_TFS = 78.6    # MI355X_MICROARCH.md: FP64 vector
 METRIC = "Gibbs iters/sec (constrained-realization + C_l draw), Nside=%d lmax=%d"
 HARMONIC = ("noncentered", "centered", "asis")
 SURFACE = ("surface_noncentered",)
-MASKED_HEAD = ("masked_centered_ula", "masked_asis")
+MASKED_HEAD = ("masked_centered_ula", "masked_asis", "masked_centered_pcg", "masked_noncentered")
 
 
 def parse():
@@ -438,14 +442,31 @@ def run_masked_head(args, ctx):
     init = {s: bin_spectrum(dl[s], bins[s]) for s in ("EE", "BB")}
     noise_t, noise_p = np.ones(Npix) * 40.0 ** 2, np.ones(Npix) * 0.2 ** 2
     kw = dict(mask_path=mask, polarization=True, bins=bins, rng="native", seed=args.seed, chain0=ctx.chain0)
-    if args.workload == "masked_centered_ula":
-        smp = G.CenteredGibbs(pix, noise_t, noise_p, 0.5, N, L, Npix, n_iter=args.warmup, gibbs_cr=True, ula=True,
+    pcg = None
+    if args.workload in ("masked_centered_ula", "masked_centered_pcg"):
+        ula = args.workload == "masked_centered_ula"
+        smp = G.CenteredGibbs(pix, noise_t, noise_p, 0.5, N, L, Npix, n_iter=args.warmup, gibbs_cr=ula, ula=ula,
                               **kw)
         runner = MaskedRunner(smp.constrained_sampler, smp.bins)
-        n_sht, what = 6, "aux-variable CR (n_gibbs 1) + MALA (CenteredGibbs.py:831-834), EB"
+        if ula:
+            n_sht, what = 6, "aux-variable CR (n_gibbs 1) + MALA (CenteredGibbs.py:831-834), EB"
+        else:
+            n_sht, what = None, ("PCG CR every iteration (CenteredGibbs.py:448-491, pcg_accuracy 1e-5, per-l "
+                                 "preconditioner, device-resident CG) + C_l draw, EB")
+            pcg = smp.constrained_sampler
         h = runner.run(init, max(args.warmup, 1), None)[0]
         last = {s: h[s][-1] for s in h}
         go = lambda: runner.run(last, args.steps, runner.s)
+    elif args.workload == "masked_noncentered":
+        smp = G.NonCenteredGibbs(pix, noise_t, noise_p, 0.5, N, L, Npix, pv, metropolis_blocks=blocks,
+                                 n_iter=args.warmup, all_sph=True, **kw)
+        runner = smp.masked_runner
+        pcg = runner.cr
+        n_sht, what = None, ("PCG CR every iteration (NonCenteredGibbs.py:178-196, device-resident CG), C^-1/2, "
+                             f"pixel-domain MH over {runner.mh.K} blocks decided on the device (f2), EB")
+        h = runner.run(init, max(args.warmup, 1))[0]
+        last = {s: h[s][-1] for s in h}
+        go = lambda: runner.run(last, args.steps, s_init=runner.s)
     else:
         smp = G.ASIS(pix, noise_t, noise_p, 0.5, N, L, Npix, pv, metropolis_blocks=blocks, n_iter=args.warmup,
                      all_sph=False, gibbs_cr=True, n_gibbs=20, overrelaxation=True, **kw)
@@ -458,12 +479,23 @@ def run_masked_head(args, ctx):
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
+    n_solves0 = len(pcg.pcg_iterations) if pcg is not None else 0
     t0 = time.perf_counter()
     go()
     torch.cuda.synchronize()
     elapsed = ctx.max(time.perf_counter() - t0)
     if ctx.rank != 0:
         return None
+    pcg_info = None
+    if pcg is not None:
+        its = pcg.pcg_iterations[n_solves0:]
+        syncs = pcg.pcg_syncs[n_solves0:]
+        # per CG iteration one alm2map + one map2alm; the rhs adds map2alm iter 3 (7 transforms)
+        n_sht = 2 * float(np.mean(its)) + 7
+        pcg_info = {"solves": len(its), "cg_iterations_per_solve": round(float(np.mean(its)), 1),
+                    "host_syncs_per_solve": round(float(np.mean(syncs)), 2),
+                    "ms_per_cg_iteration": round(elapsed / args.steps * 1e3 / max(float(np.mean(its)), 1.0), 4),
+                    "tolerance": pcg.pcg_accuracy, "residual_last": pcg.pcg_residual}
     fl = n_sht * sht_flops(N, L, 16)
     achieved = fl / (elapsed / args.steps) / 1e12
     return {
@@ -478,11 +510,12 @@ def run_masked_head(args, ctx):
                    "nside": N, "lmax": L, "nfields": 2, "chains_per_gpu": 1, "global_chains": ctx.world,
                    "bins": "config.py:45 Planck BB", "blocks": "config.py:51-55",
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
-        "roofline": {"bound": "fp64", "kernel": f"{n_sht} spin-2 SHT-equivalents per iteration",
+        "roofline": {"bound": "fp64", "kernel": f"{n_sht:.1f} spin-2 SHT-equivalents per iteration",
                      "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP64_VALU_PEAK_TFS, 4), "traffic": None,
                      "algorithmic_flops_per_step": fl},
         "cpu_baseline": None,
+        "pcg": pcg_info,
         "notes": "healpy is absent: no CPU SHT baseline for the masked modes (DESIGN.md 7)",
     }
 

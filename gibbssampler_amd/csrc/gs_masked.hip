@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <cmath>
 #include <string>
 #include <vector>
 #include <algorithm>
@@ -401,97 +402,191 @@ __global__ void k_pcg_rhs(int L, const double* __restrict__ dl, const double* __
     }
 }
 
-// out = C^+ x + (b / w) r,  r = complex_to_real(map2alm(N^-1 A b x))
-template <int F>
-__global__ void k_pcg_qfinish(int L, const double* __restrict__ dl, const double* __restrict__ bl,
-                              const double* __restrict__ x, const double* __restrict__ r_alm, double inv_w,
-                              double* __restrict__ out) {
-    const long long NR = (long long)(L + 1) * (L + 1);
-    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
-    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (i >= nlm) return;
-    int l, m;
-    cidx_lm(L, i, l, m);
-    const long long r = m == 0 ? l : 2 * i - (L + 1);
-    const int nv = m == 0 ? 1 : 2;
-    const PriorPinv q = prior_pinv<F>(dl, L, l);
-    const double bw = bl[l] * inv_w;
-    for (int c = 0; c < nv; ++c) {
-        double cx[3];
-        if constexpr (F != 3) {
-            cx[0] = q.ie * q.ie * x[r + c];
-            if constexpr (F == 2) cx[1] = q.ib * q.ib * x[NR + r + c];
-        } else {
-            const double xt = x[r + c], xe = x[NR + r + c];
-            const double y0 = q.i00 * xt, y1 = q.t10 * xt + q.i11 * xe;
-            cx[0] = q.i00 * y0 + q.t10 * y1;
-            cx[1] = q.i11 * y1;
-            cx[2] = q.iB * q.iB * x[2 * NR + r + c];
-        }
-#pragma unroll
-        for (int f = 0; f < F; ++f) out[f * NR + r + c] = cx[f] + r_alm[f * NR + r + c] * bw;
-    }
-}
+// Device-resident CG state (one solve at a time per context).  The scalars of
+// the recurrence live on the device; every iteration kernel reads them there
+// and returns at once when the solve has converged, so the host launches whole
+// batches of iterations and reads the state once per batch, never per iteration.
+struct PcgState {
+    double bn, rz, rn, alpha, beta, tol;
+    int it, done, maxiter, pad;
+};
 
-// z = Sigma r, Sigma = L L^T the centered block for kappa_f = nbar_f / w
+// z = Sigma r at one slot (all fields), Sigma = L L^T the centered block for
+// kappa_f = nbar_f / w (the per-l "diag_cl" preconditioner of qcinv's chain,
+// CenteredGibbs.py:282)
 template <int F>
-__global__ void k_pcg_prec(int L, const double* __restrict__ params, const double* __restrict__ rr,
-                           double* __restrict__ z) {
-    const long long NR = (long long)(L + 1) * (L + 1);
-    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g >= NR) return;
-    int l;
-    if (g <= L) l = (int)g;
-    else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
-    const double* p = params + (long long)l * GS_NPARAM;
+__device__ __forceinline__ void pcg_prec_slot(const double* __restrict__ p, const double (&r)[3], double (&z)[3]) {
     if constexpr (F != 3) {
 #pragma unroll
-        for (int f = 0; f < F; ++f) z[f * NR + g] = p[F + f] * p[F + f] * rr[f * NR + g];
+        for (int f = 0; f < F; ++f) z[f] = p[F + f] * p[F + f] * r[f];
     } else {
-        const double r0 = rr[g], r1 = rr[NR + g], r2 = rr[2 * NR + g];
-        const double t0 = p[5] * r0 + p[6] * r1, t1 = p[7] * r1;        // L^T r
-        z[g] = p[5] * t0;
-        z[NR + g] = p[6] * t0 + p[7] * t1;
-        z[2 * NR + g] = p[8] * p[8] * r2;
+        const double t0 = p[5] * r[0] + p[6] * r[1], t1 = p[7] * r[1];        // L^T r
+        z[0] = p[5] * t0;
+        z[1] = p[6] * t0 + p[7] * t1;
+        z[2] = p[8] * p[8] * r[2];
     }
 }
 
-// x += a p ; r -= a q
-__global__ void k_pcg_update(long long n, double a, const double* __restrict__ p, const double* __restrict__ q,
-                             double* __restrict__ x, double* __restrict__ r) {
-    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g >= n) return;
-    x[g] += a * p[g];
-    r[g] -= a * q[g];
-}
-
-// p = z + b p
-__global__ void k_pcg_dir(long long n, double b, const double* __restrict__ z, double* __restrict__ p) {
-    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g < n) p[g] = z[g] + b * p[g];
-}
-
-// fixed-order dot products: out[0] = a.b, out[1] = c.d (per-block partials, then one block)
-__global__ __launch_bounds__(RED_BLOCK) void k_dot2(long long n, const double* __restrict__ a,
-                                                    const double* __restrict__ b, const double* __restrict__ c,
-                                                    const double* __restrict__ d, double* __restrict__ partial) {
-    double s0 = 0.0, s1 = 0.0;
-    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x) {
-        s0 += a[g] * b[g];
-        s1 += c[g] * d[g];
-    }
-    __shared__ double red[2][RED_BLOCK];
-    red[0][threadIdx.x] = s0;
-    red[1][threadIdx.x] = s1;
+// fixed-order block reduction of NV per-thread sums -> partial[block][NV]
+template <int NV>
+__device__ __forceinline__ void block_partial(const double (&v)[NV], double* __restrict__ partial) {
+    __shared__ double red[NV][RED_BLOCK];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[k][threadIdx.x] = v[k];
     __syncthreads();
     for (int h = RED_BLOCK / 2; h > 0; h >>= 1) {
-        if ((int)threadIdx.x < h) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + h];
-            red[1][threadIdx.x] += red[1][threadIdx.x + h];
-        }
+        if ((int)threadIdx.x < h)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + h];
         __syncthreads();
     }
-    if (threadIdx.x == 0) { partial[2 * blockIdx.x] = red[0][0]; partial[2 * blockIdx.x + 1] = red[1][0]; }
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) partial[(long long)blockIdx.x * NSUM + k] = red[k][0];
+}
+
+// q = C^+ x + (b / w) r,  r = complex_to_real(map2alm(N^-1 A b x)); with
+// partial != NULL also the per-block sums of x . q (the CG's p . Q p)
+template <int F>
+__global__ __launch_bounds__(RED_BLOCK) void k_pcg_qdot(int L, const double* __restrict__ dl,
+                                                        const double* __restrict__ bl, const double* __restrict__ x,
+                                                        const double* __restrict__ r_alm, double inv_w,
+                                                        double* __restrict__ out, double* __restrict__ partial,
+                                                        const PcgState* __restrict__ st) {
+    if (st && st->done) return;
+    const long long NR = (long long)(L + 1) * (L + 1);
+    const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    double acc[1] = {0.0};
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nlm; i += (long long)gridDim.x * blockDim.x) {
+        int l, m;
+        cidx_lm(L, i, l, m);
+        const long long r = m == 0 ? l : 2 * i - (L + 1);
+        const int nv = m == 0 ? 1 : 2;
+        const PriorPinv q = prior_pinv<F>(dl, L, l);
+        const double bw = bl[l] * inv_w;
+        for (int c = 0; c < nv; ++c) {
+            double cx[3];
+            if constexpr (F != 3) {
+                cx[0] = q.ie * q.ie * x[r + c];
+                if constexpr (F == 2) cx[1] = q.ib * q.ib * x[NR + r + c];
+            } else {
+                const double xt = x[r + c], xe = x[NR + r + c];
+                const double y0 = q.i00 * xt, y1 = q.t10 * xt + q.i11 * xe;
+                cx[0] = q.i00 * y0 + q.t10 * y1;
+                cx[1] = q.i11 * y1;
+                cx[2] = q.iB * q.iB * x[2 * NR + r + c];
+            }
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+                const double o = cx[f] + r_alm[f * NR + r + c] * bw;
+                out[f * NR + r + c] = o;
+                acc[0] += x[f * NR + r + c] * o;
+            }
+        }
+    }
+    if (partial) block_partial<1>(acc, partial);
+}
+
+// initial residual: z = M r, p = z, per-block sums of (rhs . rhs, r . z, r . r)
+template <int F>
+__global__ __launch_bounds__(RED_BLOCK) void k_pcg_init(int L, const double* __restrict__ params,
+                                                        const double* __restrict__ rhs, const double* __restrict__ rr,
+                                                        double* __restrict__ z, double* __restrict__ pdir,
+                                                        double* __restrict__ partial) {
+    const long long NR = (long long)(L + 1) * (L + 1);
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < NR; g += (long long)gridDim.x * blockDim.x) {
+        int l;
+        if (g <= L) l = (int)g;
+        else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
+        double rv[3] = {0, 0, 0}, zv[3] = {0, 0, 0};
+#pragma unroll
+        for (int f = 0; f < F; ++f) rv[f] = rr[f * NR + g];
+        pcg_prec_slot<F>(params + (long long)l * GS_NPARAM, rv, zv);
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            z[f * NR + g] = zv[f];
+            pdir[f * NR + g] = zv[f];
+            const double b = rhs[f * NR + g];
+            acc[0] += b * b;
+            acc[1] += rv[f] * zv[f];
+            acc[2] += rv[f] * rv[f];
+        }
+    }
+    block_partial<3>(acc, partial);
+}
+
+// x += alpha p; r -= alpha q; z = M r; per-block sums of (r . z, r . r)
+template <int F>
+__global__ __launch_bounds__(RED_BLOCK) void k_pcg_upd(int L, const double* __restrict__ params,
+                                                       const double* __restrict__ p, const double* __restrict__ q,
+                                                       double* __restrict__ x, double* __restrict__ rr,
+                                                       double* __restrict__ z, double* __restrict__ partial,
+                                                       const PcgState* __restrict__ st) {
+    if (st->done) return;
+    const double a = st->alpha;
+    const long long NR = (long long)(L + 1) * (L + 1);
+    double acc[2] = {0.0, 0.0};
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < NR; g += (long long)gridDim.x * blockDim.x) {
+        int l;
+        if (g <= L) l = (int)g;
+        else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
+        double rv[3] = {0, 0, 0}, zv[3] = {0, 0, 0};
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const long long o = f * NR + g;
+            x[o] += a * p[o];
+            rv[f] = rr[o] - a * q[o];
+            rr[o] = rv[f];
+        }
+        pcg_prec_slot<F>(params + (long long)l * GS_NPARAM, rv, zv);
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            z[f * NR + g] = zv[f];
+            acc[0] += rv[f] * zv[f];
+            acc[1] += rv[f] * rv[f];
+        }
+    }
+    block_partial<2>(acc, partial);
+}
+
+// the CG scalars from the block partials (fixed order), on the device:
+// MODE 0 init (bn, rz, rn, done), 1 alpha = rz / p.Qp, 2 beta / rz / rn / it / done
+template <int MODE>
+__global__ __launch_bounds__(RED_BLOCK) void k_pcg_scal(int nblk, const double* __restrict__ partial,
+                                                        PcgState* __restrict__ st, double tol, int maxiter) {
+    if (MODE != 0 && st->done) return;
+    constexpr int NV = MODE == 0 ? 3 : (MODE == 1 ? 1 : 2);
+    double t[NV];
+    block_sums<NV>(nblk, partial, NSUM, t);
+    if (threadIdx.x != 0) return;
+    if constexpr (MODE == 0) {
+        st->bn = sqrt(t[0]);
+        st->rz = t[1];
+        st->rn = sqrt(t[2]);
+        st->tol = tol;
+        st->maxiter = maxiter;
+        st->it = 0;
+        st->alpha = st->beta = 0.0;
+        st->done = (0 < maxiter && st->rn > tol * st->bn) ? 0 : 1;
+    } else if constexpr (MODE == 1) {
+        st->alpha = st->rz / t[0];
+    } else {
+        st->beta = t[0] / st->rz;
+        st->rz = t[0];
+        st->rn = sqrt(t[1]);
+        st->it += 1;
+        st->done = (st->it < st->maxiter && st->rn > st->tol * st->bn) ? 0 : 1;
+    }
+}
+
+// p = z + beta p (after the iteration's last scalar update)
+__global__ void k_pcg_dir(long long n, const PcgState* __restrict__ st, const double* __restrict__ z,
+                          double* __restrict__ p) {
+    if (st->done) return;
+    const double b = st->beta;
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x)
+        p[g] = z[g] + b * p[g];
 }
 
 __global__ __launch_bounds__(RED_BLOCK) void k_dot2_finish(int nblk, const double* __restrict__ partial,
@@ -502,6 +597,12 @@ __global__ __launch_bounds__(RED_BLOCK) void k_dot2_finish(int nblk, const doubl
         out[0] = t[0];
         out[1] = t[1];
     }
+}
+
+// y = a - y (the residual of an initial guess)
+__global__ void k_sub_from(long long n, const double* __restrict__ a, double* __restrict__ y) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g < n) y[g] = a[g] - y[g];
 }
 
 // ---------------------------------------------------------------------------
@@ -896,6 +997,8 @@ struct gs_masked {
     double *grad0 = nullptr, *grad1 = nullptr, *snew = nullptr, *pix0 = nullptr, *pix1 = nullptr, *vtmp = nullptr;
     double *partial = nullptr, *lr = nullptr;
     double *pr = nullptr, *pz = nullptr, *pp = nullptr, *pq = nullptr, *params_pcg = nullptr, *dots = nullptr;
+    double* pcgs = nullptr;          // PcgState of the device CG
+    int pcg_syncs = 0;               // host synchronisations of the last solve
     // f2 block MH workspace (allocated on first use, grown as needed)
     double *f2_da = nullptr, *f2_r = nullptr, *f2_Y = nullptr, *f2_phib = nullptr, *f2_part = nullptr,
            *f2_G = nullptr, *f2_taken = nullptr;
@@ -909,7 +1012,7 @@ void mc_free(gs_masked* c) {
     if (c->sht) gs_sht_destroy(c->sht);
     double* bufs[] = {c->bl, c->dpix, c->ninv, c->g2, c->params, c->params_mala, c->x, c->Abs, c->y, c->r,
                       c->grad0, c->grad1, c->snew, c->pix0, c->pix1, c->vtmp, c->partial, c->lr,
-                      c->pr, c->pz, c->pp, c->pq, c->params_pcg, c->dots, c->f2_da, c->f2_r, c->f2_Y,
+                      c->pr, c->pz, c->pp, c->pq, c->params_pcg, c->dots, c->pcgs, c->f2_da, c->f2_r, c->f2_Y,
                       c->f2_phib, c->f2_part, c->f2_G, c->f2_taken};
     for (double* b : bufs)
         if (b) (void)hipFree(b);
@@ -1047,6 +1150,7 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     rc |= mc_alloc(&c->pq, FR);
     rc |= mc_alloc(&c->params_pcg, (size_t)(c->L + 1) * GS_NPARAM);
     rc |= mc_alloc(&c->dots, 2);
+    rc |= mc_alloc(&c->pcgs, 8);
     if (rc) { mc_free(c); return -1; }
     std::vector<int> e2b((size_t)4 * (c->L + 1));
     for (int sp = 0; sp < 4; ++sp)
@@ -1114,29 +1218,20 @@ int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* 
 }
 
 // ---- f1 PCG ----------------------------------------------------------------
-static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, hipStream_t st) {
+// A Q p without its dot product (partial == nullptr) or with the per-block p . Q p
+static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, double* partial, int nb,
+                     const PcgState* state, hipStream_t st) {
     if (mc_synth(c, x, c->pix0, st)) return -1;
     const long long n = c->F * c->npix;
     hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->ninv, c->pix0, c->y);
     GS_LAUNCH_CHECK("k_mc_mul");
     if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
-    const dim3 g(nblocks(c->nlm, 256)), b(256);
-    if (c->F == 1) hipLaunchKernelGGL(k_pcg_qfinish<1>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
-    else if (c->F == 2) hipLaunchKernelGGL(k_pcg_qfinish<2>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
-    else hipLaunchKernelGGL(k_pcg_qfinish<3>, g, b, 0, st, c->L, dl, c->bl, x, c->r, 1.0 / c->w, out);
-    GS_LAUNCH_CHECK("k_pcg_qfinish");
-    return 0;
-}
-
-static int pcg_dots(gs_masked* c, const double* a, const double* b, const double* d, const double* e, double* host2,
-                    hipStream_t st) {
-    const long long n = c->F * c->NR;
-    const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
-    hipLaunchKernelGGL(k_dot2, dim3(nb), dim3(RED_BLOCK), 0, st, n, a, b, d, e, c->partial);
-    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(RED_BLOCK), 0, st, nb, c->partial, c->dots);
-    GS_LAUNCH_CHECK("k_dot2");
-    GS_CHECK(hipMemcpyAsync(host2, c->dots, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
-    GS_CHECK(hipStreamSynchronize(st));
+    const dim3 g(partial ? nb : nblocks(c->nlm, RED_BLOCK)), b(RED_BLOCK);
+    const double iw = 1.0 / c->w;
+    if (c->F == 1) hipLaunchKernelGGL(k_pcg_qdot<1>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);
+    else if (c->F == 2) hipLaunchKernelGGL(k_pcg_qdot<2>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);
+    else hipLaunchKernelGGL(k_pcg_qdot<3>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);
+    GS_LAUNCH_CHECK("k_pcg_qdot");
     return 0;
 }
 
@@ -1167,58 +1262,91 @@ int gs_masked_pcg_rhs(gs_masked* c, const double* dl, const double* zv, const do
     return 0;
 }
 
+// Preconditioned CG on the device.  One iteration = A Q p (two SHTs) with the
+// fused p . Q p partials, alpha on the device, the fused update / preconditioner
+// / (r . z, r . r) pass, beta / rz / rn / convergence on the device, the new
+// direction.  Every kernel reads the scalars from the device state and returns
+// at once after convergence, so the host launches whole batches of iterations
+// and reads the state once per batch: the batch length follows the residual's
+// observed decay (the predicted remaining iterations, 1..64), so an extra batch
+// costs one stream synchronisation and an overshoot at most a few iterations'
+// transforms -- never one host round trip per iteration (the qcinv loop,
+// CenteredGibbs.py:484-488, and this build's r02 form both synchronised per
+// iteration).
 int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
                         int maxiter, int* iters, double* rel_residual, void* stream) {
     if (!c) return set_error("null masked context");
     if (!dl || !rhs || !x) return set_error("gs_masked_pcg_solve: null argument");
+    if (maxiter < 0) return set_error("gs_masked_pcg_solve: maxiter < 0");
     const hipStream_t st = S(stream);
     const long long n = c->F * c->NR;
+    PcgState* dst = reinterpret_cast<PcgState*>(c->pcgs);
     // preconditioner: centered per-l block with kappa_f = nbar_f / w ("diag_cl")
     double kap[3] = {0, 0, 0};
     for (int k = 0; k < c->F; ++k) kap[k] = c->nbar[c->rows.r[k]] / c->w;
     if (mc_params(c, dl, kap, c->params_pcg, st)) return -1;
+    const int nb = (int)std::min<long long>(c->nblk, nblocks(c->nlm, RED_BLOCK));
     if (x_is_guess) {
-        if (pcg_apply(c, dl, x, c->pq, st)) return -1;
-        hipLaunchKernelGGL(k_pcg_dir, dim3(nblocks(n, 256)), dim3(256), 0, st, n, -1.0, rhs, c->pq);   // pq = rhs - Qx
-        GS_CHECK(hipMemcpyAsync(c->pr, c->pq, n * sizeof(double), hipMemcpyDeviceToDevice, st));
+        if (pcg_apply(c, dl, x, c->pr, nullptr, 0, nullptr, st)) return -1;
+        hipLaunchKernelGGL(k_sub_from, dim3(nblocks(n, 256)), dim3(256), 0, st, n, rhs, c->pr);   // r = rhs - Qx
+        GS_LAUNCH_CHECK("k_sub_from");
     } else {
         GS_CHECK(hipMemsetAsync(x, 0, n * sizeof(double), st));
         GS_CHECK(hipMemcpyAsync(c->pr, rhs, n * sizeof(double), hipMemcpyDeviceToDevice, st));
     }
-    const dim3 gp(nblocks(c->NR, 256)), b(256);
-    auto prec = [&](const double* r, double* z) -> int {
-        if (c->F == 1) hipLaunchKernelGGL(k_pcg_prec<1>, gp, b, 0, st, c->L, c->params_pcg, r, z);
-        else if (c->F == 2) hipLaunchKernelGGL(k_pcg_prec<2>, gp, b, 0, st, c->L, c->params_pcg, r, z);
-        else hipLaunchKernelGGL(k_pcg_prec<3>, gp, b, 0, st, c->L, c->params_pcg, r, z);
-        GS_LAUNCH_CHECK("k_pcg_prec");
+    const dim3 gb(nb), bb(RED_BLOCK);
+#define GS_PI(FF) hipLaunchKernelGGL((k_pcg_init<FF>), gb, bb, 0, st, c->L, c->params_pcg, rhs, c->pr, c->pz, c->pp, \
+                                     c->partial)
+    if (c->F == 1) GS_PI(1); else if (c->F == 2) GS_PI(2); else GS_PI(3);
+#undef GS_PI
+    hipLaunchKernelGGL(k_pcg_scal<0>, dim3(1), bb, 0, st, nb, c->partial, dst, tol, maxiter);
+    GS_LAUNCH_CHECK("k_pcg_init");
+    auto iteration = [&]() -> int {
+        if (pcg_apply(c, dl, c->pp, c->pq, c->partial, nb, dst, st)) return -1;
+        hipLaunchKernelGGL(k_pcg_scal<1>, dim3(1), bb, 0, st, nb, c->partial, dst, tol, maxiter);
+#define GS_PU(FF) hipLaunchKernelGGL((k_pcg_upd<FF>), gb, bb, 0, st, c->L, c->params_pcg, c->pp, c->pq, x, c->pr, \
+                                     c->pz, c->partial, dst)
+        if (c->F == 1) GS_PU(1); else if (c->F == 2) GS_PU(2); else GS_PU(3);
+#undef GS_PU
+        hipLaunchKernelGGL(k_pcg_scal<2>, dim3(1), bb, 0, st, nb, c->partial, dst, tol, maxiter);
+        hipLaunchKernelGGL(k_pcg_dir, dim3(nb), bb, 0, st, n, dst, c->pz, c->pp);
+        GS_LAUNCH_CHECK("pcg iteration");
         return 0;
     };
-    if (prec(c->pr, c->pz)) return -1;
-    GS_CHECK(hipMemcpyAsync(c->pp, c->pz, n * sizeof(double), hipMemcpyDeviceToDevice, st));
-    double d2[2];
-    if (pcg_dots(c, rhs, rhs, c->pr, c->pz, d2, st)) return -1;
-    const double bn = sqrt(d2[0]);
-    double rz = d2[1];
-    if (pcg_dots(c, c->pr, c->pr, c->pr, c->pr, d2, st)) return -1;
-    double rn = sqrt(d2[0]);
-    int it = 0;
-    while (it < maxiter && rn > tol * bn) {
-        if (pcg_apply(c, dl, c->pp, c->pq, st)) return -1;
-        if (pcg_dots(c, c->pp, c->pq, c->pp, c->pq, d2, st)) return -1;
-        const double alpha = rz / d2[0];
-        hipLaunchKernelGGL(k_pcg_update, dim3(nblocks(n, 256)), dim3(256), 0, st, n, alpha, c->pp, c->pq, x, c->pr);
-        GS_LAUNCH_CHECK("k_pcg_update");
-        if (prec(c->pr, c->pz)) return -1;
-        if (pcg_dots(c, c->pr, c->pz, c->pr, c->pr, d2, st)) return -1;
-        const double beta = d2[0] / rz;
-        rz = d2[0];
-        rn = sqrt(d2[1]);
-        hipLaunchKernelGGL(k_pcg_dir, dim3(nblocks(n, 256)), dim3(256), 0, st, n, beta, c->pz, c->pp);
-        GS_LAUNCH_CHECK("k_pcg_dir");
-        ++it;
+    PcgState h{};
+    auto read_state = [&]() -> int {
+        GS_CHECK(hipMemcpyAsync(&h, dst, sizeof(PcgState), hipMemcpyDeviceToHost, st));
+        GS_CHECK(hipStreamSynchronize(st));
+        return 0;
+    };
+    if (read_state()) return -1;
+    int launched = 0, batch = 8;
+    double rn_prev = h.rn;
+    c->pcg_syncs = 1;
+    while (!h.done && launched < maxiter) {
+        const int k = std::max(1, std::min(batch, maxiter - launched));
+        for (int j = 0; j < k; ++j)
+            if (iteration()) return -1;
+        launched += k;
+        if (read_state()) return -1;
+        ++c->pcg_syncs;
+        if (h.done) break;
+        // predicted remaining iterations from the residual's decay over this batch
+        const double rate = rn_prev > 0.0 && h.rn > 0.0 ? std::pow(h.rn / rn_prev, 1.0 / k) : 0.5;
+        const double want = h.tol * h.bn;
+        double rem = 64.0;
+        if (rate < 1.0 && rate > 0.0 && h.rn > want) rem = std::log(want / h.rn) / std::log(rate);
+        batch = (int)std::max(1.0, std::min(64.0, std::floor(rem)));
+        rn_prev = h.rn;
     }
-    if (iters) *iters = it;
-    if (rel_residual) *rel_residual = bn > 0 ? rn / bn : 0.0;
+    if (iters) *iters = h.it;
+    if (rel_residual) *rel_residual = h.bn > 0 ? h.rn / h.bn : 0.0;
+    return 0;
+}
+
+int gs_masked_pcg_info(const gs_masked* c, int* host_syncs) {
+    if (!c) return set_error("null masked context");
+    if (host_syncs) *host_syncs = c->pcg_syncs;
     return 0;
 }
 

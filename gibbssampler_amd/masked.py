@@ -51,6 +51,7 @@ class MaskedCR:
         self.n_gibbs, self.alpha, self.tau = int(n_gibbs), float(alpha), float(tau)
         self.pcg_accuracy, self.pcg_maxiter = float(pcg_accuracy), int(pcg_maxiter)   # CenteredGibbs.py:279-283
         self.pcg_iterations = []
+        self.pcg_syncs = []
         if rng not in ("replay", "native"):
             raise ValueError(rng)
         self.rng, self.seed, self.chain = rng, int(seed), int(chain)
@@ -213,6 +214,9 @@ class MaskedCR:
                     "gs_masked_pcg_solve")
         self.pcg_iterations.append(iters.value)
         self.pcg_residual = res.value
+        syncs = ctypes.c_int()
+        _capi.check(self.lib.gs_masked_pcg_info(self.handle, ctypes.byref(syncs)), "gs_masked_pcg_info")
+        self.pcg_syncs.append(syncs.value)          # host synchronisations of this solve (one per batch)
         return x
 
     def tt_fullsky(self, dl, noncentered=False, iteration=None, out=None):

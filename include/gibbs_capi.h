@@ -280,12 +280,15 @@ int gs_masked_cr(gs_masked* ctx, int kind, const double* dl, double* s, double* 
  * + C^-1/2 z_slot; solve (C^+ + b A^T N^-1 A b) x = rhs by preconditioned CG
  * (per-l preconditioner (C^+ + b^2 nbar/w)^-1) until |r| <= tol |rhs|.
  * zv [F][Npix], zs [F][NR]: replay normals (reference order z_Q, z_U, z_E,
- * z_B) or NULL for the native streams.  The solve synchronises the stream once
- * per CG iteration (convergence test on the host). */
+ * z_B) or NULL for the native streams.  The CG recurrence's scalars stay on
+ * the device; the host launches batches of iterations sized from the residual's
+ * decay and synchronises once per batch (no host round trip per iteration).
+ * gs_masked_pcg_info: host synchronisations of the last solve. */
 int gs_masked_pcg_rhs(gs_masked* ctx, const double* dl, const double* zv, const double* zs, uint64_t seed,
                       uint32_t iteration, int chain, double* rhs, void* stream);
 int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
                         int maxiter, int* iters, double* rel_residual, void* stream);
+int gs_masked_pcg_info(const gs_masked* ctx, int* host_syncs);
 /* f2: pixel-domain non-centered likelihood (NonCenteredGibbs.py:333-355):
  * lik = -1/2 sum_pix N^-1 (d - A b C^1/2(D) s_nc)^2 (device double).
  * gs_masked_center: out = C^1/2 in (dir = +1) or C^+1/2 in (dir = -1) per slot
