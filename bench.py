@@ -129,6 +129,31 @@ def cpu_baseline_child(args):
                                             f"GPU's per-l statistics (oracle/cpu_baseline.py nc_iteration_matched)"}}
 
 
+def cpu_baseline_masked_child(args):
+    """The masked workloads' CPU leg (oracle/cpu_baseline_masked.py: the reference's
+    masked samplers with the C++/OpenMP HEALPix SHT of oracle/sht_cpu.cpp on
+    min(affinity, 16) threads), run as a child process before this process
+    touches the GPU; a PCG workload's rate is completed with the device solve's
+    CG iteration count after the timed region (cpu_baseline_masked.finalize)."""
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "oracle.cpu_baseline_masked", "--workload", args.workload, "--nside", str(args.nside),
+           "--lmax", str(args.lmax)]
+    try:
+        # stderr passes through: the child's progress lines keep a long CPU leg visible
+        out = subprocess.run(cmd, cwd=HERE, env=env, stdout=subprocess.PIPE, text=True, timeout=900, check=True)
+        return json.loads(out.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        print(f"masked cpu baseline failed: {e}", file=sys.stderr)
+        return None
+
+
+def _finalize_cpu(cpu, cg_iters=None):
+    if cpu is None:
+        return None
+    from oracle.cpu_baseline_masked import finalize
+    return finalize(cpu, cg_iters)
+
+
 def main():
     args = parse()
     from gibbssampler_amd.distributed import ShardContext, dist_env
@@ -136,8 +161,11 @@ def main():
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
     cpu = None
-    if rank == 0 and world == 1 and args.workload == "noncentered" and not args.no_cpu_baseline:
-        cpu = cpu_baseline_child(args)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if args.workload == "noncentered":
+            cpu = cpu_baseline_child(args)
+        elif args.workload == "masked" or args.workload in MASKED_HEAD:
+            cpu = cpu_baseline_masked_child(args)
     import torch
     torch.cuda.set_device(local)
     ctx = ShardContext(args.nchains, backend="nccl")
@@ -151,9 +179,9 @@ def main():
         elif args.workload in SURFACE:
             line = run_surface(args, ctx)
         elif args.workload == "masked":
-            line = run_masked(args, ctx)
+            line = run_masked(args, ctx, cpu)
         else:
-            line = run_masked_head(args, ctx)
+            line = run_masked_head(args, ctx, cpu)
         if ctx.rank == 0:
             print(json.dumps(line))
     finally:
@@ -325,7 +353,7 @@ def _masked_data(N, L, nfields, seed=0):
     return d, mask, dl
 
 
-def run_masked(args, ctx):
+def run_masked(args, ctx, cpu=None):
     """BASELINE configs[4]: CenteredGibbs TEB, masked (f_sky 0.8), aux-variable CR
     with n_gibbs = 1 (a9, TEB) + inverse-Wishart / inverse-Gamma C_l draw, one
     chain per GPU.  Per iteration: b s -> alm2map (TEB) -> v | s -> map2alm
@@ -405,12 +433,12 @@ def run_masked(args, ctx):
                      "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFS, 4),
                      "traffic": None, "algorithmic_flops_per_launch": fl,
                      "avg_launch_ms": {"alm2map": round(t_syn, 3), "map2alm": round(t_ana, 3)}},
-        "cpu_baseline": None,
-        "notes": "healpy is absent, so no CPU SHT baseline at this size; see DESIGN.md",
+        "cpu_baseline": _finalize_cpu(cpu),
+        "notes": "healpy is absent: the CPU leg's transforms are oracle/sht_cpu.cpp (C++/OpenMP); see DESIGN.md",
     }
 
 
-def run_masked_head(args, ctx):
+def run_masked_head(args, ctx, cpu=None):
     """HEAD's real run modes (main_polarization.py:109-126,154) through the
     drop-in class surface, EB, one chain per GPU, N_side 256 / L 512 with the
     reference's Planck BB bins and 1 + 134 Metropolis blocks (config.py:45-55):
@@ -514,9 +542,9 @@ def run_masked_head(args, ctx):
                      "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP64_VALU_PEAK_TFS, 4), "traffic": None,
                      "algorithmic_flops_per_step": fl},
-        "cpu_baseline": None,
+        "cpu_baseline": _finalize_cpu(cpu, pcg_info["cg_iterations_per_solve"] if pcg_info else None),
         "pcg": pcg_info,
-        "notes": "healpy is absent: no CPU SHT baseline for the masked modes (DESIGN.md 7)",
+        "notes": "healpy is absent: the CPU leg's transforms are oracle/sht_cpu.cpp (C++/OpenMP) (DESIGN.md 7)",
     }
 
 

@@ -88,8 +88,11 @@ class MaskedModel:
     maps: [3, Npix] (T, Q, U); inv_noise: [3, Npix] mask-multiplied N^-1
     (T row ignored for nfields = 2)."""
 
-    def __init__(self, L, nside, nfields, bl, maps, inv_noise, mu_eps=1e-14, adj_iter=0):
+    def __init__(self, L, nside, nfields, bl, maps, inv_noise, mu_eps=1e-14, adj_iter=0, sht=None):
         self.L, self.nside, self.F = int(L), int(nside), int(nfields)
+        # the transform module (alm2map / map2alm with oracle.sht's interface): the
+        # dense oracle by default; oracle.sht_cpu for the CPU baseline at full size
+        self.sht = O if sht is None else sht
         self.adj_iter = int(adj_iter)
         self.Npix = 12 * self.nside ** 2
         self.w = FOURPI / self.Npix
@@ -110,21 +113,21 @@ class MaskedModel:
         """maps of b * s (s real layout [F, NR]) -> [F, Npix] for the field rows."""
         ls = O._cidx(self.L)[0]
         if self.F == 1:          # temperature only: the spin-0 transform alone
-            return O.alm2map(H.real_to_complex(s_real[0], self.L) * self.bl[ls], self.nside, self.L)[None]
+            return self.sht.alm2map(H.real_to_complex(s_real[0], self.L) * self.bl[ls], self.nside, self.L)[None]
         a = np.zeros((3, ls.shape[0]), dtype=np.complex128)
         for k, r in enumerate(self.rows):
             a[r] = H.real_to_complex(s_real[k], self.L) * self.bl[ls]
-        m = O.alm2map(a, self.nside, self.L)
+        m = self.sht.alm2map(a, self.nside, self.L)
         return np.stack([m[r] for r in self.rows])
 
     def analysis(self, mp, iter=0):
         """complex_to_real(map2alm(maps, iter)) for the field rows: [F, NR]."""
         if self.F == 1:          # temperature only: the spin-0 transform alone
-            return H.complex_to_real(O.map2alm(np.asarray(mp)[0], self.nside, self.L, iter=iter), self.L)[None]
+            return H.complex_to_real(self.sht.map2alm(np.asarray(mp)[0], self.nside, self.L, iter=iter), self.L)[None]
         full = np.zeros((3, self.Npix))
         for k, r in enumerate(self.rows):
             full[r] = mp[k]
-        a = O.map2alm(full, self.nside, self.L, iter=iter)
+        a = self.sht.map2alm(full, self.nside, self.L, iter=iter)
         return np.stack([H.complex_to_real(a[r], self.L) for r in self.rows])
 
     def second_part_grad(self):
@@ -318,7 +321,7 @@ def pcg_fluctuation(mm, dl_unbinned, z_pix, z_slot):
     full = np.zeros((3, mm.Npix))
     for k, r in enumerate(mm.rows):
         full[r] = y[k]
-    a = O.map2alm(full, mm.nside, mm.L, iter=3)
+    a = mm.sht.map2alm(full, mm.nside, mm.L, iter=3)
     adj = np.stack([H.complex_to_real(a[r], mm.L) for r in mm.rows]) * (mm.Npix / FOURPI)
     return adj * mm.bl[mm.slot_ell][None] + _prior_pinv_apply(mm, dl_unbinned, z_slot, half=True)
 

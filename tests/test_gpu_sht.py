@@ -304,3 +304,29 @@ def test_ring_stage_merged_and_per_class_vs_oracle(monkeypatch, merge, N, L):
     wa = _oracle_alm(maps, N, L, 3, 0)
     ga = sht.map2alm(torch.from_numpy(maps).cuda(), iter=0, layout="complex", ncomp=3).cpu().numpy().reshape(3, -1)
     np.testing.assert_allclose(ga, wa, rtol=0, atol=1e-11 * np.abs(wa).max())
+
+
+@pytest.mark.parametrize("N,L,comps", [(256, 512, 2), (512, 1024, 3)])
+def test_cpu_baseline_sht_equals_device(N, L, comps):
+    """The CPU baseline's transforms (oracle/sht_cpu.cpp: own FFTs and scaled
+    recurrence) equal the device SHT at the masked workloads' sizes (1e-10
+    relative, both directions): the CPU leg computes the same transform."""
+    torch = _torch()
+    from gibbssampler_amd.sht import HealpixSHT
+    from oracle import sht_cpu as C
+    nc = 3 if comps == 3 else 2
+    sht = HealpixSHT(N, L)
+    rng = np.random.default_rng(N)
+    a = np.zeros((3, (L + 1) * (L + 2) // 2), dtype=np.complex128)
+    ls, ms = O._cidx(L)
+    a[3 - nc:] = rng.normal(size=(nc, len(ls))) + 1j * rng.normal(size=(nc, len(ls)))
+    a[:, ms == 0] = a[:, ms == 0].real
+    a[1:, ls < 2] = 0
+    dev = sht.alm2map(torch.from_numpy(a).cuda(), ncomp=3, layout="complex").cpu().numpy()
+    cpu = C.alm2map(a[3 - nc:], N, L, comps=comps)
+    np.testing.assert_allclose(cpu, dev[3 - nc:], rtol=0, atol=1e-10 * np.abs(dev).max())
+    mp = rng.normal(size=(3, 12 * N * N))
+    mp[: 3 - nc] = 0.0
+    dev = sht.map2alm(torch.from_numpy(mp).cuda(), iter=0, layout="complex", ncomp=3).cpu().numpy()
+    cpu = C.map2alm(mp[3 - nc:], N, L, comps=comps)
+    np.testing.assert_allclose(cpu, dev[3 - nc:], rtol=0, atol=1e-10 * np.abs(dev).max())
