@@ -7,6 +7,8 @@ Variants (debug builds):
     -fsanitize=address; device code unchanged) for the plan-building and
     argument-validation paths; -> libgibbs_hip_asan.so, loaded with the clang
     ASan runtime preloaded (tests/test_capi_asan.py)
+  * ``variant="timeline"``: -DGS_MH_TIMELINE -- s_memrealtime stamps at the
+    MH kernel's stage boundaries (gs_debug_mh_timeline; tools/mh_timeline.py)
 Select a variant at run time with GIBBS_HIP_LIB=<path>.
 """
 import glob
@@ -31,6 +33,7 @@ COMMON = ["-ffp-contract=on"]
 VARIANTS = {
     None: (LIB, ["-O3"] + COMMON),
     "debug": (os.path.join(HERE, "libgibbs_hip_debug.so"), ["-O3", "-DGS_DEBUG"] + COMMON),
+    "timeline": (os.path.join(HERE, "libgibbs_hip_timeline.so"), ["-O3", "-DGS_MH_TIMELINE"] + COMMON),
     "asan": (os.path.join(HERE, "libgibbs_hip_asan.so"),
              ["-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", "-fsanitize=address", "-shared-libasan"] + COMMON),
 }

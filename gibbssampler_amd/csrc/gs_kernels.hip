@@ -61,6 +61,9 @@ struct gs_plan {
     // the latency form of the sweep (all loads first) may be used for short tasks;
     // GS_SWEEP_THROUGHPUT at plan creation forces the throughput form (A/B timing)
     bool sweep_latency = true;
+    // the register / LDS-resident MH kernel where it fits (GS_MH_FUSED at plan
+    // creation: the older k_mh_fused, for A/B timing)
+    bool mh_reg = true;
     // MH phases: spectra whose blocks are mutually independent run in one launch
     int nphase = 0;
     int phase_n[4] = {0, 0, 0, 0};
@@ -535,23 +538,14 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
 }
 
-// fixed-order reduction of the sweep partials: stats[chain][q][l].  One
-// workgroup per (chain, statistic, tile): wave w sums chunks w, w + 4, ... of
-// the tile's 64 l (lanes; coalesced rows of the partials), four loads in
-// flight, then the four wave sums in wave order -- the same order for any
-// batch size, so every chain's trajectory is bit-identical for any chain
-// count or GPU count
+// one wave's share of a (chain, statistic, tile) finish: the sum of chunks w,
+// w + 4, ... of the tile's 64 l (lanes; coalesced rows of the partials)
 template <int G>
-__global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int ntile, int nchunkg, int tm, int nstat,
-                                                      const double* __restrict__ partials,
-                                                      double* __restrict__ stats) {
-    const int t = blockIdx.x % ntile;
-    const int q = (blockIdx.x / ntile) % nstat;
-    const int chain = blockIdx.x / (ntile * nstat);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int Lp1 = L + 1;
+__device__ __forceinline__ double stats_finish_sum(int L, int ntile, int nchunkg, int tm, int nstat,
+                                                   const double* __restrict__ partials, int chain, int q, int t,
+                                                   int w, int lane) {
     const int cmax = (L - WAVE * t) / tm;               // last chunk of tile t
-    GS_ASSERT(chain < nchains && cmax < nchunkg);
+    GS_ASSERT(cmax < nchunkg);
     const double* pp = partials + ((long long)chain * ntile + t) * nchunkg * nstat * WAVE + q * WAVE + lane;
     const long long cs = (long long)nstat * WAVE;
     // groups of G of this wave's chunks, every load of a group issued before
@@ -584,6 +578,25 @@ __global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int nt
                 if (c + 4 * j <= cmax) acc += v[j];
         }
     }
+    return acc;
+}
+
+// fixed-order reduction of the sweep partials: stats[chain][q][l].  One
+// workgroup per (chain, statistic, tile): wave w sums chunks w, w + 4, ... of
+// the tile's 64 l, then the four wave sums in wave order -- the same order for
+// any batch size, so every chain's trajectory is bit-identical for any chain
+// count or GPU count
+template <int G>
+__global__ __launch_bounds__(256) void k_stats_finish(int L, int nchains, int ntile, int nchunkg, int tm, int nstat,
+                                                      const double* __restrict__ partials,
+                                                      double* __restrict__ stats) {
+    const int t = blockIdx.x % ntile;
+    const int q = (blockIdx.x / ntile) % nstat;
+    const int chain = blockIdx.x / (ntile * nstat);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int Lp1 = L + 1;
+    GS_ASSERT(chain < nchains);
+    const double acc = stats_finish_sum<G>(L, ntile, nchunkg, tm, nstat, partials, chain, q, t, w, lane);
     __shared__ double red[4][WAVE];
     red[w][lane] = acc;
     __syncthreads();
@@ -783,23 +796,24 @@ __device__ __forceinline__ double log_ndtr(double x) {
     return log(0.5 * erfcx(t)) - t * t;
 }
 
-// per-l log-likelihood term without the constant S_dd (NonCenteredGibbs.py:357-377)
+// per-l log-likelihood term without the constant S_dd (NonCenteredGibbs.py:357-377),
+// from this l's statistics sv[q] = stats[q][l]
 template <int F>
-__device__ __forceinline__ double f_ell(const double* __restrict__ st, int Lp1, int l, double b, double k0, double k1,
-                                        double k2, double v0, double v1, double v2, double v3) {
+__device__ __forceinline__ double f_ell_v(const double (&sv)[SweepAcc<F>::NS], double b, double k0, double k1,
+                                          double k2, double v0, double v1, double v2, double v3) {
     if constexpr (F == 1) {
         const double a = sqrt(v0);
-        return -0.5 * k0 * (-2.0 * b * (a * st[1 * Lp1 + l]) + b * b * (a * a * st[0 * Lp1 + l]));
+        return -0.5 * k0 * (-2.0 * b * (a * sv[1]) + b * b * (a * a * sv[0]));
     } else if constexpr (F == 2) {
         const double aE = sqrt(v0), aB = sqrt(v1);
-        const double fE = -0.5 * k0 * (-2.0 * b * (aE * st[2 * Lp1 + l]) + b * b * (aE * aE * st[0 * Lp1 + l]));
-        const double fB = -0.5 * k1 * (-2.0 * b * (aB * st[3 * Lp1 + l]) + b * b * (aB * aB * st[1 * Lp1 + l]));
+        const double fE = -0.5 * k0 * (-2.0 * b * (aE * sv[2]) + b * b * (aE * aE * sv[0]));
+        const double fB = -0.5 * k1 * (-2.0 * b * (aB * sv[3]) + b * b * (aB * aB * sv[1]));
         return fE + fB;
     } else {
         // v0..v3 = TT, EE, BB, TE
         const CovChol A = cov_chol_teb(v0, v1, v3, v2);
-        const double ssTT = st[0 * Lp1 + l], ssEE = st[1 * Lp1 + l], ssBB = st[2 * Lp1 + l], ssTE = st[3 * Lp1 + l];
-        const double dTsT = st[4 * Lp1 + l], dEsT = st[5 * Lp1 + l], dEsE = st[6 * Lp1 + l], dBsB = st[7 * Lp1 + l];
+        const double ssTT = sv[0], ssEE = sv[1], ssBB = sv[2], ssTE = sv[3];
+        const double dTsT = sv[4], dEsT = sv[5], dEsE = sv[6], dBsB = sv[7];
         const double fT = -0.5 * k0 * (-2.0 * b * (A.a00 * dTsT) + b * b * (A.a00 * A.a00 * ssTT));
         const double linE = A.a10 * dEsT + A.a11 * dEsE;
         const double quadE = A.a10 * A.a10 * ssTT + A.a10 * A.a11 * ssTE + A.a11 * A.a10 * ssTE + A.a11 * A.a11 * ssEE;
@@ -807,6 +821,15 @@ __device__ __forceinline__ double f_ell(const double* __restrict__ st, int Lp1, 
         const double fB = -0.5 * k2 * (-2.0 * b * (A.aB * dBsB) + b * b * (A.aB * A.aB * ssBB));
         return fT + fE + fB;
     }
+}
+
+template <int F>
+__device__ __forceinline__ double f_ell(const double* __restrict__ st, int Lp1, int l, double b, double k0, double k1,
+                                        double k2, double v0, double v1, double v2, double v3) {
+    double sv[SweepAcc<F>::NS];
+#pragma unroll
+    for (int q = 0; q < SweepAcc<F>::NS; ++q) sv[q] = st[q * Lp1 + l];
+    return f_ell_v<F>(sv, b, k0, k1, k2, v0, v1, v2, v3);
 }
 
 __device__ __forceinline__ bool psd_ok(double tt, double ee, double te) {
@@ -1215,6 +1238,383 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     if (epi.counter) ticket_advance(epi.counter, gridDim.x, epi.adv);
 }
 
+// The MH phases with every global load issued once, at the start (r03): each
+// thread owns one multipole l = lmin + tid and keeps that l's statistics, beam,
+// l -> bin and l -> block indices in registers for the whole kernel; the
+// chain's D_l, proposals, proposal log ratios and log accept uniforms are
+// staged in LDS in the same round of loads (log u taken once, not per
+// decision), and so is each thread's first narrow block per phase.  The phases
+// then run on registers and LDS alone (no memory latency inside a phase):
+//  * per-l terms: the likelihood is separable into the TE-block part
+//    f_TE(TT, EE, TE) and the B part f_B(BB) (F = 3; F = 2: f_E + f_B), so a
+//    proposal's difference is taken on its own part, g = f_part(new) -
+//    f_part(old) (k_mh_fused differenced the whole per-l sum);
+//  * wide blocks: one wave per block, lane-strided sums in l order and a
+//    fixed-order butterfly (permlane swaps + DPP rotations) that leaves the
+//    total on every lane -- no workgroup barrier inside a phase; narrow blocks
+//    (one thread each) run beside them (disjoint bins).
+// Decisions are the reference's (NonCenteredGibbs.py:427-442); the sums differ
+// from k_mh_fused's only in rounding order.  k_mh_fused stays for plans whose
+// l range exceeds one l per thread or whose arrays exceed the LDS.
+//
+// this thread's l -> bin / l -> block index of a spectrum (runtime sp): packed
+// 16 bits per spectrum (value + 1) in one 64-bit word, so selecting by sp is a
+// shift, not a dynamically indexed (scratch) register array
+__device__ __forceinline__ int unpack16(uint64_t w, int sp) { return (int)((w >> (16 * sp)) & 0xFFFFu) - 1; }
+
+constexpr int MH_REG_THREADS = 1024;
+
+// the graph-step tail of an MH launch: this chain's D_l into the trace (each
+// thread re-reads the D_l words it just wrote) and the device counter advance
+// by the last of the nblk MH workgroups
+__device__ __forceinline__ void mh_epilogue(const MhEpi& epi, uint32_t iter, int chain, int nrow,
+                                            const double* __restrict__ dl, unsigned nblk) {
+    if (epi.trace) {
+        const long long slot = (long long)((iter + (uint32_t)epi.cap - 1u) % (uint32_t)epi.cap);
+        double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
+        const double* D = dl + (long long)chain * nrow;
+        for (int k = threadIdx.x; k < nrow; k += blockDim.x) tr[k] = D[k];
+    }
+    if (epi.counter) ticket_advance(epi.counter, nblk, epi.adv);
+}
+
+// diagnostic timeline of the MH body (build variant "timeline", -DGS_MH_TIMELINE):
+// thread 0 of chain 0's MH workgroup stamps s_memrealtime (100 MHz) at the
+// stage boundaries
+#if defined(GS_MH_TIMELINE)
+__device__ unsigned long long g_mh_tl[32];
+#define GS_TL(k) do { if (tl_on && threadIdx.x == 0) g_mh_tl[(k)] = wall_clock64(); } while (0)
+#else
+#define GS_TL(k) do { } while (0)
+#endif
+
+// fixed-order sum over the 64 lanes, the same bits on every lane: lane ^ 32
+// (v_permlane32_swap), lane ^ 16 (v_permlane16_swap), then rotations by 8, 4,
+// 2, 1 within each row of 16 (DPP row_ror); every step adds a symmetric pair,
+// and fp addition is commutative, so both lanes of a pair hold the same value
+__device__ __forceinline__ double wave_sum_bcast(double v) {
+    {
+        const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+        v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+    }
+    {
+        const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+        v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+    }
+#define GS_ROR(CTRL)                                                                                     \
+    {                                                                                                    \
+        const int slo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);        \
+        const int shi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);        \
+        v = v + __hiloint2double(shi, slo);                                                              \
+    }
+    GS_ROR(0x128) GS_ROR(0x124) GS_ROR(0x122) GS_ROR(0x121)
+#undef GS_ROR
+    return v;
+}
+
+// the part of the per-l likelihood term (f_ell_v) that spectrum sp enters:
+// F = 1: all; F = 2: f_E (sp 0) or f_B (sp 1); F = 3: f_B (sp 2) or the
+// TE-block part f_T + f_E (TT, EE, TE).  v = (v0..v3) in the spectra order.
+template <int F>
+__device__ __forceinline__ double f_part(const double (&sv)[SweepAcc<F>::NS], double b, double k0, double k1,
+                                         double k2, int sp, double v0, double v1, double v2, double v3) {
+    if constexpr (F == 1) {
+        const double a = sqrt(v0);
+        return -0.5 * k0 * (-2.0 * b * (a * sv[1]) + b * b * (a * a * sv[0]));
+    } else if constexpr (F == 2) {
+        const bool e = sp == 0;
+        const double a = sqrt(e ? v0 : v1);
+        const double kk = e ? k0 : k1, ss = e ? sv[0] : sv[1], ds = e ? sv[2] : sv[3];
+        return -0.5 * kk * (-2.0 * b * (a * ds) + b * b * (a * a * ss));
+    } else {
+        if (sp == 2) {
+            const double aB = sqrt(v2);
+            return -0.5 * k2 * (-2.0 * b * (aB * sv[7]) + b * b * (aB * aB * sv[2]));
+        }
+        double a00, a10, a11;
+        if (v0 != 0.0) {
+            a00 = sqrt(v0);
+            a10 = v3 / a00;
+            a11 = sqrt(fmax(v1 - a10 * a10, 0.0));
+        } else {
+            a00 = 0.0; a10 = 0.0; a11 = sqrt(v1);
+        }
+        const double fT = -0.5 * k0 * (-2.0 * b * (a00 * sv[4]) + b * b * (a00 * a00 * sv[0]));
+        const double linE = a10 * sv[5] + a11 * sv[6];
+        const double quadE = a10 * a10 * sv[0] + a10 * a11 * sv[3] + a11 * a10 * sv[3] + a11 * a11 * sv[1];
+        const double fE = -0.5 * k1 * (-2.0 * b * linE + b * b * quadE);
+        return fT + fE;
+    }
+}
+
+// the f_part group of spectrum sp: F = 3: 0 = the TE block (TT, EE, TE), 1 = B;
+// F = 2: 0 = E, 1 = B; F = 1: 0
+template <int F>
+__device__ __forceinline__ int f_group(int sp) { return F == 3 ? (sp == 2 ? 1 : 0) : (F == 2 ? sp : 0); }
+
+// lane-strided sum a[lo + lane], a[lo + lane + 64], ... (< hi) in index order,
+// U loads in flight per round
+template <int U>
+__device__ __forceinline__ double lane_strided_sum(const double* a, int lo, int hi, int lane) {
+    double s = 0.0;
+    for (int k0 = lo + lane; k0 < hi; k0 += 64 * U) {
+        double v[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) v[j] = a[min(k0 + 64 * j, hi - 1)];
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+            if (k0 + 64 * j < hi) s += v[j];
+    }
+    return s;
+}
+
+// one phase-ordered MH sweep of one chain (workgroup = blockDim.x threads).
+// Per thread, the current state of its l is kept across phases: the raw D_l
+// and variance of every spectrum and the value of each f_part group; a phase
+// evaluates only its proposals (one variance and one f_part each), and after
+// the phase's decisions a thread whose D_l changed takes the proposal's values
+// (identical bits to re-evaluating the new state).
+template <int F>
+__device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int maxbins, const MhPhases& ph, int ntab,
+                                            const int2* __restrict__ phase_tab, const int4* __restrict__ phase_rng,
+                                            const int* __restrict__ meta, int nacc, int n_iter_mh,
+                                            const int* __restrict__ ell2blk, const int* __restrict__ ell2bin,
+                                            const double* __restrict__ bl, double k0, double k1, double k2,
+                                            const double* __restrict__ stats, double* __restrict__ dl,
+                                            const double* __restrict__ prop, const double* __restrict__ logr,
+                                            const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
+                                            uint32_t iter, int chain0, int32_t* __restrict__ accept_out,
+                                            double* smem) {
+    (void)tl_on;
+    GS_TL(0);
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    constexpr int NS = SweepAcc<F>::NS;
+    constexpr int NG = F == 1 ? 1 : 2;
+    const int Lp1 = L + 1;
+    const int nrow = NSP * maxbins;
+    double* g = smem;                    // [2][L+1] per-l likelihood differences of the phase
+    double* lu = g + 2 * Lp1;            // [nacc] log accept uniforms, flat accept order
+    double* Ds = lu + nacc;              // [NSP][maxbins] this chain's D_l
+    double* Ps = Ds + nrow;              // [NSP][maxbins] proposals
+    double* Rs = Ps + nrow;              // [NSP][maxbins] proposal log ratios
+    // [ntab] phase entries (lo bin, hi bin, l0, l1), 16-B aligned, then (spectrum, block)
+    int4* rngs = reinterpret_cast<int4*>(Rs + nrow + ((2 * Lp1 + nacc + 3 * nrow) & 1));
+    int2* tabs = reinterpret_cast<int2*>(rngs + ntab); // [ntab] phase entries: (spectrum, block)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
+    const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    __shared__ int s_ao[4];
+    double* D = dl + (long long)chain * nrow;
+    const double* P = prop + (long long)chain * nrow;
+    const double* R = logr + (long long)chain * nrow;
+    const double* stg = stats + (long long)chain * NS * Lp1;
+    const int* acc_off = meta + 8;
+    // ---- one round of loads: this thread's l ...
+    const int l = ph.lmin + tid;
+    const bool lok = l < Lp1;
+    const int lc = lok ? l : L;
+    int eb[NSP], ek[NSP];
+    double sv[NS];
+#pragma unroll
+    for (int q = 0; q < NSP; ++q) { eb[q] = ell2bin[q * Lp1 + lc]; ek[q] = ell2blk[q * Lp1 + lc]; }
+#pragma unroll
+    for (int q = 0; q < NS; ++q) sv[q] = stg[q * Lp1 + lc];
+    if (tid < NSP) s_ao[tid] = acc_off[tid];
+    const double b = bl[lc];
+    // ... and the LDS arrays: up to MH_FILL rows of D / P / R per thread with
+    // every load issued before the stores (one memory round trip; a loop over
+    // rows would make one per row), the phase tables likewise
+    constexpr int MH_FILL = 8;
+    if (nrow <= MH_FILL * MH_REG_THREADS) {
+        double dv[MH_FILL], pv[MH_FILL], rv[MH_FILL];
+#pragma unroll
+        for (int j = 0; j < MH_FILL; ++j) {
+            const int k = min(tid + j * MH_REG_THREADS, nrow - 1);
+            dv[j] = D[k]; pv[j] = P[k]; rv[j] = R[k];
+        }
+        int4 rr[2];
+        int2 tt[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = min(tid + j * MH_REG_THREADS, max(ntab - 1, 0));
+            rr[j] = phase_rng[k]; tt[j] = phase_tab[k];
+        }
+#pragma unroll
+        for (int j = 0; j < MH_FILL; ++j) {
+            const int k = tid + j * MH_REG_THREADS;
+            if (k < nrow) { Ds[k] = dv[j]; Ps[k] = pv[j]; Rs[k] = rv[j]; }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = tid + j * MH_REG_THREADS;
+            if (k < ntab) { rngs[k] = rr[j]; tabs[k] = tt[j]; }
+        }
+        for (int k = tid + 2 * MH_REG_THREADS; k < ntab; k += MH_REG_THREADS) {
+            rngs[k] = phase_rng[k];
+            tabs[k] = phase_tab[k];
+        }
+    } else {
+        for (int k = tid; k < nrow; k += MH_REG_THREADS) { Ds[k] = D[k]; Ps[k] = P[k]; Rs[k] = R[k]; }
+        for (int k = tid; k < ntab; k += MH_REG_THREADS) { rngs[k] = phase_rng[k]; tabs[k] = phase_tab[k]; }
+    }
+    if (u_acc) {
+        for (int k = tid; k < nacc; k += MH_REG_THREADS) lu[k] = log(u_acc[(long long)chain * nacc + k]);
+    } else {
+        // in-kernel uniforms (the flat order's (spectrum, block, attempt) counters)
+        for (int k = tid; k < nacc; k += MH_REG_THREADS) {
+            int sp = 0, base = 0;
+#pragma unroll
+            for (int q = 0; q < NSP; ++q) {
+                const int a = acc_off[q];
+                if (k >= a && k < a + meta[4 + q] * n_iter_mh) { sp = q; base = a; }
+            }
+            const int r = k - base;
+            lu[k] = log(uniform1(key, r / n_iter_mh, (uint32_t)sp | ((uint32_t)(r % n_iter_mh) << 8), TAG_MH_U, iter));
+        }
+    }
+    uint64_t ebp = 0, ekp = 0;
+#pragma unroll
+    for (int q = 0; q < NSP; ++q) {
+        ebp |= (uint64_t)(uint32_t)(eb[q] + 1) << (16 * q);
+        ekp |= (uint64_t)(uint32_t)(ek[q] + 1) << (16 * q);
+    }
+    __syncthreads();
+    GS_TL(1);
+    // ---- the current state of this l
+    double dcur[NSP], vcur[4] = {0.0, 0.0, 0.0, 0.0}, fcur[NG];
+#pragma unroll
+    for (int s = 0; s < NSP; ++s) {
+        dcur[s] = eb[s] < 0 ? 0.0 : Ds[s * maxbins + eb[s]];
+        vcur[s] = var_from_dl(dcur[s], l);
+    }
+    fcur[0] = f_part<F>(sv, b, k0, k1, k2, 0, vcur[0], vcur[1], vcur[2], vcur[3]);
+    if constexpr (NG > 1) fcur[NG - 1] = f_part<F>(sv, b, k0, k1, k2, F == 3 ? 2 : 1, vcur[0], vcur[1], vcur[2], vcur[3]);
+    bool okcur = true;
+    if constexpr (F == 3) okcur = psd_ok(vcur[0], vcur[1], vcur[3]);
+    for (int q = 0; q < ph.nphase; ++q) {
+        const int nb = ph.n[q];
+        if (nb == 0) continue;
+        const int sp0 = ph.sp[q][0], sp1 = ph.sp[q][1];
+        const int2* tab = tabs + ph.off[q];
+        const int4* rng = rngs + ph.off[q];
+        const int nwide = ph.nwide[q];
+        // per-l likelihood differences of the phase's proposals on their own parts
+        double pvk[2] = {0.0, 0.0}, fnk[2] = {0.0, 0.0};
+        bool okk[2] = {false, false};
+        if (lok) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int sp = k == 0 ? sp0 : sp1;
+                if (sp < 0) continue;
+                double out = 0.0;
+                if (unpack16(ekp, sp) >= 0) {
+                    const double pv = var_from_dl(Ps[sp * maxbins + unpack16(ebp, sp)], l);
+                    double vn[4] = {vcur[0], vcur[1], vcur[2], vcur[3]};
+#pragma unroll
+                    for (int s = 0; s < NSP; ++s) vn[s] = s == sp ? pv : vn[s];
+                    bool ok = true;
+                    if constexpr (F == 3) ok = sp == 2 ? okcur : psd_ok(vn[0], vn[1], vn[3]);
+                    const double fn = ok ? f_part<F>(sv, b, k0, k1, k2, sp, vn[0], vn[1], vn[2], vn[3]) : 0.0;
+                    const double fo = NG > 1 && f_group<F>(sp) == 1 ? fcur[NG - 1] : fcur[0];
+                    out = ok ? fn - fo : -INFINITY;
+                    pvk[k] = pv; fnk[k] = fn; okk[k] = ok;
+                }
+                g[k * Lp1 + l] = out;
+            }
+        }
+        __syncthreads();
+        GS_TL(2 + 4 * q);
+        // narrow blocks: one thread each
+        for (int j = nwide + tid; j < nb; j += blockDim.x) {
+            const int2 sb = tab[j];
+            const int4 r = rng[j];
+            const int sp = sb.x, blk = sb.y, k = sp == sp0 ? 0 : 1;
+            const int lo = r.x, hi = r.y, l0 = r.z, l1 = r.w;
+            GS_ASSERT(lo >= 0 && hi <= maxbins && l0 >= 0 && l1 <= Lp1);
+            double diff = 0.0, lrs = 0.0;
+            for (int ll = l0; ll < l1; ++ll) diff += g[k * Lp1 + ll];
+            for (int bb = lo; bb < hi; ++bb) lrs += Rs[sp * maxbins + bb];
+            bool taken = false;
+            const int flat0 = s_ao[sp] + blk * n_iter_mh;
+            for (int att = 0; att < n_iter_mh; ++att) {
+                const bool acc = lu[flat0 + att] < (taken ? 0.0 : diff) + lrs;
+                if (acc && !taken)
+                    for (int bb = lo; bb < hi; ++bb) Ds[sp * maxbins + bb] = Ps[sp * maxbins + bb];
+                taken = taken || acc;
+                if (accept_out) accept_out[(long long)chain * nacc + flat0 + att] = acc ? 1 : 0;
+            }
+        }
+        GS_TL(3 + 4 * q);
+        // wide blocks: one wave each (lane-strided sums in l / bin order with
+        // eight loads in flight, then the fixed-order butterfly), decided and
+        // applied by that wave
+        for (int j = wv; j < nwide; j += nwv) {
+            const int2 sb = tab[j];
+            const int4 r = rng[j];
+            const int sp = sb.x, blk = sb.y, k = sp == sp0 ? 0 : 1;
+            double diff = lane_strided_sum<8>(g + k * Lp1, r.z, r.w, lane);
+            double lrs = lane_strided_sum<8>(Rs + sp * maxbins, r.x, r.y, lane);
+            diff = wave_sum_bcast(diff);
+            lrs = wave_sum_bcast(lrs);
+            bool taken = false;
+            const int flat0 = s_ao[sp] + blk * n_iter_mh;
+            for (int att = 0; att < n_iter_mh; ++att) {
+                const bool acc = lu[flat0 + att] < (taken ? 0.0 : diff) + lrs;
+                taken = taken || acc;
+                if (accept_out && lane == 0) accept_out[(long long)chain * nacc + flat0 + att] = acc ? 1 : 0;
+            }
+            if (taken)
+                for (int bb = r.x + lane; bb < r.y; bb += 64) Ds[sp * maxbins + bb] = Ps[sp * maxbins + bb];
+        }
+        GS_TL(4 + 4 * q);
+        __syncthreads();
+        GS_TL(5 + 4 * q);
+        // take the accepted proposals into this l's state
+        if (lok) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int sp = k == 0 ? sp0 : sp1;
+                if (sp < 0 || !okk[k]) continue;
+                const double d = Ds[sp * maxbins + unpack16(ebp, sp)];
+                bool changed = false;
+#pragma unroll
+                for (int s = 0; s < NSP; ++s)
+                    if (s == sp && d != dcur[s]) { dcur[s] = d; vcur[s] = pvk[k]; changed = true; }
+                if (changed) {
+                    if (NG > 1 && f_group<F>(sp) == 1) fcur[NG - 1] = fnk[k]; else fcur[0] = fnk[k];
+                    if constexpr (F == 3) okcur = psd_ok(vcur[0], vcur[1], vcur[3]);
+                }
+            }
+        }
+    }
+    for (int k = tid; k < nrow; k += blockDim.x) D[k] = Ds[k];
+    GS_TL(20);
+}
+
+template <int F>
+__global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, MhPhases ph, int ntab,
+                                                           const int2* __restrict__ phase_tab,
+                                                           const int4* __restrict__ phase_rng,
+                                                           const int* __restrict__ meta, int nacc, int n_iter_mh,
+                                                           const int* __restrict__ ell2blk,
+                                                           const int* __restrict__ ell2bin,
+                                                           const double* __restrict__ bl, double k0, double k1,
+                                                           double k2, const double* __restrict__ stats,
+                                                           double* __restrict__ dl, const double* __restrict__ prop,
+                                                           const double* __restrict__ logr,
+                                                           const double* __restrict__ u_acc, uint32_t seed_lo,
+                                                           uint32_t seed_hi, IterArg itarg, int chain0,
+                                                           int32_t* __restrict__ accept_out, MhEpi epi) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const uint32_t iter = itarg.get();
+    const int chain = blockIdx.x;
+    mh_reg_body<F>(chain, chain == 0, L, maxbins, ph, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
+                   ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
+                   smem);
+    mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x);
+}
+
 // stats of s_nc = A^+ s, A = chol(C(dl)) (ASIS.py:185-189)
 template <int F>
 __global__ void k_stats_to_nc(int L, int nchains, int maxbins, const double* __restrict__ dl,
@@ -1549,6 +1949,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     build_tasks(p);
     p->inkernel_params = p->nchains <= 4;
     p->sweep_latency = getenv("GS_SWEEP_THROUGHPUT") == nullptr;
+    p->mh_reg = getenv("GS_MH_FUSED") == nullptr;
     const size_t nc = (size_t)p->nchains;
     rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunkg * p->nstat * WAVE);
     rc |= dev_alloc(&p->params, nc * (L + 1) * NP);
@@ -1856,6 +2257,29 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
     const size_t lds = (2 * (size_t)(p->L + 1) + (size_t)maxnb * p->n_iter_mh + (size_t)p->nspec * p->maxbins) *
                            sizeof(double) + (size_t)p->nspec * (p->L + 1) * sizeof(int);
     const size_t lds_u = u_acc ? (size_t)p->nacc * sizeof(double) : 0;
+    // r03: the register / LDS-resident form when the phase l range is at most
+    // one l per thread and its arrays fit the LDS (GS_MH_FUSED=1: the older form)
+    int ntab = 0;
+    for (int q = 0; q < p->nphase; ++q) ntab += p->phase_n[q];
+    const size_t lds_reg = (2 * (size_t)(p->L + 1) + (size_t)p->nacc + 3 * (size_t)p->nspec * p->maxbins) *
+                           sizeof(double) + 16 + (size_t)ntab * (sizeof(int4) + sizeof(int2));
+    const bool reg = p->mh_reg && p->L + 1 - p->mh_lmin <= MH_REG_THREADS && lds_reg <= 150 * 1024;
+    if (reg) {
+        static bool attr_set[4] = {false, false, false, false};
+#define GS_MR(FF) do {                                                                                                 \
+        if (!attr_set[FF])                                                                                             \
+            GS_CHECK(hipFuncSetAttribute((const void*)k_mh_reg<FF>, hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                         150 * 1024));                                                                 \
+        attr_set[FF] = true;                                                                                           \
+        hipLaunchKernelGGL((k_mh_reg<FF>), dim3(p->nchains), dim3(MH_REG_THREADS), lds_reg, S(stream), p->L,           \
+                           p->maxbins, ph, ntab, p->phase_tab, p->phase_rng, p->meta, p->nacc, p->n_iter_mh, p->ell2blk,     \
+                           p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop, p->logr,      \
+                           u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out, E); } while (0)
+        if (p->F == 1) GS_MR(1); else if (p->F == 2) GS_MR(2); else GS_MR(3);
+#undef GS_MR
+        GS_LAUNCH_CHECK("k_mh_reg");
+        return 0;
+    }
     const size_t lds_sc = lds + lds_u + (size_t)p->nstat * (p->L + 1) * sizeof(double);
     // the LDS statistics cache is off by default: measured 37.6 us with it
     // against 35.8 us reading the statistics from L2 (GS_MH_STATS_CACHE=1 on)
@@ -2073,6 +2497,14 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
     }
     return 0;
 }
+
+#if defined(GS_MH_TIMELINE)
+int gs_debug_mh_timeline(unsigned long long* out) {
+    GS_CHECK(hipDeviceSynchronize());
+    GS_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mh_tl), sizeof(unsigned long long) * 32));
+    return 0;
+}
+#endif
 
 int gs_iteration_counter(gs_plan* p, int enable, uint32_t start) {
     if (check_plan(p)) return -1;
