@@ -532,10 +532,26 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
             i += L - m;
         }
     }
-    if (!active) return;
-    double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
+    if (tw == 4) {
+        if (!active) return;
+        double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
 #pragma unroll
-    for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
+        for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
+        return;
+    }
+    // 2 tiles x 2 chunks: the second chunk's wave hands its sums to the first
+    // through LDS (c0 + c1, one partial per chunk pair: half the partial bytes)
+    __shared__ double pair_red[2][NS][WAVE];
+    if (w >= tw) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) pair_red[w - tw][q][lane] = acc[q];
+    }
+    __syncthreads();
+    if (w < tw && tile_ok && m0 < lhi + 1) {
+        double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q] + pair_red[w][q][lane];
+    }
 }
 
 // one wave's share of a (chain, statistic, tile) finish: the sum of chunks w,
@@ -1773,11 +1789,19 @@ void build_tasks(gs_plan* p) {
     p->rows_per_task = tm;
     p->nchunk = L / tm + 1;
     p->ntask = (int)waves(tm);
-    // workgroup shape: 4 tiles x 1 chunk (each row one 4 KiB run per field).
-    // 1 tile x 4 chunks with the 4 waves' partials summed in LDS (a quarter of
-    // the partial traffic) was measured slower at the bench size (sweep
-    // 282-294 vs 261-281 us, interleaved in one process) and removed (r02)
-    const int tw = 4;
+    // workgroup shape: 2 tiles x 2 chunks (r03; each row one 2 KiB run per
+    // field, the two chunks' statistic sums added in LDS: half the partial
+    // bytes of 4 tiles x 1 chunk): NC TEB 32 chains at L 1024, whole steps
+    // interleaved in one process (tools/step_ab.py), 289.6-291.4 against
+    // 294.3 us.  1 tile x 4 chunks (a quarter of the partials, 1 KiB runs)
+    // measured slower in r02 (sweep 282-294 vs 261-281 us).  Short tasks (the
+    // latency form) keep 4 x 1.  GS_SWEEP_TW=4 selects 4 x 1 for A/B timing.
+    int tw = 2;
+    if (const char* env = getenv("GS_SWEEP_TW")) {
+        const int v = atoi(env);
+        if (v == 2 || v == 4) tw = v;
+    }
+    if (tm <= 4) tw = 4;             // the latency form writes one partial per chunk
     const int cw = 4 / tw;
     p->sweep_tw = tw;
     p->nchunkg = (p->nchunk + cw - 1) / cw;
@@ -2116,10 +2140,10 @@ static int stats_finish(gs_plan* p, double* stats, void* stream) {
     const long long n = (long long)p->nchains * p->nstat * p->ntile;
     if (p->nchains <= 4)
         hipLaunchKernelGGL(k_stats_finish<16>, dim3((unsigned)n), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
-                           p->nchunkg, p->rows_per_task, p->nstat, p->partials, stats);
+                           p->nchunkg, p->rows_per_task * (4 / p->sweep_tw), p->nstat, p->partials, stats);
     else
         hipLaunchKernelGGL(k_stats_finish<4>, dim3((unsigned)n), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
-                           p->nchunkg, p->rows_per_task, p->nstat, p->partials, stats);
+                           p->nchunkg, p->rows_per_task * (4 / p->sweep_tw), p->nstat, p->partials, stats);
     GS_LAUNCH_CHECK("k_stats_finish");
     return 0;
 }
