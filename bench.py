@@ -66,6 +66,10 @@ def parse():
                     help="bracket the CR sweep of every N-th timed step with hipEvents (graph mode); each "
                          "event pair is an extra pair of graph nodes in its step, so sampling every 10th "
                          "sweep keeps the timed steps close to the un-instrumented graph")
+    ap.add_argument("--skymap", default="store", choices=["store", "none"],
+                    help="harmonic workloads: 'none' runs the CR sweep without writing the sky map s (a full-sky "
+                         "driver's run() never reads it: the next CR, the MH and the C_l draw use the per-l "
+                         "statistics only, NonCenteredGibbs.py:529-571); the default keeps the store")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     one = a.workload == "masked" or a.workload in MASKED_HEAD
@@ -81,13 +85,14 @@ def parse():
     return a
 
 
-def sweep_algorithmic_bytes(L, F, nchains):
+def sweep_algorithmic_bytes(L, F, nchains, store=True):
     """Unique HBM bytes one CR-sweep launch must move (DESIGN.md 'Roofline'):
-    write s (8 F (L+1)^2 per chain) + read the shared data once (8 F (L+1)^2)
-    + read the per-l operator table (80 B per chain and l).  The per-task
-    statistics partials are implementation traffic and are not counted."""
+    write s (8 F (L+1)^2 per chain; none with --skymap none) + read the shared
+    data once (8 F (L+1)^2) + read the per-l operator table (80 B per chain and
+    l).  The per-task statistics partials are implementation traffic and are
+    not counted."""
     NR = (L + 1) ** 2
-    return 8 * F * NR * nchains + 8 * F * NR + 80 * (L + 1) * nchains
+    return (8 * F * NR * nchains if store else 0) + 8 * F * NR + 80 * (L + 1) * nchains
 
 
 def sht_flops(nside, L, c):
@@ -197,18 +202,22 @@ def run_harmonic(args, ctx, cpu):
     runner = BatchedRunner(kind=args.workload, lmax=P["lmax"], nside=P["nside"], nfields=P["nfields"],
                            nchains=args.nchains, bl=P["bl"], noise_var=P["noise_var"], bins=P["bins"],
                            d_alm=P["d_alm"], blocks=P["blocks"], proposal_variances=P["proposal_variances"],
-                           rng="native", seed=args.seed, chain0=ctx.chain0)
+                           rng="native", seed=args.seed, chain0=ctx.chain0,
+                           store_skymap=args.skymap == "store")
     p = runner.plan
     runner.init(P["dls_init"])
     trace = p.zeros(args.steps, p.nchains, p.nspec, p.maxbins)
     one_graph = not args.no_graph
+    warm_graph = None
     if one_graph and args.warmup > 0:
-        # the W warmup steps as one replayed hipGraph: besides warming the
-        # kernels this pays the process's one-time cost of its first graph launch
-        # (~1.9 ms at configs[2], measured), which would otherwise land in the
-        # timed replay
-        runner.capture_steps(args.warmup)
-        runner.step()
+        # the W warmup steps as one hipGraph, replayed right before the timed
+        # replay (below): besides warming the kernels this pays the process's
+        # one-time cost of its first graph launch (~1.9 ms at configs[2],
+        # measured), and the GPU enters the timed region busy -- capturing the
+        # timed graph after the warmup left the GPU idle for the capture's host
+        # time, and the timed replay then ran ~5 % slower than later replays
+        # (tools/replay_probe.py)
+        warm_graph = runner.capture_steps(args.warmup)
     else:
         for _ in range(args.warmup):
             runner.step()
@@ -218,6 +227,9 @@ def run_harmonic(args, ctx, cpu):
         # so its duration is measured on its stream over the timed region itself
         runner.capture_steps(args.steps, trace=trace, trace_capacity=args.steps, time_sweeps=True,
                              time_every=args.time_every)
+        if warm_graph is not None:
+            warm_graph.replay()
+            runner.iteration += args.warmup
     else:
         p.sweep_timing(True)
     torch.cuda.synchronize()
@@ -243,9 +255,10 @@ def run_harmonic(args, ctx, cpu):
         return None
     total = args.steps * ctx.global_chains
     sweep_avg_ms = sweep_ms / max(sweep_n, 1)
-    alg_bytes = sweep_algorithmic_bytes(p.L, p.F, p.nchains)
+    alg_bytes = sweep_algorithmic_bytes(p.L, p.F, p.nchains, store=args.skymap == "store")
     achieved = alg_bytes / (sweep_avg_ms * 1e-3) / 1e9
-    prof = load_profile(args.profile_json, f"{args.workload}_L{args.lmax}_F{args.fields}_c{p.nchains}")
+    prof = load_profile(args.profile_json, f"{args.workload}_L{args.lmax}_F{args.fields}_c{p.nchains}"
+                        + ("" if args.skymap == "store" else "_nostore"))
     return {
         "metric": METRIC % (args.nside, args.lmax),
         "value": round(total / elapsed, 3),
@@ -264,6 +277,9 @@ def run_harmonic(args, ctx, cpu):
                                               "parity for TT/TE pinned against the oracle only)"
                                               if args.fields == 3 else ""),
                    "launch": "one hipGraph of all timed iterations" if one_graph else "eager",
+                   "skymap": "stored every iteration" if args.skymap == "store" else
+                             "not stored (CR draw reduced to the per-l statistics in registers; s is never read "
+                             "by a full-sky run)",
                    "nside": args.nside, "lmax": args.lmax, "nfields": args.fields,
                    "chains_per_gpu": args.nchains, "global_chains": ctx.global_chains,
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
@@ -275,7 +291,8 @@ def run_harmonic(args, ctx, cpu):
                                "hipEvents around each sweep of the timed loop",
                      "valu_issue_frac": prof.get("valu_issue_frac"),
                      "note": "the sweep is issue-bound (Philox + Box-Muller per normal, DESIGN.md 3): "
-                             "valu_issue_frac = SQ_INST_CYCLES_VALU / (SIMDs x cycles) from profiles/"},
+                             "valu_issue_frac = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) "
+                             "from the profile pass (profiles/pmc_traffic.json)"},
         "cpu_baseline": cpu,
     }
 

@@ -793,7 +793,12 @@ __global__ void k_f2_resid(long long n, const double* __restrict__ d, const doub
 __global__ __launch_bounds__(256) void k_f2_gram(int R, long long n, const double* __restrict__ Y,
                                                  const double* __restrict__ r, const double* __restrict__ w,
                                                  double* __restrict__ partial) {
-    __shared__ double S[F2_RMAX + 4][F2_GSUB + 1];
+    // S[column][row]: a thread's 4 x 4 block reads rows ra..ra+3 and rb..rb+3 of
+    // one column as two 32-B runs; consecutive lanes own consecutive rb (row
+    // blocks 32 B apart), so a wave's reads are contiguous (no bank conflicts;
+    // the [row][column] layout put lanes 4 rows apart on 4 bank groups)
+    constexpr int SROW = F2_RMAX + 6;                 // even: 16-B aligned columns
+    __shared__ __attribute__((aligned(16))) double S[F2_GSUB][SROW];
     const int nb4 = (R + 3) / 4;
     const int nblk4 = nb4 * (nb4 + 1) / 2;
     const int tid = threadIdx.x;
@@ -819,26 +824,48 @@ __global__ __launch_bounds__(256) void k_f2_gram(int R, long long n, const doubl
             for (int y = 0; y < 4; ++y) acc[q][x][y] = 0.0;
     const long long e0 = blockIdx.x * F2_CHUNK, e1 = min(n, e0 + F2_CHUNK);
     const int rows = nb4 * 4;
+    // stage loads: thread t always stages element column c = t % 32 and rows
+    // t / 32 + 8 j, so sqrt(N^-1) is one load and one sqrt per thread and stage;
+    // all of a stage's loads are issued together into registers, and the next
+    // stage's loads are issued before this stage's products (one memory latency
+    // per stage, hidden under the FMAs; the r02 loop waited on every load)
+    constexpr int LPT = (F2_RMAX + 4 + 7) / 8;
+    const int c = tid & (F2_GSUB - 1), r0 = tid / F2_GSUB;
+    double v[LPT], sw;
+    auto issue = [&](long long es) {
+        const long long e = es + c;
+        const bool ein = e < e1;
+        const long long ec = ein ? e : e1 - 1;
+        sw = w[ec];
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const int row = r0 + 8 * j;
+            const int rr = min(row, R - 1);
+            v[j] = rr < R - 1 ? Y[(long long)rr * n + ec] : r[ec];
+        }
+        if (!ein) sw = 0.0;
+    };
+    issue(e0);
     for (long long es = e0; es < e1; es += F2_GSUB) {
-        for (int k = tid; k < rows * F2_GSUB; k += 256) {
-            const int row = k / F2_GSUB, c = k % F2_GSUB;
-            const long long e = es + c;
-            double v = 0.0;
-            if (row < R && e < e1) {
-                const double y = row < R - 1 ? Y[(long long)row * n + e] : r[e];
-                v = y * sqrt(w[e]);
-            }
-            S[row][c] = v;
+        const double s = sqrt(sw);
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const int row = r0 + 8 * j;
+            if (row < rows) S[c][row] = row < R ? v[j] * s : 0.0;
         }
         __syncthreads();
+        if (es + F2_GSUB < e1) issue(es + F2_GSUB);
 #pragma unroll
         for (int q = 0; q < F2_BPT; ++q) {
             if (!own[q]) continue;
             const int ra = 4 * bi[q], rb = 4 * bj[q];
-            for (int c = 0; c < F2_GSUB; ++c) {
-                double a[4], b[4];
-#pragma unroll
-                for (int x = 0; x < 4; ++x) { a[x] = S[ra + x][c]; b[x] = S[rb + x][c]; }
+#pragma unroll 4
+            for (int cc = 0; cc < F2_GSUB; ++cc) {
+                const double2 a01 = *reinterpret_cast<const double2*>(&S[cc][ra]);
+                const double2 a23 = *reinterpret_cast<const double2*>(&S[cc][ra + 2]);
+                const double2 b01 = *reinterpret_cast<const double2*>(&S[cc][rb]);
+                const double2 b23 = *reinterpret_cast<const double2*>(&S[cc][rb + 2]);
+                const double a[4] = {a01.x, a01.y, a23.x, a23.y}, b[4] = {b01.x, b01.y, b23.x, b23.y};
 #pragma unroll
                 for (int x = 0; x < 4; ++x)
 #pragma unroll
