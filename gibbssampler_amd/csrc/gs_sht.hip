@@ -666,7 +666,17 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
     constexpr int NF = NC;                      // input fields
     constexpr int NCO = NC == 1 ? 1 : 2;        // output comps per block
     const int L = D.L, npair = D.npair, nlm = D.nlm;
-    const int q = blockIdx.x, tile = blockIdx.y;
+    // XCD-aware remap (bijective): workgroups are dealt round-robin over the 8
+    // XCDs; give each XCD a contiguous range of (tile, m) items, m fastest, so
+    // the four m of one [m/4] group of the phase planes are written by
+    // neighbouring workgroups of one XCD and their 16-B pieces of each 64-B run
+    // meet in that XCD's L2 before write-back (the planes are written 16 B per
+    // lane at a 64-B stride)
+    const int gx = gridDim.x, nwg = gx * gridDim.y;
+    const int bl = blockIdx.x + blockIdx.y * gx;
+    const int xcd = bl & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bl >> 3);
+    const int q = wgl % gx, tile = wgl / gx;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g0 = tile * (LEG_BLOCK / 64) * SR + wave * SR;
