@@ -97,6 +97,10 @@ struct gs_plan {
     bool u_nat_ready = false;
     // device iteration counter (hipGraph replay of whole steps)
     uint32_t* iter_dev = nullptr;
+    // arrival counters of the one-launch centered step (k_centered_fused)
+    uint32_t* fsync = nullptr;
+    int ncu = 0;                     // compute units of the device
+    bool centered_fused = false;     // GS_CENTERED_FUSED at plan creation: the one-launch step (measured slower)
     bool iter_dev_on = false;
     const uint32_t* itp() const { return iter_dev_on ? iter_dev : nullptr; }
     // graph-captured steps (gs_graph_step): this step's offset from the device
@@ -337,19 +341,69 @@ __device__ __forceinline__ void sweep_operator(bool ok, int chain, int ell, int 
     }
 }
 
+// The workgroup's statistic partials.  tw = 4 (4 tiles x 1 chunk): one store
+// per wave.  tw = 2 / 1 (2 tiles x 2 chunks, 1 tile x 4 chunks): the cw = 4 / tw
+// chunk-waves of a tile add their sums in LDS in chunk order ((c0 + c1) + c2) +
+// c3, and the tile's first chunk-wave stores one partial per chunk group (every
+// wave of the workgroup reaches the barrier; an inactive wave adds zeros).
+// a statistic word: a plain load, or (SC1: statistics handed over inside one
+// launch by write-through stores) an sc1 load, served past the CU's L1
+template <bool SC1>
+__device__ __forceinline__ double ld_stat(const double* p) {
+    if constexpr (SC1)
+        return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    else
+        return *p;
+}
+
+// SC1: write-through (sc1) stores, for a hand-off inside the launch (k_centered_fused)
+template <bool SC1>
+__device__ __forceinline__ void st_word(double* p, double v) {
+    if constexpr (SC1)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
+template <int NS, bool SC1 = false>
+__device__ __forceinline__ void sweep_partials_store(const double (&acc)[NS], int tw, int w, int lane, bool store_ok,
+                                                     double* __restrict__ po, double* red) {
+    if (tw == 4) {
+        if (store_ok)
+#pragma unroll
+            for (int q = 0; q < NS; ++q) st_word<SC1>(po + q * WAVE + lane, acc[q]);
+        return;
+    }
+    const int cw = 4 / tw, ci = w / tw, ti = w % tw;
+    if (ci > 0)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) red[(((ci - 1) * tw + ti) * NS + q) * WAVE + lane] = acc[q];
+    __syncthreads();
+    if (ci == 0 && store_ok) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            double v = acc[q];
+            for (int k = 1; k < cw; ++k) v += red[(((k - 1) * tw + ti) * NS + q) * WAVE + lane];
+            st_word<SC1>(po + q * WAVE + lane, v);
+        }
+    }
+}
+
 // Latency form of the sweep for few chains (PRE = the most rows a task holds):
 // there the launch has ~one wave per SIMD and each wave's time is its chain of
 // memory latencies, so every global load of the wave -- its PRE data rows, the
 // Box-Muller tables, the operator's D_l -- is issued before any of them is
 // used (one memory round trip instead of one per row plus two for the
 // prologue).  Same arithmetic in the same order as the throughput form below.
-template <int F, bool STORE, int PRE>
+template <int F, bool STORE, int PRE, bool SC1 = false>
 __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
                                                  const int2* __restrict__ tasks, const double* __restrict__ d,
                                                  double* __restrict__ s,
                                                  double* __restrict__ partials, uint32_t seed_lo, uint32_t seed_hi,
                                                  uint32_t iter, uint32_t substep, int chain0, const SweepOp& op,
-                                                 double* tab) {
+                                                 double* tab, double* red) {
     constexpr int NS = SweepAcc<F>::NS;
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
@@ -422,7 +476,6 @@ __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, 
         if (j < BM_TAB_DOUBLES) tab[j] = tv[k];
     }
     __syncthreads();
-    if (!active) return;
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
     const uint32_t tag = TAG_CR | (substep << 8);
     double acc[NS];
@@ -432,7 +485,7 @@ __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, 
 #pragma unroll
     for (int k = 0; k < PRE; ++k) {
         const int m = m0 + k;
-        if (m < m1 && lane_ok && ell >= m) {
+        if (active && m < m1 && lane_ok && ell >= m) {
             if (m == 0) {
                 sweep_entry<F, 0, STORE, 1>(dq[k], nullptr, sc, NR, ell, (uint32_t)ell, tag, iter, key, pm, acc, tab);
             } else {
@@ -443,8 +496,7 @@ __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, 
         }
     }
     double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
+    sweep_partials_store<NS, SC1>(acc, tw, w, lane, t < ntile && (cw * gc.y) * tm <= lhi, po, red);
 }
 
 template <int F, int ZM, bool STORE, int PRE = 0>
@@ -457,10 +509,11 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     const uint32_t iter = itarg.get();
     constexpr int NS = SweepAcc<F>::NS;
     __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
+    __shared__ double red[3 * NS * WAVE];           // chunk-wave sums of tw < 4 shapes
     if constexpr (PRE > 0) {
         static_assert(ZM == 0, "latency form: native draws only");
         cr_sweep_latency<F, STORE, PRE>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo,
-                                        seed_hi, iter, substep, chain0, op, tab);
+                                        seed_hi, iter, substep, chain0, op, tab, red);
         return;
     }
     if constexpr (ZM == 0) {
@@ -532,33 +585,15 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
             i += L - m;
         }
     }
-    if (tw == 4) {
-        if (!active) return;
-        double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
-        return;
-    }
-    // 2 tiles x 2 chunks: the second chunk's wave hands its sums to the first
-    // through LDS (c0 + c1, one partial per chunk pair: half the partial bytes)
-    __shared__ double pair_red[2][NS][WAVE];
-    if (w >= tw) {
-#pragma unroll
-        for (int q = 0; q < NS; ++q) pair_red[w - tw][q][lane] = acc[q];
-    }
-    __syncthreads();
-    if (w < tw && tile_ok && m0 < lhi + 1) {
-        double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q] + pair_red[w][q][lane];
-    }
+    double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
+    sweep_partials_store<NS>(acc, tw, w, lane, tile_ok && (cw * gc.y) * tm <= lhi, po, red);
 }
 
 // one wave's share of a (chain, statistic, tile) finish: the sum of chunks w,
 // w + 4, ... of the tile's 64 l (lanes; coalesced rows of the partials)
-template <int G>
+template <int G, bool SC1 = false>
 __device__ __forceinline__ double stats_finish_sum(int L, int ntile, int nchunkg, int tm, int nstat,
-                                                   const double* __restrict__ partials, int chain, int q, int t,
+                                                   const double* partials, int chain, int q, int t,
                                                    int w, int lane) {
     const int cmax = (L - WAVE * t) / tm;               // last chunk of tile t
     GS_ASSERT(cmax < nchunkg);
@@ -579,16 +614,16 @@ __device__ __forceinline__ double stats_finish_sum(int L, int ntile, int nchunkg
         for (; c + 12 <= cmax; c += 16) {
             double v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = pp[(c + 4 * j) * cs];
+            for (int j = 0; j < 4; ++j) v[j] = ld_stat<SC1>(pp + (c + 4 * j) * cs);
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc += v[j];
         }
-        for (; c <= cmax; c += 4) acc += pp[c * cs];
+        for (; c <= cmax; c += 4) acc += ld_stat<SC1>(pp + c * cs);
     } else {
         for (int c = w; c <= cmax; c += 4 * G) {
             double v[G];
 #pragma unroll
-            for (int j = 0; j < G; ++j) v[j] = pp[min(c + 4 * j, cmax) * cs];
+            for (int j = 0; j < G; ++j) v[j] = ld_stat<SC1>(pp + min(c + 4 * j, cmax) * cs);
 #pragma unroll
             for (int j = 0; j < G; ++j)
                 if (c + 4 * j <= cmax) acc += v[j];
@@ -648,19 +683,16 @@ __device__ __forceinline__ void ticket_advance(uint32_t* counter, uint32_t nblk,
     }
 }
 
-template <int F>
-__device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __restrict__ bins,
-                                              const int* __restrict__ nbins_arr, const double* __restrict__ stats,
+template <int F, bool SC1 = false>
+__device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, int maxbins, const int* __restrict__ bins,
+                                              const int* __restrict__ nbins_arr, const double* stats,
                                               const double* __restrict__ variates, uint32_t seed_lo, uint32_t seed_hi,
                                               uint32_t iter, int chain0, double* __restrict__ dl_out,
                                               double* __restrict__ trace, int cap, int nchains) {
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
-    const int chain = blockIdx.x;
-    const int sp = blockIdx.y;
     const int Lp1 = L + 1;
     const int nb = nbins_arr[sp];
-    const int b = blockIdx.z * blockDim.x + threadIdx.x;
     // trace slot of this iteration: trace[(iter - 1) % cap][chain][nspec][maxbins]
     double* tr = trace ? trace + ((long long)((iter + (uint32_t)cap - 1u) % (uint32_t)cap) * nchains + chain) * NSP * maxbins
                        : nullptr;
@@ -692,7 +724,8 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int l = max(min(l0 + j, l1 - 1), 0);
-                va[j] = st[0 * Lp1 + l]; vd[j] = st[1 * Lp1 + l]; vc[j] = st[3 * Lp1 + l];
+                va[j] = ld_stat<SC1>(st + 0 * Lp1 + l); vd[j] = ld_stat<SC1>(st + 1 * Lp1 + l);
+                vc[j] = ld_stat<SC1>(st + 3 * Lp1 + l);
             }
             const double nu = (double)(l1 * l1 - l0 * l0) - 3.0;
             double g1 = 0.0, g2 = 0.0, n = 0.0;
@@ -706,7 +739,8 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int l = min(lg + j, l1 - 1);
-                        va[j] = st[0 * Lp1 + l]; vd[j] = st[1 * Lp1 + l]; vc[j] = st[3 * Lp1 + l];
+                        va[j] = ld_stat<SC1>(st + 0 * Lp1 + l); vd[j] = ld_stat<SC1>(st + 1 * Lp1 + l);
+                        vc[j] = ld_stat<SC1>(st + 3 * Lp1 + l);
                     }
                 }
 #pragma unroll
@@ -755,7 +789,7 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
         constexpr int G = 24;
         double v[G];
 #pragma unroll
-        for (int j = 0; j < G; ++j) v[j] = st[ssrow * Lp1 + max(min(l0 + j, l1 - 1), 0)];
+        for (int j = 0; j < G; ++j) v[j] = ld_stat<SC1>(st + ssrow * Lp1 + max(min(l0 + j, l1 - 1), 0));
         const double expo = (double)(l1 * l1 - l0 * l0) / 2.0;
         const double alpha = b == 0 ? 1.0 : expo - 1.0;
         double X;
@@ -765,7 +799,7 @@ __device__ __forceinline__ void cls_draw_body(int L, int maxbins, const int* __r
         for (int lg = l0; lg < l1; lg += G) {
             if (lg > l0) {
 #pragma unroll
-                for (int j = 0; j < G; ++j) v[j] = st[ssrow * Lp1 + min(lg + j, l1 - 1)];
+                for (int j = 0; j < G; ++j) v[j] = ld_stat<SC1>(st + ssrow * Lp1 + min(lg + j, l1 - 1));
             }
 #pragma unroll
             for (int j = 0; j < G; ++j) {
@@ -789,11 +823,104 @@ __global__ __launch_bounds__(64) void k_cls_draw(int L, int nchains, int maxbins
                                                  double* __restrict__ dl_out, double* __restrict__ trace, int cap,
                                                  uint32_t* __restrict__ counter, uint32_t adv) {
     const uint32_t iter = itarg.get();
-    cls_draw_body<F>(L, maxbins, bins, nbins_arr, stats, variates, seed_lo, seed_hi, iter, chain0, dl_out, trace,
+    cls_draw_body<F>(blockIdx.x, blockIdx.y, blockIdx.z * blockDim.x + threadIdx.x, L, maxbins, bins, nbins_arr,
+                     stats, variates, seed_lo, seed_hi, iter, chain0, dl_out, trace,
                      cap, nchains);
     if (counter) ticket_advance(counter, gridDim.x * gridDim.y * gridDim.z, adv);
 }
 
+
+// One launch per centered step for few chains (configs[1], r03): the CR sweep
+// (latency form), the statistics finish and the C_l draw with in-launch
+// hand-offs instead of two kernel boundaries (CenteredGibbs.py:54-93,317-353).
+// Every workgroup runs its sweep task and stores its partials write-through
+// (sc1); after every wave's vmcnt(0) and a barrier one lane takes an arrival
+// ticket.  The last nhelp arrivers become helpers: they wait for all tickets
+// (sc1 polls), finish the statistics (one (chain, statistic, tile) per wave,
+// the same sums as k_stats_finish; sc1 loads and stores), meet at a second
+// counter, and draw the C_l (the k_cls_draw items, sc1 loads of the
+// statistics).  The last helper resets the counters and advances the device
+// iteration counter.  Deadlock freedom: a workgroup waits only once it is one
+// of the last nhelp arrivers, i.e. when at most nhelp - 1 workgroups have not
+// arrived, and the host launches this form only when nhelp is below the
+// device's CU count (each waiting helper holds at most one CU's slot).
+template <int F>
+__global__ __launch_bounds__(256, 1) void k_centered_fused(int L, int nchains, int ntile, int nchunkg, int tm, int tmf,
+                                                           int tw,
+                                                           const int2* __restrict__ tasks, const double* __restrict__ d,
+                                                           double* __restrict__ s, double* partials,
+                                                           uint32_t seed_lo, uint32_t seed_hi, IterArg itarg,
+                                                           int chain0, SweepOp op, int nhelp, uint32_t* sync,
+                                                           double* stats, int maxbins, const int* __restrict__ bins,
+                                                           const int* __restrict__ nbins_arr, double* __restrict__ dl_out,
+                                                           double* __restrict__ trace, int cap,
+                                                           uint32_t* __restrict__ counter, uint32_t adv) {
+    constexpr int NS = SweepAcc<F>::NS;
+    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+    const uint32_t iter = itarg.get();
+    __shared__ double tab[BM_TAB_DOUBLES];
+    __shared__ double red[3 * NS * WAVE];
+    __shared__ uint32_t s_ticket;
+    cr_sweep_latency<F, true, 4, true>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo, seed_hi,
+                                       iter, 0, chain0, op, tab, red);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's sc1 partial stores have completed
+    __syncthreads();
+    const uint32_t nwg = gridDim.x;
+    if (threadIdx.x == 0)
+        s_ticket = __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t tk = s_ticket;
+    if (tk < nwg - (uint32_t)nhelp) return;
+    const int h = (int)(tk - (nwg - (uint32_t)nhelp));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg) __builtin_amdgcn_s_sleep(1);
+    __syncthreads();
+    // ---- the statistics finish: one (chain, statistic, tile) per helper, its
+    // four waves as k_stats_finish's (chunk groups w, w + 4, ...; the same sums)
+    const int Lp1 = L + 1;
+    const int nunit = nchains * NS * ntile;
+    for (int u = h; u < nunit; u += nhelp) {
+        const int t = u % ntile, q = (u / ntile) % NS, chain = u / (ntile * NS);
+        // tmf: the rows of one chunk group (tm x 4 / tw), the finish's chunk unit
+        const double a = stats_finish_sum<16, true>(L, ntile, nchunkg, tmf, NS, partials, chain, q, t, w, lane);
+        red[w * WAVE + lane] = a;
+        __syncthreads();
+        if (w == 0) {
+            const int ell = L - WAVE * t - 63 + lane;
+            const double v = ((red[lane] + red[WAVE + lane]) + red[2 * WAVE + lane]) + red[3 * WAVE + lane];
+            if (ell >= 0) st_word<true>(stats + ((long long)chain * NS + q) * Lp1 + ell, v);
+        }
+        __syncthreads();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)nhelp)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+    // ---- the C_l draw: k_cls_draw's (chain, spectrum, bin) items ----
+    const int nitem = nchains * NSP * maxbins;
+    for (int i = h * blockDim.x + threadIdx.x; i < nitem; i += nhelp * blockDim.x) {
+        const int b = i % maxbins, sp = (i / maxbins) % NSP, chain = i / (maxbins * NSP);
+        cls_draw_body<F, true>(chain, sp, b, L, maxbins, bins, nbins_arr, stats, nullptr, seed_lo, seed_hi, iter,
+                               chain0, dl_out, trace, cap, nchains);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t e = __hip_atomic_fetch_add(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == (uint32_t)nhelp - 1) {
+            // every workgroup has read the iteration counter (all arrived) and
+            // every helper has passed both waits: reset for the next launch
+            __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sync[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (counter) __hip_atomic_fetch_add(&counter[0], adv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
 
 // ============================================================================
 // non-centered Metropolis-within-Gibbs (NonCenteredGibbs.py:292-445)
@@ -1794,14 +1921,15 @@ void build_tasks(gs_plan* p) {
     // bytes of 4 tiles x 1 chunk): NC TEB 32 chains at L 1024, whole steps
     // interleaved in one process (tools/step_ab.py), 289.6-291.4 against
     // 294.3 us.  1 tile x 4 chunks (a quarter of the partials, 1 KiB runs)
-    // measured slower in r02 (sweep 282-294 vs 261-281 us).  Short tasks (the
-    // latency form) keep 4 x 1.  GS_SWEEP_TW=4 selects 4 x 1 for A/B timing.
-    int tw = 2;
+    // measured slower there in r02 (sweep 282-294 vs 261-281 us), but short
+    // tasks (the latency form, few chains) take it: their finish is a chain of
+    // memory latencies, one per group of chunk partials it reads.
+    // GS_SWEEP_TW=1|2|4 overrides (A/B timing).
+    int tw = tm <= 4 ? 1 : 2;
     if (const char* env = getenv("GS_SWEEP_TW")) {
         const int v = atoi(env);
-        if (v == 2 || v == 4) tw = v;
+        if (v == 1 || v == 2 || v == 4) tw = v;
     }
-    if (tm <= 4) tw = 4;             // the latency form writes one partial per chunk
     const int cw = 4 / tw;
     p->sweep_tw = tw;
     p->nchunkg = (p->nchunk + cw - 1) / cw;
@@ -1983,6 +2111,9 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->dl_tmp, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->u_nat, nc * std::max(p->nacc, 1));
     rc |= dev_alloc(&p->iter_dev, 4);
+    rc |= dev_alloc(&p->fsync, 4);
+    if (hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) p->ncu = 0;
+    p->centered_fused = getenv("GS_CENTERED_FUSED") != nullptr;
     if (rc) { gs_plan_destroy(p); return -1; }
     *out = p;
     return 0;
@@ -1990,7 +2121,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
-    void* bufs[] = {p->iter_dev, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
+    void* bufs[] = {p->iter_dev, p->fsync, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
                     p->params, p->stats, p->prop, p->logr, p->dl_tmp};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2380,12 +2511,49 @@ static int step_sweep(gs_plan* p, int mode, const double* d_alm, const double* d
 }
 
 // ---- fused iterations ------------------------------------------------------
+static int centered_fused_launch(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed,
+                                 uint32_t it, double* trace, int cap, uint32_t* counter, void* stream);
+
 int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
                      const double* igvar, uint64_t seed, uint32_t it, void* stream) {
     if (check_plan(p)) return -1;
     if (!d_alm || !dl) return set_error("gs_step_centered: null argument");
+    if (!z && !igvar) {
+        // native draws: the one-launch step where the plan allows it
+        const int rc = centered_fused_launch(p, d_alm, dl, s_out, seed, it, nullptr, 1, nullptr, stream);
+        if (rc <= 0) return rc;
+    }
     if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, z, seed, it, s_out, stream)) return -1;
     return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
+}
+
+// the one-launch centered step (k_centered_fused) where the plan allows it:
+// the latency form of the sweep (few chains, short tasks, s stored) and fewer
+// helpers than the device's CUs (at most nhelp - 1 workgroups wait while the
+// rest are still to arrive).  Opt-in (GS_CENTERED_FUSED): measured slower than
+// the three launches.  Returns 1 when not taken (the caller launches three).
+static int centered_fused_launch(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed,
+                                 uint32_t it, double* trace, int cap, uint32_t* counter, void* stream) {
+    if (!p->centered_fused || !p->inkernel_params || p->rows_per_task > 4 || !p->sweep_latency || !s_out) return 1;
+    const int nunit = p->nchains * p->nstat * p->ntile;
+    const int nitem = p->nchains * p->nspec * p->maxbins;
+    const int nwg = p->nchains * p->npair;
+    const int nhelp = std::min(nwg, std::max(nunit, (nitem + 255) / 256));
+    if (p->ncu <= 0 || nhelp >= p->ncu) return 1;
+    const SweepOp op{GS_MODE_CENTERED, p->maxbins, dl, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2]};
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing_begin(p, S(stream), &e0, &e1)) return -1;
+#define GS_CF(FF) hipLaunchKernelGGL((k_centered_fused<FF>), dim3((unsigned)nwg), dim3(256), 0, S(stream), p->L,          \
+                                     p->nchains, p->ntile, p->nchunkg, p->rows_per_task,                             \
+                                     p->rows_per_task * (4 / p->sweep_tw), p->sweep_tw, p->tasks, d_alm, s_out, p->partials, slo, shi, p->ita(it), p->chain0, \
+                                     op, nhelp, p->fsync, p->stats, p->maxbins, p->bins, p->meta, dl, trace, cap,      \
+                                     counter, p->graph_adv)
+    if (p->F == 1) GS_CF(1); else if (p->F == 2) GS_CF(2); else GS_CF(3);
+#undef GS_CF
+    GS_LAUNCH_CHECK("k_centered_fused");
+    if (p->timing && record_ev(e1, S(stream))) return -1;
+    return 0;
 }
 
 int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed, uint32_t it,
@@ -2394,6 +2562,11 @@ int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* 
     if (!p->iter_dev_on) return set_error("gs_step_centered_fused: device iteration counter not enabled");
     if (trace && capacity < 1) return set_error("gs_step_centered_fused: capacity < 1");
     if (!d_alm || !dl) return set_error("gs_step_centered_fused: null argument");
+    {
+        const int rc = centered_fused_launch(p, d_alm, dl, s_out, seed, it, trace, trace ? capacity : 1,
+                                             p->adv_counter(), stream);
+        if (rc <= 0) return rc;
+    }
     if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream)) return -1;
     return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->adv_counter(), stream);
 }

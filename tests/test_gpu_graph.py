@@ -175,3 +175,42 @@ def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
         a, b = run(False, graph), run(True, graph)
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("F,nch", [(3, 1), (1, 2), (2, 2)])
+def test_centered_one_launch_bit_identical(monkeypatch, F, nch):
+    """The one-launch centered step (k_centered_fused: sweep, statistics finish
+    and C_l draw with in-launch hand-offs; GS_CENTERED_FUSED=1 at plan creation)
+    gives the same bits as the three launches: maps and D_l over 3 native steps,
+    eager and as one captured 3-step graph (the counter advance and the trace
+    ride in the fused launch)."""
+    from gibbssampler_amd.problem import synthetic_problem
+    from gibbssampler_amd.samplers import BatchedRunner
+    P = synthetic_problem(300, 128, F, seed=7)
+
+    def run(fused, graph):
+        if fused:
+            monkeypatch.setenv("GS_CENTERED_FUSED", "1")
+        else:
+            monkeypatch.delenv("GS_CENTERED_FUSED", raising=False)
+        r = BatchedRunner("centered", P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
+                          rng="native", seed=23)
+        assert r.plan.rows_per_task == 4
+        r.init(P["dls_init"])
+        trace = None
+        if graph:
+            trace = r.plan.zeros(3, nch, r.plan.nspec, r.plan.maxbins)
+            r.capture_steps(3, trace=trace, trace_capacity=3)
+            r.step()
+        else:
+            for _ in range(3):
+                r.step()
+        out = [r.dl.cpu().numpy(), r.s.cpu().numpy()]
+        if trace is not None:
+            out.append(trace.cpu().numpy())
+        return out
+
+    for graph in (False, True):
+        a, b = run(True, graph), run(False, graph)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)

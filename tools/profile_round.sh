@@ -2,7 +2,7 @@
 # Round evidence on the GPU box (rocprofv3 + bench lines), all under gpurun_out/:
 #   prof_<tag>/trace        kernel trace + stats of the default bench (BASELINE configs[2])
 #   prof_<tag>/fetch|write  separate PMC passes (FETCH_SIZE, WRITE_SIZE) of k_cr_sweep
-#   prof_<tag>/valu         PMC pass: SQ_INST_CYCLES_VALU, SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE
+#   prof_<tag>/valu         PMC pass: SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE
 #   bench_<tag>_*.json      bench lines: default (with cpu_baseline), centered C2, asis C4 (per GPU),
 #                           masked C5, HEAD's masked modes (masked_asis, masked_centered_ula)
 #   prof_<tag>_<mode>       kernel stats of the masked workloads, SHT at N_side 2048
@@ -18,7 +18,7 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_cr_sweep
     --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT.fetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_cr_sweep -d "$OUT/write" -o run \
     --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT.write.log" 2>&1
-timeout -s KILL 120 rocprofv3 --pmc SQ_INST_CYCLES_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
     --kernel-include-regex k_cr_sweep -d "$OUT/valu" -o run \
     --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT.valu.log" 2>&1
 echo "profiles done"
@@ -33,6 +33,8 @@ timeout -k 10 300 python3 bench.py --workload masked_asis > gpurun_out/bench_${T
     2> gpurun_out/bench_${TAG}_masked_asis.err
 timeout -k 10 300 python3 bench.py --workload masked_centered_ula > gpurun_out/bench_${TAG}_masked_ula.json \
     2> gpurun_out/bench_${TAG}_masked_ula.err
+timeout -k 10 400 python3 bench.py --no-cpu-baseline --skymap none > gpurun_out/bench_${TAG}_default_nostore.json \
+    2> gpurun_out/bench_${TAG}_default_nostore.err
 echo "bench lines done"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "${OUT}_c2" -o run --output-format csv -- \
     python3 bench.py --workload centered --nside 256 --lmax 512 --nchains 1 --steps 200 --time-every 100 > "${OUT}_c2.log" 2>&1
