@@ -41,6 +41,8 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VALU_PEAK_TFS = 78.6    # MI355X_MICROARCH.md: FP64 vector
+VALU_SIMDS = 1024            # 256 CUs x 4 SIMDs
+VALU_CLOCK_GHZ = 2.4         # peak engine clock
 METRIC = "Gibbs iters/sec (constrained-realization + C_l draw), Nside=%d lmax=%d"
 HARMONIC = ("noncentered", "centered", "asis")
 SURFACE = ("surface_noncentered",)
@@ -66,10 +68,11 @@ def parse():
                     help="bracket the CR sweep of every N-th timed step with hipEvents (graph mode); each "
                          "event pair is an extra pair of graph nodes in its step, so sampling every 10th "
                          "sweep keeps the timed steps close to the un-instrumented graph")
-    ap.add_argument("--skymap", default="store", choices=["store", "none"],
-                    help="harmonic workloads: 'none' runs the CR sweep without writing the sky map s (a full-sky "
-                         "driver's run() never reads it: the next CR, the MH and the C_l draw use the per-l "
-                         "statistics only, NonCenteredGibbs.py:529-571); the default keeps the store")
+    ap.add_argument("--skymap", default="none", choices=["store", "none"],
+                    help="harmonic workloads: 'none' (default) runs the CR sweep without writing the sky map s -- "
+                         "a full-sky run never reads it: the next CR, the MH and the C_l draw use the per-l "
+                         "statistics only, and the reference's run() returns D_l and accept flags only "
+                         "(NonCenteredGibbs.py:529-571); 'store' writes s every iteration (HBM roofline)")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     one = a.workload == "masked" or a.workload in MASKED_HEAD
@@ -93,6 +96,38 @@ def sweep_algorithmic_bytes(L, F, nchains, store=True):
     not counted."""
     NR = (L + 1) ** 2
     return (8 * F * NR * nchains if store else 0) + 8 * F * NR + 80 * (L + 1) * nchains
+
+
+def sweep_roofline(args, prof, alg_bytes, achieved, sweep_avg_ms, sweep_n, one_graph):
+    """The dominant kernel's roofline.  With the sky map stored (--skymap store)
+    the sweep is bounded by HBM: unique bytes (write s, read d once, the operator)
+    per launch / the launch's measured duration.  Without the store the sweep
+    moves ~83 MB per launch and is bounded by VALU issue: the SIMD-busy cycles
+    one launch needs (SQ_ACTIVE_INST_VALU x 4, counted by the profile pass for
+    this kernel and configuration, profiles/pmc_traffic.json) / the launch's
+    measured duration, against 1024 SIMDs x the 2.4 GHz peak engine clock."""
+    timing = ("hipEvents around each sweep inside the timed graph" if one_graph else
+              "hipEvents around each sweep of the timed loop")
+    common = {"avg_launch_ms": round(sweep_avg_ms, 5), "launches": sweep_n, "timing": timing,
+              "traffic": prof.get("hbm_bytes_per_launch"), "algorithmic_bytes_per_launch": alg_bytes}
+    if args.skymap == "store":
+        return {"bound": "hbm", "kernel": "k_cr_sweep", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), **common,
+                "valu_issue_frac": prof.get("valu_issue_frac"),
+                "note": "the sweep is close to issue-bound as well (Philox + Box-Muller per normal, DESIGN.md 3): "
+                        "valu_issue_frac = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) from "
+                        "the profile pass (profiles/pmc_traffic.json)"}
+    cyc = prof.get("valu_busy_simd_cycles_per_launch")
+    peak = VALU_SIMDS * VALU_CLOCK_GHZ
+    ach = cyc / (sweep_avg_ms * 1e-3) / 1e9 if cyc else None
+    return {"bound": "valu", "kernel": "k_cr_sweep (sky map not stored)",
+            "achieved": round(ach, 1) if ach else None, "peak": peak, "unit": "G SIMD-busy cycles/s",
+            "frac": round(ach / peak, 4) if ach else None, **common,
+            "valu_busy_simd_cycles_per_launch": cyc, "valu_issue_frac_at_run_clock": prof.get("valu_issue_frac"),
+            "hbm_frac_unique_bytes": round(achieved / HBM_PEAK_GBS, 4),
+            "note": "issue-bound: Philox4x32-10 + fp64 Box-Muller per normal (DESIGN.md 3); achieved = the launch's "
+                    "SIMD-busy cycles (SQ_ACTIVE_INST_VALU x 4 from the profile pass of this kernel and config) / "
+                    "its duration measured here; peak = 1024 SIMDs x 2.4 GHz"}
 
 
 def sht_flops(nside, L, c):
@@ -283,16 +318,7 @@ def run_harmonic(args, ctx, cpu):
                    "nside": args.nside, "lmax": args.lmax, "nfields": args.fields,
                    "chains_per_gpu": args.nchains, "global_chains": ctx.global_chains,
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
-        "roofline": {"bound": "hbm", "kernel": "k_cr_sweep", "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": prof.get("hbm_bytes_per_launch"), "algorithmic_bytes_per_launch": alg_bytes,
-                     "avg_launch_ms": round(sweep_avg_ms, 5), "launches": sweep_n,
-                     "timing": "hipEvents around each sweep inside the timed graph" if one_graph else
-                               "hipEvents around each sweep of the timed loop",
-                     "valu_issue_frac": prof.get("valu_issue_frac"),
-                     "note": "the sweep is issue-bound (Philox + Box-Muller per normal, DESIGN.md 3): "
-                             "valu_issue_frac = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) "
-                             "from the profile pass (profiles/pmc_traffic.json)"},
+        "roofline": sweep_roofline(args, prof, alg_bytes, achieved, sweep_avg_ms, sweep_n, one_graph),
         "cpu_baseline": cpu,
     }
 

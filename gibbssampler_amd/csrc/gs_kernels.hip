@@ -2293,13 +2293,14 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
     const bool rep = z != nullptr, st = s_out != nullptr;
     // latency form (all loads first) for few chains with short tasks; the
     // throughput form otherwise (more chains: its registers buy occupancy)
-    const bool lat = pmode >= 0 && p->rows_per_task <= 4 && !given && !rep && st &&
-                     p->sweep_latency;
+    const bool lat = pmode >= 0 && p->rows_per_task <= 4 && !given && !rep && p->sweep_latency;
     if (lat) {
-#define GS_SWL(FF) hipLaunchKernelGGL((k_cr_sweep<FF, 0, true, 4>), g, b, 0, S(stream), p->L, p->nchains, p->ntile,   \
-                                      p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z, s_out,     \
-                                      p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op)
-        if (p->F == 1) GS_SWL(1); else if (p->F == 2) GS_SWL(2); else GS_SWL(3);
+#define GS_SWL(FF, SS) hipLaunchKernelGGL((k_cr_sweep<FF, 0, SS, 4>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
+                                          p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,    \
+                                          s_out, p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op)
+#define GS_SWL2(FF) do { if (st) GS_SWL(FF, true); else GS_SWL(FF, false); } while (0)
+        if (p->F == 1) GS_SWL2(1); else if (p->F == 2) GS_SWL2(2); else GS_SWL2(3);
+#undef GS_SWL2
 #undef GS_SWL
         GS_LAUNCH_CHECK("k_cr_sweep");
         if (p->timing && record_ev(e1, S(stream))) return -1;

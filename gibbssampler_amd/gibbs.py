@@ -34,7 +34,11 @@ reference's draw order), ``seed`` (native streams), ``fields`` ("EB" or
 ``distributed`` (one process per GPU under torchrun: this rank runs global
 chains [rank * nchains, (rank + 1) * nchains) and ``run()`` returns every
 rank's chains, all-gathered over RCCL -- the reference's SLURM array,
-job-script.sh:6-8), ``dist_backend`` ("nccl" = RCCL, or "gloo").
+job-script.sh:6-8), ``dist_backend`` ("nccl" = RCCL, or "gloo"),
+``keep_skymap`` (full-sky runs: keep each iteration's CR map on the device
+for the ``skymap`` property; off by default -- the reference's ``run`` returns
+D_l and accept histories only, and without the map store the CR sweep is ~20 %
+faster).
 """
 import time
 
@@ -140,8 +144,9 @@ class GibbsSampler:
                  gibbs_cr=False, rj_step=False, ula=False, *, nchains=1, rng="native", seed=0, fields=None,
                  chain0=0, reference_quirks=True, noise_pol=None, proposal_variances=None,
                  metropolis_blocks=None, n_iter_metropolis=1, mask_path=None, distributed=False,
-                 dist_backend=None):
+                 dist_backend=None, keep_skymap=False):
         self.shard = None
+        self.keep_skymap = bool(keep_skymap)
         if distributed:
             # one process per GPU under torchrun: this rank runs global chains
             # [rank * nchains, (rank + 1) * nchains); run() returns every rank's
@@ -267,7 +272,8 @@ class GibbsSampler:
                                          bins=self.bins, d_alm=d, blocks=blocks, proposal_variances=pv,
                                          rng=self.rng, seed=self.seed, chain0=self.chain0,
                                          quirks=C.GS_QUIRK_ASIS_RECENTRE_CENTERED if self.reference_quirks else 0,
-                                         n_iter_metropolis=self.n_iter_metropolis)
+                                         n_iter_metropolis=self.n_iter_metropolis,
+                                         store_skymap=self.keep_skymap)
         return self._runner
 
     def _masked_cr(self, noise_temp, noise_pol, gibbs_cr=False, n_gibbs=1, alpha=-0.995, overrelaxation=False,
@@ -318,8 +324,9 @@ class GibbsSampler:
 
     @property
     def skymap(self):
-        """Current batched sky map [nchains, F, (L+1)^2] (device tensor)."""
-        return None if self._runner is None else self._runner.skymap()
+        """Current batched sky map [nchains, F, (L+1)^2] (device tensor); None
+        unless the sampler was built with keep_skymap=True."""
+        return None if self._runner is None or self._runner.s is None else self._runner.skymap()
 
 
 class CenteredGibbs(GibbsSampler):
