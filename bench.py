@@ -52,7 +52,7 @@ MASKED_HEAD = ("masked_centered_ula", "masked_asis", "masked_centered_pcg", "mas
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="timed steps (50; masked modes fewer)")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (500; masked: 50; HEAD modes: 5)")
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", default="noncentered",
                     choices=list(HARMONIC) + ["masked"] + list(MASKED_HEAD) + list(SURFACE))
@@ -83,8 +83,11 @@ def parse():
     else:
         a.lmax = a.lmax or (4096 if a.workload == "masked" else 1024)
         a.nside = a.nside or (2048 if a.workload == "masked" else 512)
-        a.steps = a.steps or 50
-        a.warmup = a.warmup if a.warmup is not None else 5
+        # harmonic modes: 500 timed steps (a timed region of ~0.1 s, past the GPU's
+        # clock ramp; the reference's runs are 10^4 iterations), 20 warmup steps
+        harmonic = a.workload != "masked"
+        a.steps = a.steps or (500 if harmonic else 50)
+        a.warmup = a.warmup if a.warmup is not None else (20 if harmonic else 5)
     return a
 
 
@@ -328,8 +331,10 @@ def run_surface(args, ctx):
     main_polarization.py caller uses (gibbs.NonCenteredGibbs, all_sph, TEB,
     native streams): wall time of ``run(dls_init)`` for --steps iterations --
     the runner's replays of captured hipGraph chunks (32 steps each), the
-    per-chunk trace copies and the histories' one transfer to the host
-    included.  A warmup run of --warmup iterations builds the plan first."""
+    per-chunk trace copies and the histories' transfer to the host included.
+    An untimed run of the same --steps iterations first builds the plan and
+    captures the chunk graphs (run() keeps them: a sampler's later runs replay
+    them without capturing)."""
     import torch
     from gibbssampler_amd.gibbs import NonCenteredGibbs
     from gibbssampler_amd.problem import synthetic_problem
@@ -340,10 +345,9 @@ def run_surface(args, ctx):
     nv = P["noise_var"]
     ncg = NonCenteredGibbs(pix, float(nv[0]), float(nv[1]), 0.5, N, L, 12 * N * N, P["proposal_variances"],
                            metropolis_blocks=P["blocks"], polarization=True, bins=P["bins"], all_sph=True,
-                           n_iter=max(args.warmup, 1), rng="native", seed=args.seed, nchains=args.nchains,
+                           n_iter=args.steps, rng="native", seed=args.seed, nchains=args.nchains,
                            fields="TEB", chain0=ctx.chain0)
     ncg.run(P["dls_init"])
-    ncg.n_iter = args.steps
     torch.cuda.synchronize()
     ctx.barrier()
     t0 = time.perf_counter()
@@ -364,7 +368,7 @@ def run_surface(args, ctx):
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (analytic fiducial spectra, d = b s + n in harmonic space, seed 0)",
         "config": {"workload": "noncentered TEB all_sph full-sky through gibbs.NonCenteredGibbs.run (drop-in surface)",
-                   "launch": "run(): replays of captured 32-step hipGraph chunks, histories to the host once",
+                   "launch": "run(): replays of the sampler's captured 32-step hipGraph chunks, each chunk's histories to pinned host memory on a copy stream under the next chunk",
                    "nside": N, "lmax": L, "nfields": 3, "chains_per_gpu": args.nchains,
                    "global_chains": ctx.global_chains, "rng": "native philox4x32-10",
                    "parallelism": f"chains sharded over {ctx.world} GPU(s)"},

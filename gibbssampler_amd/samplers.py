@@ -194,25 +194,49 @@ class BatchedRunner:
             H[0].copy_(self.dl)
         t_steps = []
         if self.rng == "native" and graph_chunk and n_iter > 0:
-            # the iterations as replays of one captured hipGraph of `chunk` steps
+            # the iterations as replays of captured hipGraphs of `chunk` steps
             # (device-side D_l / accept traces, no host synchronisation inside a
-            # chunk); step times = chunk time / steps from events on the stream
+            # chunk); step times = chunk time / steps from events on the stream.
+            # The graphs (and the trace buffers they write) are kept per chunk
+            # length across run() calls: a later run replays them without
+            # capturing again (the device counter base is set before each run)
             chunk = min(int(graph_chunk), n_iter)
             off = 1 if with_start else 0
-            trace = p.zeros(chunk, p.nchains, p.nspec, p.maxbins)
-            acc_tr = p.zeros(chunk, p.nchains, max(p.nacc, 1), dtype=torch.int32)
-            done, gsteps = 0, 0
+            cache = self.__dict__.setdefault("_run_graphs", {})
+            if cache.get("chunk") != chunk:
+                cache.clear()
+                cache["chunk"] = chunk
+                cache["trace"] = p.zeros(chunk, p.nchains, p.nspec, p.maxbins)
+                cache["acc"] = p.zeros(chunk, p.nchains, max(p.nacc, 1), dtype=torch.int32)
+            trace, acc_tr = cache["trace"], cache["acc"]
+            # single-rank runs: each finished chunk of the histories goes to pinned
+            # host memory on a copy stream while the next chunk computes (only the
+            # last chunk's transfer is left after the loop)
+            if gather is None:
+                Hh = torch.empty(H.shape, dtype=H.dtype, pin_memory=True)
+                Ah = torch.empty(A.shape, dtype=A.dtype, pin_memory=True)
+                cs = cache.setdefault("copy_stream", torch.cuda.Stream())
+            p.iteration_counter(True, self.iteration + 1)
+            done = 0
             while done < n_iter:
                 k = min(chunk, n_iter - done)
-                if k != gsteps:
-                    self.capture_steps(k, trace=trace, trace_capacity=chunk, accept_trace=acc_tr)
-                    gsteps = k
+                if k not in cache:
+                    cache[k] = self.capture_steps(k, trace=trace, trace_capacity=chunk, accept_trace=acc_tr)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                self.step()
+                cache[k].replay()
+                self.iteration += k
                 e1.record()
-                H[off + done:off + done + k].copy_(trace[:k])
+                h0, h1 = (0 if done == 0 else off + done), off + done + k
+                H[off + done:h1].copy_(trace[:k])
                 A[done:done + k].copy_(acc_tr[:k])
+                if gather is None:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    cs.wait_event(ev)
+                    with torch.cuda.stream(cs):
+                        Hh[h0:h1].copy_(H[h0:h1], non_blocking=True)
+                        Ah[done:done + k].copy_(A[done:done + k], non_blocking=True)
                 if timings:
                     e1.synchronize()
                     t_steps += [e0.elapsed_time(e1) * 1e-3 / k] * k
@@ -223,6 +247,9 @@ class BatchedRunner:
             self.graph = None
             p.iteration_counter(False)
             n_iter = 0
+            if gather is None:
+                cs.synchronize()
+                H, A = Hh, Ah
         for i in range(n_iter):
             t0 = time.perf_counter() if timings else 0.0
             self.step()

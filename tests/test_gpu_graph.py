@@ -106,6 +106,30 @@ def test_run_after_capture_restarts_cleanly():
     assert g.graph is None
 
 
+@pytest.mark.parametrize("kind", ["noncentered", "centered", "asis"])
+def test_run_reuses_chunk_graphs(kind):
+    """run() keeps its captured chunk graphs (and the trace buffers they write)
+    across calls and streams each chunk's histories to pinned host memory: a
+    second and third run() replaying the kept graphs (chunks 4 + 3 of a 7-step
+    run, then a 5-step run with a 4 + 1 split needing one new capture) give the
+    histories of the eager path, bit for bit."""
+    from gibbssampler_amd.problem import synthetic_problem
+    P = synthetic_problem(64, 32, 3, seed=3)
+    g = _runner(kind, 3)
+    first = g.run(P["dls_init"], 7, graph_chunk=4)
+    again = g.run(P["dls_init"], 7, graph_chunk=4)
+    short = g.run(P["dls_init"], 5, graph_chunk=4)
+    eager = _runner(kind, 3).run(P["dls_init"], 7, graph_chunk=0)
+    n0 = 0 if kind == "asis" else 1
+    for s in eager[0]:
+        np.testing.assert_array_equal(first[0][s], eager[0][s])
+        np.testing.assert_array_equal(again[0][s], eager[0][s])
+        np.testing.assert_array_equal(short[0][s], eager[0][s][:5 + n0])
+        if eager[1] is not None:
+            np.testing.assert_array_equal(again[1][s], eager[1][s])
+            np.testing.assert_array_equal(short[1][s], eager[1][s][:5])
+
+
 @pytest.mark.parametrize("F", [2, 3])
 def test_asis_skymap_without_quirk(F):
     """ASIS with reference_quirks off: the lazily re-centred skymap() is

@@ -10,3 +10,6 @@ TAG=c2; run --no-cpu-baseline --workload centered --nside 256 --lmax 512 --nchai
 TAG=c2store; run --no-cpu-baseline --workload centered --nside 256 --lmax 512 --nchains 1 --steps 500 --time-every 100 --skymap store
 TAG=c4; run --no-cpu-baseline --workload asis
 TAG=surface; run --no-cpu-baseline --workload surface_noncentered
+GS_AB_NOSTORE=1 timeout -k 10 300 python -u tools/step_ab.py noncentered 1024 512 32 50 GS_SWEEP_TW=2 GS_SWEEP_TW=1 GS_SWEEP_TW=4 > gpurun_out/r03_ba_twab.log 2>&1 || { tail -20 gpurun_out/r03_ba_twab.log; exit 1; }
+cat gpurun_out/r03_ba_twab.log
+timeout -k 10 120 python -u tools/prologue_probe.py > gpurun_out/r03_prologue.log 2>&1 || { tail -20 gpurun_out/r03_prologue.log; exit 1; }; cat gpurun_out/r03_prologue.log

@@ -6,7 +6,8 @@ BatchedRunner with K steps captured in a hipGraph; replays alternate.
 usage (GPU box):
   python tools/step_ab.py KIND L NSIDE NCHAINS STEPS "VAR=a" "VAR=b" ...
   e.g.  python tools/step_ab.py centered 512 256 1 200 GS_SWEEP_ROWS=4 GS_SWEEP_ROWS=8
-The r02 sweep-shape A/B (1 tile x 4 chunks vs 4 x 1, GS_SWEEP_TW) ran this way."""
+The r02 sweep-shape A/B (1 tile x 4 chunks vs 4 x 1, GS_SWEEP_TW) ran this way.
+GS_AB_NOSTORE=1 in the environment: runners without the sky-map store."""
 import os
 import sys
 
@@ -27,7 +28,8 @@ def main(kind, L, nside, nch, steps, *settings, rounds=9):
         old = os.environ.get(k)
         os.environ[k] = v
         r = BatchedRunner(kind, P["lmax"], P["nside"], 3, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
-                          blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=5)
+                          blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=5,
+                          store_skymap=os.environ.get("GS_AB_NOSTORE") is None)
         r.init(P["dls_init"])
         r.step()
         r.capture_steps(steps)
