@@ -122,6 +122,9 @@ _SIGS = [
     ("gs_masked_pcg_solve", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_double, ctypes.c_int, c_int_p,
                                            c_double_p, _VP]),
     ("gs_masked_pcg_info", ctypes.c_int, [_VP, c_int_p]),
+    ("gs_masked_pcg_apply", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("gs_masked_rj_accept", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_int, _VP, _VP, _VP]),
     ("gs_masked_center", ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_masked_nc_loglik", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     ("gs_masked_pixel_mh", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [_VP] * 13),

@@ -45,6 +45,7 @@ namespace {
 constexpr double PI = 3.14159265358979323846;
 constexpr uint32_t TAG_AUX_V = 8;
 constexpr uint32_t TAG_MALA_U = 9;
+constexpr uint32_t TAG_RJ_U = 10;   // RJPO accept uniform: Philox(0, 0, TAG_RJ_U, iteration)
 constexpr int SUB_S = 16;
 constexpr int SUB_V_INIT = 255;
 constexpr int SUB_MALA = 200;
@@ -327,6 +328,47 @@ __global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long l
     __syncthreads();
     if (acc)
         for (long long g = threadIdx.x; g < nslot; g += blockDim.x) s0[g] = s1[g];
+}
+
+// RJPO (CenteredGibbs.py:606-674): per-block partials of (rhs - Q x) . (s - x)
+// with y = Q x, in a fixed order (grid-stride per thread, then an LDS tree)
+__global__ __launch_bounds__(RED_BLOCK) void k_rj_dot(long long n, const double* __restrict__ rhs,
+                                                      const double* __restrict__ y, const double* __restrict__ s,
+                                                      const double* __restrict__ x, double* __restrict__ partial) {
+    double a = 0.0;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += stride)
+        a += (rhs[g] - y[g]) * (s[g] - x[g]);
+    __shared__ double red[RED_BLOCK];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int h = RED_BLOCK / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// log_proba = -sum (rhs - Q x) . (s_old - x) (:664-669); accept when
+// log u < log_proba (:670), then s <- x (the PCG solution), else s stays
+__global__ __launch_bounds__(RED_BLOCK) void k_rj_accept(int nblk, const double* __restrict__ partial, long long n,
+                                                         const double* __restrict__ um, uint32_t seed_lo,
+                                                         uint32_t seed_hi, uint32_t chain, uint32_t iter,
+                                                         const double* __restrict__ x, double* __restrict__ s,
+                                                         int32_t* __restrict__ accept, double* __restrict__ log_ratio) {
+    __shared__ int acc;
+    double t[1];
+    block_sums<1>(nblk, partial, 1, t);
+    if (threadIdx.x == 0) {
+        const double lr = -t[0];
+        const double u = um ? um[0] : uniform1(chain_key(seed_lo, seed_hi, chain), 0u, 0u, TAG_RJ_U, iter);
+        acc = log(u) < lr ? 1 : 0;
+        if (accept) *accept = acc;
+        if (log_ratio) *log_ratio = lr;
+    }
+    __syncthreads();
+    if (acc)
+        for (long long g = threadIdx.x; g < n; g += blockDim.x) s[g] = x[g];
 }
 
 // ---------------------------------------------------------------------------
@@ -1368,6 +1410,30 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
     }
     if (iters) *iters = h.it;
     if (rel_residual) *rel_residual = h.bn > 0 ? h.rn / h.bn : 0.0;
+    return 0;
+}
+
+int gs_masked_pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (!dl || !x || !out) return set_error("gs_masked_pcg_apply: null argument");
+    return pcg_apply(c, dl, x, out, nullptr, 0, nullptr, S(stream));
+}
+
+int gs_masked_rj_accept(gs_masked* c, const double* dl, const double* rhs, const double* x, double* s,
+                        const double* um, uint64_t seed, uint32_t iteration, int chain, int32_t* accept,
+                        double* log_ratio, void* stream) {
+    if (!c) return set_error("null masked context");
+    if (!dl || !rhs || !x || !s) return set_error("gs_masked_rj_accept: null argument");
+    const hipStream_t st = S(stream);
+    const long long n = c->F * c->NR;
+    if (pcg_apply(c, dl, x, c->pr, nullptr, 0, nullptr, st)) return -1;          // Q x (fwd_op, :655)
+    const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
+    hipLaunchKernelGGL(k_rj_dot, dim3(nb), dim3(RED_BLOCK), 0, st, n, rhs, c->pr, s, x, c->partial);
+    GS_LAUNCH_CHECK("k_rj_dot");
+    hipLaunchKernelGGL(k_rj_accept, dim3(1), dim3(RED_BLOCK), 0, st, nb, c->partial, n, um,
+                       (uint32_t)(seed & 0xFFFFFFFFu), (uint32_t)(seed >> 32), (uint32_t)chain, iteration, x, s,
+                       accept, log_ratio);
+    GS_LAUNCH_CHECK("k_rj_accept");
     return 0;
 }
 

@@ -277,7 +277,7 @@ class GibbsSampler:
         return self._runner
 
     def _masked_cr(self, noise_temp, noise_pol, gibbs_cr=False, n_gibbs=1, alpha=-0.995, overrelaxation=False,
-                   ula=False, tau=0.02):
+                   ula=False, tau=0.02, rj=False):
         from .masked import MaskedCR
         if not self.polarization:
             raise NotImplementedError("masked temperature-only runs: the reference's TT masked path is broken "
@@ -287,7 +287,7 @@ class GibbsSampler:
         return MaskedCR(self.pix_map, noise_temp, noise_pol, self.bl_gauss, self.lmax, self.nside, mask=self.mask,
                         nfields=self.nfields, gibbs_cr=gibbs_cr, n_gibbs=n_gibbs, alpha=alpha,
                         overrelaxation=overrelaxation, ula=ula, tau=tau, rng=self.rng, seed=self.seed,
-                        chain=self.chain0)
+                        chain=self.chain0, rj=rj)
 
     def _masked_mh_runner(self, kind, cr, cr_kind_):
         from .masked import MaskedMHRunner
@@ -337,9 +337,11 @@ class CenteredGibbs(GibbsSampler):
     def __init__(self, pix_map, noise_temp, noise_pol, beam, nside, lmax, Npix, mask_path=None,
                  polarization=False, bins=None, n_iter=100000, rj_step=False, all_sph=False, gibbs_cr=False,
                  overrelaxation=False, ula=False, **kw):
-        if rj_step and mask_path is not None:
-            raise NotImplementedError("RJPO CR (sample_mask_rj) is disabled at HEAD (CenteredGibbs.py:839) and "
-                                      "needs the qcinv PCG (SURVEY.md 8 row f1)")
+        # rj_step with a mask: HEAD's ladder never reaches sample_mask_rj (its
+        # branch is "and False", CenteredGibbs.py:837), so the run is the PCG
+        # CR, as at HEAD; rj_active=True turns the RJPO branch back on.
+        # constrained_sampler.sample_mask_rj is callable either way.
+        rj_active = bool(kw.pop("rj_active", False))
         self.n_gibbs = int(kw.pop("n_gibbs", 1))
         self.alpha = float(kw.pop("alpha", -0.995))
         self.tau = float(kw.pop("tau", 0.02))
@@ -360,7 +362,7 @@ class CenteredGibbs(GibbsSampler):
         if self.mask is not None:
             self.constrained_sampler = self._masked_cr(noise_temp, noise_pol, gibbs_cr=gibbs_cr, n_gibbs=self.n_gibbs,
                                                        alpha=self.alpha, overrelaxation=overrelaxation, ula=ula,
-                                                       tau=self.tau)
+                                                       tau=self.tau, rj=rj_step and rj_active)
         else:
             self.constrained_sampler = CenteredConstrainedRealization(self)
         self.cls_sampler = CenteredClsSampler(self)

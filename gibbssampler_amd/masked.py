@@ -40,7 +40,7 @@ class MaskedCR:
 
     def __init__(self, pix_map, noise_temp, noise_pol, bl, lmax, nside, mask=None, nfields=2, gibbs_cr=True,
                  n_gibbs=1, alpha=-0.995, overrelaxation=False, ula=False, tau=0.02, rng="replay", seed=0, chain=0,
-                 device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000):
+                 device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000, rj=False):
         if nfields not in (1, 2, 3):
             raise ValueError("nfields must be 1 (T), 2 (EB, the reference) or 3 (TEB)")
         self.lib = _capi.load()
@@ -48,6 +48,9 @@ class MaskedCR:
         self.Npix = 12 * self.nside ** 2
         self.NR = (self.L + 1) ** 2
         self.gibbs_cr, self.overrelaxation, self.ula = bool(gibbs_cr), bool(overrelaxation), bool(ula)
+        # rj: the RJPO branch of the ladder (CenteredGibbs.py:837-838, disabled at
+        # HEAD by "and False"; sample_mask_rj itself is always callable)
+        self.rj = bool(rj)
         self.n_gibbs, self.alpha, self.tau = int(n_gibbs), float(alpha), float(tau)
         self.pcg_accuracy, self.pcg_maxiter = float(pcg_accuracy), int(pcg_maxiter)   # CenteredGibbs.py:279-283
         self.pcg_iterations = []
@@ -219,6 +222,39 @@ class MaskedCR:
         self.pcg_syncs.append(syncs.value)          # host synchronisations of this solve (one per batch)
         return x
 
+    def pcg_apply(self, dl, x, out=None):
+        """out = Q x, the PCG system operator (qcinv fwd_op, CenteredGibbs.py:631,655)."""
+        out = torch.empty_like(x) if out is None else out
+        _capi.check(self.lib.gs_masked_pcg_apply(self.handle, _capi.ptr(dl), _capi.ptr(x), _capi.ptr(out),
+                                                 _capi.stream_ptr()), "gs_masked_pcg_apply")
+        return out
+
+    def rj_step(self, dl, s, iteration=None):
+        """RJPO CR on device tensors (sample_mask_rj, CenteredGibbs.py:606-674), s
+        [F, NR] updated in place: the PCG right-hand side with fresh fluctuations
+        (the draws of sample_mask, :622-643), the solve started from -s (:645-650),
+        then log_proba = -sum (rhs - Q x) . (s - x) and log u < log_proba on the
+        device (:652-672).  Replay: the uniform is np.random.uniform() after the
+        normals, the reference's order."""
+        it = self.iteration if iteration is None else int(iteration)
+        rhs = self.pcg_rhs(dl, iteration=it)
+        um = None
+        if self.rng == "replay":
+            um = torch.tensor([np.random.uniform()], dtype=torch.float64, device=self.device)
+        x = self.pcg_solve(dl, rhs, x=-s)
+        _capi.check(self.lib.gs_masked_rj_accept(self.handle, _capi.ptr(dl), _capi.ptr(rhs), _capi.ptr(x),
+                                                 _capi.ptr(s), _capi.ptr(um), self.seed, it, self.chain,
+                                                 _capi.ptr(self._acc), _capi.ptr(self._lr), _capi.stream_ptr()),
+                    "gs_masked_rj_accept")
+        return s
+
+    def sample_mask_rj(self, all_dls, s_old):
+        """CenteredGibbs.py:606-674: (map, 1) when the RJPO proposal is accepted,
+        (s_old, 0) otherwise."""
+        s = self._s(s_old)
+        self.rj_step(self._dl(all_dls), s)
+        return self._out(s), int(self._acc.item())
+
     def tt_fullsky(self, dl, noncentered=False, iteration=None, out=None):
         """temperature full-sky CR from the pixel map (gs_masked_tt_fullsky):
         CenteredGibbs.py:108-132 or NonCenteredGibbs.py:22-38; replay draws
@@ -253,22 +289,28 @@ class MaskedCR:
             return self.sample_gibbs_change_variable(all_dls, s_old)
         if self.gibbs_cr and self.ula:
             return self._run(_capi.GS_MCR_AUX_MALA, all_dls, s_old)
+        if self.rj:
+            return self.sample_mask_rj(all_dls, s_old)
         if self.ula:
             return self.sample_mala(all_dls, s_old)
         return self.sample_mask(all_dls)
 
 
 KIND_PCG = -1     # sample_mask (f1), driven from the host (CG loop)
+KIND_RJ = -2      # sample_mask_rj (RJPO: the PCG from -s_old + an accept step)
 
 
-def cr_kind(gibbs_cr, overrelaxation, ula):
-    """The flag ladder of CenteredGibbs.py:828-850 for a masked run with a map."""
+def cr_kind(gibbs_cr, overrelaxation, ula, rj=False):
+    """The flag ladder of CenteredGibbs.py:828-850 for a masked run with a map
+    (rj: the RJPO branch of :837-838, which HEAD disables)."""
     if gibbs_cr and overrelaxation:
         return _capi.GS_MCR_OVERRELAX
     if gibbs_cr and not ula:
         return _capi.GS_MCR_AUX
     if gibbs_cr and ula:
         return _capi.GS_MCR_AUX_MALA
+    if rj:
+        return KIND_RJ
     if ula:
         return _capi.GS_MCR_MALA
     return KIND_PCG
@@ -284,7 +326,7 @@ class MaskedRunner:
     def __init__(self, cr, bins, kind=None):
         from .engine import GibbsPlan
         self.cr = cr
-        self.kind = cr_kind(cr.gibbs_cr, cr.overrelaxation, cr.ula) if kind is None else kind
+        self.kind = cr_kind(cr.gibbs_cr, cr.overrelaxation, cr.ula, cr.rj) if kind is None else kind
         F = cr.F
         self.spectra = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
         self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
@@ -319,6 +361,9 @@ class MaskedRunner:
             if self.kind == KIND_PCG:
                 s = cr.pcg_solve(dl, cr.pcg_rhs(dl, iteration=it))
                 acc.append(1)
+            elif self.kind == KIND_RJ:
+                cr.rj_step(dl, s, iteration=it)
+                acc.append(int(cr._acc.item()))
             else:
                 cr.step(self.kind, dl, s, iteration=it)
                 acc.append(int(cr._acc.item()))

@@ -289,6 +289,18 @@ int gs_masked_pcg_rhs(gs_masked* ctx, const double* dl, const double* zv, const 
 int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
                         int maxiter, int* iters, double* rel_residual, void* stream);
 int gs_masked_pcg_info(const gs_masked* ctx, int* host_syncs);
+/* out = Q x, the PCG system operator (C^+ + b A^T N^-1 A b) applied to x
+ * (qcinv opfilt_pp fwd_op, CenteredGibbs.py:631,655). */
+int gs_masked_pcg_apply(gs_masked* ctx, const double* dl, const double* x, double* out, void* stream);
+/* RJPO accept step (sample_mask_rj, CenteredGibbs.py:606-674): x is the PCG
+ * solution of Q x = rhs started from -s (gs_masked_pcg_solve with x = -s as the
+ * guess, :645-650); log_ratio = -sum (rhs - Q x) . (s - x) (:657-669), accept
+ * when log u < log_ratio (:670) and then s <- x.  um: device [1] replay uniform
+ * or NULL for the native stream (Philox(0, 0, TAG_RJ_U, iteration)); accept,
+ * log_ratio: device int32 [1] / double [1] or NULL.  Nothing is read back. */
+int gs_masked_rj_accept(gs_masked* ctx, const double* dl, const double* rhs, const double* x, double* s,
+                        const double* um, uint64_t seed, uint32_t iteration, int chain, int32_t* accept,
+                        double* log_ratio, void* stream);
 /* f2: pixel-domain non-centered likelihood (NonCenteredGibbs.py:333-355):
  * lik = -1/2 sum_pix N^-1 (d - A b C^1/2(D) s_nc)^2 (device double).
  * gs_masked_center: out = C^1/2 in (dir = +1) or C^+1/2 in (dir = -1) per slot

@@ -37,6 +37,7 @@ from . import sht as O
 FOURPI = 4.0 * math.pi
 TAG_AUX_V = 8        # pixel normals of v | s; c0 = pixel, c1 = map (0 T, 1 Q, 2 U)
 TAG_MALA_U = 9       # MALA accept uniform
+TAG_RJ_U = 10        # RJPO accept uniform (c0 = c1 = 0)
 SUB_S = 16           # CR substep base of the s | v draws: SUB_S + 2k (+1: second OR draw)
 SUB_V_INIT = 255     # substep of the over-relaxation's initial v | s
 SUB_MALA = 200       # CR substep of the MALA proposal normals (+ call index)
@@ -77,9 +78,9 @@ class NativeDraws:
     def slot_normals(self, nfields, nreal, substep=0):
         return np.stack([H.cr_normals(self.seed, self.chain, self.it, substep, f, self.L) for f in range(nfields)])
 
-    def uniform(self, substep=0):
+    def uniform(self, substep=0, tag=TAG_MALA_U):
         k0, k1 = H.chain_key(self.seed, self.chain)
-        return H._uniform1(k0, k1, 0, substep, TAG_MALA_U, self.it)
+        return H._uniform1(k0, k1, 0, substep, tag, self.it)
 
 
 class MaskedModel:
@@ -380,6 +381,24 @@ def pcg_sample(mm, dl_unbinned, draws, tol=1e-12, maxiter=2000):
     rhs = mm.second_part_grad() + pcg_fluctuation(mm, dl_unbinned, z_pix, z_slot)
     x, it = pcg_solve(mm, dl_unbinned, rhs, tol, maxiter)
     return x, 1, it
+
+
+def rj_sample(mm, dl_unbinned, draws, s_old, tol=1e-12, maxiter=2000):
+    """sample_mask_rj (CenteredGibbs.py:606-674): the rhs of sample_mask (same
+    draws, :622-643), the PCG started from -s_old (:645-650), then
+    log_proba = -sum (rhs - Q x) . (s_old - x) (:652-669) and accept when
+    log u < log_proba (:670; the uniform drawn after the normals).
+    Returns (map, accept, log_proba, CG iterations)."""
+    z_pix = draws.pixel_normals(mm.F, mm.Npix, maps=mm.rows, substep=SUB_PCG_V)
+    z_slot = draws.slot_normals(mm.F, (mm.L + 1) ** 2, substep=SUB_PCG_S)
+    rhs = mm.second_part_grad() + pcg_fluctuation(mm, dl_unbinned, z_pix, z_slot)
+    u = draws.uniform(tag=TAG_RJ_U)
+    x, it = pcg_solve(mm, dl_unbinned, rhs, tol, maxiter, x0=-np.asarray(s_old, dtype=np.float64))
+    r = rhs - pcg_operator(mm, dl_unbinned, x)
+    lp = -float(np.sum(r * (s_old - x)))
+    if math.log(u) < lp:
+        return x, 1, lp, it
+    return np.array(s_old, dtype=np.float64), 0, lp, it
 
 
 # ----------------------------------------------------------------------------

@@ -245,6 +245,46 @@ def test_f1_pcg_sample_native_vs_oracle(F):
         _close(s[f], want[k])
 
 
+@pytest.mark.parametrize("F,rng", [(2, "native"), (3, "native"), (2, "replay")])
+def test_rj_sample_vs_oracle(F, rng):
+    """sample_mask_rj (CenteredGibbs.py:606-674) against the oracle restatement
+    (oracle/masked.py: rj_sample; the reference's RJPO needs qcinv, absent here,
+    so this row is pinned by the oracle only): the PCG started from -s_old and
+    cut at 6 iterations (tol 0), so the log ratio -sum (rhs - Q x).(s_old - x)
+    is macroscopic; the map, the log ratio and the decision agree."""
+    import torch
+    from gibbssampler_amd.masked import MaskedCR
+    N, L, mask, maps, ntemp, npol, bl, dl, s0 = _teb_problem(seed=11)
+    seed, it, chain = 77, 3, 1
+    cr = MaskedCR({"T": maps[0], "Q": maps[1], "U": maps[2]}, ntemp, npol, bl, L, N, mask=mask, nfields=F,
+                  gibbs_cr=False, ula=False, rng=rng, seed=seed, chain=chain, pcg_accuracy=0.0, pcg_maxiter=6, rj=True)
+    cr.iteration = it
+    rows = (1, 2) if F == 2 else (0, 1, 2)
+    fields = ("EE", "BB") if F == 2 else ("TT", "EE", "BB")
+    s_in = {k: s0[r] for k, r in zip(fields, rows)}
+    if rng == "replay":
+        np.random.seed(5)
+    s, acc = cr.sample(dl, s_in)                # the ladder's RJ branch (rj=True)
+    assert cr.pcg_iterations[-1] == 6
+    mm = MK.MaskedModel(L, N, F, bl, maps, np.stack([mask / ntemp, mask / npol, mask / npol]))
+    spec = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
+    draws = MK.NativeDraws(seed, chain, it, L, 12 * N * N) if rng == "native" else MK.ReplayDraws(5)
+    want, wacc, lp, wit = MK.rj_sample(mm, np.stack([dl[k] for k in spec]), draws, np.stack([s0[r] for r in rows]),
+                                       tol=0.0, maxiter=6)
+    assert wit == 6
+    assert abs(cr.last_log_ratio() - lp) <= 1e-8 * max(1.0, abs(lp))
+    assert acc == wacc
+    for k, f in enumerate(fields):
+        _close(s[f], want[k])
+    # the same step through the runner kind (device state in place, no host copy)
+    s_t = torch.from_numpy(np.ascontiguousarray(np.stack([s0[r] for r in rows]))).cuda()
+    dl_t = torch.from_numpy(np.ascontiguousarray(np.stack([dl[k] for k in spec]))).cuda()
+    if rng == "replay":
+        np.random.seed(5)
+    cr.rj_step(dl_t, s_t, iteration=it)
+    np.testing.assert_array_equal(s_t.cpu().numpy(), np.stack([s[f] for f in fields]))
+
+
 def test_f1_pcg_driver_replay_vs_oracle(g):
     """CenteredGibbs(mask, gibbs_cr=False, ula=False): PCG init CR + PCG CR +
     invgamma draws (HEAD's default masked path) against the oracle chain."""
