@@ -40,9 +40,11 @@ for the ``skymap`` property; off by default -- the reference's ``run`` returns
 D_l and accept histories only, and without the map store the CR sweep is ~20 %
 faster).
 """
+import os
 import time
 
 import numpy as np
+import torch
 
 from .problem import gauss_beam
 from . import _capi as C
@@ -304,17 +306,38 @@ class GibbsSampler:
 
     def _run_common(self, dls_init):
         runner = self._make_runner()
-        init = dls_init if isinstance(dls_init, dict) else {self.spectra[0]: dls_init}
+        resume, self._resume_state = getattr(self, "_resume_state", None), None
+        init = dls_init if isinstance(dls_init, dict) or resume is not None else {self.spectra[0]: dls_init}
         h, acc, t = runner.run(init, self.n_iter, timings=True,
-                               gather=self.shard.gather if self.shard is not None else None)
+                               gather=self.shard.gather if self.shard is not None else None, resume=resume)
         h = {s: self._squeeze(v) for s, v in h.items()}
         if acc is not None:
             acc = {s: self._squeeze(v) for s, v in acc.items()}
         return h, acc, t
 
-    def run(self, dls_init):
-        """GibbsSampler.py:183-192."""
+    def run(self, dls_init, resume=None):
+        """GibbsSampler.py:183-192.  resume: a checkpoint() state (or the path of
+        a save_checkpoint file) to continue from instead of dls_init -- full-sky
+        (all_sph) runs; the histories then start at the checkpoint's D_l."""
+        if resume is not None:
+            if self.mask is not None or getattr(self, "tt_pixel", False):
+                raise NotImplementedError("resume: full-sky (all_sph) runs only")
+            self._resume_state = self.load_checkpoint(resume) if isinstance(resume, (str, os.PathLike)) else resume
         return self.run_polarization(dls_init) if self.polarization else self.run_temperature(dls_init)
+
+    # -- checkpoint / resume (SURVEY.md 5) ---------------------------------------------
+    def checkpoint(self):
+        """State of the chains after the last run (samplers.BatchedRunner.state_dict)."""
+        if self._runner is None:
+            raise RuntimeError("checkpoint: nothing has run yet")
+        return self._runner.state_dict()
+
+    def save_checkpoint(self, path):
+        torch.save(self.checkpoint(), path)
+
+    @staticmethod
+    def load_checkpoint(path):
+        return torch.load(path, weights_only=True)
 
     def run_polarization(self, dls_init):
         raise NotImplementedError

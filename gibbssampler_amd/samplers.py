@@ -79,6 +79,54 @@ class BatchedRunner:
             p.cr_sweep(self.d, params, z=z, seed=self.seed, iteration=INIT_ITER, s_out=self.s,
                        store=self.s is not None)
 
+    # -- checkpoint / resume -----------------------------------------------------------
+    def state_dict(self):
+        """The chains' whole state between iterations, as host tensors and plain
+        values (``torch.save`` / ``torch.load(weights_only=True)`` round-trip it):
+        D_l, the last accept flags, ASIS's D_l before the MH, the sky map when
+        stored, and the iteration count.  The native streams are counter-based
+        (seed, chain id, iteration), so a restored runner continues the same
+        trajectory bit for bit.  Replay runs draw from numpy's global RNG: its
+        state is saved too (``numpy_rng_*``) and restored by load_state_dict."""
+        if self.dl is None:
+            raise RuntimeError("state_dict: the runner has not been initialised (run() or init() first)")
+        p = self.plan
+        st = {"kind": self.kind, "rng": self.rng, "seed": self.seed, "iteration": int(self.iteration),
+              "chain0": p.chain0, "nchains": p.nchains, "lmax": p.L, "nfields": p.F,
+              "dl": self.dl.cpu().clone(), "dl_tmp": self.dl_tmp.cpu().clone(), "accept": self.accept.cpu().clone(),
+              "s": None if self.s is None else self.s.cpu().clone()}
+        if self.rng == "replay":
+            name, keys, pos, has_gauss, cached = np.random.get_state()
+            st.update(numpy_rng_keys=torch.from_numpy(np.asarray(keys, dtype=np.int64)), numpy_rng_pos=int(pos),
+                      numpy_rng_has_gauss=int(has_gauss), numpy_rng_cached=float(cached))
+        return st
+
+    def load_state_dict(self, st):
+        """Restore a state_dict() (same kind, chains, l_max, fields and RNG mode);
+        the device buffers are kept (a kept graph still points at them)."""
+        p = self.plan
+        want = {"kind": self.kind, "rng": self.rng, "chain0": p.chain0, "nchains": p.nchains, "lmax": p.L,
+                "nfields": p.F}
+        bad = {k: (st.get(k), v) for k, v in want.items() if st.get(k) != v}
+        if bad:
+            raise ValueError(f"load_state_dict: state does not match this runner: {bad}")
+        dl = st["dl"].to(self.dl_tmp.device)
+        if self.dl is None:
+            self.dl = dl.clone()
+        else:
+            self.dl.copy_(dl)
+        self.dl_tmp.copy_(st["dl_tmp"])
+        self.accept.copy_(st["accept"])
+        if self.s is not None and st.get("s") is not None:
+            self.s.copy_(st["s"])
+        self.seed = int(st["seed"])
+        self.iteration = int(st["iteration"])
+        self.graph = None
+        p.iteration_counter(False)
+        if self.rng == "replay" and "numpy_rng_keys" in st:
+            np.random.set_state(("MT19937", st["numpy_rng_keys"].numpy().astype(np.uint32), st["numpy_rng_pos"],
+                                 st["numpy_rng_has_gauss"], st["numpy_rng_cached"]))
+
     # -- hipGraph: capture one whole iteration, replay it per step ------------------
     def capture_graph(self, trace=None, trace_capacity=None):
         """Capture one iteration (plus an optional device-side trace record) in a
@@ -180,13 +228,18 @@ class BatchedRunner:
         self.iteration = it
 
     # -- a whole run --------------------------------------------------------------------
-    def run(self, dls_init, n_iter, timings=False, gather=None, graph_chunk=32):
+    def run(self, dls_init, n_iter, timings=False, gather=None, graph_chunk=32, resume=None):
         """n_iter iterations from dls_init; returns (histories, accepts[, step
         times]).  gather: ShardContext.gather of a torchrun job -- the device
         histories of every rank are all-gathered along the chain axis (global
-        chain order) before the one copy to the host."""
+        chain order) before the one copy to the host.  resume: a state_dict()
+        to continue from instead of starting at dls_init (the history's first
+        row is then the restored D_l, i.e. the previous run's last row)."""
         p = self.plan
-        self.init(dls_init)
+        if resume is not None:
+            self.load_state_dict(resume)
+        else:
+            self.init(dls_init)
         with_start = self.kind != "asis"
         H = p.zeros(n_iter + (1 if with_start else 0), p.nchains, p.nspec, p.maxbins)
         A = p.zeros(n_iter, p.nchains, max(p.nacc, 1), dtype=torch.int32)
@@ -223,12 +276,19 @@ class BatchedRunner:
                 if k not in cache:
                     cache[k] = self.capture_steps(k, trace=trace, trace_capacity=chunk, accept_trace=acc_tr)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                # the trace record of iteration it goes to slot (it - 1) % chunk: a
+                # run resumed at an iteration that is not a multiple of chunk starts
+                # mid-ring
+                r0 = self.iteration % chunk
                 e0.record()
                 cache[k].replay()
                 self.iteration += k
                 e1.record()
                 h0, h1 = (0 if done == 0 else off + done), off + done + k
-                H[off + done:h1].copy_(trace[:k])
+                if r0 == 0:
+                    H[off + done:h1].copy_(trace[:k])
+                else:
+                    H[off + done:h1].copy_(trace[(torch.arange(k) + r0) % chunk])
                 A[done:done + k].copy_(acc_tr[:k])
                 if gather is None:
                     ev = torch.cuda.Event()
