@@ -101,6 +101,14 @@ struct gs_plan {
     uint32_t* fsync = nullptr;
     int ncu = 0;                     // compute units of the device
     bool centered_fused = false;     // GS_CENTERED_FUSED at plan creation: the one-launch step (measured slower)
+    // few-chain centered steps: the C_l draw's random variates (Gamma / normal)
+    // depend on the bins' degrees of freedom and the counters only, so extra
+    // workgroups of the latency-form sweep draw them while the sweep runs, and
+    // the draw after the statistics does the algebra alone.  (A side-stream
+    // kernel as a parallel graph branch was measured first: 35.5 against 18.3
+    // us per configs[1] step -- the branch's cross-queue synchronisation.)
+    bool cls_pre = false;
+    double* cls_var = nullptr;       // [nchains][nspec][maxbins][3]
     bool iter_dev_on = false;
     const uint32_t* itp() const { return iter_dev_on ? iter_dev : nullptr; }
     // graph-captured steps (gs_graph_step): this step's offset from the device
@@ -403,10 +411,11 @@ __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, 
                                                  double* __restrict__ s,
                                                  double* __restrict__ partials, uint32_t seed_lo, uint32_t seed_hi,
                                                  uint32_t iter, uint32_t substep, int chain0, const SweepOp& op,
-                                                 double* tab, double* red) {
+                                                 double* tab, double* red, int bid = -1, int nwg = 0) {
     constexpr int NS = SweepAcc<F>::NS;
-    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    if (bid < 0) { bid = blockIdx.x; nwg = gridDim.x; }
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int pair = wg / nchains;
     const int chain = wg % nchains;
     const int lane = threadIdx.x & 63;
@@ -499,21 +508,41 @@ __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, 
     sweep_partials_store<NS, SC1>(acc, tw, w, lane, t < ntile && (cw * gc.y) * tm <= lhi, po, red);
 }
 
+// the C_l draw's variates computed by extra workgroups of the latency-form
+// sweep (few-chain centered steps): n workgroups ahead of the sweep's, 256
+// items (chain, spectrum, bin) each; the draw after the statistics reads them
+struct ClsPre {
+    int n = 0;                       // extra workgroups (0: none)
+    int nitem = 0;                   // nchains * nspec * maxbins
+    int nspec = 0, maxbins = 0;
+    const int* bins = nullptr;
+    const int* nbins = nullptr;
+    double* out = nullptr;           // [nchains][nspec][maxbins][3]
+};
+template <int F>
+__device__ void cls_variates_item(const ClsPre& cp, int item, uint32_t seed_lo, uint32_t seed_hi, uint32_t iter,
+                                  int chain0);
+
 template <int F, int ZM, bool STORE, int PRE = 0>
 __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
                                                   const double* __restrict__ params, const double* __restrict__ z,
                                                   double* __restrict__ s, double* __restrict__ partials,
                                                   uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, uint32_t substep,
-                                                  int chain0, SweepOp op) {
+                                                  int chain0, SweepOp op, ClsPre cp) {
     const uint32_t iter = itarg.get();
     constexpr int NS = SweepAcc<F>::NS;
     __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
     __shared__ double red[3 * NS * WAVE];           // chunk-wave sums of tw < 4 shapes
     if constexpr (PRE > 0) {
         static_assert(ZM == 0, "latency form: native draws only");
+        if ((int)blockIdx.x < cp.n) {
+            cls_variates_item<F>(cp, blockIdx.x * blockDim.x + threadIdx.x, seed_lo, seed_hi, iter, chain0);
+            return;
+        }
         cr_sweep_latency<F, STORE, PRE>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo,
-                                        seed_hi, iter, substep, chain0, op, tab, red);
+                                        seed_hi, iter, substep, chain0, op, tab, red, (int)blockIdx.x - cp.n,
+                                        (int)gridDim.x - cp.n);
         return;
     }
     if constexpr (ZM == 0) {
@@ -683,12 +712,34 @@ __device__ __forceinline__ void ticket_advance(uint32_t* counter, uint32_t nblk,
     }
 }
 
+// the random variates of bin b's draw, which need only the bin's degrees of
+// freedom and the counters (not the statistics): the TEB block's two Gamma
+// variates and the Bartlett normal, or the inverse-Gamma draw 1 / Gamma.
+// Computed here (in the draw, or ahead of it by k_cls_variates on a side
+// stream while the sweep runs) by the same code, so either way gives the same bits.
+template <int F>
+__device__ __forceinline__ void cls_variates(int sp, int b, int l0, int l1, Key key, uint32_t iter, double (&v)[3]) {
+    v[0] = v[1] = v[2] = 0.0;
+    if ((F == 3) && (sp != 2)) {
+        if (b >= 2) {
+            const double nu = (double)(l1 * l1 - l0 * l0) - 3.0;
+            gamma_mt_pair(0.5 * nu, 0.5 * (nu - 1.0), key, b, 16, 17, iter, 0, v[0], v[1]);
+            v[2] = normal1(key, b, 0, TAG_IW_N, iter);
+        }
+    } else {
+        const double expo = (double)(l1 * l1 - l0 * l0) / 2.0;
+        const double alpha = b == 0 ? 1.0 : expo - 1.0;
+        v[0] = b < 2 ? 0.0 : 1.0 / gamma_mt(alpha, key, b, sp, iter, 0);
+    }
+}
+
 template <int F, bool SC1 = false>
 __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, int maxbins, const int* __restrict__ bins,
                                               const int* __restrict__ nbins_arr, const double* stats,
                                               const double* __restrict__ variates, uint32_t seed_lo, uint32_t seed_hi,
                                               uint32_t iter, int chain0, double* __restrict__ dl_out,
-                                              double* __restrict__ trace, int cap, int nchains) {
+                                              double* __restrict__ trace, int cap, int nchains,
+                                              const double* __restrict__ pre = nullptr) {
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
     const int Lp1 = L + 1;
@@ -727,12 +778,14 @@ __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, i
                 va[j] = ld_stat<SC1>(st + 0 * Lp1 + l); vd[j] = ld_stat<SC1>(st + 1 * Lp1 + l);
                 vc[j] = ld_stat<SC1>(st + 3 * Lp1 + l);
             }
-            const double nu = (double)(l1 * l1 - l0 * l0) - 3.0;
-            double g1 = 0.0, g2 = 0.0, n = 0.0;
-            if (b >= 2) {
-                gamma_mt_pair(0.5 * nu, 0.5 * (nu - 1.0), key, b, 16, 17, iter, 0, g1, g2);
-                n = normal1(key, b, 0, TAG_IW_N, iter);
+            double vr[3];
+            if (pre) {
+                const double* q = pre + (((long long)chain * NSP + sp) * maxbins + b) * 3;
+                vr[0] = q[0]; vr[1] = q[1]; vr[2] = q[2];
+            } else {
+                cls_variates<F>(sp, b, l0, l1, key, iter, vr);
             }
+            const double g1 = vr[0], g2 = vr[1], n = vr[2];
             double a = 0.0, dd = 0.0, c = 0.0;
             for (int lg = l0; lg < l1; lg += 8) {
                 if (lg > l0) {
@@ -790,11 +843,10 @@ __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, i
         double v[G];
 #pragma unroll
         for (int j = 0; j < G; ++j) v[j] = ld_stat<SC1>(st + ssrow * Lp1 + max(min(l0 + j, l1 - 1), 0));
-        const double expo = (double)(l1 * l1 - l0 * l0) / 2.0;
-        const double alpha = b == 0 ? 1.0 : expo - 1.0;
         double X;
         if (variates) X = variates[((long long)chain * NSP + sp) * maxbins + b];
-        else X = b < 2 ? 0.0 : 1.0 / gamma_mt(alpha, key, b, sp, iter, 0);
+        else if (pre) X = pre[(((long long)chain * NSP + sp) * maxbins + b) * 3];
+        else { double vr[3]; cls_variates<F>(sp, b, l0, l1, key, iter, vr); X = vr[0]; }
         double beta = 0.0;
         for (int lg = l0; lg < l1; lg += G) {
             if (lg > l0) {
@@ -821,12 +873,28 @@ __global__ __launch_bounds__(64) void k_cls_draw(int L, int nchains, int maxbins
                                                  const double* __restrict__ variates, uint32_t seed_lo,
                                                  uint32_t seed_hi, IterArg itarg, int chain0,
                                                  double* __restrict__ dl_out, double* __restrict__ trace, int cap,
-                                                 uint32_t* __restrict__ counter, uint32_t adv) {
+                                                 uint32_t* __restrict__ counter, uint32_t adv,
+                                                 const double* __restrict__ pre) {
     const uint32_t iter = itarg.get();
     cls_draw_body<F>(blockIdx.x, blockIdx.y, blockIdx.z * blockDim.x + threadIdx.x, L, maxbins, bins, nbins_arr,
                      stats, variates, seed_lo, seed_hi, iter, chain0, dl_out, trace,
-                     cap, nchains);
+                     cap, nchains, pre);
     if (counter) ticket_advance(counter, gridDim.x * gridDim.y * gridDim.z, adv);
+}
+
+// one (chain, spectrum, bin) item of the draw's variates (the sweep's extra
+// workgroups); bins past a spectrum's count are not drawn
+template <int F>
+__device__ void cls_variates_item(const ClsPre& cp, int item, uint32_t seed_lo, uint32_t seed_hi, uint32_t iter,
+                                  int chain0) {
+    if (item >= cp.nitem) return;                   // the last workgroup's tail
+    const int b = item % cp.maxbins, sp = (item / cp.maxbins) % cp.nspec, chain = item / (cp.maxbins * cp.nspec);
+    if (b >= cp.nbins[sp] || ((F == 3) && sp != 0 && sp != 2)) return;
+    const int* be = cp.bins + sp * (cp.maxbins + 1);
+    double v[3];
+    cls_variates<F>(sp, b, be[b], be[b + 1], chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain)), iter, v);
+    double* q = cp.out + (long long)item * 3;
+    q[0] = v[0]; q[1] = v[1]; q[2] = v[2];
 }
 
 
@@ -2114,6 +2182,11 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->fsync, 4);
     if (hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) p->ncu = 0;
     p->centered_fused = getenv("GS_CENTERED_FUSED") != nullptr;
+    {
+        const char* e = getenv("GS_CLS_PRE");
+        p->cls_pre = e ? std::atoi(e) != 0 : p->nchains <= 4;
+    }
+    if (p->cls_pre) rc |= dev_alloc(&p->cls_var, nc * p->nspec * maxbins * 3);
     if (rc) { gs_plan_destroy(p); return -1; }
     *out = p;
     return 0;
@@ -2122,7 +2195,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
     void* bufs[] = {p->iter_dev, p->fsync, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
-                    p->params, p->stats, p->prop, p->logr, p->dl_tmp};
+                    p->params, p->stats, p->prop, p->logr, p->dl_tmp, p->cls_var};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -2281,23 +2354,34 @@ static int stats_finish(gs_plan* p, double* stats, void* stream) {
 
 static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, const double* z, uint64_t seed,
                         uint32_t iteration, uint32_t substep, double* s_out, double* stats, bool given,
-                        void* stream, bool finish = true, int pmode = -1, const double* dl = nullptr) {
+                        void* stream, bool finish = true, int pmode = -1, const double* dl = nullptr,
+                        bool* cls_pre_done = nullptr) {
     if (check_plan(p)) return -1;
     if (!d_alm || !stats || (!given && !params && pmode < 0) || (given && !s_out) || (pmode >= 0 && !dl))
         return set_error("gs_cr_sweep: null argument");
     const SweepOp op{pmode, p->maxbins, dl, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2]};
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    const dim3 g((unsigned)((long long)p->nchains * p->npair)), b(256);
+    dim3 g((unsigned)((long long)p->nchains * p->npair)), b(256);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing_begin(p, S(stream), &e0, &e1)) return -1;
     const bool rep = z != nullptr, st = s_out != nullptr;
     // latency form (all loads first) for few chains with short tasks; the
     // throughput form otherwise (more chains: its registers buy occupancy)
     const bool lat = pmode >= 0 && p->rows_per_task <= 4 && !given && !rep && p->sweep_latency;
+    const ClsPre none{};
+    if (cls_pre_done) *cls_pre_done = false;
     if (lat) {
+        ClsPre cp{};
+        if (cls_pre_done && p->cls_pre) {
+            cp.nspec = p->nspec; cp.maxbins = p->maxbins; cp.bins = p->bins; cp.nbins = p->meta; cp.out = p->cls_var;
+            cp.nitem = p->nchains * p->nspec * p->maxbins;
+            cp.n = (cp.nitem + 255) / 256;
+            g.x += cp.n;
+            *cls_pre_done = true;
+        }
 #define GS_SWL(FF, SS) hipLaunchKernelGGL((k_cr_sweep<FF, 0, SS, 4>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                           p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,    \
-                                          s_out, p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op)
+                                          s_out, p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op, cp)
 #define GS_SWL2(FF) do { if (st) GS_SWL(FF, true); else GS_SWL(FF, false); } while (0)
         if (p->F == 1) GS_SWL2(1); else if (p->F == 2) GS_SWL2(2); else GS_SWL2(3);
 #undef GS_SWL2
@@ -2310,7 +2394,7 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
                                              p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,   \
                                              s_out,                                                                   \
                                              p->partials, slo, shi, p->ita(iteration), substep, p->chain0, \
-                                             op)
+                                             op, none)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
                         else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
                         else GS_SW(FF, 0, false); } while (0)
@@ -2333,19 +2417,20 @@ int gs_sweep_stats(gs_plan* p, const double* d_alm, const double* s, double* sta
 
 static int cls_draw_launch(gs_plan* p, const double* stats, const double* variates, uint64_t seed,
                            uint32_t iteration, double* dl_out, double* trace, int cap, uint32_t* counter,
-                           void* stream) {
+                           void* stream, const double* pre = nullptr) {
     if (check_plan(p)) return -1;
     if (!stats || !dl_out) return set_error("gs_cls_draw: null argument");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const dim3 g(p->nchains, p->nspec, (p->maxbins + 63) / 64), b(64);
 #define GS_CD(FF) hipLaunchKernelGGL((k_cls_draw<FF>), g, b, 0, S(stream), p->L, p->nchains, p->maxbins, p->bins, p->meta, \
                                      stats, variates, slo, shi, p->ita(iteration), p->chain0, dl_out, trace, \
-                                     cap, counter, p->graph_adv)
+                                     cap, counter, p->graph_adv, pre)
     if (p->F == 1) GS_CD(1); else if (p->F == 2) GS_CD(2); else GS_CD(3);
 #undef GS_CD
     GS_LAUNCH_CHECK("k_cls_draw");
     return 0;
 }
+
 
 int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_t seed, uint32_t iteration,
                 double* dl_out, void* stream) {
@@ -2504,9 +2589,11 @@ int gs_recentre(gs_plan* p, const double* dl_new, const double* dl_old, double* 
 // the CR of a step: block parameters of dl (mode) + the sweep, the operator
 // either from the parameter table (many chains) or computed inside the sweep
 static int step_sweep(gs_plan* p, int mode, const double* d_alm, const double* dl, const double* z, uint64_t seed,
-                      uint32_t it, double* s_out, void* stream, bool finish = true) {
+                      uint32_t it, double* s_out, void* stream, bool finish = true, bool* cls_pre_done = nullptr) {
+    if (cls_pre_done) *cls_pre_done = false;
     if (p->inkernel_params)
-        return sweep_launch(p, d_alm, nullptr, z, seed, it, 0, s_out, p->stats, false, stream, finish, mode, dl);
+        return sweep_launch(p, d_alm, nullptr, z, seed, it, 0, s_out, p->stats, false, stream, finish, mode, dl,
+                            cls_pre_done);
     if (gs_block_params(p, mode, dl, p->params, stream)) return -1;
     return sweep_launch(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, false, stream, finish);
 }
@@ -2524,8 +2611,10 @@ int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out,
         const int rc = centered_fused_launch(p, d_alm, dl, s_out, seed, it, nullptr, 1, nullptr, stream);
         if (rc <= 0) return rc;
     }
-    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, z, seed, it, s_out, stream)) return -1;
-    return gs_cls_draw(p, p->stats, igvar, seed, it, dl, stream);
+    bool pre = false;
+    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, z, seed, it, s_out, stream, true, igvar ? nullptr : &pre))
+        return -1;
+    return cls_draw_launch(p, p->stats, igvar, seed, it, dl, nullptr, 1, nullptr, stream, pre ? p->cls_var : nullptr);
 }
 
 // the one-launch centered step (k_centered_fused) where the plan allows it:
@@ -2568,8 +2657,10 @@ int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* 
                                              p->adv_counter(), stream);
         if (rc <= 0) return rc;
     }
-    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream)) return -1;
-    return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->adv_counter(), stream);
+    bool pre = false;
+    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream, true, &pre)) return -1;
+    return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->adv_counter(), stream,
+                           pre ? p->cls_var : nullptr);
 }
 
 int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t it, void* stream) {

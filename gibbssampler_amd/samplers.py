@@ -16,6 +16,8 @@ lock-step on one GPU:
 
 Everything stays in HBM; only the returned histories are copied back.
 """
+import contextlib
+import gc
 import time
 
 import numpy as np
@@ -25,6 +27,23 @@ from . import _capi as C
 from .engine import GibbsPlan, MH_ORDER
 
 INIT_ITER = 0xFFFFFFFF
+
+
+@contextlib.contextmanager
+def _capture(g):
+    """torch.cuda.graph(g) with the cyclic garbage collector paused while the
+    stream is being captured: a collection inside the capture may destroy
+    objects of other samplers (their kept hipGraphs, streams, device buffers),
+    and those destructors' HIP calls are not allowed while a capture is open.
+    torch.cuda.graph collects once itself before the capture begins."""
+    was = gc.isenabled()
+    with torch.cuda.graph(g):
+        gc.disable()
+        try:
+            yield
+        finally:
+            if was:
+                gc.enable()
 
 
 class BatchedRunner:
@@ -138,7 +157,7 @@ class BatchedRunner:
         p.iteration_counter(True, self.iteration + 1)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _capture(g):
             if self.kind == "noncentered":
                 # NC: prologue, sweep (+ statistics), MH decisions with the trace record
                 # and the counter advance fused into the decision launch
@@ -174,7 +193,7 @@ class BatchedRunner:
             p.sweep_timing(True)
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
+            with _capture(g):
                 for i in range(nsteps):
                     # step i reads base + i; only the last step's last launch advances
                     # the base (by nsteps): one counter ticket per replay
