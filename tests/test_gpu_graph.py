@@ -251,6 +251,42 @@ def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
             np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("F,nch", [(3, 1), (2, 2), (1, 4)])
+def test_centered_predrawn_variates_bit_identical(monkeypatch, F, nch):
+    """Few-chain centered steps draw the C_l variates in extra workgroups of the
+    sweep, and the draw after the statistics reads them (GS_CLS_PRE=0 at plan
+    creation: the draw computes them itself).  Same bits: maps, D_l and the
+    trace over 4 native steps at L 512 with the Planck BB bins, eager and as
+    one captured 4-step graph."""
+    from gibbssampler_amd.problem import synthetic_problem
+    from gibbssampler_amd.samplers import BatchedRunner
+    P = synthetic_problem(512, 128, F, seed=9)
+
+    def run(pre, graph):
+        monkeypatch.setenv("GS_CLS_PRE", "1" if pre else "0")
+        r = BatchedRunner("centered", P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
+                          rng="native", seed=29, chain0=3)
+        r.init(P["dls_init"])
+        trace = None
+        if graph:
+            trace = r.plan.zeros(4, nch, r.plan.nspec, r.plan.maxbins)
+            r.capture_steps(4, trace=trace, trace_capacity=4)
+            r.step()
+        else:
+            for _ in range(4):
+                r.step()
+        out = [r.dl.cpu().numpy(), r.s.cpu().numpy()]
+        if trace is not None:
+            out.append(trace.cpu().numpy())
+        return out
+
+    for graph in (False, True):
+        a, b = run(True, graph), run(False, graph)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    monkeypatch.delenv("GS_CLS_PRE", raising=False)
+
+
 @pytest.mark.parametrize("F,nch", [(3, 1), (1, 2), (2, 2)])
 def test_centered_one_launch_bit_identical(monkeypatch, F, nch):
     """The one-launch centered step (k_centered_fused: sweep, statistics finish
