@@ -788,7 +788,6 @@ constexpr int F2_GSUB = 32;          // elements per LDS stage of the Gram pass
 constexpr int F2_RMAX = 176;         // rows (blocks + residual) per Gram pass
 // dynamic LDS k_f2_decide may use: 160 KB less its static arrays (5 x F2_RMAX words + 1)
 constexpr size_t F2_DECIDE_LDS = 160 * 1024 - (2 * sizeof(double) + 3 * sizeof(int)) * F2_RMAX - 64;
-constexpr int F2_BPT = 4;            // 4 x 4 output blocks per thread
 constexpr long long F2_CHUNK = 2048; // elements per Gram workgroup
 
 // delta a (real layout) of blocks [k0, k0 + kn) and their local block table
@@ -828,50 +827,57 @@ __global__ void k_f2_resid(long long n, const double* __restrict__ d, const doub
     if (g < n) r[g] = d[g] - m[g];
 }
 
-// lower triangle of the R x R weighted Gram matrix of rows 0..R-2 = Y, R-1 = r,
-// over one chunk of elements: every row staged once per element (times
-// sqrt(N^-1)) in LDS; thread t owns the 4 x 4 output blocks t, t + 256, ...
-// Per-chunk partials [chunk][nblk4][16], summed in chunk order by k_f2_gram_finish.
-__global__ __launch_bounds__(256) void k_f2_gram(int R, long long n, const double* __restrict__ Y,
-                                                 const double* __restrict__ r, const double* __restrict__ w,
-                                                 double* __restrict__ partial) {
-    // S[column][row]: a thread's 4 x 4 block reads rows ra..ra+3 and rb..rb+3 of
-    // one column as two 32-B runs; consecutive lanes own consecutive rb (row
-    // blocks 32 B apart), so a wave's reads are contiguous (no bank conflicts;
-    // the [row][column] layout put lanes 4 rows apart on 4 bank groups)
-    constexpr int SROW = F2_RMAX + 6;                 // even: 16-B aligned columns
+// Lower triangle of the R x R weighted Gram matrix of rows 0..R-2 = Y, R-1 = r,
+// over one chunk of F2_CHUNK elements, on the fp64 matrix cores
+// (v_mfma_f64_16x16x4_f64).  Every row is staged once per element (times
+// sqrt(N^-1)) in LDS, S[element][row]: thread t stages element column t % 32
+// and rows t / 32 + 8 j, all of a stage's loads issued together and the next
+// stage's issued before this stage's MFMAs (one memory latency per stage,
+// hidden).  The triangle is cut into 16 x 16 tiles (I >= J), tile pairs dealt
+// round-robin to the 4 waves, one accumulator tile per owned pair; per k-step
+// of 4 staged elements a pair costs two 8-B LDS reads -- lane l holds row
+// 16 I + (l & 15) (A) / 16 J + (l & 15) (B) of element 4 s + (l >> 4) -- and one
+// MFMA (1024 FMAs).  The r02/r03 VALU form (4 x 4 blocks per thread, 4 x 16-B
+// LDS reads per 16 FMAs) was LDS-bound at about half the FMA rate: 1182 us
+// against 736 us here at N_side 256 / 136 rows.  D layout (gfx950 f64): row
+// (l >> 4) + 4 reg, col l & 15.  Per-chunk partials [chunk][nblk4][16] (4 x 4
+// blocks of the lower triangle), summed in chunk order by k_f2_gram_finish.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int F2_TMAX = (F2_RMAX + 15) / 16;
+// T = 16-row tiles of this group (compile-time: the pair loop and the staging
+// are branch-free, so a k-step's LDS reads are issued together ahead of its
+// MFMAs).  A wave's slots past the last pair repeat its previous pair and are
+// not stored.
+template <int T>
+__global__ __launch_bounds__(256) void k_f2_gram_mfma(int R, long long n, const double* __restrict__ Y,
+                                                      const double* __restrict__ r, const double* __restrict__ w,
+                                                      double* __restrict__ partial) {
+    constexpr int SROW = F2_RMAX + 6;
+    static_assert(16 * F2_TMAX <= SROW, "tile rows exceed the staged column");
+    constexpr int NPAIR = T * (T + 1) / 2;
+    constexpr int PPW = (NPAIR + 3) / 4;
+    constexpr int ROWS = 16 * T;
+    constexpr int LPT = (ROWS + 7) / 8;
     __shared__ __attribute__((aligned(16))) double S[F2_GSUB][SROW];
     const int nb4 = (R + 3) / 4;
     const int nblk4 = nb4 * (nb4 + 1) / 2;
-    const int tid = threadIdx.x;
-    GS_ASSERT(R <= F2_RMAX && nblk4 <= 256 * F2_BPT);
-    int bi[F2_BPT], bj[F2_BPT];
-    bool own[F2_BPT];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    GS_ASSERT(R <= ROWS && R > ROWS - 16);
+    int ti[PPW], tj[PPW];
 #pragma unroll
-    for (int q = 0; q < F2_BPT; ++q) {
-        const int b = tid + q * 256;
-        own[q] = b < nblk4;
-        int i = (int)((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
-        while ((i + 1) * (i + 2) / 2 <= b) ++i;
-        while (i * (i + 1) / 2 > b) --i;
-        bi[q] = own[q] ? i : 0;
-        bj[q] = own[q] ? b - i * (i + 1) / 2 : 0;
+    for (int q = 0; q < PPW; ++q) {
+        const int p0 = wave + 4 * q;
+        const int p = p0 < NPAIR ? p0 : p0 - 4;
+        int i = 0;
+        while ((i + 1) * (i + 2) / 2 <= p) ++i;
+        ti[q] = i;
+        tj[q] = p - i * (i + 1) / 2;
     }
-    double acc[F2_BPT][4][4];
+    f64x4 acc[PPW];
 #pragma unroll
-    for (int q = 0; q < F2_BPT; ++q)
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) acc[q][x][y] = 0.0;
+    for (int q = 0; q < PPW; ++q) acc[q] = f64x4{0.0, 0.0, 0.0, 0.0};
     const long long e0 = blockIdx.x * F2_CHUNK, e1 = min(n, e0 + F2_CHUNK);
-    const int rows = nb4 * 4;
-    // stage loads: thread t always stages element column c = t % 32 and rows
-    // t / 32 + 8 j, so sqrt(N^-1) is one load and one sqrt per thread and stage;
-    // all of a stage's loads are issued together into registers, and the next
-    // stage's loads are issued before this stage's products (one memory latency
-    // per stage, hidden under the FMAs; the r02 loop waited on every load)
-    constexpr int LPT = (F2_RMAX + 4 + 7) / 8;
     const int c = tid & (F2_GSUB - 1), r0 = tid / F2_GSUB;
     double v[LPT], sw;
     auto issue = [&](long long es) {
@@ -888,43 +894,51 @@ __global__ __launch_bounds__(256) void k_f2_gram(int R, long long n, const doubl
         if (!ein) sw = 0.0;
     };
     issue(e0);
+    const int rl = lane & 15, kq = lane >> 4;
     for (long long es = e0; es < e1; es += F2_GSUB) {
         const double s = sqrt(sw);
 #pragma unroll
         for (int j = 0; j < LPT; ++j) {
             const int row = r0 + 8 * j;
-            if (row < rows) S[c][row] = row < R ? v[j] * s : 0.0;
+            if (row < ROWS) S[c][row] = row < R ? v[j] * s : 0.0;
         }
         __syncthreads();
         if (es + F2_GSUB < e1) issue(es + F2_GSUB);
 #pragma unroll
-        for (int q = 0; q < F2_BPT; ++q) {
-            if (!own[q]) continue;
-            const int ra = 4 * bi[q], rb = 4 * bj[q];
-#pragma unroll 4
-            for (int cc = 0; cc < F2_GSUB; ++cc) {
-                const double2 a01 = *reinterpret_cast<const double2*>(&S[cc][ra]);
-                const double2 a23 = *reinterpret_cast<const double2*>(&S[cc][ra + 2]);
-                const double2 b01 = *reinterpret_cast<const double2*>(&S[cc][rb]);
-                const double2 b23 = *reinterpret_cast<const double2*>(&S[cc][rb + 2]);
-                const double a[4] = {a01.x, a01.y, a23.x, a23.y}, b[4] = {b01.x, b01.y, b23.x, b23.y};
+        for (int ks = 0; ks < F2_GSUB / 4; ++ks) {
+            const double* col = &S[4 * ks + kq][rl];
+            double a[PPW], b[PPW];
 #pragma unroll
-                for (int x = 0; x < 4; ++x)
+            for (int q = 0; q < PPW; ++q) { a[q] = col[16 * ti[q]]; b[q] = col[16 * tj[q]]; }
 #pragma unroll
-                    for (int y = 0; y < 4; ++y) acc[q][x][y] = fma(a[x], b[y], acc[q][x][y]);
-            }
+            for (int q = 0; q < PPW; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc[q], 0, 0, 0);
         }
         __syncthreads();
     }
     double* po = partial + (long long)blockIdx.x * nblk4 * 16;
 #pragma unroll
-    for (int q = 0; q < F2_BPT; ++q) {
-        if (!own[q]) continue;
-        const int b = tid + q * 256;
+    for (int q = 0; q < PPW; ++q) {
+        if (wave + 4 * q >= NPAIR) break;                    // repeated slot
+        const int gj = 16 * tj[q] + rl;
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) po[(long long)b * 16 + x * 4 + y] = acc[q][x][y];
+        for (int g = 0; g < 4; ++g) {
+            const int gi = 16 * ti[q] + kq + 4 * g;
+            const int bi = gi >> 2, bj = gj >> 2;
+            if (bi < nb4 && bj <= bi)
+                po[(long long)(bi * (bi + 1) / 2 + bj) * 16 + (gi & 3) * 4 + (gj & 3)] = acc[q][g];
+        }
+    }
+}
+
+template <int T>
+void launch_gram_mfma_t(int Tr, unsigned nchunk, hipStream_t st, int R, long long n, const double* Y,
+                        const double* r, const double* w, double* part) {
+    if constexpr (T <= F2_TMAX) {
+        if (Tr == T) {
+            hipLaunchKernelGGL(k_f2_gram_mfma<T>, dim3(nchunk), dim3(256), 0, st, R, n, Y, r, w, part);
+            return;
+        }
+        launch_gram_mfma_t<T + 1>(Tr, nchunk, st, R, n, Y, r, w, part);
     }
 }
 
@@ -1554,9 +1568,8 @@ int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* 
         GS_LAUNCH_CHECK("k_f2_delta");
         if (gs_sht_synth_blocks(c->sht, F, c->f2_da, c->f2_blk, kn, blk_lmax + k0, c->f2_phib, c->f2_Y, stream))
             return -1;
-        hipLaunchKernelGGL(k_f2_gram, dim3((unsigned)nchunk), dim3(256), 0, st, R, n, c->f2_Y, c->f2_r, c->ninv,
-                           c->f2_part);
-        GS_LAUNCH_CHECK("k_f2_gram");
+        launch_gram_mfma_t<1>((R + 15) / 16, (unsigned)nchunk, st, R, n, c->f2_Y, c->f2_r, c->ninv, c->f2_part);
+        GS_LAUNCH_CHECK("k_f2_gram_mfma");
         hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256)), dim3(256), 0, st, R, (int)nchunk,
                            c->f2_part, c->f2_G);
         GS_LAUNCH_CHECK("k_f2_gram_finish");

@@ -141,6 +141,22 @@ __device__ __forceinline__ double2 expi_pi_frac(long long t, long long n) {
     sincospi((double)r / (double)n, &sn, &cs);
     return make_double2(cs, sn);
 }
+// the same values for the ring stage's small arguments (0 <= t < 2^32, n < 2^30)
+// with a 32-bit reduction instead of a 64-bit division: e^{i pi t / n} ...
+__device__ __forceinline__ double2 expi_pi_u32(unsigned t, unsigned n) {
+    const unsigned r = t % (2u * n);
+    double sn, cs;
+    sincospi((double)r / (double)n, &sn, &cs);
+    return make_double2(cs, sn);
+}
+// ... and e^{-i pi t / n} (bit for bit expi_pi_frac(-t, n))
+__device__ __forceinline__ double2 expi_pi_neg_u32(unsigned t, unsigned n) {
+    unsigned r = t % (2u * n);
+    r = r ? 2u * n - r : 0u;
+    double sn, cs;
+    sincospi((double)r / (double)n, &sn, &cs);
+    return make_double2(cs, sn);
+}
 
 // ---------------------------------------------------------------------------
 // a_lm access in the caller's layout: 0 = real m-major (utils.py:49-76),
@@ -870,7 +886,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
 // NB butterflies per stage (M / 2 <= NB * blockDim).
 #if defined(GS_FFT_RADIX2)
 template <int NB>
-__device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
+__device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
     const int half = M >> 1;
     for (int Ns = 1; Ns < M; Ns <<= 1) {
         double2 o0[NB], o1[NB];
@@ -985,7 +1001,7 @@ __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int 
 // mixed-radix Stockham, one radix-2 or radix-4 stage first (M = 2^(3q+1) or
 // 2^(3q+2)), then radix-8 stages -- 5 block-wide passes at M = 8192 instead of 13
 template <int NB>
-__device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
+__device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
     constexpr int NV = 2 * NB;
     const int p = 31 - __clz(M);
     int Ns = 1;
@@ -998,10 +1014,10 @@ __device__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict
 // forward DFT of length n held in buf[0..n) (Bluestein when n is not a power
 // of two: M = g.M, kernel V = FFT of the chirp); result in buf[0..n)
 template <int NB>
-__device__ void bluestein_forward(double2* buf, int n, int M, const double2* __restrict__ V,
+__device__ __forceinline__ void bluestein_forward(double2* buf, int n, int M, const double2* __restrict__ V,
                                   const double2* __restrict__ tw, int Mmax) {
     for (int j = threadIdx.x; j < M; j += blockDim.x) {
-        if (j < n) buf[j] = cmul(buf[j], expi_pi_frac(-(long long)j * j, n));   // c_j = e^{-i pi j^2/n}
+        if (j < n) buf[j] = cmul(buf[j], expi_pi_neg_u32((unsigned)j * (unsigned)j, n));   // c_j = e^{-i pi j^2/n}
         else buf[j] = make_double2(0.0, 0.0);
     }
     __syncthreads();
@@ -1011,7 +1027,7 @@ __device__ void bluestein_forward(double2* buf, int n, int M, const double2* __r
     fft_pow2<NB>(buf, M, +1, tw, Mmax);
     const double inv = 1.0 / M;
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        const double2 c = expi_pi_frac(-(long long)j * j, n);
+        const double2 c = expi_pi_neg_u32((unsigned)j * (unsigned)j, n);
         const double2 v = cmul(buf[j], c);
         buf[j] = make_double2(v.x * inv, v.y * inv);
     }
@@ -1020,7 +1036,7 @@ __device__ void bluestein_forward(double2* buf, int n, int M, const double2* __r
 
 // conj(DFT(conj x)) = unnormalised inverse DFT, Bluestein of length n
 template <int NB>
-__device__ void bluestein_inverse(double2* buf, int n, int M, const double2* __restrict__ V,
+__device__ __forceinline__ void bluestein_inverse(double2* buf, int n, int M, const double2* __restrict__ V,
                                   const double2* __restrict__ tw, int Mmax) {
     for (int j = threadIdx.x; j < n; j += blockDim.x) buf[j].y = -buf[j].y;
     __syncthreads();
@@ -1030,7 +1046,7 @@ __device__ void bluestein_inverse(double2* buf, int n, int M, const double2* __r
 }
 
 template <int NB>
-__device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
+__device__ __forceinline__ void dft_forward(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
                             const double2* __restrict__ bsk) {
     if (g.bs_off < 0) { fft_pow2<NB>(buf, g.M, -1, tw, Mmax); return; }
     bluestein_forward<NB>(buf, g.nphi, g.M, bsk + g.bs_off, tw, Mmax);
@@ -1038,7 +1054,7 @@ __device__ void dft_forward(double2* buf, const PairGeom& g, const double2* __re
 
 // inverse (unnormalised) DFT: y_j = sum_k Z_k e^{+2 pi i jk/n}
 template <int NB>
-__device__ void dft_inverse(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
+__device__ __forceinline__ void dft_inverse(double2* buf, const PairGeom& g, const double2* __restrict__ tw, int Mmax,
                             const double2* __restrict__ bsk) {
     if (g.bs_off < 0) { fft_pow2<NB>(buf, g.M, +1, tw, Mmax); return; }
     bluestein_inverse<NB>(buf, g.nphi, g.M, bsk + g.bs_off, tw, Mmax);
@@ -1073,6 +1089,18 @@ __global__ void k_sht_twiddles(int Mmax, double2* __restrict__ tw) {
 // threads per FFT workgroup for a class of length M, and butterflies per thread
 inline int ring_block(int M) { return std::min(1024, std::max(64, M / 8)); }
 
+// the ring's twiddle table e^{-2 pi i t / M}, t < M / 2, copied into LDS at the
+// kernel start (its loads overlap the fold / map loads): the FFT stages then
+// read twiddles from LDS instead of one global-memory round trip per stage.
+// Visible to the FFT after the barrier that precedes it.
+__device__ __forceinline__ const double2* ring_twiddles_lds(double2* twl, int M, const double2* __restrict__ tw,
+                                                            int Mmax, int& twM) {
+    const int st = Mmax / M;
+    for (int t = threadIdx.x; t < M / 2; t += blockDim.x) twl[t] = tw[t * st];
+    twM = M;
+    return twl;
+}
+
 // ---------------------------------------------------------------------------
 // synthesis: ring stage.  grid (pairs of this M class, ncomp)
 // ---------------------------------------------------------------------------
@@ -1092,7 +1120,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
                                                          const double2* __restrict__ bsk,
                                                          double2* __restrict__ gscratch, double* __restrict__ maps,
                                                          double2* __restrict__ sscr, int nsplit, int sstride,
-                                                         const int* __restrict__ comp_lmax, int comp_div) {
+                                                         const int* __restrict__ comp_lmax, int comp_div, int twoff) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -1102,8 +1130,13 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     const PairGeom g = geom[p];
     const int BD = blockDim.x;
     double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
-    Fold4* red = reinterpret_cast<Fold4*>(lbuf + (gscratch ? 0 : g.M));   // J > 1 only (short rings)
+    // fold reduction slots (J > 1 only, short rings) alias the FFT buffer: with
+    // J > 1 the fold is one pass whose reduction ends before buf is written
+    Fold4* red = reinterpret_cast<Fold4*>(lbuf);
     const int n = g.nphi;
+    const double2* twx = tw;
+    int twM = Mmax;
+    if (twoff >= 0) twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
     const long long plane = phi_plane(L, npair);
     const double2* PN = phi + (2LL * comp + 0) * plane;
     const double2* PS = phi + (2LL * comp + 1) * plane;
@@ -1113,7 +1146,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     auto H = [&](const double2* P, int m) {
         const double2 v = P[phi_at(m, p, npair)];
         const double cm = m == 0 ? 1.0 : 2.0;
-        const double2 t = g.phi_half ? cmul(v, expi_pi_frac(m, n)) : v;
+        const double2 t = g.phi_half ? cmul(v, expi_pi_u32(m, n)) : v;
         return make_double2(cm * t.x, cm * t.y);
     };
     for (int s0 = 0; s0 < K * J; s0 += BD) {
@@ -1182,14 +1215,14 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         }
         __syncthreads();
         const double2* V = bsk + g.bs_off;
-        bluestein_inverse<NB>(buf, h, g.M, V, tw, Mmax);
+        bluestein_inverse<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += BD) A[k] = buf[k];
         __syncthreads();
         for (int k = threadIdx.x; k < h; k += BD) buf[k] = Zo[k];
         __syncthreads();
-        bluestein_inverse<NB>(buf, h, g.M, V, tw, Mmax);
+        bluestein_inverse<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += BD) {
-            const double2 b = cmul(buf[k], expi_pi_frac(2LL * k, n));
+            const double2 b = cmul(buf[k], expi_pi_u32(2u * k, n));
             const double2 a = A[k];
             const double2 y0 = make_double2(a.x + b.x, a.y + b.y), y1 = make_double2(a.x - b.x, a.y - b.y);
             mc[g.startN + k] = y0.x;
@@ -1198,7 +1231,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         }
         return;
     }
-    dft_inverse<NB>(buf, g, tw, Mmax, bsk);
+    dft_inverse<NB>(buf, g, twx, twM, bsk);
     for (int j = threadIdx.x; j < n; j += BD) {
         const double2 y = buf[j];
         mc[g.startN + j] = y.x;
@@ -1217,12 +1250,15 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
                                                         const double2* __restrict__ tw, int Mmax,
                                                         const double2* __restrict__ bsk,
                                                         double2* __restrict__ gscratch, double2* __restrict__ phi,
-                                                        double2* __restrict__ sscr, int nsplit, int sstride) {
+                                                        double2* __restrict__ sscr, int nsplit, int sstride, int twoff) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
     const PairGeom g = geom[p];
     double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
+    const double2* twx = tw;
+    int twM = Mmax;
+    if (twoff >= 0) twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
     const int n = g.nphi;
     const bool eq = g.startS < 0;
     const double* mc = maps + (long long)comp * npix;
@@ -1235,16 +1271,16 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         for (int k = threadIdx.x; k < h; k += blockDim.x)
             buf[k] = make_double2(mc[g.startN + 2 * k + 1], eq ? 0.0 : mc[g.startS + 2 * k + 1]);
         __syncthreads();
-        bluestein_forward<NB>(buf, h, g.M, V, tw, Mmax);
+        bluestein_forward<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += blockDim.x) O[k] = buf[k];
         __syncthreads();
         for (int k = threadIdx.x; k < h; k += blockDim.x)
             buf[k] = make_double2(mc[g.startN + 2 * k], eq ? 0.0 : mc[g.startS + 2 * k]);
         __syncthreads();
-        bluestein_forward<NB>(buf, h, g.M, V, tw, Mmax);
+        bluestein_forward<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += blockDim.x) {
             const double2 e = buf[k];
-            const double2 o = cmul(O[k], expi_pi_frac(-2LL * k, n));
+            const double2 o = cmul(O[k], expi_pi_neg_u32(2u * k, n));
             buf[k] = make_double2(e.x + o.x, e.y + o.y);
             buf[k + h] = make_double2(e.x - o.x, e.y - o.y);
         }
@@ -1253,7 +1289,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         for (int j = threadIdx.x; j < n; j += blockDim.x)
             buf[j] = make_double2(mc[g.startN + j], eq ? 0.0 : mc[g.startS + j]);
         __syncthreads();
-        dft_forward<NB>(buf, g, tw, Mmax, bsk);
+        dft_forward<NB>(buf, g, twx, twM, bsk);
     }
     const long long plane = phi_plane(L, npair);
     double2* oN = phi + (2LL * comp + 0) * plane;
@@ -1266,7 +1302,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         double2 xn = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
         double2 xs = make_double2(0.5 * (a.y + b.y), -0.5 * (a.x - b.x));
         if (g.phi_half) {
-            const double2 e = expi_pi_frac(-(long long)m, n);
+            const double2 e = expi_pi_neg_u32(m, n);
             xn = cmul(xn, e);
             xs = cmul(xs, e);
         }
@@ -1974,6 +2010,24 @@ int gs_sht_info(const gs_sht* p, int* nside, int* lmax, long long* npix, long lo
     return 0;
 }
 
+// LDS of a ring launch (double2 entries): the FFT buffer (M; global scratch
+// instead when glob), the fold reduction of short rings (4 per thread) aliasing
+// it, then the twiddle table (M / 2) when the total stays within RING_LDS_TW_MAX
+// (else the FFT reads the plan's global table; twoff = -1)
+constexpr size_t RING_LDS_TW_MAX = 96 * 1024;
+static void ring_lds(int M, int bd, bool glob, bool short_red, size_t& lds, int& twoff) {
+    const long long red = short_red ? 4LL * bd : 0;
+    const long long r0 = glob ? red : std::max<long long>(M, red);
+    const long long with_tw = r0 + M / 2;
+    if (!glob && (size_t)with_tw * sizeof(double2) <= RING_LDS_TW_MAX) {
+        twoff = (int)r0;
+        lds = (size_t)with_tw * sizeof(double2);
+    } else {
+        twoff = -1;
+        lds = (size_t)r0 * sizeof(double2);
+    }
+}
+
 static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const double* maps_in, double* maps_out,
                           hipStream_t st, const double2* phi = nullptr, const int* comp_lmax = nullptr,
                           int comp_div = 1) {
@@ -1982,27 +2036,27 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
     const bool glob = M > p->lds_fft_max;
     const int bd = ring_block(M);
     const bool nb8 = M / 2 > 4 * bd;
-    // LDS: FFT buffer (+ fold reduction slots for short rings)
-    const size_t red = M < 8 * bd ? (size_t)bd * 4 * sizeof(double2) : 0;   // fold reduction, short rings
-    const size_t lds = (glob ? 0 : (size_t)M * sizeof(double2)) + red;
+    size_t lds = 0;
+    int twoff = -1;
+    ring_lds(M, bd, glob, M < 8 * bd, lds, twoff);
     const dim3 grid(p->cls_n[c], ncomp);
     double2* scr = glob ? p->gscr : nullptr;
     if (synth) {
         if (nb8)
             hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
                                p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
-                               comp_lmax, comp_div);
+                               comp_lmax, comp_div, twoff);
         else
             hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
                                p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
-                               comp_lmax, comp_div);
+                               comp_lmax, comp_div, twoff);
     } else {
         if (nb8)
             hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff);
         else
             hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff);
     }
     GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
     return 0;
@@ -2021,27 +2075,29 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
         // J = block / K aliases per bin pair, as a short-ring class does)
         const int M = p->merged_M, bd = ring_block(M);
         const bool nb8 = M / 2 > 4 * bd;
-        const size_t lds = (size_t)M * sizeof(double2) + (size_t)bd * 4 * sizeof(double2);
+        size_t lds = 0;
+        int twoff = -1;
+        ring_lds(M, bd, false, true, lds, twoff);
         const dim3 grid(p->merged_n, ncomp);
         const double2* ph = phi ? phi : p->phi;
         if (synth) {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
-                                   p->nsplit, p->split_n, comp_lmax, comp_div);
+                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff);
             else
                 hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
-                                   p->nsplit, p->split_n, comp_lmax, comp_div);
+                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff);
         } else {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n);
+                                   p->nsplit, p->split_n, twoff);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n);
+                                   p->nsplit, p->split_n, twoff);
         }
         GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring (merged)" : "k_sht_anal_ring (merged)");
         return 0;

@@ -53,7 +53,13 @@ class ShardContext:
                 self._owns_group = True
             if dist.get_world_size() != self.world:
                 raise RuntimeError("WORLD_SIZE does not match the process group")
-        self.dist = dist if self.world > 1 else None
+        elif dist.is_available() and dist.is_initialized():
+            # a group the caller initialised (any size, e.g. one RCCL rank on a
+            # one-GPU box): its collectives are used as for world > 1
+            if dist.get_world_size() != self.world:
+                raise RuntimeError("WORLD_SIZE does not match the process group")
+        grouped = self.world > 1 or (dist.is_available() and dist.is_initialized())
+        self.dist = dist if grouped else None
 
     @property
     def global_chains(self):
