@@ -105,6 +105,7 @@ struct ShtDev {
     // [m + s seg, m + (s + 1) seg); the recurrence state at each segment start
     // s >= 1 is a plan-time table (0: no segments, one walk from m to L)
     int seg;
+    int segmul;              // table rows per segment of this launch (seg / the table's)
     const int* segoff;       // [L+1] first table row of m's segments s >= 1
     const double2* sst;      // [rows][npair] (lambda_{lA-1}, lambda_lA), scaled
     const int* sstk;         // [rows][npair] scale exponent at lA
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
     double v0 = 0.0, v1 = 0.0;
     int kk = 0;
     if (tab && ls <= L && act) {
-        const long long o = (long long)(D.segoff[m] + sg - 1) * npair + pr;
+        const long long o = (long long)(D.segoff[m] + sg * D.segmul - 1) * npair + pr;
         const double2 s0 = D.sst[o];
         v1 = s0.x; v0 = s0.y;
         kk = D.sstk[o];
@@ -1408,7 +1409,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         for (int r = 0; r < ASR; ++r) {
             v0[r] = 0.0; v1[r] = 0.0; kk[r] = 0;
             if (tab[r] && ls[r] <= L && act[r]) {
-                const long long o = (long long)(D.segoff[m] + sg - 1) * npair + pr[r];
+                const long long o = (long long)(D.segoff[m] + sg * D.segmul - 1) * npair + pr[r];
                 const double2 s0 = D.sst[o];
                 v1[r] = s0.x; v0[r] = s0.y;
                 kk[r] = D.sstk[o];
@@ -1666,8 +1667,12 @@ struct gs_sht {
     // Legendre launch shapes chosen for occupancy (~4 waves per SIMD): ring
     // pairs per lane (sr) and m pairing, synthesis and analysis
     int syn_sr = 2, syn_paired = 1, ana_sr = 4, ana_paired = 1;
-    // l-segments of the analysis (0: none) and their state table
-    int seg = 0, nseg = 1;
+    // l-segments (0: none): the state table's granularity seg, and per launch
+    // kind the segment length (a multiple of seg) -- synthesis, and analysis
+    // per ncomp with its own ring groups per lane (index ncomp)
+    int seg = 0;
+    int syn_seg = 0;
+    int ana_sr_nc[4] = {4, 4, 4, 4}, ana_seg_nc[4] = {0, 0, 0, 0};
     int* segoff = nullptr;
     double2* sst = nullptr;
     int* sstk = nullptr;
@@ -1705,7 +1710,14 @@ struct gs_sht {
         ShtDev D;
         D.L = L; D.npair = npair; D.ngroup = ngroup; D.nlm = nlm;
         D.geom = geom; D.coef = coef; D.lstart = lstart; D.st = st; D.stk = stk;
-        D.seg = seg; D.segoff = segoff; D.sst = sst; D.sstk = sstk;
+        D.seg = seg; D.segmul = 1; D.segoff = segoff; D.sst = sst; D.sstk = sstk;
+        return D;
+    }
+    // a launch whose segments are sl l long (a multiple of the table's seg)
+    ShtDev devseg(int sl) const {
+        ShtDev D = dev();
+        D.seg = sl;
+        D.segmul = (seg > 0 && sl > 0) ? sl / seg : 1;
         return D;
     }
 };
@@ -1777,23 +1789,36 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
             return set_error("gs_sht_create: bad GS_SHT_SYN / GS_SHT_ANA override");
         }
     }
-    p->ntile = (p->ngroup + 4 * p->ana_sr - 1) / (4 * p->ana_sr);
     // small maps (one ring group per lane, unpaired m: still few waves per SIMD,
     // each walking up to L + 1 recurrence steps in a latency-bound chain): split
-    // every m's l range into segments of GS_SHT_SEG (default 64) l, entered with
-    // a plan-time recurrence state -- independent waves with short chains.
-    // GS_SHT_SEG=0 turns it off; an explicit value applies to any shape (tests)
+    // every m's l range into segments entered with a plan-time recurrence state
+    // -- independent waves with short chains.  Default: synthesis and TEB
+    // analysis in 64-l segments with one ring group per lane; T and spin-2
+    // analysis in 32-l segments with two ring groups per lane (half the
+    // per-chunk wave reductions per ring pair; N_side 256 spin-2 map2alm 0.176 ->
+    // 0.162 ms, TEB slower so it keeps the first shape), all from one table at
+    // 32-l granularity.  GS_SHT_SEG (0 = off) / GS_SHT_ANA set one segment length
+    // and one analysis shape for every launch (tests)
     {
         const char* e = std::getenv("GS_SHT_SEG");
-        int sg = (p->ana_sr == 1 && !p->ana_paired) ? 64 : 0;
+        const bool small = p->ana_sr == 1 && !p->ana_paired;
+        int sg = small ? 64 : 0;
         if (e) sg = std::atoi(e);
         if (sg < 0 || (sg & 1) || (sg > 0 && sg % ANA_C != 0)) {
             delete p;
             return set_error("gs_sht_create: GS_SHT_SEG must be 0 or a positive multiple of 4");
         }
         p->seg = sg >= L + 1 ? 0 : sg;
-        p->nseg = p->seg ? (L + p->seg) / p->seg : 1;
+        p->syn_seg = p->seg;
+        for (int nc = 1; nc <= 3; ++nc) { p->ana_sr_nc[nc] = p->ana_sr; p->ana_seg_nc[nc] = p->seg; }
+        if (small && !e && !std::getenv("GS_SHT_ANA") && p->seg == 64) {
+            p->seg = 32;
+            for (int nc = 1; nc <= 2; ++nc) { p->ana_sr_nc[nc] = 2; p->ana_seg_nc[nc] = 32; }
+        }
     }
+    p->ntile = 0;
+    for (int nc = 1; nc <= 3; ++nc)
+        p->ntile = std::max(p->ntile, (p->ngroup + 4 * p->ana_sr_nc[nc] - 1) / (4 * p->ana_sr_nc[nc]));
     // ---- geometry (ring pair r: north ring r+1, south ring 4N-1-r) ----
     std::vector<PairGeom> geom(p->npair);
     int Mmax = 2;
@@ -2133,11 +2158,14 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, ncomp, alm, layout,
                        p->ain);
     GS_LAUNCH_CHECK("k_sht_alm_in");
-    if (p->seg > 0 && p->syn_sr == 1 && !p->syn_paired && p->nseg <= 16) {
-        // small maps: l-segmented synthesis, one wave per segment
-        const dim3 g2(p->L + 1, p->ngroup), b2(64 * p->nseg);
-        const size_t lds = (size_t)p->nseg * (66 * 8 + 3 * 64 * 2) * sizeof(double);
-#define GS_SS(NC) hipLaunchKernelGGL((k_sht_synth_leg_seg<NC>), g2, b2, lds, S(stream), p->dev(), p->coef, p->ain, p->phi)
+    const int syn_nseg = p->syn_seg ? (p->L + p->syn_seg) / p->syn_seg : 1;
+    if (p->syn_seg > 0 && p->syn_seg <= 64 && p->syn_sr == 1 && !p->syn_paired && syn_nseg <= 16) {
+        // small maps: l-segmented synthesis, one wave per segment (<= 64 l: the
+        // wave's LDS slice stages 64 l of coefficients and a_lm)
+        const dim3 g2(p->L + 1, p->ngroup), b2(64 * syn_nseg);
+        const size_t lds = (size_t)syn_nseg * (66 * 8 + 3 * 64 * 2) * sizeof(double);
+#define GS_SS(NC) hipLaunchKernelGGL((k_sht_synth_leg_seg<NC>), g2, b2, lds, S(stream), p->devseg(p->syn_seg), p->coef, \
+                                     p->ain, p->phi)
         if (ncomp == 1) GS_SS(1); else if (ncomp == 2) GS_SS(2); else GS_SS(3);
 #undef GS_SS
         GS_LAUNCH_CHECK("k_sht_synth_leg_seg");
@@ -2156,13 +2184,16 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
 
 static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream) {
     if (sht_rings(p, false, ncomp, maps, nullptr, stream)) return -1;
-    const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, p->ntile, p->nseg);
-#define GS_AL(NC, SR) do { if (p->seg > 0 && p->seg <= 64) \
-        hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, true>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, \
+    const int sr = p->ana_sr_nc[ncomp], sl = p->ana_seg_nc[ncomp];
+    const int ntile = (p->ngroup + 4 * sr - 1) / (4 * sr);
+    const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, ntile, sl ? (p->L + sl) / sl : 1);
+    const ShtDev D = p->devseg(sl);
+#define GS_AL(NC, SR) do { if (sl > 0 && sl <= 64) \
+        hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, true>), grid, dim3(LEG_BLOCK), 0, S(stream), D, p->coef, \
                            p->phi, p->part, p->ana_paired); \
-    else hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), p->coef, \
+    else hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), D, p->coef, \
                             p->phi, p->part, p->ana_paired); } while (0)
-#define GS_AL2(NC) do { if (p->ana_sr == 4) GS_AL(NC, 4); else if (p->ana_sr == 2) GS_AL(NC, 2); \
+#define GS_AL2(NC) do { if (sr == 4) GS_AL(NC, 4); else if (sr == 2) GS_AL(NC, 2); \
                         else GS_AL(NC, 1); } while (0)
     if (ncomp == 1) GS_AL2(1); else if (ncomp == 2) GS_AL2(2); else GS_AL2(3);
 #undef GS_AL2
@@ -2171,7 +2202,7 @@ static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, do
     const double w = 4.0 * PI / (double)p->npix;
     const long long n = (long long)ncomp * p->nlm;
 #define GS_AF(NC) hipLaunchKernelGGL((k_sht_anal_finish<NC>), dim3(nblocks(n, 256)), dim3(256), 0, S(stream), p->L, p->nlm, \
-                                     p->ntile * 4, p->part, w, layout, acc, alm)
+                                     ntile * 4, p->part, w, layout, acc, alm)
     if (ncomp == 1) GS_AF(1); else if (ncomp == 2) GS_AF(2); else GS_AF(3);
 #undef GS_AF
     GS_LAUNCH_CHECK("k_sht_anal_finish");

@@ -330,3 +330,33 @@ def test_cpu_baseline_sht_equals_device(N, L, comps):
     dev = sht.map2alm(torch.from_numpy(mp).cuda(), iter=0, layout="complex", ncomp=3).cpu().numpy()
     cpu = C.map2alm(mp[3 - nc:], N, L, comps=comps)
     np.testing.assert_allclose(cpu, dev[3 - nc:], rtol=0, atol=1e-10 * np.abs(dev).max())
+
+
+@pytest.mark.parametrize("N,L", [(64, 100), (256, 512)])
+def test_default_small_map_shapes_match_single_walk(monkeypatch, N, L):
+    """The small-map default plan mixes launch shapes over one 32-l segment
+    table: synthesis and TEB analysis in 64-l segments with one ring group per
+    lane (two table rows per segment), T and spin-2 analysis in 32-l segments
+    with two ring groups per lane.  Every ncomp against the unsegmented single
+    walk of the same plan shape family, to rounding."""
+    torch = _torch()
+    from gibbssampler_amd.sht import HealpixSHT
+    rng = np.random.default_rng(N + L + 7)
+    out = {}
+    for mode in ("default", "walk"):
+        if mode == "walk":
+            monkeypatch.setenv("GS_SHT_SEG", "0")
+            monkeypatch.setenv("GS_SHT_ANA", "1,0")
+            monkeypatch.setenv("GS_SHT_SYN", "1,0")
+        sht = HealpixSHT(N, L)
+        res = []
+        for ncomp in (1, 2, 3):
+            r2 = np.random.default_rng(ncomp)
+            maps = torch.from_numpy(r2.standard_normal((ncomp, 12 * N * N))).cuda()
+            alm = torch.from_numpy(_rand_alm(L, ncomp, r2)).cuda()
+            res.append(sht.map2alm(maps, iter=0, layout="complex", ncomp=ncomp).cpu().numpy())
+            res.append(sht.alm2map(alm, ncomp=ncomp, layout="complex").cpu().numpy())
+        out[mode] = res
+        del sht
+    for a, b in zip(out["walk"], out["default"]):
+        np.testing.assert_allclose(b, a, rtol=0, atol=1e-12 * np.abs(a).max())
