@@ -1144,11 +1144,14 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     const bool eq = g.startS < 0;
     const int K = n / 2 + 1;
     const int J = K >= BD ? 1 : BD / K;          // threads per bin pair
-    auto H = [&](const double2* P, int m) {
+    // c_m Phi_m; the half-pixel phase e^{i pi m / n} of phi_half rings is
+    // e^{i pi k / n} (-1)^q for m = k + q n: the fold sums (-1)^q c_m Phi_m and
+    // the bin's one phase factor is applied after the fold (one sincospi per bin
+    // pair instead of one per m)
+    auto H = [&](const double2* P, int m, bool neg) {
         const double2 v = P[phi_at(m, p, npair)];
-        const double cm = m == 0 ? 1.0 : 2.0;
-        const double2 t = g.phi_half ? cmul(v, expi_pi_u32(m, n)) : v;
-        return make_double2(cm * t.x, cm * t.y);
+        const double cm = (m == 0 ? 1.0 : 2.0) * (neg ? -1.0 : 1.0);
+        return make_double2(cm * v.x, cm * v.y);
     };
     for (int s0 = 0; s0 < K * J; s0 += BD) {
         const int sl = s0 + threadIdx.x;
@@ -1156,16 +1159,18 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         const int k = sl % K, j0 = sl / K;
         const int nk = (n - k) % n;
         if (sl < K * J) {
-            for (int m = k + j0 * n; m <= Lc; m += J * n) {
-                const double2 a = H(PN, m);
+            for (int m = k + j0 * n, q = j0; m <= Lc; m += J * n, q += J) {
+                const bool neg = g.phi_half && (q & 1);
+                const double2 a = H(PN, m, neg);
                 f.nk.x += a.x; f.nk.y += a.y;
-                if (!eq) { const double2 b = H(PS, m); f.sk.x += b.x; f.sk.y += b.y; }
+                if (!eq) { const double2 b = H(PS, m, neg); f.sk.x += b.x; f.sk.y += b.y; }
             }
             if (nk != k)
-                for (int m = nk + j0 * n; m <= Lc; m += J * n) {
-                    const double2 a = H(PN, m);
+                for (int m = nk + j0 * n, q = j0; m <= Lc; m += J * n, q += J) {
+                    const bool neg = g.phi_half && (q & 1);
+                    const double2 a = H(PN, m, neg);
                     f.nmk.x += a.x; f.nmk.y += a.y;
-                    if (!eq) { const double2 b = H(PS, m); f.smk.x += b.x; f.smk.y += b.y; }
+                    if (!eq) { const double2 b = H(PS, m, neg); f.smk.x += b.x; f.smk.y += b.y; }
                 }
         }
         if (J > 1) {
@@ -1181,6 +1186,15 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
             __syncthreads();
         }
         if (sl < K * J && j0 == 0) {
+            if (g.phi_half) {
+                // e^{i pi k / n}; for nk = n - k: e^{i pi (n - k) / n} = -conj(e^{i pi k / n})
+                const double2 ek = expi_pi_u32(k, n);
+                const double2 enk = make_double2(-ek.x, ek.y);
+                f.nk = cmul(f.nk, ek);
+                f.sk = cmul(f.sk, ek);
+                f.nmk = cmul(f.nmk, enk);
+                f.smk = cmul(f.smk, enk);
+            }
             if (nk == k) { f.nmk = f.nk; f.smk = f.sk; }
             // Z_k = hN_k + i hS_k, hX_k = (G_k + conj G_-k)/2
             const double2 hn = make_double2(0.5 * (f.nk.x + f.nmk.x), 0.5 * (f.nk.y - f.nmk.y));
