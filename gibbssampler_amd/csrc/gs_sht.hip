@@ -1013,12 +1013,16 @@ __device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const dou
 #endif
 
 // forward DFT of length n held in buf[0..n) (Bluestein when n is not a power
-// of two: M = g.M, kernel V = FFT of the chirp); result in buf[0..n)
+// of two: M = g.M, kernel V = FFT of the chirp, followed in the plan's table by
+// the chirp c_j = e^{-i pi j^2 / n}, j < n, itself -- tabulated at plan time
+// with the same function, so the ring kernels load it instead of two fp64
+// sincospi per element); result in buf[0..n)
 template <int NB>
 __device__ __forceinline__ void bluestein_forward(double2* buf, int n, int M, const double2* __restrict__ V,
                                   const double2* __restrict__ tw, int Mmax) {
+    const double2* __restrict__ C = V + M;
     for (int j = threadIdx.x; j < M; j += blockDim.x) {
-        if (j < n) buf[j] = cmul(buf[j], expi_pi_neg_u32((unsigned)j * (unsigned)j, n));   // c_j = e^{-i pi j^2/n}
+        if (j < n) buf[j] = cmul(buf[j], C[j]);   // c_j = e^{-i pi j^2/n}
         else buf[j] = make_double2(0.0, 0.0);
     }
     __syncthreads();
@@ -1028,8 +1032,7 @@ __device__ __forceinline__ void bluestein_forward(double2* buf, int n, int M, co
     fft_pow2<NB>(buf, M, +1, tw, Mmax);
     const double inv = 1.0 / M;
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        const double2 c = expi_pi_neg_u32((unsigned)j * (unsigned)j, n);
-        const double2 v = cmul(buf[j], c);
+        const double2 v = cmul(buf[j], C[j]);
         buf[j] = make_double2(v.x * inv, v.y * inv);
     }
     __syncthreads();
@@ -1061,7 +1064,8 @@ __device__ __forceinline__ void dft_inverse(double2* buf, const PairGeom& g, con
     bluestein_inverse<NB>(buf, g.nphi, g.M, bsk + g.bs_off, tw, Mmax);
 }
 
-// plan time: V = FFT_M(w), w_t = e^{+i pi t^2/n} for |t| < n (cyclic)
+// plan time: V = FFT_M(w), w_t = e^{+i pi t^2/n} for |t| < n (cyclic), then the
+// chirp e^{-i pi j^2/n}, j < n, at V + M
 __global__ __launch_bounds__(1024) void k_sht_bluestein_setup(const int* __restrict__ pairs,
                                                               const PairGeom* __restrict__ geom,
                                                               const double2* __restrict__ tw, int Mmax,
@@ -1075,6 +1079,7 @@ __global__ __launch_bounds__(1024) void k_sht_bluestein_setup(const int* __restr
         else if (t > M - n) tt = M - t;
         buf[t] = tt >= 0 ? expi_pi_frac(tt * tt, n) : make_double2(0.0, 0.0);
     }
+    for (int j = threadIdx.x; j < n; j += blockDim.x) buf[M + j] = expi_pi_neg_u32((unsigned)j * (unsigned)j, n);
     __syncthreads();
     fft_pow2<8>(buf, M, -1, tw, Mmax);
 }
@@ -1876,7 +1881,11 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     long long bs_total = 0;
     std::vector<int> bs_pairs;
     for (int r = 0; r < p->npair; ++r) {
-        if (geom[r].M != geom[r].nphi) { geom[r].bs_off = bs_total; bs_total += geom[r].M; bs_pairs.push_back(r); }
+        if (geom[r].M != geom[r].nphi) {          // kernel V (M) then the chirp (the transform's length)
+            geom[r].bs_off = bs_total;
+            bs_total += geom[r].M + (geom[r].split ? geom[r].nphi / 2 : geom[r].nphi);
+            bs_pairs.push_back(r);
+        }
         if (geom[r].split) geom[r].sslot = p->nsplit++;
     }
     p->Mmax = Mmax;
