@@ -7,12 +7,16 @@
 #   bench_<tag>_*.json        bench lines: default (with cpu_baseline), stored sky map, centered C2,
 #                             asis C4 (per GPU), the drop-in surface, masked C5, HEAD's masked modes
 #   prof_<tag>_<mode>         kernel stats of configs[1], the masked workloads, SHT at N_side 2048
-# usage (GPU box): bash tools/profile_round.sh <tag>   (then python tools/summarize_profile.py <tag>)
+# usage (GPU box): bash tools/profile_round.sh <tag> [a|b|all]   (then python tools/summarize_profile.py <tag>)
+#   a: the harmonic trace, PMC passes and harmonic bench lines; b: the masked bench lines and the
+#   masked / configs[1] / SHT kernel stats (two gpurun calls stay within one call's time limit)
 set -e
 TAG=${1:-r03}
+PART=${2:-all}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
-rm -rf "$OUT" "${OUT}_masked" "${OUT}_sht" "${OUT}_masked_asis" "${OUT}_c2"
+if [ "$PART" != b ]; then
+rm -rf "$OUT"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline --time-every 100 > "$OUT.trace.log" 2>&1
@@ -40,6 +44,9 @@ timeout -k 10 300 python3 bench.py --workload asis \
     > gpurun_out/bench_${TAG}_asis_C4.json 2> gpurun_out/bench_${TAG}_asis_C4.err
 timeout -k 10 300 python3 bench.py --workload surface_noncentered --no-cpu-baseline \
     > gpurun_out/bench_${TAG}_surface_C3.json 2> gpurun_out/bench_${TAG}_surface_C3.err
+fi
+if [ "$PART" != a ]; then
+rm -rf "${OUT}_masked" "${OUT}_sht" "${OUT}_masked_asis" "${OUT}_c2"
 timeout -k 10 600 python3 bench.py --workload masked > gpurun_out/bench_${TAG}_masked_C5.json \
     2> gpurun_out/bench_${TAG}_masked_C5.err
 for m in masked_asis masked_centered_ula masked_centered_pcg masked_noncentered; do
@@ -55,3 +62,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "${OUT}_masked_asis" -o ru
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "${OUT}_sht" -o run --output-format csv -- \
     python3 tools/sht_bench.py --nside 2048 --reps 3 > "${OUT}_sht.log" 2>&1
 echo "profile $TAG done"
+fi
