@@ -332,20 +332,28 @@ class MaskedRunner:
         self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
         self.plan = GibbsPlan(cr.L, cr.nside, F, 1, cr.bl, [1.0] * F, self.bins, chain0=cr.chain)
         self.d0 = self.plan.zeros(F, cr.NR)
-
-    def _unfold(self, binned):
-        out = np.zeros((len(self.spectra), self.cr.L + 1))
-        for k, s in enumerate(self.spectra):
-            b = self.bins[s]
+        L = cr.L
+        idx = np.full((len(self.spectra), L + 1), -1, dtype=np.int64)
+        for k, sp in enumerate(self.spectra):
+            b = self.bins[sp]
             for i in range(len(b) - 1):
-                out[k, b[i]:b[i + 1]] = binned[s][i]
-        return torch.from_numpy(out).to(self.cr.device)
+                idx[k, b[i]:min(b[i + 1], L + 1)] = i
+        self._idx = torch.from_numpy(np.maximum(idx, 0)).to(cr.device)
+        self._valid = torch.from_numpy(idx >= 0).to(cr.device)
+
+    def _unfold(self, binned_t):
+        """utils.unfold_bins on the device: binned [1, nspec, maxbins] -> [nspec, L+1]."""
+        return torch.where(self._valid, torch.gather(binned_t[0], 1, self._idx), 0.0).contiguous()
 
     def run(self, dls_init, n_iter, s_init):
+        """The loop stays on the device: D_l, the accept flags and the histories are
+        device tensors until the end (one host transfer per run instead of a sync
+        and two copies per iteration); the per-iteration CR / C_l times come from
+        events read after the loop."""
         cr, plan = self.cr, self.plan
-        binned = {s: np.asarray(dls_init[s], dtype=np.float64) for s in self.spectra}
-        h = {s: [binned[s].copy()] for s in self.spectra}
-        acc, t_cr, t_cls = [], [], []
+        binned0 = {s: np.asarray(dls_init[s], dtype=np.float64) for s in self.spectra}
+        binned = plan.dl_tensor(binned0)
+        hist, acc, evs = [binned], [], []
         if s_init is None:
             # GibbsSampler.py:136-138: the first CR is sample(dls) without a map ->
             # the PCG (sample_mask), iteration 0 of the native streams
@@ -353,31 +361,37 @@ class MaskedRunner:
             s = cr.pcg_solve(dl0, cr.pcg_rhs(dl0, iteration=0))
         else:
             s = cr._s(s_init)
+        one = torch.ones(1, dtype=torch.int32, device=cr.device)
         for i in range(n_iter):
             it = i + 1
             cr.iteration = it
-            t0 = time.perf_counter()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
             dl = self._unfold(binned)
             if self.kind == KIND_PCG:
                 s = cr.pcg_solve(dl, cr.pcg_rhs(dl, iteration=it))
-                acc.append(1)
+                acc.append(one)
             elif self.kind == KIND_RJ:
                 cr.rj_step(dl, s, iteration=it)
-                acc.append(int(cr._acc.item()))
+                acc.append(cr._acc.reshape(1).clone())
             else:
                 cr.step(self.kind, dl, s, iteration=it)
-                acc.append(int(cr._acc.item()))
-            t1 = time.perf_counter()
+                acc.append(cr._acc.reshape(1).clone())
+            ev[1].record()
             stats = plan.sweep_stats(self.d0, s[None])
             var = plan.replay_invgamma() if cr.rng == "replay" else None
-            dlt = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)
-            binned = plan.dl_dicts(dlt)[0]
-            t_cls.append(time.perf_counter() - t1)
-            t_cr.append(t1 - t0)
-            for sp in self.spectra:
-                h[sp].append(binned[sp])
+            binned = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)
+            ev[2].record()
+            hist.append(binned)
+            evs.append(ev)
         self.s = s
-        return {sp: np.array(v) for sp, v in h.items()}, np.array(acc), np.array(t_cr), np.array(t_cls)
+        torch.cuda.synchronize()
+        t_cr = np.array([e[0].elapsed_time(e[1]) * 1e-3 for e in evs])
+        t_cls = np.array([e[1].elapsed_time(e[2]) * 1e-3 for e in evs])
+        H = torch.cat(hist).cpu().numpy()                     # [n_iter + 1, nspec, maxbins]
+        A = torch.cat(acc).cpu().numpy().astype(np.int64) if acc else np.zeros(0, dtype=np.int64)
+        h = {sp: H[:, k, :len(self.bins[sp]) - 1].copy() for k, sp in enumerate(self.spectra)}
+        return h, A, t_cr, t_cls
 
 
 # ---------------------------------------------------------------------------------------
