@@ -556,12 +556,12 @@ class MaskedMHRunner:
 
     def run(self, dls_init, n_iter, s_init=None):
         """n_iter iterations from dls_init (binned dict).  s_init: continue from
-        this map instead of the reference's PCG start map (ASIS.py:153-156)."""
+        this map instead of the reference's PCG start map (ASIS.py:153-156).
+        The loop stays on the device (D_l, accept flags and histories are device
+        tensors until the end; the stage times come from events read after it)."""
         cr, mh, plan = self.cr, self.mh, self.plan
         cur = plan.dl_tensor({s: np.asarray(dls_init[s], dtype=np.float64) for s in mh.spectra})[0]
-        h = {s: [np.asarray(dls_init[s], dtype=np.float64).copy()] for s in mh.spectra}
-        acc = {s: [] for s in mh.spectra}
-        acc_cr, t_it, t_cr, t_cls, t_nc = [], [], [], [], []
+        hist, flags, acc_cr, evs = [cur], [], [], []
         dl = mh.unfold(cur)
         s = None
         if s_init is not None:
@@ -571,41 +571,52 @@ class MaskedMHRunner:
         for i in range(n_iter):
             it = i + 1
             cr.iteration = it
-            t0 = time.perf_counter()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record()
             if self.kind == "noncentered":
                 s = self._pcg(dl, it)
                 s_nc = mh.noncentre(dl, s)
-                t1 = time.perf_counter()
-                cur, a = mh.sample_t(s_nc, cur, it)
-                t2 = t1
+                ev[1].record()
+                ev[2].record()
+                cur, f = mh.sweep_t(s_nc, cur, it)
+                dl = mh.unfold(cur)
             else:
                 if self.cr_kind == KIND_PCG:
                     s = self._pcg(dl, it)
                 else:
                     cr.step(self.cr_kind, dl, s, iteration=it)
-                    acc_cr.append(int(cr._acc.item()))
-                t1 = time.perf_counter()
+                    acc_cr.append(cr._acc.reshape(1).clone())
+                ev[1].record()
                 stats = plan.sweep_stats(self.d0[None], s[None])
                 var = plan.replay_invgamma() if cr.rng == "replay" else None
                 tmp = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)[0]
                 dl_tmp = mh.unfold(tmp)
                 s_nc = mh.noncentre(dl_tmp, s)
-                t2 = time.perf_counter()
-                cur, a = mh.sample_t(s_nc, tmp, it)
+                ev[2].record()
+                cur, f = mh.sweep_t(s_nc, tmp, it)
                 dl = mh.unfold(cur)
                 s = mh.centre(dl, s if self.quirk else s_nc)
-            if self.kind == "noncentered":
-                dl = mh.unfold(cur)
-            t3 = time.perf_counter()
-            b = plan.dl_dicts(cur[None])[0]
-            for sp in mh.spectra:
-                acc[sp].append(a[sp])
-                h[sp].append(b[sp])
-            t_it.append(t3 - t0)
-            t_cr.append(t1 - t0)
-            t_cls.append(t2 - t1)
-            t_nc.append(t3 - t2)
+            ev[3].record()
+            flags.append(f.clone())           # sweep_t reuses its flags tensor
+            hist.append(cur)
+            evs.append(ev)
         self.s = s
+        torch.cuda.synchronize()
+        el = lambda e, a, b: e[a].elapsed_time(e[b]) * 1e-3
+        t_it = np.array([el(e, 0, 3) for e in evs])
+        t_cr = np.array([el(e, 0, 1) for e in evs])
+        t_cls = np.array([el(e, 1, 2) for e in evs])
+        t_nc = np.array([el(e, 2, 3) for e in evs])
+        H = torch.stack(hist).cpu().numpy()                   # [n_iter + 1, nspec, maxbins]
+        h = {sp: H[:, k, :len(mh.bins[sp]) - 1].copy() for k, sp in enumerate(mh.spectra)}
+        acc = {sp: [] for sp in mh.spectra}
+        if flags:
+            Fl = torch.stack(flags).cpu().numpy()
+            for row in Fl:
+                off = 0
+                for sp, n in mh._acc_layout:
+                    acc[sp].append([int(v) for v in row[off:off + n]])
+                    off += n
+        a_cr = torch.cat(acc_cr).cpu().numpy().astype(np.int64) if acc_cr else None
         out = ({sp: np.array(v) for sp, v in h.items()}, {sp: np.array(v) for sp, v in acc.items()})
-        return out + (np.array(acc_cr) if acc_cr else None, np.array(t_it), np.array(t_cr), np.array(t_cls),
-                      np.array(t_nc))
+        return out + (a_cr, t_it, t_cr, t_cls, t_nc)
