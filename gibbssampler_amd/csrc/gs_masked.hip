@@ -311,9 +311,8 @@ __device__ __forceinline__ void block_sums(int nblk, const double* __restrict__ 
 
 __global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long long nslot, const double* __restrict__ um,
                             uint32_t seed_lo, uint32_t seed_hi, uint32_t chain, uint32_t call, uint32_t iter,
-                            const double* __restrict__ s1, double* __restrict__ s0, int32_t* __restrict__ accept,
+                            int32_t* __restrict__ flag, int32_t* __restrict__ accept,
                             double* __restrict__ log_ratio) {
-    __shared__ int acc;
     double t[NSUM];
     block_sums<NSUM>(nblk, partial, NSUM, t);
     if (threadIdx.x == 0) {
@@ -321,13 +320,20 @@ __global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long l
         const double lp0 = -0.5 * t[0] + -0.5 * t[6] + t[2];
         const double lr = lp1 + (-0.5 * t[4]) - (lp0 + (-0.5 * t[5]));
         const double u = um ? um[0] : uniform1(chain_key(seed_lo, seed_hi, chain), 0u, call, TAG_MALA_U, iter);
-        acc = log(u) < lr ? 1 : 0;
+        const int acc = log(u) < lr ? 1 : 0;
+        *flag = acc;
         if (accept) *accept = acc;
         if (log_ratio) *log_ratio = lr;
     }
-    __syncthreads();
-    if (acc)
-        for (long long g = threadIdx.x; g < nslot; g += blockDim.x) s0[g] = s1[g];
+}
+
+// dst <- src when the accept flag is set: the whole grid moves the map (the
+// accept workgroup alone took ~257 us for the 4.2 MB of an N_side 256 EB map)
+__global__ void k_select_copy(long long n, const int32_t* __restrict__ flag, const double* __restrict__ src,
+                              double* __restrict__ dst) {
+    if (!*flag) return;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += stride) dst[g] = src[g];
 }
 
 // RJPO (CenteredGibbs.py:606-674): per-block partials of (rhs - Q x) . (s - x)
@@ -354,21 +360,18 @@ __global__ __launch_bounds__(RED_BLOCK) void k_rj_dot(long long n, const double*
 __global__ __launch_bounds__(RED_BLOCK) void k_rj_accept(int nblk, const double* __restrict__ partial, long long n,
                                                          const double* __restrict__ um, uint32_t seed_lo,
                                                          uint32_t seed_hi, uint32_t chain, uint32_t iter,
-                                                         const double* __restrict__ x, double* __restrict__ s,
+                                                         int32_t* __restrict__ flag,
                                                          int32_t* __restrict__ accept, double* __restrict__ log_ratio) {
-    __shared__ int acc;
     double t[1];
     block_sums<1>(nblk, partial, 1, t);
     if (threadIdx.x == 0) {
         const double lr = -t[0];
         const double u = um ? um[0] : uniform1(chain_key(seed_lo, seed_hi, chain), 0u, 0u, TAG_RJ_U, iter);
-        acc = log(u) < lr ? 1 : 0;
+        const int acc = log(u) < lr ? 1 : 0;
+        *flag = acc;
         if (accept) *accept = acc;
         if (log_ratio) *log_ratio = lr;
     }
-    __syncthreads();
-    if (acc)
-        for (long long g = threadIdx.x; g < n; g += blockDim.x) s[g] = x[g];
 }
 
 // ---------------------------------------------------------------------------
@@ -1079,6 +1082,7 @@ struct gs_masked {
     double *x = nullptr, *Abs = nullptr, *y = nullptr, *r = nullptr;
     double *grad0 = nullptr, *grad1 = nullptr, *snew = nullptr, *pix0 = nullptr, *pix1 = nullptr, *vtmp = nullptr;
     double *partial = nullptr, *lr = nullptr;
+    int32_t* accd = nullptr;         // the last MALA / RJPO accept decision (device)
     double *pr = nullptr, *pz = nullptr, *pp = nullptr, *pq = nullptr, *params_pcg = nullptr, *dots = nullptr;
     double* pcgs = nullptr;          // PcgState of the device CG
     int pcg_syncs = 0;               // host synchronisations of the last solve
@@ -1100,6 +1104,7 @@ void mc_free(gs_masked* c) {
     for (double* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ell2bin) (void)hipFree(c->ell2bin);
+    if (c->accd) (void)hipFree(c->accd);
     if (c->f2_blk) (void)hipFree(c->f2_blk);
     delete c;
 }
@@ -1227,6 +1232,7 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     rc |= mc_alloc(&c->vtmp, FP);
     rc |= mc_alloc(&c->partial, (size_t)c->nblk * NSUM);
     rc |= mc_alloc(&c->lr, 1);
+    rc |= mc_alloc(&c->accd, 1);
     rc |= mc_alloc(&c->pr, FR);
     rc |= mc_alloc(&c->pz, FR);
     rc |= mc_alloc(&c->pp, FR);
@@ -1445,9 +1451,11 @@ int gs_masked_rj_accept(gs_masked* c, const double* dl, const double* rhs, const
     hipLaunchKernelGGL(k_rj_dot, dim3(nb), dim3(RED_BLOCK), 0, st, n, rhs, c->pr, s, x, c->partial);
     GS_LAUNCH_CHECK("k_rj_dot");
     hipLaunchKernelGGL(k_rj_accept, dim3(1), dim3(RED_BLOCK), 0, st, nb, c->partial, n, um,
-                       (uint32_t)(seed & 0xFFFFFFFFu), (uint32_t)(seed >> 32), (uint32_t)chain, iteration, x, s,
+                       (uint32_t)(seed & 0xFFFFFFFFu), (uint32_t)(seed >> 32), (uint32_t)chain, iteration, c->accd,
                        accept, log_ratio);
     GS_LAUNCH_CHECK("k_rj_accept");
+    hipLaunchKernelGGL(k_select_copy, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->accd, x, s);
+    GS_LAUNCH_CHECK("k_select_copy");
     return 0;
 }
 
@@ -1678,8 +1686,10 @@ int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v,
                        c->tau, s, c->snew, c->grad0, c->grad1, c->g2, c->ninv, c->pix0, c->pix1, c->partial);
     GS_LAUNCH_CHECK("k_mc_sums");
     hipLaunchKernelGGL(k_mc_accept, dim3(1), dim3(256), 0, st, c->nblk, c->partial, FR, um, slo, shi, ch, call,
-                       iteration, c->snew, s, accept, log_ratio ? log_ratio : c->lr);
+                       iteration, c->accd, accept, log_ratio ? log_ratio : c->lr);
     GS_LAUNCH_CHECK("k_mc_accept");
+    hipLaunchKernelGGL(k_select_copy, dim3(nblocks(FR, 256)), dim3(256), 0, st, FR, c->accd, c->snew, s);
+    GS_LAUNCH_CHECK("k_select_copy");
     return 0;
 }
 
