@@ -113,6 +113,8 @@ _SIGS = [
                                    ctypes.POINTER(ctypes.c_longlong)]),
     ("gs_sht_alm2map", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
     ("gs_sht_map2alm", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP]),
+    ("gs_sht_alm2map_beamed", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP]),
+    ("gs_sht_map2alm_weighted", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP]),
     ("gs_masked_create", ctypes.c_int, [ctypes.POINTER(GsMaskedDesc), _VP, _VP, ctypes.POINTER(_VP)]),
     ("gs_masked_destroy", ctypes.c_int, [_VP]),
     ("gs_masked_info", ctypes.c_int, [_VP, c_double_p, _VP]),

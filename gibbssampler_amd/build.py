@@ -14,6 +14,7 @@ Select a variant at run time with GIBBS_HIP_LIB=<path>.
 import glob
 import os
 import subprocess
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -59,8 +60,8 @@ def build(force=False, verbose=True, variant=None):
         return lib
     cmd = ["hipcc", f"--offload-arch={ARCH}"] + flags + ["-std=c++17", "-shared", "-fPIC",
                                                           "-I", os.path.join(ROOT, "include"), "-o", lib + ".tmp"] + SOURCES
-    if verbose:
-        print(" ".join(cmd))
+    if verbose:   # stderr: a rebuild must never precede bench.py's JSON line on stdout
+        print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(lib + ".tmp", lib)
     return lib

@@ -561,15 +561,23 @@ __global__ __launch_bounds__(RED_BLOCK) void k_pcg_init(int L, const double* __r
     block_partial<3>(acc, partial);
 }
 
-// x += alpha p; r -= alpha q; z = M r; per-block sums of (r . z, r . r)
+// alpha = rz / p.Qp from k_pcg_qdot's partials (slot 0), computed by every
+// workgroup in the fixed order of k_pcg_scal (the same block_sums at the same
+// block size: the same alpha bits, one launch fewer per CG iteration); then
+// x += alpha p; r -= alpha q; z = M r; per-block sums of (r . z, r . r) into
+// slots PCG_UPD_SLOT.. (disjoint from the slot the other workgroups still read)
+constexpr int PCG_UPD_SLOT = 4;
 template <int F>
-__global__ __launch_bounds__(RED_BLOCK) void k_pcg_upd(int L, const double* __restrict__ params,
+__global__ __launch_bounds__(RED_BLOCK) void k_pcg_upd(int L, int nb, const double* __restrict__ params,
                                                        const double* __restrict__ p, const double* __restrict__ q,
                                                        double* __restrict__ x, double* __restrict__ rr,
                                                        double* __restrict__ z, double* __restrict__ partial,
-                                                       const PcgState* __restrict__ st) {
+                                                       PcgState* __restrict__ st) {
     if (st->done) return;
-    const double a = st->alpha;
+    double pq[1];
+    block_sums<1>(nb, partial, NSUM, pq);
+    const double a = st->rz / pq[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->alpha = a;
     const long long NR = (long long)(L + 1) * (L + 1);
     double acc[2] = {0.0, 0.0};
     for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < NR; g += (long long)gridDim.x * blockDim.x) {
@@ -592,18 +600,19 @@ __global__ __launch_bounds__(RED_BLOCK) void k_pcg_upd(int L, const double* __re
             acc[1] += rv[f] * rv[f];
         }
     }
-    block_partial<2>(acc, partial);
+    block_partial<2>(acc, partial + PCG_UPD_SLOT);
 }
 
 // the CG scalars from the block partials (fixed order), on the device:
-// MODE 0 init (bn, rz, rn, done), 1 alpha = rz / p.Qp, 2 beta / rz / rn / it / done
+// MODE 0 init (bn, rz, rn, done), 1 alpha = rz / p.Qp (the CG loop folds it into
+// k_pcg_upd), 2 beta / rz / rn / it / done
 template <int MODE>
 __global__ __launch_bounds__(RED_BLOCK) void k_pcg_scal(int nblk, const double* __restrict__ partial,
                                                         PcgState* __restrict__ st, double tol, int maxiter) {
     if (MODE != 0 && st->done) return;
     constexpr int NV = MODE == 0 ? 3 : (MODE == 1 ? 1 : 2);
     double t[NV];
-    block_sums<NV>(nblk, partial, NSUM, t);
+    block_sums<NV>(nblk, partial + (MODE == 2 ? PCG_UPD_SLOT : 0), NSUM, t);
     if (threadIdx.x != 0) return;
     if constexpr (MODE == 0) {
         st->bn = sqrt(t[0]);
@@ -1136,11 +1145,9 @@ int mc_params(gs_masked* c, const double* dl, const double* kap, double* out, hi
     return 0;
 }
 
-// maps of b s  -> Abs
+// maps of b s  -> Abs (the beam applied on the transform's input load)
 int mc_synth(gs_masked* c, const double* s, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_mc_beam, dim3(nblocks(c->F * c->nlm, 256)), dim3(256), 0, st, c->L, c->F, c->bl, s, c->x);
-    GS_LAUNCH_CHECK("k_mc_beam");
-    return gs_sht_alm2map(c->sht, c->F, GS_ALM_REAL, c->x, out, st);
+    return gs_sht_alm2map_beamed(c->sht, c->F, s, c->bl, out, st);
 }
 
 // one v | s then s | v pass (plain or over-relaxed)
@@ -1177,10 +1184,7 @@ int mc_s(gs_masked* c, int over, double* s, const double* zs, uint32_t slo, uint
 
 int mc_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, hipStream_t st) {
     if (mc_synth(c, s, pix, st)) return -1;
-    const long long n = c->F * c->npix;
-    hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->ninv, pix, c->y);
-    GS_LAUNCH_CHECK("k_mc_mul");
-    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
+    if (gs_sht_map2alm_weighted(c->sht, c->F, pix, c->ninv, c->r, st)) return -1;      // map2alm(N^-1 A b s)
     hipLaunchKernelGGL(k_mc_grad, dim3(nblocks(c->F * c->nlm, 256)), dim3(256), 0, st, c->L, c->F, dl, c->bl, s, c->r,
                        c->g2, 1.0 / c->w, grad);
     GS_LAUNCH_CHECK("k_mc_grad");
@@ -1311,10 +1315,7 @@ int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* 
 static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, double* partial, int nb,
                      const PcgState* state, hipStream_t st) {
     if (mc_synth(c, x, c->pix0, st)) return -1;
-    const long long n = c->F * c->npix;
-    hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->ninv, c->pix0, c->y);
-    GS_LAUNCH_CHECK("k_mc_mul");
-    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 0, st)) return -1;
+    if (gs_sht_map2alm_weighted(c->sht, c->F, c->pix0, c->ninv, c->r, st)) return -1;   // map2alm(N^-1 A b x)
     const dim3 g(partial ? nb : nblocks(c->nlm, RED_BLOCK)), b(RED_BLOCK);
     const double iw = 1.0 / c->w;
     if (c->F == 1) hipLaunchKernelGGL(k_pcg_qdot<1>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);
@@ -1392,8 +1393,7 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
     GS_LAUNCH_CHECK("k_pcg_init");
     auto iteration = [&]() -> int {
         if (pcg_apply(c, dl, c->pp, c->pq, c->partial, nb, dst, st)) return -1;
-        hipLaunchKernelGGL(k_pcg_scal<1>, dim3(1), bb, 0, st, nb, c->partial, dst, tol, maxiter);
-#define GS_PU(FF) hipLaunchKernelGGL((k_pcg_upd<FF>), gb, bb, 0, st, c->L, c->params_pcg, c->pp, c->pq, x, c->pr, \
+#define GS_PU(FF) hipLaunchKernelGGL((k_pcg_upd<FF>), gb, bb, 0, st, c->L, nb, c->params_pcg, c->pp, c->pq, x, c->pr, \
                                      c->pz, c->partial, dst)
         if (c->F == 1) GS_PU(1); else if (c->F == 2) GS_PU(2); else GS_PU(3);
 #undef GS_PU

@@ -303,17 +303,36 @@ __global__ __launch_bounds__(256) void k_sht_segstate(ShtDev D) {
 // phi layout: [comp][ns][m][pair] (double2), ns 0 = north, 1 = south
 
 // a_lm in the caller's layout -> ain[comp][nlm] (healpy-ordered complex)
+// l of healpy m-major complex index i (m > 0 part of the real layout)
+__device__ __forceinline__ int l_of_cidx(int L, long long i) {
+    const double b = 2.0 * L + 3.0;
+    int m = (int)floor((b - sqrt(fmax(b * b - 8.0 * (double)i, 0.0))) / 2.0);
+    m = max(0, min(m, L));
+    while (m > 0 && (long long)m * (2 * L + 3 - m) / 2 > i) --m;
+    while (m < L && (long long)(m + 1) * (2 * L + 2 - m) / 2 <= i) ++m;
+    return (int)(i - (long long)m * (2 * L + 1 - m) / 2);
+}
+
+// a_lm -> the Legendre stage's complex layout; bl != nullptr (real layout only)
+// applies the per-l beam on the way in: (b_l s) rounded, then the 1/sqrt 2 --
+// the same two roundings as a separate beam pass (the masked CR's b s, whose
+// k_mc_beam launch and scratch write this replaces)
 __global__ void k_sht_alm_in(int L, int nlm, int ncomp, const double* __restrict__ alm, int layout,
-                             double2* __restrict__ ain) {
+                             double2* __restrict__ ain, const double* __restrict__ bl) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (g >= (long long)ncomp * nlm) return;
     const int comp = (int)(g / nlm);
     const long long i = g % nlm;
     const double* a = alm + comp * alm_comp_stride(layout, L);
     if (layout == GS_ALM_COMPLEX) { ain[g] = make_double2(a[2 * i], a[2 * i + 1]); return; }
-    if (i <= L) { ain[g] = make_double2(a[i], 0.0); return; }
+    if (i <= L) { ain[g] = make_double2(bl ? bl[i] * a[i] : a[i], 0.0); return; }
     constexpr double IS2 = 0.70710678118654752440;
     const long long r = 2 * i - (L + 1);
+    if (bl) {
+        const double b = bl[l_of_cidx(L, i)];
+        ain[g] = make_double2((b * a[r]) * IS2, (b * a[r + 1]) * IS2);
+        return;
+    }
     ain[g] = make_double2(a[r] * IS2, a[r + 1] * IS2);
 }
 
@@ -1270,7 +1289,8 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
                                                         const double2* __restrict__ tw, int Mmax,
                                                         const double2* __restrict__ bsk,
                                                         double2* __restrict__ gscratch, double2* __restrict__ phi,
-                                                        double2* __restrict__ sscr, int nsplit, int sstride, int twoff) {
+                                                        double2* __restrict__ sscr, int nsplit, int sstride, int twoff,
+                                                        const double* __restrict__ wts) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -1282,6 +1302,10 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
     const int n = g.nphi;
     const bool eq = g.startS < 0;
     const double* mc = maps + (long long)comp * npix;
+    // wts != nullptr: the transform of the pixel product wts * maps (the masked
+    // CR's N^-1 A b s, one rounding as in a separate multiply pass)
+    const double* wc = wts ? wts + (long long)comp * npix : nullptr;
+    auto mv = [&](long long i) { return wc ? wc[i] * mc[i] : mc[i]; };
     if (g.split) {
         // X_k = E_k + e^{-2 pi i k / n} O_k, X_(k+h) = E_k - (...) O_k with E / O the
         // length-h DFTs of the even / odd samples (Bluestein in LDS; O waits in scratch)
@@ -1289,13 +1313,13 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         double2* O = sscr + ((long long)comp * nsplit + g.sslot) * sstride;
         const double2* V = bsk + g.bs_off;
         for (int k = threadIdx.x; k < h; k += blockDim.x)
-            buf[k] = make_double2(mc[g.startN + 2 * k + 1], eq ? 0.0 : mc[g.startS + 2 * k + 1]);
+            buf[k] = make_double2(mv(g.startN + 2 * k + 1), eq ? 0.0 : mv(g.startS + 2 * k + 1));
         __syncthreads();
         bluestein_forward<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += blockDim.x) O[k] = buf[k];
         __syncthreads();
         for (int k = threadIdx.x; k < h; k += blockDim.x)
-            buf[k] = make_double2(mc[g.startN + 2 * k], eq ? 0.0 : mc[g.startS + 2 * k]);
+            buf[k] = make_double2(mv(g.startN + 2 * k), eq ? 0.0 : mv(g.startS + 2 * k));
         __syncthreads();
         bluestein_forward<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += blockDim.x) {
@@ -1307,7 +1331,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         __syncthreads();
     } else {
         for (int j = threadIdx.x; j < n; j += blockDim.x)
-            buf[j] = make_double2(mc[g.startN + j], eq ? 0.0 : mc[g.startS + j]);
+            buf[j] = make_double2(mv(g.startN + j), eq ? 0.0 : mv(g.startS + j));
         __syncthreads();
         dft_forward<NB>(buf, g, twx, twM, bsk);
     }
@@ -2078,7 +2102,7 @@ static void ring_lds(int M, int bd, bool glob, bool short_red, size_t& lds, int&
 
 static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const double* maps_in, double* maps_out,
                           hipStream_t st, const double2* phi = nullptr, const int* comp_lmax = nullptr,
-                          int comp_div = 1) {
+                          int comp_div = 1, const double* wts = nullptr) {
     if (!phi) phi = p->phi;
     const int M = p->cls_M[c];
     const bool glob = M > p->lds_fft_max;
@@ -2101,10 +2125,10 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
     } else {
         if (nb8)
             hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts);
         else
             hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts);
     }
     GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
     return 0;
@@ -2116,7 +2140,7 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
 // classes -- a dozen small, latency-bound launches -- run on the plan's side
 // stream while the largest class runs on the caller's.
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
-                     const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1) {
+                     const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1, const double* wts = nullptr) {
     if (p->merged_n > 0) {
         // all ring pairs in one launch: the block size and LDS of the longest FFT
         // (shorter rings leave threads idle; their fold reduction uses the
@@ -2141,11 +2165,11 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             if (nb8)
                 hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n, twoff);
+                                   p->nsplit, p->split_n, twoff, wts);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n, twoff);
+                                   p->nsplit, p->split_n, twoff, wts);
         }
         GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring (merged)" : "k_sht_anal_ring (merged)");
         return 0;
@@ -2162,7 +2186,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
     for (size_t c = 0; c < ncls; ++c) {
         const bool on_side = fork && c != big && p->cls_M[c] <= p->lds_fft_max;
         if (sht_ring_class(p, c, synth, ncomp, maps_in, maps_out, on_side ? p->side : S(stream), phi, comp_lmax,
-                           comp_div))
+                           comp_div, wts))
             return -1;
     }
     if (fork) {
@@ -2172,14 +2196,23 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
     return 0;
 }
 
+static int sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, const double* bl, double* maps,
+                       void* stream);
+
 int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* maps, void* stream) {
+    return sht_alm2map(p, ncomp, layout, alm, nullptr, maps, stream);
+}
+
+static int sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, const double* bl, double* maps,
+                       void* stream) {
     if (check_sht(p)) return -1;
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_alm2map: ncomp must be 1 (T), 2 (E,B) or 3 (T,E,B)");
     if (layout != GS_ALM_REAL && layout != GS_ALM_COMPLEX) return set_error("gs_sht_alm2map: bad layout");
+    if (bl && layout != GS_ALM_REAL) return set_error("gs_sht_alm2map: the beamed input needs the real layout");
     if (!alm || !maps) return set_error("gs_sht_alm2map: null argument");
     const long long nin = (long long)ncomp * p->nlm;
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, ncomp, alm, layout,
-                       p->ain);
+                       p->ain, bl);
     GS_LAUNCH_CHECK("k_sht_alm_in");
     const int syn_nseg = p->syn_seg ? (p->L + p->syn_seg) / p->syn_seg : 1;
     if (p->syn_seg > 0 && p->syn_seg <= 64 && p->syn_sr == 1 && !p->syn_paired && syn_nseg <= 16) {
@@ -2205,8 +2238,9 @@ int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* 
     return sht_rings(p, true, ncomp, nullptr, maps, stream);
 }
 
-static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream) {
-    if (sht_rings(p, false, ncomp, maps, nullptr, stream)) return -1;
+static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream,
+                        const double* wts = nullptr) {
+    if (sht_rings(p, false, ncomp, maps, nullptr, stream, nullptr, nullptr, 1, wts)) return -1;
     const int sr = p->ana_sr_nc[ncomp], sl = p->ana_seg_nc[ncomp];
     const int ntile = (p->ngroup + 4 * sr - 1) / (4 * sr);
     const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, ntile, sl ? (p->L + sl) / sl : 1);
@@ -2241,7 +2275,7 @@ int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int
     if (K < 1 || !alm_real || !blk || !blk_lmax || !phib || !maps) return set_error("gs_sht_synth_blocks: null argument");
     const long long nin = (long long)nfield * p->nlm;
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nfield, alm_real,
-                       GS_ALM_REAL, p->ain);
+                       GS_ALM_REAL, p->ain, nullptr);
     GS_LAUNCH_CHECK("k_sht_alm_in");
     double2* ph = reinterpret_cast<double2*>(phib);
     const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr));
@@ -2291,6 +2325,19 @@ int gs_sht_map2alm(gs_sht* p, int ncomp, int layout, const double* maps, double*
         if (sht_analysis(p, ncomp, layout, p->mapw, alm, 1, stream)) return -1;
     }
     return 0;
+}
+
+int gs_sht_alm2map_beamed(gs_sht* p, int ncomp, const double* alm_real, const double* bl, double* maps, void* stream) {
+    if (!bl) return set_error("gs_sht_alm2map_beamed: null beam");
+    return sht_alm2map(p, ncomp, GS_ALM_REAL, alm_real, bl, maps, stream);
+}
+
+int gs_sht_map2alm_weighted(gs_sht* p, int ncomp, const double* maps, const double* weights, double* alm_real,
+                            void* stream) {
+    if (check_sht(p)) return -1;
+    if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_map2alm_weighted: ncomp must be 1 (T), 2 (Q,U) or 3 (T,Q,U)");
+    if (!alm_real || !maps || !weights) return set_error("gs_sht_map2alm_weighted: null argument");
+    return sht_analysis(p, ncomp, GS_ALM_REAL, maps, alm_real, 0, stream, weights);
 }
 
 }  // extern "C"

@@ -99,6 +99,38 @@ class HealpixSHT:
                                             int(iter), _capi.stream_ptr()), "gs_sht_map2alm")
         return out
 
+    def alm2map_beamed(self, alm, bl, ncomp=None, out=None):
+        """alm2map of b_l * alm (real layout) with the beam applied on the input
+        load: hp.alm2map(almxfl(alm, bl)) of CenteredGibbs.py:698-699."""
+        if ncomp is None:
+            ncomp = 1 if alm.dim() == 1 else alm.shape[0]
+        a = self._alm_view(alm, "real", ncomp)
+        bl = bl.contiguous()
+        if bl.dtype != torch.float64 or bl.numel() < self.lmax + 1:
+            raise ValueError("bl must be float64 [lmax + 1]")
+        if out is None:
+            out = torch.empty((ncomp, self.npix) if ncomp > 1 else (self.npix,), dtype=torch.float64,
+                              device=alm.device)
+        _capi.check(self.lib.gs_sht_alm2map_beamed(self.handle, ncomp, _capi.ptr(a), _capi.ptr(bl), _capi.ptr(out),
+                                                   _capi.stream_ptr()), "gs_sht_alm2map_beamed")
+        return out
+
+    def map2alm_weighted(self, maps, weights, ncomp=None, out=None):
+        """map2alm(weights * maps, iter=0) into the real layout, the product formed
+        on the ring stage's input load (CenteredGibbs.py:298-299,510-513)."""
+        if ncomp is None:
+            ncomp = 1 if maps.dim() == 1 else maps.shape[0]
+        maps, weights = maps.contiguous(), weights.contiguous()
+        for t in (maps, weights):
+            if t.dtype != torch.float64 or t.numel() != ncomp * self.npix:
+                raise ValueError("maps / weights must be float64 [ncomp, 12 nside^2]")
+        if out is None:
+            out = torch.empty((ncomp, self.nreal) if ncomp > 1 else (self.nreal,), dtype=torch.float64,
+                              device=maps.device)
+        _capi.check(self.lib.gs_sht_map2alm_weighted(self.handle, ncomp, _capi.ptr(maps), _capi.ptr(weights),
+                                                     _capi.ptr(out), _capi.stream_ptr()), "gs_sht_map2alm_weighted")
+        return out
+
     def adjoint_synthesis(self, maps, bl=None, iter=3):
         """utils.adjoint_synthesis_hp (utils.py:79-111): map2alm(iter) rescaled by
         Npix/(4pi), real layout, optionally times the per-slot beam ``bl``

@@ -224,6 +224,14 @@ int gs_sht_destroy(gs_sht* sht);
 int gs_sht_info(const gs_sht* sht, int* nside, int* lmax, long long* npix, long long* device_bytes);
 int gs_sht_alm2map(gs_sht* sht, int ncomp, int layout, const double* alm, double* maps, void* stream);
 int gs_sht_map2alm(gs_sht* sht, int ncomp, int layout, const double* maps, double* alm, int niter, void* stream);
+/* Fused forms of the masked CR's transform pairs (real layout, iter 0):
+ *   alm2map_beamed   = hp.alm2map(almxfl(alm, b_l))       (CenteredGibbs.py:698-699,752-753)
+ *   map2alm_weighted = hp.map2alm(weights * maps, iter=0) (CenteredGibbs.py:298-299,510-513)
+ * bit-identical to a separate per-l / per-pixel multiply followed by the plain
+ * transform (the product is rounded once, on the transform's input load). */
+int gs_sht_alm2map_beamed(gs_sht* sht, int ncomp, const double* alm_real, const double* bl, double* maps, void* stream);
+int gs_sht_map2alm_weighted(gs_sht* sht, int ncomp, const double* maps, const double* weights, double* alm_real,
+                            void* stream);
 
 /* ---- masked (pixel-domain) constrained realisation (gs_masked.hip) -------
  * Replaces PolarizedCenteredConstrainedRealization's masked samplers:

@@ -360,3 +360,34 @@ def test_default_small_map_shapes_match_single_walk(monkeypatch, N, L):
         del sht
     for a, b in zip(out["walk"], out["default"]):
         np.testing.assert_allclose(b, a, rtol=0, atol=1e-12 * np.abs(a).max())
+
+
+@pytest.mark.parametrize("N,L,ncomp,env", [(16, 32, 2, None), (64, 100, 3, None), (256, 512, 2, None),
+                                           (64, 128, 2, "split"), (32, 64, 1, None)])
+def test_fused_beam_and_weight_bit_identical(N, L, ncomp, env, monkeypatch):
+    """gs_sht_alm2map_beamed / gs_sht_map2alm_weighted (the masked CR's b s
+    synthesis and N^-1-weighted analysis, CenteredGibbs.py:298-299,510-513,698-699)
+    equal the separate multiply + plain transform bit for bit: merged and
+    per-class ring launches, and ("split") the half-length Bluestein / global
+    scratch ring paths forced by a small LDS FFT cap."""
+    torch = _torch()
+    if env == "split":
+        monkeypatch.setenv("GS_SHT_LDS_FFT_MAX", "64")
+        monkeypatch.setenv("GS_SHT_MERGE_RINGS", "0")
+    from gibbssampler_amd.sht import HealpixSHT
+    sht = HealpixSHT(N, L)
+    rng = np.random.default_rng(7 * N + L + ncomp)
+    a = _rand_alm(L, ncomp, rng)
+    ar = torch.from_numpy(np.stack([H.complex_to_real(x, L) for x in a])).cuda()
+    bl = torch.from_numpy(np.exp(-0.5 * np.arange(L + 1) * (np.arange(L + 1) + 1) * 1e-4) * 1.3).cuda()
+    ell = torch.from_numpy(H.slot_ell(L)).cuda()
+    want = sht.alm2map(bl[ell][None] * ar, ncomp=ncomp)
+    got = sht.alm2map_beamed(ar, bl, ncomp=ncomp)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    maps = torch.from_numpy(rng.standard_normal((ncomp, 12 * N * N))).cuda()
+    w = torch.from_numpy(rng.uniform(0.0, 3.0, (ncomp, 12 * N * N)) * (rng.uniform(size=(ncomp, 12 * N * N)) > 0.2)).cuda()
+    want = sht.map2alm(w * maps, iter=0, ncomp=ncomp)
+    got = sht.map2alm_weighted(maps, w, ncomp=ncomp)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
