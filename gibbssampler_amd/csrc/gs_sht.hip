@@ -1405,6 +1405,9 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     __shared__ double red_all[4][2 * 16 * (NV + 2)];   // per wave: two chunk buffers
     const int L = D.L, npair = D.npair;
     const int q = blockIdx.x, tile = blockIdx.y;
+    // l-segmented launch: segments starting past L (about half of the grid at
+    // small maps) leave before any load
+    if (D.seg > 0 && !paired && q + (int)blockIdx.z * D.seg > D.L) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = tile * (LEG_BLOCK / 64) * ASR + wave * ASR;
