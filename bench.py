@@ -197,18 +197,68 @@ def _finalize_cpu(cpu, cg_iters=None):
     return finalize(cpu, cg_iters)
 
 
+def cpu_leg(args):
+    """The CPU baseline of this workload (None when it has none)."""
+    if args.no_cpu_baseline:
+        return None
+    if args.workload == "noncentered":
+        return cpu_baseline_child(args)
+    if args.workload == "masked" or args.workload in MASKED_HEAD:
+        return cpu_baseline_masked_child(args)
+    return None
+
+
+def self_launch(args):
+    """``bench.py --gpus N`` (N > 1) started without torchrun: the CPU baseline
+    first (this process never touches the GPU), then N ranks of this script under
+    torch.distributed.run (one per GPU, RCCL), rank 0's JSON line completed with
+    the CPU baseline.  Exits non-zero when the ranks fail or report another GPU
+    count -- one GPU is never measured in place of N."""
+    from gibbssampler_amd.distributed import launch_ranks
+    cpu = cpu_leg(args)
+    argv = [a for a in sys.argv[1:]]
+    if "--no-cpu-baseline" not in argv:
+        argv.append("--no-cpu-baseline")
+    try:
+        # GS_BENCH_RANK_SCRIPT: a stand-in rank program (the CPU launcher test)
+        script = os.environ.get("GS_BENCH_RANK_SCRIPT", os.path.abspath(__file__))
+        line, _ = launch_ranks(args.gpus, script, argv, cwd=HERE)
+    except Exception as e:            # noqa: BLE001 -- reported, then a non-zero exit
+        print(f"bench.py --gpus {args.gpus}: the rank launch failed: {e}", file=sys.stderr)
+        raise SystemExit(2)
+    if line.get("n_gpus") != args.gpus:
+        print(f"bench.py --gpus {args.gpus}: the ranks reported n_gpus={line.get('n_gpus')}", file=sys.stderr)
+        raise SystemExit(2)
+    return attach_cpu(line, cpu)
+
+
+def attach_cpu(line, cpu):
+    """rank 0's line + the CPU baseline measured before the ranks started (a PCG
+    workload's CPU rate takes the device solve's CG iteration count)."""
+    if cpu is not None and line.get("cpu_baseline") is None:
+        if "seconds_per_iteration" in cpu:          # the masked legs' raw form
+            pcg = line.get("pcg") or {}
+            cpu = _finalize_cpu(cpu, pcg.get("cg_iterations_per_solve"))
+        line["cpu_baseline"] = cpu
+        line.setdefault("notes_cpu", "cpu_baseline measured by the launching process before the ranks started")
+    return line
+
+
 def main():
     args = parse()
     from gibbssampler_amd.distributed import ShardContext, dist_env
     world, rank, local = dist_env()
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if args.workload == "noncentered":
-            cpu = cpu_baseline_child(args)
-        elif args.workload == "masked" or args.workload in MASKED_HEAD:
-            cpu = cpu_baseline_masked_child(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        print(json.dumps(self_launch(args)))
+        return
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+              f"(python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}, "
+              f"or plain python bench.py --gpus {args.gpus})", file=sys.stderr)
+        raise SystemExit(2)
+    # under torchrun (N > 1) the CPU baseline is the launcher's (self_launch);
+    # at N = 1 this process runs it before touching the GPU
+    cpu = cpu_leg(args) if rank == 0 and world == 1 else None
     import torch
     torch.cuda.set_device(local)
     ctx = ShardContext(args.nchains, backend="nccl")

@@ -180,3 +180,67 @@ def stream_ptr(stream=None):
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+# ---------------------------------------------------------------------------------------
+# capture-safe teardown
+# ---------------------------------------------------------------------------------------
+# A destructor that runs while a hipGraph capture is open (a reference dropped
+# inside the captured code, or a cyclic collection there) must not call HIP:
+# hipFree / hipGraphExecDestroy / hipStreamDestroy are illegal during capture
+# and invalidate it (the intermittent fault of r03, commit 2ac910f).  Objects
+# that own device resources hand them to ``release`` / ``park``: outside a
+# capture they are freed at once; inside one they wait in the graveyard until
+# the outermost capture of samplers._capture has ended (``end_capture``).
+_GRAVEYARD = []
+_CAPTURE_DEPTH = [0]
+
+
+def capturing():
+    """True while one of this package's captures is open, or while the current
+    stream is being captured by anyone (torch.cuda.graph used directly)."""
+    if _CAPTURE_DEPTH[0] > 0:
+        return True
+    try:
+        import torch
+        return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    except Exception:       # interpreter shutdown
+        return False
+
+
+def release(fn, handle):
+    """Call fn(handle) now, or after the open capture ends."""
+    if capturing():
+        _GRAVEYARD.append((fn, handle))
+    else:
+        fn(handle)
+
+
+def park(obj):
+    """Keep obj (e.g. a dying runner's graphs, streams and tensors) alive until
+    the open capture ends; False when no capture is open (nothing to do)."""
+    if capturing():
+        _GRAVEYARD.append((None, obj))
+        return True
+    return False
+
+
+def begin_capture():
+    _CAPTURE_DEPTH[0] += 1
+
+
+def end_capture():
+    """Leave a capture; after the outermost one, run the deferred releases."""
+    _CAPTURE_DEPTH[0] = max(0, _CAPTURE_DEPTH[0] - 1)
+    if _CAPTURE_DEPTH[0] == 0:
+        while _GRAVEYARD:
+            fn, h = _GRAVEYARD.pop()
+            if fn is not None:
+                try:
+                    fn(h)
+                except Exception:
+                    pass
+
+
+def graveyard_size():
+    return len(_GRAVEYARD)

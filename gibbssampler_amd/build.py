@@ -58,11 +58,26 @@ def build(force=False, verbose=True, variant=None):
     deps = SOURCES + HEADERS + [os.path.abspath(__file__)]
     if not force and not _stale(lib, deps):
         return lib
-    cmd = ["hipcc", f"--offload-arch={ARCH}"] + flags + ["-std=c++17", "-shared", "-fPIC",
-                                                          "-I", os.path.join(ROOT, "include"), "-o", lib + ".tmp"] + SOURCES
-    if verbose:   # stderr: a rebuild must never precede bench.py's JSON line on stdout
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    # one object per source, compiled in parallel (no device code crosses a
+    # translation unit, so no -fgpu-rdc), then one link
+    base = ["hipcc", f"--offload-arch={ARCH}"] + flags + ["-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include")]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = lib + "." + os.path.splitext(os.path.basename(src))[0] + ".o"
+        cmd = base + ["-c", "-o", obj, src]
+        if verbose:   # stderr: a rebuild must never precede bench.py's JSON line on stdout
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    bad = [p.wait() for p in procs]
+    if any(bad):
+        raise subprocess.CalledProcessError(max(bad), "hipcc -c")
+    link = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
+    if "-shared-libasan" in flags:
+        link += ["-fsanitize=address", "-shared-libasan"]
+    subprocess.run(link, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(lib + ".tmp", lib)
     return lib
 

@@ -536,13 +536,17 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     __shared__ double red[3 * NS * WAVE];           // chunk-wave sums of tw < 4 shapes
     if constexpr (PRE > 0) {
         static_assert(ZM == 0, "latency form: native draws only");
-        if ((int)blockIdx.x < cp.n) {
-            cls_variates_item<F>(cp, blockIdx.x * blockDim.x + threadIdx.x, seed_lo, seed_hi, iter, chain0);
+        // the variate workgroups sit at the END of the grid, so the sweep's
+        // workgroups keep physical ids 0.. and their XCD-aware remap (b % 8 =
+        // the XCD) stays exact for any cp.n
+        const int nsw = (int)gridDim.x - cp.n;
+        if ((int)blockIdx.x >= nsw) {
+            cls_variates_item<F>(cp, ((int)blockIdx.x - nsw) * blockDim.x + threadIdx.x, seed_lo, seed_hi, iter,
+                                 chain0);
             return;
         }
         cr_sweep_latency<F, STORE, PRE>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo,
-                                        seed_hi, iter, substep, chain0, op, tab, red, (int)blockIdx.x - cp.n,
-                                        (int)gridDim.x - cp.n);
+                                        seed_hi, iter, substep, chain0, op, tab, red, (int)blockIdx.x, nsw);
         return;
     }
     if constexpr (ZM == 0) {

@@ -19,6 +19,46 @@ def dist_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc, script, args, env=None, timeout=None, cwd=None):
+    """Run ``script args`` as ``nproc`` ranks of one node under
+    ``python -m torch.distributed.run`` (rendezvous on 127.0.0.1), as a child
+    process, and return (rank 0's last JSON line as a dict, the child's stdout).
+    The caller must not have initialised the GPU (the ranks own it); this
+    process only waits.  Raises RuntimeError when the ranks fail or rank 0
+    prints no JSON line."""
+    import json
+    import subprocess
+    import sys
+    e = dict(os.environ if env is None else env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+              "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID"):
+        e.pop(k, None)
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(nproc)}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script] + [str(a) for a in args]
+    out = subprocess.run(cmd, env=e, cwd=cwd, stdout=subprocess.PIPE, text=True, timeout=timeout)
+    if out.returncode != 0:
+        raise RuntimeError(f"launch_ranks: {nproc} ranks of {script} exited with {out.returncode}")
+    line = None
+    for ln in out.stdout.splitlines():
+        ln = ln.strip()
+        if ln.startswith("{"):
+            try:
+                line = json.loads(ln)
+            except ValueError:
+                pass
+    if line is None:
+        raise RuntimeError(f"launch_ranks: rank 0 of {script} printed no JSON line")
+    return line, out.stdout
+
+
 def shard_chains(world_size, rank, chains_per_rank):
     """Global chain ids owned by ``rank``."""
     if not (0 <= rank < world_size):

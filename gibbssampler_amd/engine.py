@@ -106,8 +106,9 @@ class GibbsPlan:
 
     def __del__(self):
         try:
+            C.park(dict(self.__dict__))       # inside a capture: tensors freed after it
             if getattr(self, "_h", None) is not None and self.lib is not None:
-                self.lib.gs_plan_destroy(self._h)
+                C.release(self.lib.gs_plan_destroy, self._h)
                 self._h = None
         except Exception:
             pass

@@ -92,9 +92,10 @@ class MaskedCR:
         self._lr = torch.zeros(1, dtype=torch.float64, device=device)
 
     def __del__(self):
+        _capi.park(dict(self.__dict__))       # inside a capture: tensors freed after it
         h = getattr(self, "handle", None)
         if h is not None and h.value:
-            self.lib.gs_masked_destroy(h)
+            _capi.release(self.lib.gs_masked_destroy, h)
             self.handle = None
 
     # -- conversions -------------------------------------------------------------------

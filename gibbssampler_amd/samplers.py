@@ -31,19 +31,24 @@ INIT_ITER = 0xFFFFFFFF
 
 @contextlib.contextmanager
 def _capture(g):
-    """torch.cuda.graph(g) with the cyclic garbage collector paused while the
-    stream is being captured: a collection inside the capture may destroy
-    objects of other samplers (their kept hipGraphs, streams, device buffers),
-    and those destructors' HIP calls are not allowed while a capture is open.
-    torch.cuda.graph collects once itself before the capture begins."""
+    """torch.cuda.graph(g), capture-safe for other objects' teardown:
+    - the cyclic collector is paused from before the capture opens until after
+      it has closed (torch.cuda.graph's own gc.collect() in __enter__ still runs:
+      an explicit collect ignores gc.disable);
+    - any destructor that does run inside (a plain refcount drop in the
+      captured code, or an explicit gc.collect()) parks its device resources
+      in _capi's graveyard instead of calling HIP; they are released after the
+      capture (_capi.end_capture)."""
     was = gc.isenabled()
-    with torch.cuda.graph(g):
-        gc.disable()
-        try:
+    gc.disable()
+    C.begin_capture()
+    try:
+        with torch.cuda.graph(g):
             yield
-        finally:
-            if was:
-                gc.enable()
+    finally:
+        C.end_capture()
+        if was:
+            gc.enable()
 
 
 class BatchedRunner:
@@ -68,6 +73,15 @@ class BatchedRunner:
         self.materialize_recentre = materialize_recentre
         self.iteration = 0
         self.graph = None
+
+    def __del__(self):
+        # dropped inside another sampler's capture: keep the kept hipGraphs, the
+        # copy stream and the tensors alive until that capture has ended
+        # (their destructors call HIP, which is illegal while a capture is open)
+        try:
+            C.park(dict(self.__dict__))
+        except Exception:
+            pass
 
     # -- one iteration ---------------------------------------------------------------
     def _replay(self):
@@ -138,6 +152,10 @@ class BatchedRunner:
         self.accept.copy_(st["accept"])
         if self.s is not None and st.get("s") is not None:
             self.s.copy_(st["s"])
+        if int(st["seed"]) != self.seed:
+            # the kept chunk graphs of run() hold the old seed as a kernel
+            # argument: drop them, so the resumed run captures with the new one
+            self.__dict__.pop("_run_graphs", None)
         self.seed = int(st["seed"])
         self.iteration = int(st["iteration"])
         self.graph = None

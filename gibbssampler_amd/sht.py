@@ -39,7 +39,7 @@ class HealpixSHT:
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:
-            self.lib.gs_sht_destroy(h)
+            _capi.release(self.lib.gs_sht_destroy, h)
             self.handle = None
 
     # -- shapes -----------------------------------------------------------------
