@@ -56,6 +56,7 @@ class GsMaskedDesc(ctypes.Structure):
         ("noise_pol0", ctypes.c_double),
         ("mu_eps", ctypes.c_double),
         ("adj_iter", ctypes.c_int),
+        ("nchains", ctypes.c_int),
     ]
 
 
@@ -115,15 +116,21 @@ _SIGS = [
     ("gs_sht_map2alm", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP]),
     ("gs_sht_alm2map_beamed", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP]),
     ("gs_sht_map2alm_weighted", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP]),
+    ("gs_sht_reserve", ctypes.c_int, [_VP, ctypes.c_int, _VP]),
+    ("gs_sht_alm2map_batch", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP]),
+    ("gs_sht_map2alm_batch", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP,
+                                            ctypes.c_int, _VP]),
     ("gs_masked_create", ctypes.c_int, [ctypes.POINTER(GsMaskedDesc), _VP, _VP, ctypes.POINTER(_VP)]),
     ("gs_masked_destroy", ctypes.c_int, [_VP]),
     ("gs_masked_info", ctypes.c_int, [_VP, c_double_p, _VP]),
+    ("gs_masked_nchains", ctypes.c_int, [_VP]),
     ("gs_masked_gradient", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     ("gs_masked_pcg_rhs", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, _VP,
                                          _VP]),
     ("gs_masked_pcg_solve", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_double, ctypes.c_int, c_int_p,
                                            c_double_p, _VP]),
     ("gs_masked_pcg_info", ctypes.c_int, [_VP, c_int_p]),
+    ("gs_masked_pcg_info2", ctypes.c_int, [_VP, c_int_p, c_int_p]),
     ("gs_masked_pcg_apply", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     ("gs_masked_rj_accept", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_int, _VP, _VP, _VP]),

@@ -7,9 +7,13 @@
 //   a10 overrelaxation_sampler         CenteredGibbs.py:733-825
 //   a11 sample_mala (+ gradient, log density, log proposal) 494-603
 //   a12 the dispatch ladder of sample  CenteredGibbs.py:828-850
-// One chain per call; the HEALPix SHTs run through gs_sht (gs_sht.hip); every
-// pixel- and slot-wise step is one fused kernel; the MALA accept test reduces
-// its eight sums in a fixed order (bitwise reproducible).
+// A context runs a batch of B chains (chains chain0 .. chain0 + B - 1 on the same
+// data): every per-chain array is [B][...] contiguous, every pixel- and slot-wise
+// kernel carries the chain in blockIdx.y, and each transform is ONE batched SHT
+// over the B maps (gs_sht_*_batch) -- so B small-map chains fill the GPU that
+// one leaves mostly idle.  Chain b of a batch does exactly the arithmetic of a
+// one-chain context with chain id chain0 + b (bit-identical; tested).  The MALA
+// accept test reduces its eight sums in a fixed order (bitwise reproducible).
 //
 // Per-pixel arrays are [F][Npix] over the field rows (F = 2: Q, U; F = 3:
 // T, Q, U); a_lm are real m-major [F][(L+1)^2].  Native draws: pixel normals
@@ -91,10 +95,15 @@ __global__ void k_mc_beam(int L, int F, const double* __restrict__ bl, const dou
 // y = v + N^-1 d (711-713), per pixel and field row
 __global__ void k_mc_v(long long npix, int F, Rows rows, int over, double alpha, const double* __restrict__ Abs,
                        const double* __restrict__ ninv, const double* __restrict__ dpix, double mu0, double mu1,
-                       double mu2, const double* __restrict__ zv, uint32_t seed_lo, uint32_t seed_hi, uint32_t chain,
-                       uint32_t sub, uint32_t iter, double* __restrict__ v, double* __restrict__ y) {
+                       double mu2, const double* __restrict__ zv, long long zvs, uint32_t seed_lo, uint32_t seed_hi,
+                       uint32_t chain, uint32_t sub, uint32_t iter, double* __restrict__ v, double* __restrict__ y) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (g >= F * npix) return;
+    // chain b of the batch: its maps (zvs: the chain stride of the replay normals)
+    const long long cb = (long long)blockIdx.y * F * npix;
+    Abs += cb; v += cb; y += cb;
+    if (zv) zv += (long long)blockIdx.y * zvs;
+    chain += blockIdx.y;
     const int k = (int)(g / npix);
     const long long p = g % npix;
     const int row = rows.r[k];
@@ -132,12 +141,18 @@ __device__ __forceinline__ void slot_normals(const double* __restrict__ zs, long
 // s' = mean + alpha (s - mean) + sqrt(1 - alpha^2) L z
 template <int F>
 __global__ void k_mc_s(int L, const double* __restrict__ params, const double* __restrict__ r_alm, double imu0,
-                       double imu1, double imu2, const double* __restrict__ zs, uint32_t seed_lo, uint32_t seed_hi,
-                       uint32_t chain, uint32_t sub, uint32_t iter, int over, double alpha, double* __restrict__ s) {
+                       double imu1, double imu2, const double* __restrict__ zs, long long zss, uint32_t seed_lo,
+                       uint32_t seed_hi, uint32_t chain, uint32_t sub, uint32_t iter, int over, double alpha,
+                       double* __restrict__ s) {
     const long long NR = (long long)(L + 1) * (L + 1);
     const long long nlm = (long long)(L + 1) * (L + 2) / 2;
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= nlm) return;
+    params += (long long)blockIdx.y * (L + 1) * GS_NPARAM;
+    r_alm += (long long)blockIdx.y * F * NR;
+    s += (long long)blockIdx.y * F * NR;
+    if (zs) zs += (long long)blockIdx.y * zss;
+    chain += blockIdx.y;
     int l, m;
     cidx_lm(L, i, l, m);
     const long long r = m == 0 ? l : 2 * i - (L + 1);
@@ -170,7 +185,9 @@ __global__ void k_mc_s(int L, const double* __restrict__ params, const double* _
     }
 }
 
-__global__ void k_set_one(int32_t* a) { *a = 1; }
+__global__ void k_set_one(int n, int32_t* a) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = 1;
+}
 
 __global__ void k_mc_mul(long long n, const double* __restrict__ a, const double* __restrict__ b,
                          double* __restrict__ out) {
@@ -192,6 +209,9 @@ __global__ void k_mc_grad(int L, int F, const double* __restrict__ dl, const dou
     const long long nlm = (long long)(L + 1) * (L + 2) / 2;
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (g >= F * nlm) return;
+    const long long cb = (long long)blockIdx.y * F * NR;
+    dl += (long long)blockIdx.y * (F == 3 ? 4 : F) * (L + 1);
+    s += cb; r_alm += cb; grad += cb;
     const int f = (int)(g / nlm);
     const long long i = g % nlm;
     int l, m;
@@ -214,6 +234,11 @@ __global__ void k_mc_propose(int L, int F, const double* __restrict__ params, co
     const long long nlm = (long long)(L + 1) * (L + 2) / 2;
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= nlm) return;
+    const long long cb = (long long)blockIdx.y * F * NR;
+    params += (long long)blockIdx.y * (L + 1) * GS_NPARAM;
+    s += cb; grad += cb; snew += cb;
+    if (zm) zm += cb;
+    chain += blockIdx.y;
     int l, m;
     cidx_lm(L, i, l, m);
     const long long r = m == 0 ? l : 2 * i - (L + 1);
@@ -243,6 +268,13 @@ __global__ __launch_bounds__(RED_BLOCK) void k_mc_sums(int L, int F, long long n
                                                        double* __restrict__ partial) {
     const long long NR = (long long)(L + 1) * (L + 1);
     const long long nslot = F * NR, npx = F * npix;
+    {
+        const long long cb = (long long)blockIdx.y * nslot, pb = (long long)blockIdx.y * npx;
+        dl += (long long)blockIdx.y * (F == 3 ? 4 : F) * (L + 1);
+        params += (long long)blockIdx.y * (L + 1) * GS_NPARAM;
+        s0 += cb; s1 += cb; g0 += cb; g1 += cb; p0 += pb; p1 += pb;
+        partial += (long long)blockIdx.y * gridDim.x * NSUM;
+    }
     double a[NSUM] = {0, 0, 0, 0, 0, 0, 0, 0};
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < nslot; g += stride) {
@@ -313,6 +345,14 @@ __global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long l
                             uint32_t seed_lo, uint32_t seed_hi, uint32_t chain, uint32_t call, uint32_t iter,
                             int32_t* __restrict__ flag, int32_t* __restrict__ accept,
                             double* __restrict__ log_ratio) {
+    // chain b = blockIdx.y of the batch (one workgroup per chain)
+    const int b = blockIdx.y;
+    partial += (long long)b * nblk * NSUM;
+    if (um) um += b;
+    chain += b;
+    flag += b;
+    if (accept) accept += b;
+    if (log_ratio) log_ratio += b;
     double t[NSUM];
     block_sums<NSUM>(nblk, partial, NSUM, t);
     if (threadIdx.x == 0) {
@@ -331,7 +371,9 @@ __global__ void k_mc_accept(int nblk, const double* __restrict__ partial, long l
 // accept workgroup alone took ~257 us for the 4.2 MB of an N_side 256 EB map)
 __global__ void k_select_copy(long long n, const int32_t* __restrict__ flag, const double* __restrict__ src,
                               double* __restrict__ dst) {
-    if (!*flag) return;
+    if (!flag[blockIdx.y]) return;
+    src += (long long)blockIdx.y * n;
+    dst += (long long)blockIdx.y * n;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += stride) dst[g] = src[g];
 }
@@ -341,6 +383,11 @@ __global__ void k_select_copy(long long n, const int32_t* __restrict__ flag, con
 __global__ __launch_bounds__(RED_BLOCK) void k_rj_dot(long long n, const double* __restrict__ rhs,
                                                       const double* __restrict__ y, const double* __restrict__ s,
                                                       const double* __restrict__ x, double* __restrict__ partial) {
+    {
+        const long long cb = (long long)blockIdx.y * n;
+        rhs += cb; y += cb; s += cb; x += cb;
+        partial += (long long)blockIdx.y * gridDim.x;
+    }
     double a = 0.0;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += stride)
@@ -362,6 +409,13 @@ __global__ __launch_bounds__(RED_BLOCK) void k_rj_accept(int nblk, const double*
                                                          uint32_t seed_hi, uint32_t chain, uint32_t iter,
                                                          int32_t* __restrict__ flag,
                                                          int32_t* __restrict__ accept, double* __restrict__ log_ratio) {
+    const int b = blockIdx.y;
+    partial += (long long)b * nblk;
+    if (um) um += b;
+    chain += b;
+    flag += b;
+    if (accept) accept += b;
+    if (log_ratio) log_ratio += b;
     double t[1];
     block_sums<1>(nblk, partial, 1, t);
     if (threadIdx.x == 0) {
@@ -409,6 +463,9 @@ __global__ void k_pcg_zpix(long long npix, int F, Rows rows, const double* __res
                            uint32_t iter, double* __restrict__ y) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (g >= F * npix) return;
+    y += (long long)blockIdx.y * F * npix;
+    if (zv) zv += (long long)blockIdx.y * F * npix;
+    chain += blockIdx.y;
     const int k = (int)(g / npix);
     const long long p = g % npix;
     const double z = zv ? zv[g]
@@ -427,6 +484,13 @@ __global__ void k_pcg_rhs(int L, const double* __restrict__ dl, const double* __
     const long long nlm = (long long)(L + 1) * (L + 2) / 2;
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= nlm) return;
+    {
+        const long long cb = (long long)blockIdx.y * F * NR;
+        dl += (long long)blockIdx.y * (F == 3 ? 4 : F) * (L + 1);
+        r_alm += cb; rhs += cb;
+        if (zs) zs += cb;
+        chain += blockIdx.y;
+    }
     int l, m;
     cidx_lm(L, i, l, m);
     const long long r = m == 0 ? l : 2 * i - (L + 1);
@@ -498,9 +562,17 @@ __global__ __launch_bounds__(RED_BLOCK) void k_pcg_qdot(int L, const double* __r
                                                         const double* __restrict__ r_alm, double inv_w,
                                                         double* __restrict__ out, double* __restrict__ partial,
                                                         const PcgState* __restrict__ st) {
-    if (st && st->done) return;
     const long long NR = (long long)(L + 1) * (L + 1);
     const long long nlm = (long long)(L + 1) * (L + 2) / 2;
+    {
+        const int b = blockIdx.y;
+        const long long cb = (long long)b * F * NR;
+        dl += (long long)b * (F == 3 ? 4 : F) * (L + 1);
+        x += cb; r_alm += cb; out += cb;
+        if (partial) partial += (long long)b * gridDim.x * NSUM;
+        if (st) st += b;
+    }
+    if (st && st->done) return;
     double acc[1] = {0.0};
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nlm; i += (long long)gridDim.x * blockDim.x) {
         int l, m;
@@ -539,6 +611,12 @@ __global__ __launch_bounds__(RED_BLOCK) void k_pcg_init(int L, const double* __r
                                                         double* __restrict__ z, double* __restrict__ pdir,
                                                         double* __restrict__ partial) {
     const long long NR = (long long)(L + 1) * (L + 1);
+    {
+        const long long cb = (long long)blockIdx.y * F * NR;
+        params += (long long)blockIdx.y * (L + 1) * GS_NPARAM;
+        rhs += cb; rr += cb; z += cb; pdir += cb;
+        partial += (long long)blockIdx.y * gridDim.x * NSUM;
+    }
     double acc[3] = {0.0, 0.0, 0.0};
     for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < NR; g += (long long)gridDim.x * blockDim.x) {
         int l;
@@ -573,6 +651,13 @@ __global__ __launch_bounds__(RED_BLOCK) void k_pcg_upd(int L, int nb, const doub
                                                        double* __restrict__ x, double* __restrict__ rr,
                                                        double* __restrict__ z, double* __restrict__ partial,
                                                        PcgState* __restrict__ st) {
+    {
+        const long long cb = (long long)blockIdx.y * F * (long long)(L + 1) * (L + 1);
+        params += (long long)blockIdx.y * (L + 1) * GS_NPARAM;
+        p += cb; q += cb; x += cb; rr += cb; z += cb;
+        partial += (long long)blockIdx.y * gridDim.x * NSUM;
+        st += blockIdx.y;
+    }
     if (st->done) return;
     double pq[1];
     block_sums<1>(nb, partial, NSUM, pq);
@@ -609,6 +694,8 @@ __global__ __launch_bounds__(RED_BLOCK) void k_pcg_upd(int L, int nb, const doub
 template <int MODE>
 __global__ __launch_bounds__(RED_BLOCK) void k_pcg_scal(int nblk, const double* __restrict__ partial,
                                                         PcgState* __restrict__ st, double tol, int maxiter) {
+    partial += (long long)blockIdx.y * nblk * NSUM;         // chain b: one workgroup
+    st += blockIdx.y;
     if (MODE != 0 && st->done) return;
     constexpr int NV = MODE == 0 ? 3 : (MODE == 1 ? 1 : 2);
     double t[NV];
@@ -637,7 +724,10 @@ __global__ __launch_bounds__(RED_BLOCK) void k_pcg_scal(int nblk, const double* 
 // p = z + beta p (after the iteration's last scalar update)
 __global__ void k_pcg_dir(long long n, const PcgState* __restrict__ st, const double* __restrict__ z,
                           double* __restrict__ p) {
+    st += blockIdx.y;
     if (st->done) return;
+    z += (long long)blockIdx.y * n;
+    p += (long long)blockIdx.y * n;
     const double b = st->beta;
     for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x)
         p[g] = z[g] + b * p[g];
@@ -645,6 +735,8 @@ __global__ void k_pcg_dir(long long n, const PcgState* __restrict__ st, const do
 
 __global__ __launch_bounds__(RED_BLOCK) void k_dot2_finish(int nblk, const double* __restrict__ partial,
                                                            double* __restrict__ out) {
+    partial += (long long)blockIdx.y * nblk * 2;
+    out += 2 * blockIdx.y;
     double t[2];
     block_sums<2>(nblk, partial, 2, t);
     if (threadIdx.x == 0) {
@@ -671,6 +763,9 @@ __global__ void k_mc_center(int L, const double* __restrict__ dl, int dir, const
     const long long NR = (long long)(L + 1) * (L + 1);
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (g >= NR) return;
+    dl += (long long)blockIdx.y * (F == 3 ? 4 : F) * (L + 1);
+    in += (long long)blockIdx.y * F * NR;
+    out += (long long)blockIdx.y * F * NR;
     int l;
     if (g <= L) l = (int)g;
     else { int m; cidx_lm(L, (g + L + 1) / 2, l, m); }
@@ -727,6 +822,8 @@ __global__ void k_synalm(int L, const double* __restrict__ cl, const double* __r
 __global__ __launch_bounds__(RED_BLOCK) void k_mc_resid(long long n, const double* __restrict__ d,
                                                         const double* __restrict__ m, const double* __restrict__ w,
                                                         double* __restrict__ partial) {
+    m += (long long)blockIdx.y * n;                          // chain b's model map (d, w shared)
+    partial += (long long)blockIdx.y * gridDim.x * 2;
     double s0 = 0.0;
     for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < n; g += (long long)gridDim.x * blockDim.x) {
         const double r = d[g] - m[g];
@@ -742,8 +839,8 @@ __global__ __launch_bounds__(RED_BLOCK) void k_mc_resid(long long n, const doubl
     if (threadIdx.x == 0) { partial[2 * blockIdx.x] = red[0]; partial[2 * blockIdx.x + 1] = 0.0; }
 }
 
-__global__ void k_mc_halfneg(const double* __restrict__ two, double* __restrict__ out) {
-    if (threadIdx.x == 0) *out = -0.5 * two[0];
+__global__ void k_mc_halfneg(int nb, const double* __restrict__ two, double* __restrict__ out) {
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) out[b] = -0.5 * two[2 * b];
 }
 
 // f4: temperature full-sky CR from pixel data (CenteredGibbs.py:108-132 centered,
@@ -761,6 +858,11 @@ __global__ void k_tt_fullsky(int L, const double* __restrict__ dl, const double*
     const long long nlm = (long long)(L + 1) * (L + 2) / 2;
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= nlm) return;
+    dl += (long long)blockIdx.y * (L + 1);
+    r_alm += (long long)blockIdx.y * NR;
+    s += (long long)blockIdx.y * NR;
+    if (zs) zs += (long long)blockIdx.y * NR;
+    chain += blockIdx.y;
     int l, m;
     cidx_lm(L, i, l, m);
     const long long r = m == 0 ? l : 2 * i - (L + 1);
@@ -1076,7 +1178,10 @@ __global__ void k_f2_update(long long n, int kn, const double* __restrict__ Y, c
 // ============================================================================
 struct gs_masked {
     int L = 0, nside = 0, F = 0, n_gibbs = 1, nblk = 0;
+    int B = 1;                       // chains of the batch
     long long npix = 0, NR = 0, nlm = 0;
+    long long FR = 0, FP = 0;        // per-chain strides: F (L+1)^2 slots, F Npix pixels
+    int nspec = 2;                   // D_l rows per chain (1, 2 or 4)
     double w = 0, alpha = -0.995, tau = 0.02, noise_pol0 = 1.0;
     double mu[3] = {0, 0, 0};
     double nbar[3] = {0, 0, 0};      // mean N^-1 per map row (PCG preconditioner)
@@ -1085,17 +1190,20 @@ struct gs_masked {
     int adj_iter = 0;
     Rows rows{{1, 2, 0}};
     gs_sht* sht = nullptr;
+    // shared by the batch (one data set): beam, data maps, N^-1, b A^T N^-1 d
     double *bl = nullptr, *dpix = nullptr, *ninv = nullptr, *g2 = nullptr;
+    // per chain ([B][...])
     double *params = nullptr, *params_mala = nullptr;
     int* ell2bin = nullptr;
     double *x = nullptr, *Abs = nullptr, *y = nullptr, *r = nullptr;
     double *grad0 = nullptr, *grad1 = nullptr, *snew = nullptr, *pix0 = nullptr, *pix1 = nullptr, *vtmp = nullptr;
     double *partial = nullptr, *lr = nullptr;
-    int32_t* accd = nullptr;         // the last MALA / RJPO accept decision (device)
+    int32_t* accd = nullptr;         // the last MALA / RJPO accept decisions (device, [B])
     double *pr = nullptr, *pz = nullptr, *pp = nullptr, *pq = nullptr, *params_pcg = nullptr, *dots = nullptr;
-    double* pcgs = nullptr;          // PcgState of the device CG
+    double* pcgs = nullptr;          // PcgState [B] of the device CG
     int pcg_syncs = 0;               // host synchronisations of the last solve
-    // f2 block MH workspace (allocated on first use, grown as needed)
+    int pcg_launched = 0;            // CG iterations launched by the last solve (>= every chain's count)
+    // f2 block MH workspace (one chain at a time; allocated on first use, grown as needed)
     double *f2_da = nullptr, *f2_r = nullptr, *f2_Y = nullptr, *f2_phib = nullptr, *f2_part = nullptr,
            *f2_G = nullptr, *f2_taken = nullptr;
     int* f2_blk = nullptr;
@@ -1125,68 +1233,71 @@ int mc_alloc(T** p, size_t n) {
     return 0;
 }
 
-// centered per-l blocks of a plan-less model: kappa_f for unbinned D_l [nspec][L+1]
+// centered per-l blocks of a plan-less model: kappa_f for unbinned D_l
+// [B][nspec][L+1] -> params [B][L+1][NP]
 template <int F>
-__global__ void k_mc_params(int L, const double* __restrict__ dl, const int* __restrict__ ell2bin,
+__global__ void k_mc_params(int L, int nch, const double* __restrict__ dl, const int* __restrict__ ell2bin,
                             const double* __restrict__ bl, double k0, double k1, double k2, double* __restrict__ params) {
-    block_params_at<F, GS_MODE_CENTERED>(blockIdx.x * blockDim.x + threadIdx.x, L, 1, L + 1, dl, ell2bin, bl, k0, k1,
+    block_params_at<F, GS_MODE_CENTERED>(blockIdx.x * blockDim.x + threadIdx.x, L, nch, L + 1, dl, ell2bin, bl, k0, k1,
                                          k2, params);
 }
 
-int mc_params(gs_masked* c, const double* dl, const double* kap, double* out, hipStream_t st) {
-    const dim3 g(nblocks(c->L + 1, 256)), b(256);
+int mc_params(gs_masked* c, int nch, const double* dl, const double* kap, double* out, hipStream_t st) {
+    const dim3 g(nblocks((long long)nch * (c->L + 1), 256)), b(256);
     if (c->F == 1)
-        hipLaunchKernelGGL(k_mc_params<1>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
+        hipLaunchKernelGGL(k_mc_params<1>, g, b, 0, st, c->L, nch, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
     else if (c->F == 2)
-        hipLaunchKernelGGL(k_mc_params<2>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
+        hipLaunchKernelGGL(k_mc_params<2>, g, b, 0, st, c->L, nch, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
     else
-        hipLaunchKernelGGL(k_mc_params<3>, g, b, 0, st, c->L, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
+        hipLaunchKernelGGL(k_mc_params<3>, g, b, 0, st, c->L, nch, dl, c->ell2bin, c->bl, kap[0], kap[1], kap[2], out);
     GS_LAUNCH_CHECK("k_mc_params");
     return 0;
 }
 
-// maps of b s  -> Abs (the beam applied on the transform's input load)
-int mc_synth(gs_masked* c, const double* s, double* out, hipStream_t st) {
-    return gs_sht_alm2map_beamed(c->sht, c->F, s, c->bl, out, st);
+// maps of b s for nch chains (the beam applied on the transform's input load)
+int mc_synth(gs_masked* c, int nch, const double* s, double* out, hipStream_t st) {
+    return gs_sht_alm2map_batch(c->sht, nch, c->F, GS_ALM_REAL, s, c->bl, out, st);
 }
 
-// one v | s then s | v pass (plain or over-relaxed)
-int mc_v(gs_masked* c, int over, const double* s, double* v, const double* zv, uint32_t slo, uint32_t shi,
-         uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
-    if (mc_synth(c, s, c->Abs, st)) return -1;
-    hipLaunchKernelGGL(k_mc_v, dim3(nblocks(c->F * c->npix, 256)), dim3(256), 0, st, c->npix, c->F, c->rows, over,
-                       c->alpha, c->Abs, c->ninv, c->dpix, c->mu[0], c->mu[1], c->mu[2], zv, slo, shi, chain, sub, it,
-                       v, c->y);
+// one v | s pass (plain or over-relaxed) for the whole batch; zv: chain 0's
+// replay normals of this pass, zvs their chain stride
+int mc_v(gs_masked* c, int over, const double* s, double* v, const double* zv, long long zvs, uint32_t slo,
+         uint32_t shi, uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
+    if (mc_synth(c, c->B, s, c->Abs, st)) return -1;
+    hipLaunchKernelGGL(k_mc_v, dim3(nblocks(c->FP, 256), c->B), dim3(256), 0, st, c->npix, c->F, c->rows, over,
+                       c->alpha, c->Abs, c->ninv, c->dpix, c->mu[0], c->mu[1], c->mu[2], zv, zvs, slo, shi, chain, sub,
+                       it, v, c->y);
     GS_LAUNCH_CHECK("k_mc_v");
     return 0;
 }
 
-int mc_s(gs_masked* c, int over, double* s, const double* zs, uint32_t slo, uint32_t shi, uint32_t chain,
-         uint32_t sub, uint32_t it, hipStream_t st) {
+int mc_s(gs_masked* c, int over, double* s, const double* zs, long long zss, uint32_t slo, uint32_t shi,
+         uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
     // s | v analysis: iter 0 explicit for EB/TEB (CenteredGibbs.py:717,773,812),
     // healpy's default iter = 3 for TT (CenteredGibbs.py:208)
-    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, c->adj_iter, st)) return -1;
+    if (gs_sht_map2alm_batch(c->sht, c->B, c->F, GS_ALM_REAL, c->y, nullptr, c->r, c->adj_iter, st)) return -1;
     double imu[3] = {0, 0, 0};
     for (int k = 0; k < c->F; ++k) imu[k] = 1.0 / c->mu[c->rows.r[k]];
-    const dim3 g(nblocks(c->nlm, 256)), b(256);
+    const dim3 g(nblocks(c->nlm, 256), c->B), b(256);
     if (c->F == 1)
-        hipLaunchKernelGGL(k_mc_s<1>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, slo, shi, chain,
-                           sub, it, over, c->alpha, s);
+        hipLaunchKernelGGL(k_mc_s<1>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, zss, slo, shi,
+                           chain, sub, it, over, c->alpha, s);
     else if (c->F == 2)
-        hipLaunchKernelGGL(k_mc_s<2>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, slo, shi, chain,
-                           sub, it, over, c->alpha, s);
+        hipLaunchKernelGGL(k_mc_s<2>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, zss, slo, shi,
+                           chain, sub, it, over, c->alpha, s);
     else
-        hipLaunchKernelGGL(k_mc_s<3>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, slo, shi, chain,
-                           sub, it, over, c->alpha, s);
+        hipLaunchKernelGGL(k_mc_s<3>, g, b, 0, st, c->L, c->params, c->r, imu[0], imu[1], imu[2], zs, zss, slo, shi,
+                           chain, sub, it, over, c->alpha, s);
     GS_LAUNCH_CHECK("k_mc_s");
     return 0;
 }
 
 int mc_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, hipStream_t st) {
-    if (mc_synth(c, s, pix, st)) return -1;
-    if (gs_sht_map2alm_weighted(c->sht, c->F, pix, c->ninv, c->r, st)) return -1;      // map2alm(N^-1 A b s)
-    hipLaunchKernelGGL(k_mc_grad, dim3(nblocks(c->F * c->nlm, 256)), dim3(256), 0, st, c->L, c->F, dl, c->bl, s, c->r,
-                       c->g2, 1.0 / c->w, grad);
+    if (mc_synth(c, c->B, s, pix, st)) return -1;
+    // map2alm(N^-1 A b s), N^-1 applied on the ring stage's pixel load
+    if (gs_sht_map2alm_batch(c->sht, c->B, c->F, GS_ALM_REAL, pix, c->ninv, c->r, 0, st)) return -1;
+    hipLaunchKernelGGL(k_mc_grad, dim3(nblocks(c->F * c->nlm, 256), c->B), dim3(256), 0, st, c->L, c->F, dl, c->bl, s,
+                       c->r, c->g2, 1.0 / c->w, grad);
     GS_LAUNCH_CHECK("k_mc_grad");
     return 0;
 }
@@ -1201,9 +1312,11 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     if (desc->nfields < 1 || desc->nfields > 3)
         return set_error("gs_masked_create: nfields must be 1 (T), 2 (EB) or 3 (TEB)");
     if (desc->adj_iter < 0 || desc->adj_iter > 16) return set_error("gs_masked_create: adj_iter out of range");
+    if (desc->nchains < 0 || desc->nchains > 4096) return set_error("gs_masked_create: nchains out of range");
     if (!desc->bl) return set_error("gs_masked_create: null beam");
     gs_masked* c = new gs_masked();
     c->L = desc->lmax; c->nside = desc->nside; c->F = desc->nfields;
+    c->B = std::max(1, desc->nchains);
     c->n_gibbs = std::max(1, desc->n_gibbs);
     c->alpha = desc->alpha; c->tau = desc->tau; c->noise_pol0 = desc->noise_pol0;
     c->mu_eps = desc->mu_eps > 0.0 ? desc->mu_eps : 1e-14;
@@ -1211,39 +1324,44 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     c->npix = 12LL * c->nside * c->nside;
     c->NR = (long long)(c->L + 1) * (c->L + 1);
     c->nlm = (long long)(c->L + 1) * (c->L + 2) / 2;
+    c->FR = c->F * c->NR;
+    c->FP = c->F * c->npix;
+    c->nspec = c->F == 3 ? 4 : c->F;
     c->w = 4.0 * PI / (double)c->npix;
     c->rows = c->F == 2 ? Rows{{1, 2, 0}} : Rows{{0, 1, 2}};      // F = 1: the T row
     c->nblk = (int)std::min<long long>(512, nblocks(std::max(c->F * c->NR, c->F * c->npix), RED_BLOCK));
     if (gs_sht_create(c->nside, c->L, &c->sht)) { mc_free(c); return -1; }
-    const long long FR = c->F * c->NR, FP = c->F * c->npix;
+    if (gs_sht_reserve(c->sht, c->B, nullptr)) { mc_free(c); return -1; }
+    const long long FR = c->FR, FP = c->FP;
+    const size_t B = (size_t)c->B;
     int rc = 0;
     rc |= mc_alloc(&c->bl, c->L + 1);
     rc |= mc_alloc(&c->dpix, FP);
     rc |= mc_alloc(&c->ninv, FP);
     rc |= mc_alloc(&c->g2, FR);
-    rc |= mc_alloc(&c->params, (size_t)(c->L + 1) * GS_NPARAM);
-    rc |= mc_alloc(&c->params_mala, (size_t)(c->L + 1) * GS_NPARAM);
+    rc |= mc_alloc(&c->params, B * (c->L + 1) * GS_NPARAM);
+    rc |= mc_alloc(&c->params_mala, B * (c->L + 1) * GS_NPARAM);
     rc |= mc_alloc(&c->ell2bin, (size_t)4 * (c->L + 1));
-    rc |= mc_alloc(&c->x, FR);
-    rc |= mc_alloc(&c->Abs, FP);
-    rc |= mc_alloc(&c->y, FP);
-    rc |= mc_alloc(&c->r, FR);
-    rc |= mc_alloc(&c->grad0, FR);
-    rc |= mc_alloc(&c->grad1, FR);
-    rc |= mc_alloc(&c->snew, FR);
-    rc |= mc_alloc(&c->pix0, FP);
-    rc |= mc_alloc(&c->pix1, FP);
-    rc |= mc_alloc(&c->vtmp, FP);
-    rc |= mc_alloc(&c->partial, (size_t)c->nblk * NSUM);
-    rc |= mc_alloc(&c->lr, 1);
-    rc |= mc_alloc(&c->accd, 1);
-    rc |= mc_alloc(&c->pr, FR);
-    rc |= mc_alloc(&c->pz, FR);
-    rc |= mc_alloc(&c->pp, FR);
-    rc |= mc_alloc(&c->pq, FR);
-    rc |= mc_alloc(&c->params_pcg, (size_t)(c->L + 1) * GS_NPARAM);
-    rc |= mc_alloc(&c->dots, 2);
-    rc |= mc_alloc(&c->pcgs, 8);
+    rc |= mc_alloc(&c->x, B * FR);
+    rc |= mc_alloc(&c->Abs, B * FP);
+    rc |= mc_alloc(&c->y, B * FP);
+    rc |= mc_alloc(&c->r, B * FR);
+    rc |= mc_alloc(&c->grad0, B * FR);
+    rc |= mc_alloc(&c->grad1, B * FR);
+    rc |= mc_alloc(&c->snew, B * FR);
+    rc |= mc_alloc(&c->pix0, B * FP);
+    rc |= mc_alloc(&c->pix1, B * FP);
+    rc |= mc_alloc(&c->vtmp, B * FP);
+    rc |= mc_alloc(&c->partial, B * c->nblk * NSUM);
+    rc |= mc_alloc(&c->lr, B);
+    rc |= mc_alloc(&c->accd, B);
+    rc |= mc_alloc(&c->pr, B * FR);
+    rc |= mc_alloc(&c->pz, B * FR);
+    rc |= mc_alloc(&c->pp, B * FR);
+    rc |= mc_alloc(&c->pq, B * FR);
+    rc |= mc_alloc(&c->params_pcg, B * (c->L + 1) * GS_NPARAM);
+    rc |= mc_alloc(&c->dots, 2 * B);
+    rc |= mc_alloc(&c->pcgs, B * (sizeof(PcgState) / sizeof(double)));
     if (rc) { mc_free(c); return -1; }
     std::vector<int> e2b((size_t)4 * (c->L + 1));
     for (int sp = 0; sp < 4; ++sp)
@@ -1304,6 +1422,8 @@ int gs_masked_info(const gs_masked* c, double* mu3, double* second_part_grad) {
     return 0;
 }
 
+int gs_masked_nchains(const gs_masked* c) { return c ? c->B : set_error("null masked context"); }
+
 int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, void* stream) {
     if (!c) return set_error("null masked context");
     if (!dl || !s || !grad || !pix) return set_error("gs_masked_gradient: null argument");
@@ -1311,12 +1431,13 @@ int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* 
 }
 
 // ---- f1 PCG ----------------------------------------------------------------
-// A Q p without its dot product (partial == nullptr) or with the per-block p . Q p
+// A Q p for the batch, without its dot product (partial == nullptr) or with the
+// per-block p . Q p of every chain
 static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, double* partial, int nb,
                      const PcgState* state, hipStream_t st) {
-    if (mc_synth(c, x, c->pix0, st)) return -1;
-    if (gs_sht_map2alm_weighted(c->sht, c->F, c->pix0, c->ninv, c->r, st)) return -1;   // map2alm(N^-1 A b x)
-    const dim3 g(partial ? nb : nblocks(c->nlm, RED_BLOCK)), b(RED_BLOCK);
+    if (mc_synth(c, c->B, x, c->pix0, st)) return -1;
+    if (gs_sht_map2alm_batch(c->sht, c->B, c->F, GS_ALM_REAL, c->pix0, c->ninv, c->r, 0, st)) return -1;
+    const dim3 g(partial ? nb : nblocks(c->nlm, RED_BLOCK), c->B), b(RED_BLOCK);
     const double iw = 1.0 / c->w;
     if (c->F == 1) hipLaunchKernelGGL(k_pcg_qdot<1>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);
     else if (c->F == 2) hipLaunchKernelGGL(k_pcg_qdot<2>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);
@@ -1331,13 +1452,12 @@ int gs_masked_pcg_rhs(gs_masked* c, const double* dl, const double* zv, const do
     if (!dl || !rhs) return set_error("gs_masked_pcg_rhs: null argument");
     const hipStream_t st = S(stream);
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32), ch = (uint32_t)chain;
-    const long long n = c->F * c->npix;
-    hipLaunchKernelGGL(k_pcg_zpix, dim3(nblocks(n, 256)), dim3(256), 0, st, c->npix, c->F, c->rows, c->ninv, zv,
-                       slo, shi, ch, iteration, c->y);
+    hipLaunchKernelGGL(k_pcg_zpix, dim3(nblocks(c->FP, 256), c->B), dim3(256), 0, st, c->npix, c->F, c->rows, c->ninv,
+                       zv, slo, shi, ch, iteration, c->y);
     GS_LAUNCH_CHECK("k_pcg_zpix");
     // adjoint_synthesis_hp: map2alm with healpy's default iter = 3 (utils.py:89,104)
-    if (gs_sht_map2alm(c->sht, c->F, GS_ALM_REAL, c->y, c->r, 3, st)) return -1;
-    const dim3 g(nblocks(c->nlm, 256)), b(256);
+    if (gs_sht_map2alm_batch(c->sht, c->B, c->F, GS_ALM_REAL, c->y, nullptr, c->r, 3, st)) return -1;
+    const dim3 g(nblocks(c->nlm, 256), c->B), b(256);
     const double resc = (double)c->npix / (4.0 * PI);
     if (c->F == 1)
         hipLaunchKernelGGL(k_pcg_rhs<1>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, zs, slo, shi, ch,
@@ -1352,44 +1472,47 @@ int gs_masked_pcg_rhs(gs_masked* c, const double* dl, const double* zv, const do
     return 0;
 }
 
-// Preconditioned CG on the device.  One iteration = A Q p (two SHTs) with the
-// fused p . Q p partials, alpha on the device, the fused update / preconditioner
-// / (r . z, r . r) pass, beta / rz / rn / convergence on the device, the new
-// direction.  Every kernel reads the scalars from the device state and returns
-// at once after convergence, so the host launches whole batches of iterations
-// and reads the state once per batch: the batch length follows the residual's
-// observed decay (the predicted remaining iterations, 1..64), so an extra batch
-// costs one stream synchronisation and an overshoot at most a few iterations'
-// transforms -- never one host round trip per iteration (the qcinv loop,
-// CenteredGibbs.py:484-488, and this build's r02 form both synchronised per
-// iteration).
+// Preconditioned CG on the device, every chain of the batch at once.  One
+// iteration = one batched A Q p (two SHTs over the B maps) with the fused
+// p . Q p partials, alpha per chain on the device, the fused update /
+// preconditioner / (r . z, r . r) pass, beta / rz / rn / convergence per chain,
+// the new directions.  Every kernel reads its chain's scalars from the device
+// state and returns at once after that chain converged (a converged chain's x
+// no longer changes, so each chain follows exactly its one-chain solve), so the
+// host launches whole batches of iterations and reads the B states once per
+// batch: the batch length follows the slowest chain's residual decay (its
+// predicted remaining iterations, 1..64) -- never one host round trip per
+// iteration (the qcinv loop, CenteredGibbs.py:484-488, synchronised per
+// iteration).  The transforms of a converged chain keep running until the
+// batch's last chain converges (their results are not used).
 int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
                         int maxiter, int* iters, double* rel_residual, void* stream) {
     if (!c) return set_error("null masked context");
     if (!dl || !rhs || !x) return set_error("gs_masked_pcg_solve: null argument");
     if (maxiter < 0) return set_error("gs_masked_pcg_solve: maxiter < 0");
     const hipStream_t st = S(stream);
-    const long long n = c->F * c->NR;
+    const long long n = c->FR;
+    const int B = c->B;
     PcgState* dst = reinterpret_cast<PcgState*>(c->pcgs);
     // preconditioner: centered per-l block with kappa_f = nbar_f / w ("diag_cl")
     double kap[3] = {0, 0, 0};
     for (int k = 0; k < c->F; ++k) kap[k] = c->nbar[c->rows.r[k]] / c->w;
-    if (mc_params(c, dl, kap, c->params_pcg, st)) return -1;
+    if (mc_params(c, B, dl, kap, c->params_pcg, st)) return -1;
     const int nb = (int)std::min<long long>(c->nblk, nblocks(c->nlm, RED_BLOCK));
     if (x_is_guess) {
         if (pcg_apply(c, dl, x, c->pr, nullptr, 0, nullptr, st)) return -1;
-        hipLaunchKernelGGL(k_sub_from, dim3(nblocks(n, 256)), dim3(256), 0, st, n, rhs, c->pr);   // r = rhs - Qx
+        hipLaunchKernelGGL(k_sub_from, dim3(nblocks(B * n, 256)), dim3(256), 0, st, B * n, rhs, c->pr);   // r = rhs - Qx
         GS_LAUNCH_CHECK("k_sub_from");
     } else {
-        GS_CHECK(hipMemsetAsync(x, 0, n * sizeof(double), st));
-        GS_CHECK(hipMemcpyAsync(c->pr, rhs, n * sizeof(double), hipMemcpyDeviceToDevice, st));
+        GS_CHECK(hipMemsetAsync(x, 0, B * n * sizeof(double), st));
+        GS_CHECK(hipMemcpyAsync(c->pr, rhs, B * n * sizeof(double), hipMemcpyDeviceToDevice, st));
     }
-    const dim3 gb(nb), bb(RED_BLOCK);
+    const dim3 gb(nb, B), bb(RED_BLOCK), g1(1, B);
 #define GS_PI(FF) hipLaunchKernelGGL((k_pcg_init<FF>), gb, bb, 0, st, c->L, c->params_pcg, rhs, c->pr, c->pz, c->pp, \
                                      c->partial)
     if (c->F == 1) GS_PI(1); else if (c->F == 2) GS_PI(2); else GS_PI(3);
 #undef GS_PI
-    hipLaunchKernelGGL(k_pcg_scal<0>, dim3(1), bb, 0, st, nb, c->partial, dst, tol, maxiter);
+    hipLaunchKernelGGL(k_pcg_scal<0>, g1, bb, 0, st, nb, c->partial, dst, tol, maxiter);
     GS_LAUNCH_CHECK("k_pcg_init");
     auto iteration = [&]() -> int {
         if (pcg_apply(c, dl, c->pp, c->pq, c->partial, nb, dst, st)) return -1;
@@ -1397,39 +1520,54 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
                                      c->pz, c->partial, dst)
         if (c->F == 1) GS_PU(1); else if (c->F == 2) GS_PU(2); else GS_PU(3);
 #undef GS_PU
-        hipLaunchKernelGGL(k_pcg_scal<2>, dim3(1), bb, 0, st, nb, c->partial, dst, tol, maxiter);
-        hipLaunchKernelGGL(k_pcg_dir, dim3(nb), bb, 0, st, n, dst, c->pz, c->pp);
+        hipLaunchKernelGGL(k_pcg_scal<2>, g1, bb, 0, st, nb, c->partial, dst, tol, maxiter);
+        hipLaunchKernelGGL(k_pcg_dir, gb, bb, 0, st, n, dst, c->pz, c->pp);
         GS_LAUNCH_CHECK("pcg iteration");
         return 0;
     };
-    PcgState h{};
+    std::vector<PcgState> h((size_t)B);
     auto read_state = [&]() -> int {
-        GS_CHECK(hipMemcpyAsync(&h, dst, sizeof(PcgState), hipMemcpyDeviceToHost, st));
+        GS_CHECK(hipMemcpyAsync(h.data(), dst, B * sizeof(PcgState), hipMemcpyDeviceToHost, st));
         GS_CHECK(hipStreamSynchronize(st));
         return 0;
     };
+    auto all_done = [&]() {
+        for (const auto& q : h)
+            if (!q.done) return false;
+        return true;
+    };
     if (read_state()) return -1;
     int launched = 0, batch = 8;
-    double rn_prev = h.rn;
+    std::vector<double> rn_prev((size_t)B);
+    for (int b = 0; b < B; ++b) rn_prev[b] = h[b].rn;
     c->pcg_syncs = 1;
-    while (!h.done && launched < maxiter) {
+    while (!all_done() && launched < maxiter) {
         const int k = std::max(1, std::min(batch, maxiter - launched));
         for (int j = 0; j < k; ++j)
             if (iteration()) return -1;
         launched += k;
         if (read_state()) return -1;
         ++c->pcg_syncs;
-        if (h.done) break;
-        // predicted remaining iterations from the residual's decay over this batch
-        const double rate = rn_prev > 0.0 && h.rn > 0.0 ? std::pow(h.rn / rn_prev, 1.0 / k) : 0.5;
-        const double want = h.tol * h.bn;
-        double rem = 64.0;
-        if (rate < 1.0 && rate > 0.0 && h.rn > want) rem = std::log(want / h.rn) / std::log(rate);
-        batch = (int)std::max(1.0, std::min(64.0, std::floor(rem)));
-        rn_prev = h.rn;
+        if (all_done()) break;
+        // predicted remaining iterations of the slowest chain from its residual's
+        // decay over this batch
+        double rem_max = 1.0;
+        for (int b = 0; b < B; ++b) {
+            if (h[b].done) continue;
+            const double rate = rn_prev[b] > 0.0 && h[b].rn > 0.0 ? std::pow(h[b].rn / rn_prev[b], 1.0 / k) : 0.5;
+            const double want = h[b].tol * h[b].bn;
+            double rem = 64.0;
+            if (rate < 1.0 && rate > 0.0 && h[b].rn > want) rem = std::log(want / h[b].rn) / std::log(rate);
+            rem_max = std::max(rem_max, rem);
+        }
+        batch = (int)std::max(1.0, std::min(64.0, std::floor(rem_max)));
+        for (int b = 0; b < B; ++b) rn_prev[b] = h[b].rn;
     }
-    if (iters) *iters = h.it;
-    if (rel_residual) *rel_residual = h.bn > 0 ? h.rn / h.bn : 0.0;
+    c->pcg_launched = launched;
+    for (int b = 0; b < B; ++b) {
+        if (iters) iters[b] = h[b].it;
+        if (rel_residual) rel_residual[b] = h[b].bn > 0 ? h[b].rn / h[b].bn : 0.0;
+    }
     return 0;
 }
 
@@ -1445,16 +1583,16 @@ int gs_masked_rj_accept(gs_masked* c, const double* dl, const double* rhs, const
     if (!c) return set_error("null masked context");
     if (!dl || !rhs || !x || !s) return set_error("gs_masked_rj_accept: null argument");
     const hipStream_t st = S(stream);
-    const long long n = c->F * c->NR;
+    const long long n = c->FR;
     if (pcg_apply(c, dl, x, c->pr, nullptr, 0, nullptr, st)) return -1;          // Q x (fwd_op, :655)
     const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
-    hipLaunchKernelGGL(k_rj_dot, dim3(nb), dim3(RED_BLOCK), 0, st, n, rhs, c->pr, s, x, c->partial);
+    hipLaunchKernelGGL(k_rj_dot, dim3(nb, c->B), dim3(RED_BLOCK), 0, st, n, rhs, c->pr, s, x, c->partial);
     GS_LAUNCH_CHECK("k_rj_dot");
-    hipLaunchKernelGGL(k_rj_accept, dim3(1), dim3(RED_BLOCK), 0, st, nb, c->partial, n, um,
+    hipLaunchKernelGGL(k_rj_accept, dim3(1, c->B), dim3(RED_BLOCK), 0, st, nb, c->partial, n, um,
                        (uint32_t)(seed & 0xFFFFFFFFu), (uint32_t)(seed >> 32), (uint32_t)chain, iteration, c->accd,
                        accept, log_ratio);
     GS_LAUNCH_CHECK("k_rj_accept");
-    hipLaunchKernelGGL(k_select_copy, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->accd, x, s);
+    hipLaunchKernelGGL(k_select_copy, dim3(nblocks(n, 256), c->B), dim3(256), 0, st, n, c->accd, x, s);
     GS_LAUNCH_CHECK("k_select_copy");
     return 0;
 }
@@ -1465,16 +1603,28 @@ int gs_masked_pcg_info(const gs_masked* c, int* host_syncs) {
     return 0;
 }
 
+int gs_masked_pcg_info2(const gs_masked* c, int* host_syncs, int* launched) {
+    if (!c) return set_error("null masked context");
+    if (host_syncs) *host_syncs = c->pcg_syncs;
+    if (launched) *launched = c->pcg_launched;
+    return 0;
+}
+
 // ---- f2 --------------------------------------------------------------------
+static int masked_center(gs_masked* c, int nch, const double* dl, int dir, const double* in, double* out,
+                         hipStream_t st) {
+    const dim3 g(nblocks(c->NR, 256), nch), b(256);
+    if (c->F == 1) hipLaunchKernelGGL(k_mc_center<1>, g, b, 0, st, c->L, dl, dir, in, out);
+    else if (c->F == 2) hipLaunchKernelGGL(k_mc_center<2>, g, b, 0, st, c->L, dl, dir, in, out);
+    else hipLaunchKernelGGL(k_mc_center<3>, g, b, 0, st, c->L, dl, dir, in, out);
+    GS_LAUNCH_CHECK("k_mc_center");
+    return 0;
+}
+
 int gs_masked_center(gs_masked* c, const double* dl, int dir, const double* in, double* out, void* stream) {
     if (!c) return set_error("null masked context");
     if (!dl || !in || !out) return set_error("gs_masked_center: null argument");
-    const dim3 g(nblocks(c->NR, 256)), b(256);
-    if (c->F == 1) hipLaunchKernelGGL(k_mc_center<1>, g, b, 0, S(stream), c->L, dl, dir, in, out);
-    else if (c->F == 2) hipLaunchKernelGGL(k_mc_center<2>, g, b, 0, S(stream), c->L, dl, dir, in, out);
-    else hipLaunchKernelGGL(k_mc_center<3>, g, b, 0, S(stream), c->L, dl, dir, in, out);
-    GS_LAUNCH_CHECK("k_mc_center");
-    return 0;
+    return masked_center(c, c->B, dl, dir, in, out, S(stream));
 }
 
 int gs_synalm(int lmax, int nfields, const double* cl, const double* beam, const double* z, double* alm,
@@ -1494,13 +1644,13 @@ int gs_masked_nc_loglik(gs_masked* c, const double* dl, const double* s_nc, doub
     if (!c) return set_error("null masked context");
     if (!dl || !s_nc || !lik) return set_error("gs_masked_nc_loglik: null argument");
     const hipStream_t st = S(stream);
-    if (gs_masked_center(c, dl, +1, s_nc, c->snew, stream)) return -1;
-    if (mc_synth(c, c->snew, c->pix1, st)) return -1;
-    const long long n = c->F * c->npix;
+    if (masked_center(c, c->B, dl, +1, s_nc, c->snew, st)) return -1;
+    if (mc_synth(c, c->B, c->snew, c->pix1, st)) return -1;
+    const long long n = c->FP;
     const int nb = (int)std::min<long long>(c->nblk, nblocks(n, RED_BLOCK));
-    hipLaunchKernelGGL(k_mc_resid, dim3(nb), dim3(RED_BLOCK), 0, st, n, c->dpix, c->pix1, c->ninv, c->partial);
-    hipLaunchKernelGGL(k_dot2_finish, dim3(1), dim3(RED_BLOCK), 0, st, nb, c->partial, c->dots);
-    hipLaunchKernelGGL(k_mc_halfneg, dim3(1), dim3(64), 0, st, c->dots, lik);
+    hipLaunchKernelGGL(k_mc_resid, dim3(nb, c->B), dim3(RED_BLOCK), 0, st, n, c->dpix, c->pix1, c->ninv, c->partial);
+    hipLaunchKernelGGL(k_dot2_finish, dim3(1, c->B), dim3(RED_BLOCK), 0, st, nb, c->partial, c->dots);
+    hipLaunchKernelGGL(k_mc_halfneg, dim3(1), dim3(64), 0, st, c->B, c->dots, lik);
     GS_LAUNCH_CHECK("k_mc_resid");
     return 0;
 }
@@ -1516,6 +1666,65 @@ static int f2_group(const gs_masked* c) {
     return (int)std::max(1LL, std::min<long long>(F2_RMAX - 1, budget / std::max(per, 1LL)));
 }
 
+// one chain's sweep (pointers at that chain's slices; chain-0-relative scratch)
+static int pixel_mh_one(gs_masked* c, int K, int n_iter, int maxbins, const int* blk, const int* blk_lmax,
+                        const int* blk_field, const int* blk_bins, const double* s_nc, const double* dl_cur,
+                        const double* dl_prop, const double* logr, const double* u_acc, const double* prop_binned,
+                        double* binned, int32_t* accept_out, hipStream_t st) {
+    const int F = c->F;
+    const int KG = f2_group(c);
+    const long long n = (long long)F * c->npix;
+    const long long nchunk = (n + F2_CHUNK - 1) / F2_CHUNK;
+    // residual of the current state: r = d - A b C_cur^1/2 s_nc
+    if (masked_center(c, 1, dl_cur, +1, s_nc, c->snew, st)) return -1;
+    if (mc_synth(c, 1, c->snew, c->pix1, st)) return -1;
+    hipLaunchKernelGGL(k_f2_resid, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->dpix, c->pix1, c->f2_r);
+    GS_LAUNCH_CHECK("k_f2_resid");
+    for (int k0 = 0; k0 < K; k0 += KG) {
+        const int kn = std::min(KG, K - k0);
+        const int R = kn + 1;
+        const dim3 gd(nblocks(std::max<long long>(c->NR, c->L + 1), 256)), bd(256);
+        if (F == 1)
+            hipLaunchKernelGGL(k_f2_delta<1>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
+                               c->f2_blk);
+        else
+            hipLaunchKernelGGL(k_f2_delta<2>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
+                               c->f2_blk);
+        GS_LAUNCH_CHECK("k_f2_delta");
+        if (gs_sht_synth_blocks(c->sht, F, c->f2_da, c->f2_blk, kn, blk_lmax + k0, c->f2_phib, c->f2_Y, st))
+            return -1;
+        launch_gram_mfma_t<1>((R + 15) / 16, (unsigned)nchunk, st, R, n, c->f2_Y, c->f2_r, c->ninv, c->f2_part);
+        GS_LAUNCH_CHECK("k_f2_gram_mfma");
+        hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256)), dim3(256), 0, st, R, (int)nchunk,
+                           c->f2_part, c->f2_G);
+        GS_LAUNCH_CHECK("k_f2_gram_finish");
+        // dynamic LDS: G's lower triangle (<= 124.6 KB at F2_RMAX rows), plus the
+        // log uniforms when they fit in what the static arrays leave of 160 KB
+        const size_t tri = (size_t)R * (R + 1) / 2 * sizeof(double);
+        const size_t lus = (size_t)kn * n_iter * sizeof(double);
+        const int lu_lds = tri + lus <= F2_DECIDE_LDS ? 1 : 0;
+        const size_t dlds = tri + (lu_lds ? lus : 0);
+        if (dlds > F2_DECIDE_LDS) return set_error("gs_masked_pixel_mh: Gram triangle exceeds the decision LDS");
+        if (dlds > 64 * 1024 &&                 // the triangle of G beyond 64 KB of dynamic LDS
+            hipFuncSetAttribute((const void*)k_f2_decide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds) !=
+                hipSuccess) {
+            (void)hipGetLastError();
+            return set_error("gs_masked_pixel_mh: cannot raise k_f2_decide's dynamic LDS limit");
+        }
+        hipLaunchKernelGGL(k_f2_decide, dim3(1), dim3(256), dlds, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
+                           maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken, lu_lds);
+        GS_LAUNCH_CHECK("k_f2_decide");
+        if (k0 + kn < K) {
+            hipLaunchKernelGGL(k_f2_update, dim3(nblocks(n, 256)), dim3(256), 0, st, n, kn, c->f2_Y, c->f2_taken,
+                               c->f2_r);
+            GS_LAUNCH_CHECK("k_f2_update");
+        }
+    }
+    return 0;
+}
+
+// the batch: one sweep per chain (each chain's block synthesis, Gram pass and
+// decisions are whole-GPU launches already), the chains in order on one stream
 int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* blk, const int* blk_lmax,
                        const int* blk_field, const int* blk_bins, const double* s_nc, const double* dl_cur,
                        const double* dl_prop, const double* logr, const double* u_acc, const double* prop_binned,
@@ -1558,51 +1767,12 @@ int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* 
         rc |= mc_alloc(&c->f2_blk, (size_t)F * (c->L + 1));
         if (rc) return -1;
     }
-    // residual of the current state: r = d - A b C_cur^1/2 s_nc
-    if (gs_masked_center(c, dl_cur, +1, s_nc, c->snew, stream)) return -1;
-    if (mc_synth(c, c->snew, c->pix1, st)) return -1;
-    hipLaunchKernelGGL(k_f2_resid, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->dpix, c->pix1, c->f2_r);
-    GS_LAUNCH_CHECK("k_f2_resid");
-    for (int k0 = 0; k0 < K; k0 += KG) {
-        const int kn = std::min(KG, K - k0);
-        const int R = kn + 1;
-        const dim3 gd(nblocks(std::max<long long>(c->NR, c->L + 1), 256)), bd(256);
-        if (F == 1)
-            hipLaunchKernelGGL(k_f2_delta<1>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
-                               c->f2_blk);
-        else
-            hipLaunchKernelGGL(k_f2_delta<2>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
-                               c->f2_blk);
-        GS_LAUNCH_CHECK("k_f2_delta");
-        if (gs_sht_synth_blocks(c->sht, F, c->f2_da, c->f2_blk, kn, blk_lmax + k0, c->f2_phib, c->f2_Y, stream))
+    const long long dls = (long long)F * (c->L + 1), bins = (long long)F * maxbins, acc = (long long)K * n_iter;
+    for (int b = 0; b < c->B; ++b)
+        if (pixel_mh_one(c, K, n_iter, maxbins, blk, blk_lmax, blk_field, blk_bins, s_nc + b * c->FR,
+                         dl_cur + b * dls, dl_prop + b * dls, logr + b * bins, u_acc + b * acc,
+                         prop_binned + b * bins, binned + b * bins, accept_out + b * acc, st))
             return -1;
-        launch_gram_mfma_t<1>((R + 15) / 16, (unsigned)nchunk, st, R, n, c->f2_Y, c->f2_r, c->ninv, c->f2_part);
-        GS_LAUNCH_CHECK("k_f2_gram_mfma");
-        hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256)), dim3(256), 0, st, R, (int)nchunk,
-                           c->f2_part, c->f2_G);
-        GS_LAUNCH_CHECK("k_f2_gram_finish");
-        // dynamic LDS: G's lower triangle (<= 124.6 KB at F2_RMAX rows), plus the
-        // log uniforms when they fit in what the static arrays leave of 160 KB
-        const size_t tri = (size_t)R * (R + 1) / 2 * sizeof(double);
-        const size_t lus = (size_t)kn * n_iter * sizeof(double);
-        const int lu_lds = tri + lus <= F2_DECIDE_LDS ? 1 : 0;
-        const size_t dlds = tri + (lu_lds ? lus : 0);
-        if (dlds > F2_DECIDE_LDS) return set_error("gs_masked_pixel_mh: Gram triangle exceeds the decision LDS");
-        if (dlds > 64 * 1024 &&                 // the triangle of G beyond 64 KB of dynamic LDS
-            hipFuncSetAttribute((const void*)k_f2_decide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dlds) !=
-                hipSuccess) {
-            (void)hipGetLastError();
-            return set_error("gs_masked_pixel_mh: cannot raise k_f2_decide's dynamic LDS limit");
-        }
-        hipLaunchKernelGGL(k_f2_decide, dim3(1), dim3(256), dlds, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
-                           maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken, lu_lds);
-        GS_LAUNCH_CHECK("k_f2_decide");
-        if (k0 + kn < K) {
-            hipLaunchKernelGGL(k_f2_update, dim3(nblocks(n, 256)), dim3(256), 0, st, n, kn, c->f2_Y, c->f2_taken,
-                               c->f2_r);
-            GS_LAUNCH_CHECK("k_f2_update");
-        }
-    }
     return 0;
 }
 
@@ -1613,13 +1783,13 @@ int gs_masked_tt_fullsky(gs_masked* c, int noncentered, const double* dl, const 
     if (!dl || !s_out) return set_error("gs_masked_tt_fullsky: null argument");
     const hipStream_t st = S(stream);
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32), ch = (uint32_t)chain;
-    hipLaunchKernelGGL(k_pcg_zpix, dim3(nblocks(c->npix, 256)), dim3(256), 0, st, c->npix, 1, c->rows, c->ninv, zv,
-                       slo, shi, ch, iteration, c->y);
+    hipLaunchKernelGGL(k_pcg_zpix, dim3(nblocks(c->npix, 256), c->B), dim3(256), 0, st, c->npix, 1, c->rows, c->ninv,
+                       zv, slo, shi, ch, iteration, c->y);
     GS_LAUNCH_CHECK("k_pcg_zpix");
-    if (gs_sht_map2alm(c->sht, 1, GS_ALM_REAL, c->y, c->r, 3, st)) return -1;
+    if (gs_sht_map2alm_batch(c->sht, c->B, 1, GS_ALM_REAL, c->y, nullptr, c->r, 3, st)) return -1;
     const double resc = (double)c->npix / (4.0 * PI);
     const double kap = c->ninv0[0] * resc;
-    const dim3 g(nblocks(c->nlm, 256)), b(256);
+    const dim3 g(nblocks(c->nlm, 256), c->B), b(256);
     if (noncentered)
         hipLaunchKernelGGL(k_tt_fullsky<1>, g, b, 0, st, c->L, dl, c->bl, c->g2, c->r, resc, kap, zs, slo, shi, ch,
                            iteration, s_out);
@@ -1640,55 +1810,62 @@ int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v,
         return set_error("gs_masked_cr: MALA is defined for the EB model only (CenteredGibbs.py:560-603)");
     const hipStream_t st = S(stream);
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32), ch = (uint32_t)chain;
-    const long long FP = c->F * c->npix, FR = c->F * c->NR;
+    const long long FP = c->FP, FR = c->FR;
+    const int B = c->B;
     double* vv = v ? v : c->vtmp;
     if (kind != GS_MCR_MALA) {
         const double kap[3] = {c->mu[c->rows.r[0]] / c->w, c->F >= 2 ? c->mu[c->rows.r[1]] / c->w : 0.0,
                                c->F == 3 ? c->mu[c->rows.r[2]] / c->w : 0.0};
-        if (mc_params(c, dl, kap, c->params, st)) return -1;
+        if (mc_params(c, B, dl, kap, c->params, st)) return -1;
         if (kind == GS_MCR_OVERRELAX) {
-            // v | s plain, then n_gibbs x (s | v, v | s, s | v) over-relaxed
-            if (mc_v(c, 0, s, vv, zv, slo, shi, ch, SUB_V_INIT, iteration, st)) return -1;
+            // v | s plain, then n_gibbs x (s | v, v | s, s | v) over-relaxed; replay
+            // normals per chain: zv [B][1 + n_gibbs][F][Npix], zs [B][2 n_gibbs][F][NR]
+            const long long zvs = (1LL + c->n_gibbs) * FP, zss = 2LL * c->n_gibbs * FR;
+            if (mc_v(c, 0, s, vv, zv, zvs, slo, shi, ch, SUB_V_INIT, iteration, st)) return -1;
             for (int k = 0; k < c->n_gibbs; ++k) {
                 const double* zs1 = zs ? zs + (2LL * k) * FR : nullptr;
                 const double* zs2 = zs ? zs + (2LL * k + 1) * FR : nullptr;
                 const double* zvk = zv ? zv + (1LL + k) * FP : nullptr;
-                if (mc_s(c, 1, s, zs1, slo, shi, ch, SUB_S + 2 * k, iteration, st)) return -1;
-                if (mc_v(c, 1, s, vv, zvk, slo, shi, ch, k, iteration, st)) return -1;
-                if (mc_s(c, 1, s, zs2, slo, shi, ch, SUB_S + 2 * k + 1, iteration, st)) return -1;
+                if (mc_s(c, 1, s, zs1, zss, slo, shi, ch, SUB_S + 2 * k, iteration, st)) return -1;
+                if (mc_v(c, 1, s, vv, zvk, zvs, slo, shi, ch, k, iteration, st)) return -1;
+                if (mc_s(c, 1, s, zs2, zss, slo, shi, ch, SUB_S + 2 * k + 1, iteration, st)) return -1;
             }
         } else {
+            // replay normals per chain: zv [B][n_gibbs][F][Npix], zs [B][n_gibbs][F][NR]
+            const long long zvs = (long long)c->n_gibbs * FP, zss = (long long)c->n_gibbs * FR;
             for (int k = 0; k < c->n_gibbs; ++k) {
-                if (mc_v(c, 0, s, vv, zv ? zv + k * FP : nullptr, slo, shi, ch, k, iteration, st)) return -1;
-                if (mc_s(c, 0, s, zs ? zs + k * FR : nullptr, slo, shi, ch, SUB_S + 2 * k, iteration, st)) return -1;
+                if (mc_v(c, 0, s, vv, zv ? zv + k * FP : nullptr, zvs, slo, shi, ch, k, iteration, st)) return -1;
+                if (mc_s(c, 0, s, zs ? zs + k * FR : nullptr, zss, slo, shi, ch, SUB_S + 2 * k, iteration, st))
+                    return -1;
             }
         }
         if (kind != GS_MCR_AUX_MALA) {
             // the auxiliary-variable samplers always accept (CenteredGibbs.py:729,825)
             if (accept) {
-                hipLaunchKernelGGL(k_set_one, dim3(1), dim3(1), 0, st, accept);
+                hipLaunchKernelGGL(k_set_one, dim3(1), dim3(64), 0, st, B, accept);
                 GS_LAUNCH_CHECK("k_set_one");
             }
             return 0;
         }
     }
-    // MALA (CenteredGibbs.py:560-603): sigma from the full-sky kappa of noise_pol[0]
+    // MALA (CenteredGibbs.py:560-603): sigma from the full-sky kappa of noise_pol[0];
+    // replay zm [B][F][NR], um [B]
     const double km = (double)c->npix / (4.0 * PI * c->noise_pol0);
     const double kapm[3] = {km, km, km};
-    if (mc_params(c, dl, kapm, c->params_mala, st)) return -1;
+    if (mc_params(c, B, dl, kapm, c->params_mala, st)) return -1;
     if (mc_gradient(c, dl, s, c->grad0, c->pix0, st)) return -1;
     const uint32_t call = 0;
-    hipLaunchKernelGGL(k_mc_propose, dim3(nblocks(c->nlm, 256)), dim3(256), 0, st, c->L, c->F, c->params_mala, s,
+    hipLaunchKernelGGL(k_mc_propose, dim3(nblocks(c->nlm, 256), B), dim3(256), 0, st, c->L, c->F, c->params_mala, s,
                        c->grad0, c->tau, zm, slo, shi, ch, (uint32_t)(SUB_MALA + call), iteration, c->snew);
     GS_LAUNCH_CHECK("k_mc_propose");
     if (mc_gradient(c, dl, c->snew, c->grad1, c->pix1, st)) return -1;
-    hipLaunchKernelGGL(k_mc_sums, dim3(c->nblk), dim3(RED_BLOCK), 0, st, c->L, c->F, c->npix, dl, c->params_mala,
+    hipLaunchKernelGGL(k_mc_sums, dim3(c->nblk, B), dim3(RED_BLOCK), 0, st, c->L, c->F, c->npix, dl, c->params_mala,
                        c->tau, s, c->snew, c->grad0, c->grad1, c->g2, c->ninv, c->pix0, c->pix1, c->partial);
     GS_LAUNCH_CHECK("k_mc_sums");
-    hipLaunchKernelGGL(k_mc_accept, dim3(1), dim3(256), 0, st, c->nblk, c->partial, FR, um, slo, shi, ch, call,
+    hipLaunchKernelGGL(k_mc_accept, dim3(1, B), dim3(256), 0, st, c->nblk, c->partial, FR, um, slo, shi, ch, call,
                        iteration, c->accd, accept, log_ratio ? log_ratio : c->lr);
     GS_LAUNCH_CHECK("k_mc_accept");
-    hipLaunchKernelGGL(k_select_copy, dim3(nblocks(FR, 256)), dim3(256), 0, st, FR, c->accd, c->snew, s);
+    hipLaunchKernelGGL(k_select_copy, dim3(nblocks(FR, 256), B), dim3(256), 0, st, FR, c->accd, c->snew, s);
     GS_LAUNCH_CHECK("k_select_copy");
     return 0;
 }

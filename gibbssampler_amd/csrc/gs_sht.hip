@@ -174,7 +174,7 @@ __device__ __forceinline__ double2 alm_get(const double* __restrict__ a, int lay
     return make_double2(a[r] * IS2, a[r + 1] * IS2);
 }
 
-__device__ __forceinline__ long long alm_comp_stride(int layout, int L) {
+__host__ __device__ __forceinline__ long long alm_comp_stride(int layout, int L) {
     return layout == GS_ALM_COMPLEX ? (long long)(L + 1) * (L + 2) : (long long)(L + 1) * (L + 1);
 }
 
@@ -372,6 +372,9 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
                                                              double2* __restrict__ phi, int paired) {
     const int L = D.L, npair = D.npair, nlm = D.nlm;
     const int q = blockIdx.x, tile = blockIdx.y;
+    // map b of a batch (chains): its a_lm and phase planes
+    ain += (long long)blockIdx.z * NC * nlm;
+    phi += (long long)blockIdx.z * NC * 2 * phi_plane(L, npair);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g0 = tile * (LEG_BLOCK / 64) * SR + wave * SR;   // onset group of slot 0
@@ -541,6 +544,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
     extern __shared__ __attribute__((aligned(16))) double sred[];   // [waves][SEG_SLICE]
     const int L = D.L, npair = D.npair, nlm = D.nlm;
     const int m = blockIdx.x, grp = blockIdx.y;
+    ain += (long long)blockIdx.z * NC * nlm;                       // map b of a batch
+    phi += (long long)blockIdx.z * NC * 2 * phi_plane(L, npair);
     const int lane = threadIdx.x & 63;
     const int sg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lA = m + sg * D.seg;
@@ -1290,7 +1295,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
                                                         const double2* __restrict__ bsk,
                                                         double2* __restrict__ gscratch, double2* __restrict__ phi,
                                                         double2* __restrict__ sscr, int nsplit, int sstride, int twoff,
-                                                        const double* __restrict__ wts) {
+                                                        const double* __restrict__ wts, int wnc) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -1304,7 +1309,8 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
     const double* mc = maps + (long long)comp * npix;
     // wts != nullptr: the transform of the pixel product wts * maps (the masked
     // CR's N^-1 A b s, one rounding as in a separate multiply pass)
-    const double* wc = wts ? wts + (long long)comp * npix : nullptr;
+    // (a batch of maps shares one set of wnc weight maps: comp = b * wnc + c)
+    const double* wc = wts ? wts + (long long)(comp % wnc) * npix : nullptr;
     auto mv = [&](long long i) { return wc ? wc[i] * mc[i] : mc[i]; };
     if (g.split) {
         // X_k = E_k + e^{-2 pi i k / n} O_k, X_(k+h) = E_k - (...) O_k with E / O the
@@ -1405,9 +1411,14 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     __shared__ double red_all[4][2 * 16 * (NV + 2)];   // per wave: two chunk buffers
     const int L = D.L, npair = D.npair;
     const int q = blockIdx.x, tile = blockIdx.y;
+    // grid z = map b of a batch x the l-segments of one map
+    const int nsegz = D.seg > 0 ? (L + D.seg) / D.seg : 1;
+    const int sg = (int)blockIdx.z % nsegz, bmap = (int)blockIdx.z / nsegz;
+    const int ncb = (int)gridDim.z / nsegz * NC;              // comps of the whole batch
     // l-segmented launch: segments starting past L (about half of the grid at
     // small maps) leave before any load
-    if (D.seg > 0 && !paired && q + (int)blockIdx.z * D.seg > D.L) return;
+    if (D.seg > 0 && !paired && q + sg * D.seg > D.L) return;
+    phi += (long long)bmap * NC * 2 * phi_plane(L, npair);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = tile * (LEG_BLOCK / 64) * ASR + wave * ASR;
@@ -1427,7 +1438,6 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         const int m = h == 0 ? q : L - q;
         if (h == 1 && (!paired || m <= q)) break;
         // l-segment of this launch (D.seg > 0, unpaired m): [lA, lend]; else m..L
-        const int sg = blockIdx.z;
         const int lA = D.seg > 0 ? m + sg * D.seg : m;
         if (lA > L) break;
         const int lend = D.seg > 0 ? min(lA + D.seg - 1, L) : L;
@@ -1539,7 +1549,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                 if (l >= lA && l <= lend) {
                     const int comp = oo >> 1;
                     double* dst = reinterpret_cast<double*>(
-                        part + (((long long)tile * 4 + wave) * NC + comp) * D.nlm + obase + l);
+                        part + (((long long)tile * 4 + wave) * ncb + bmap * NC + comp) * D.nlm + obase + l);
                     dst[oo & 1] = sum;
                 }
             }
@@ -1652,7 +1662,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         // l below the wave's first chunk: exact zeros
         for (int l = lA + lane; l < min(lstart0, lend + 1); l += 64)
             for (int c = 0; c < NC; ++c)
-                part[(((long long)tile * 4 + wave) * NC + c) * D.nlm + obase + l] = make_double2(0.0, 0.0);
+                part[(((long long)tile * 4 + wave) * ncb + bmap * NC + c) * D.nlm + obase + l] = make_double2(0.0, 0.0);
     }
 }
 
@@ -1660,17 +1670,18 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
 // into it when acc != 0: the Jacobi steps of map2alm(iter > 0))
 template <int NC>
 __global__ void k_sht_anal_finish(int L, int nlm, int ntile, const double2* __restrict__ part, double w, int layout,
-                                  int acc, double* __restrict__ alm) {
+                                  int acc, double* __restrict__ alm, int nmap) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g >= (long long)NC * nlm) return;
+    const int ncb = NC * nmap;                     // comps of the batch: comp = b * NC + c
+    if (g >= (long long)ncb * nlm) return;
     const int comp = (int)(g / nlm);
     const long long i = g % nlm;
     double2 s = make_double2(0.0, 0.0);
     for (int t = 0; t < ntile; ++t) {
-        const double2 v = part[((long long)t * NC + comp) * nlm + i];
+        const double2 v = part[((long long)t * ncb + comp) * nlm + i];
         s.x += v.x; s.y += v.y;
     }
-    const bool spin0 = NC == 1 || (NC == 3 && comp == 0);
+    const bool spin0 = NC == 1 || (NC == 3 && comp % NC == 0);
     const double f = spin0 ? w : -w;
     s.x *= f; s.y *= f;
     // (l, m) of complex index i
@@ -1736,8 +1747,9 @@ struct gs_sht {
     double2* sscr = nullptr;     // split rings: [comp][slot][split_n] half-transform scratch
     int nsplit = 0, split_n = 0;
     int lds_fft_max = LDS_FFT_MAX;   // FFT lengths held in LDS (GS_SHT_LDS_FFT_MAX lowers it: tests)
-    double* mapw = nullptr;      // [3][npix] Jacobi residual maps
-    double2* ain = nullptr;      // [3][nlm] a_lm in healpy complex order
+    double* mapw = nullptr;      // [cap][3][npix] Jacobi residual maps
+    double2* ain = nullptr;      // [cap][3][nlm] a_lm in healpy complex order
+    int cap = 1;                 // maps of a batch the per-map workspace (phi, part, ain, mapw) holds
     // ring classes by FFT length
     std::vector<int> cls_M;      // M of each class
     std::vector<int> cls_n;      // pairs in the class
@@ -2105,7 +2117,7 @@ static void ring_lds(int M, int bd, bool glob, bool short_red, size_t& lds, int&
 
 static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const double* maps_in, double* maps_out,
                           hipStream_t st, const double2* phi = nullptr, const int* comp_lmax = nullptr,
-                          int comp_div = 1, const double* wts = nullptr) {
+                          int comp_div = 1, const double* wts = nullptr, int wnc = 3) {
     if (!phi) phi = p->phi;
     const int M = p->cls_M[c];
     const bool glob = M > p->lds_fft_max;
@@ -2128,10 +2140,10 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
     } else {
         if (nb8)
             hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts, wnc);
         else
             hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts, wnc);
     }
     GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
     return 0;
@@ -2142,8 +2154,11 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
 // global-scratch class stays on the caller's stream), so the short-ring
 // classes -- a dozen small, latency-bound launches -- run on the plan's side
 // stream while the largest class runs on the caller's.
+// ncomp = every comp of the batch (maps b * wnc + c, contiguous); wts: wnc weight
+// maps shared by the batch's maps
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
-                     const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1, const double* wts = nullptr) {
+                     const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1, const double* wts = nullptr,
+                     int wnc = 3) {
     if (p->merged_n > 0) {
         // all ring pairs in one launch: the block size and LDS of the longest FFT
         // (shorter rings leave threads idle; their fold reduction uses the
@@ -2168,11 +2183,11 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             if (nb8)
                 hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n, twoff, wts);
+                                   p->nsplit, p->split_n, twoff, wts, wnc);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n, twoff, wts);
+                                   p->nsplit, p->split_n, twoff, wts, wnc);
         }
         GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring (merged)" : "k_sht_anal_ring (merged)");
         return 0;
@@ -2189,7 +2204,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
     for (size_t c = 0; c < ncls; ++c) {
         const bool on_side = fork && c != big && p->cls_M[c] <= p->lds_fft_max;
         if (sht_ring_class(p, c, synth, ncomp, maps_in, maps_out, on_side ? p->side : S(stream), phi, comp_lmax,
-                           comp_div, wts))
+                           comp_div, wts, wnc))
             return -1;
     }
     if (fork) {
@@ -2199,38 +2214,82 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
     return 0;
 }
 
-static int sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, const double* bl, double* maps,
-                       void* stream);
+// ---- batches of maps (chains) ------------------------------------------------
+// A batch of B maps shares the plan's tables; every Legendre / ring / finish
+// launch carries the batch in its grid (Legendre: blockIdx.z; ring and finish:
+// the comp index b * ncomp + c), so one launch serves all B maps and a small map
+// (N_side <= 256: a fraction of the GPU per map) fills the chip.  A map's
+// arithmetic does not depend on B: map b of a batch is bit-identical to the same
+// map transformed alone.  Plans whose ring stage needs the global FFT scratch or
+// split rings (large maps: N_side >= 1024) run a batch as B single-map passes --
+// one map already fills the GPU there.
+static bool sht_batch_native(const gs_sht* p) { return p->gscr == nullptr && p->nsplit == 0; }
 
-int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* maps, void* stream) {
-    return sht_alm2map(p, ncomp, layout, alm, nullptr, maps, stream);
+// per-map workspace for B maps (grown outside a capture only)
+static int sht_reserve(gs_sht* p, int nmap, hipStream_t st) {
+    if (nmap <= p->cap) return 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return set_error("gs_sht: a batch larger than the plan's reserved maps inside a graph capture "
+                         "(call gs_sht_reserve first)");
+    GS_CHECK(hipDeviceSynchronize());
+    double2 *phi = nullptr, *part = nullptr, *ain = nullptr;
+    double* mapw = nullptr;
+    const size_t n = (size_t)nmap;
+    if (hipMalloc((void**)&phi, n * 3 * 2 * phi_plane(p->L, p->npair) * sizeof(double2)) != hipSuccess ||
+        hipMalloc((void**)&part, n * p->ntile * 4 * 3 * p->nlm * sizeof(double2)) != hipSuccess ||
+        hipMalloc((void**)&ain, n * 3 * p->nlm * sizeof(double2)) != hipSuccess ||
+        hipMalloc((void**)&mapw, n * 3 * p->npix * sizeof(double)) != hipSuccess) {
+        for (void* q : {(void*)phi, (void*)part, (void*)ain, (void*)mapw})
+            if (q) (void)hipFree(q);
+        return set_error("gs_sht_reserve: out of device memory");
+    }
+    (void)hipFree(p->phi); (void)hipFree(p->part); (void)hipFree(p->ain); (void)hipFree(p->mapw);
+    const long long old = (long long)p->cap;
+    p->bytes += (long long)(n - old) * (long long)(3 * 2 * phi_plane(p->L, p->npair) * 16 +
+                                                    (long long)p->ntile * 4 * 3 * p->nlm * 16 + 3LL * p->nlm * 16 +
+                                                    3LL * p->npix * 8);
+    p->phi = phi; p->part = part; p->ain = ain; p->mapw = mapw;
+    p->cap = nmap;
+    return 0;
 }
 
-static int sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, const double* bl, double* maps,
+// synthesis of B maps (alm [B][ncomp][n], maps [B][ncomp][Npix]); bl (real layout
+// only): the per-l beam applied on the input load
+static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double* alm, const double* bl, double* maps,
                        void* stream) {
     if (check_sht(p)) return -1;
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_alm2map: ncomp must be 1 (T), 2 (E,B) or 3 (T,E,B)");
     if (layout != GS_ALM_REAL && layout != GS_ALM_COMPLEX) return set_error("gs_sht_alm2map: bad layout");
     if (bl && layout != GS_ALM_REAL) return set_error("gs_sht_alm2map: the beamed input needs the real layout");
     if (!alm || !maps) return set_error("gs_sht_alm2map: null argument");
-    const long long nin = (long long)ncomp * p->nlm;
-    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, ncomp, alm, layout,
-                       p->ain, bl);
+    if (nmap < 1) return set_error("gs_sht_alm2map: nmap < 1");
+    if (nmap > 1 && !sht_batch_native(p)) {
+        const long long as = ncomp * alm_comp_stride(layout, p->L), ms = (long long)ncomp * p->npix;
+        for (int b = 0; b < nmap; ++b)
+            if (sht_alm2map(p, 1, ncomp, layout, alm + b * as, bl, maps + b * ms, stream)) return -1;
+        return 0;
+    }
+    if (sht_reserve(p, nmap, S(stream))) return -1;
+    const long long nin = (long long)nmap * ncomp * p->nlm;
+    // the batch's comps are contiguous: the input pass sees B * ncomp comps
+    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * ncomp, alm,
+                       layout, p->ain, bl);
     GS_LAUNCH_CHECK("k_sht_alm_in");
     const int syn_nseg = p->syn_seg ? (p->L + p->syn_seg) / p->syn_seg : 1;
     if (p->syn_seg > 0 && p->syn_seg <= 64 && p->syn_sr == 1 && !p->syn_paired && syn_nseg <= 16) {
         // small maps: l-segmented synthesis, one wave per segment (<= 64 l: the
         // wave's LDS slice stages 64 l of coefficients and a_lm)
-        const dim3 g2(p->L + 1, p->ngroup), b2(64 * syn_nseg);
+        const dim3 g2(p->L + 1, p->ngroup, nmap), b2(64 * syn_nseg);
         const size_t lds = (size_t)syn_nseg * (66 * 8 + 3 * 64 * 2) * sizeof(double);
 #define GS_SS(NC) hipLaunchKernelGGL((k_sht_synth_leg_seg<NC>), g2, b2, lds, S(stream), p->devseg(p->syn_seg), p->coef, \
                                      p->ain, p->phi)
         if (ncomp == 1) GS_SS(1); else if (ncomp == 2) GS_SS(2); else GS_SS(3);
 #undef GS_SS
         GS_LAUNCH_CHECK("k_sht_synth_leg_seg");
-        return sht_rings(p, true, ncomp, nullptr, maps, stream);
+        return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp);
     }
-    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr));
+    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr), nmap);
 #define GS_SL(NC, SR) hipLaunchKernelGGL((k_sht_synth_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
                                          p->coef, p->ain, p->phi, p->syn_paired)
 #define GS_SL2(NC) do { if (p->syn_sr == 2) GS_SL(NC, 2); else GS_SL(NC, 1); } while (0)
@@ -2238,15 +2297,29 @@ static int sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, cons
 #undef GS_SL2
 #undef GS_SL
     GS_LAUNCH_CHECK("k_sht_synth_leg");
-    return sht_rings(p, true, ncomp, nullptr, maps, stream);
+    return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp);
 }
 
-static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int acc, void* stream,
-                        const double* wts = nullptr) {
-    if (sht_rings(p, false, ncomp, maps, nullptr, stream, nullptr, nullptr, 1, wts)) return -1;
+int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* maps, void* stream) {
+    return sht_alm2map(p, 1, ncomp, layout, alm, nullptr, maps, stream);
+}
+
+// analysis of B maps (maps [B][ncomp][Npix] -> alm [B][ncomp][n]); wts: ncomp
+// weight maps shared by the batch (the product wts * maps is transformed)
+static int sht_analysis(gs_sht* p, int nmap, int ncomp, int layout, const double* maps, double* alm, int acc,
+                        void* stream, const double* wts = nullptr) {
+    if (nmap > 1 && !sht_batch_native(p)) {
+        const long long as = ncomp * alm_comp_stride(layout, p->L), ms = (long long)ncomp * p->npix;
+        for (int b = 0; b < nmap; ++b)
+            if (sht_analysis(p, 1, ncomp, layout, maps + b * ms, alm + b * as, acc, stream, wts)) return -1;
+        return 0;
+    }
+    if (sht_reserve(p, nmap, S(stream))) return -1;
+    if (sht_rings(p, false, nmap * ncomp, maps, nullptr, stream, nullptr, nullptr, 1, wts, ncomp)) return -1;
     const int sr = p->ana_sr_nc[ncomp], sl = p->ana_seg_nc[ncomp];
     const int ntile = (p->ngroup + 4 * sr - 1) / (4 * sr);
-    const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, ntile, sl ? (p->L + sl) / sl : 1);
+    const int nsegz = sl ? (p->L + sl) / sl : 1;
+    const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, ntile, nsegz * nmap);
     const ShtDev D = p->devseg(sl);
 #define GS_AL(NC, SR) do { if (sl > 0 && sl <= 64) \
         hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, true>), grid, dim3(LEG_BLOCK), 0, S(stream), D, p->coef, \
@@ -2260,9 +2333,9 @@ static int sht_analysis(gs_sht* p, int ncomp, int layout, const double* maps, do
 #undef GS_AL
     GS_LAUNCH_CHECK("k_sht_anal_leg");
     const double w = 4.0 * PI / (double)p->npix;
-    const long long n = (long long)ncomp * p->nlm;
+    const long long n = (long long)nmap * ncomp * p->nlm;
 #define GS_AF(NC) hipLaunchKernelGGL((k_sht_anal_finish<NC>), dim3(nblocks(n, 256)), dim3(256), 0, S(stream), p->L, p->nlm, \
-                                     ntile * 4, p->part, w, layout, acc, alm)
+                                     ntile * 4, p->part, w, layout, acc, alm, nmap)
     if (ncomp == 1) GS_AF(1); else if (ncomp == 2) GS_AF(2); else GS_AF(3);
 #undef GS_AF
     GS_LAUNCH_CHECK("k_sht_anal_finish");
@@ -2312,27 +2385,39 @@ int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int
     return 0;
 }
 
-int gs_sht_map2alm(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int niter, void* stream) {
+static int sht_map2alm(gs_sht* p, int nmap, int ncomp, int layout, const double* maps, double* alm, int niter,
+                       void* stream) {
     if (check_sht(p)) return -1;
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_map2alm: ncomp must be 1 (T), 2 (Q,U) or 3 (T,Q,U)");
     if (layout != GS_ALM_REAL && layout != GS_ALM_COMPLEX) return set_error("gs_sht_map2alm: bad layout");
     if (!alm || !maps) return set_error("gs_sht_map2alm: null argument");
     if (niter < 0) return set_error("gs_sht_map2alm: niter < 0");
-    if (sht_analysis(p, ncomp, layout, maps, alm, 0, stream)) return -1;
+    if (nmap < 1) return set_error("gs_sht_map2alm: nmap < 1");
+    if (nmap > 1 && !sht_batch_native(p)) {
+        const long long as = ncomp * alm_comp_stride(layout, p->L), ms = (long long)ncomp * p->npix;
+        for (int b = 0; b < nmap; ++b)
+            if (sht_map2alm(p, 1, ncomp, layout, maps + b * ms, alm + b * as, niter, stream)) return -1;
+        return 0;
+    }
+    if (sht_analysis(p, nmap, ncomp, layout, maps, alm, 0, stream)) return -1;
     for (int it = 0; it < niter; ++it) {
         // a += map2alm(m - alm2map(a))   (healpy iter = niter)
-        if (gs_sht_alm2map(p, ncomp, layout, alm, p->mapw, stream)) return -1;
-        const long long n = (long long)ncomp * p->npix;
+        if (sht_alm2map(p, nmap, ncomp, layout, alm, nullptr, p->mapw, stream)) return -1;
+        const long long n = (long long)nmap * ncomp * p->npix;
         hipLaunchKernelGGL(k_sub_maps, dim3(nblocks(n, 256)), dim3(256), 0, S(stream), n, maps, p->mapw);
         GS_LAUNCH_CHECK("k_sub_maps");
-        if (sht_analysis(p, ncomp, layout, p->mapw, alm, 1, stream)) return -1;
+        if (sht_analysis(p, nmap, ncomp, layout, p->mapw, alm, 1, stream)) return -1;
     }
     return 0;
 }
 
+int gs_sht_map2alm(gs_sht* p, int ncomp, int layout, const double* maps, double* alm, int niter, void* stream) {
+    return sht_map2alm(p, 1, ncomp, layout, maps, alm, niter, stream);
+}
+
 int gs_sht_alm2map_beamed(gs_sht* p, int ncomp, const double* alm_real, const double* bl, double* maps, void* stream) {
     if (!bl) return set_error("gs_sht_alm2map_beamed: null beam");
-    return sht_alm2map(p, ncomp, GS_ALM_REAL, alm_real, bl, maps, stream);
+    return sht_alm2map(p, 1, ncomp, GS_ALM_REAL, alm_real, bl, maps, stream);
 }
 
 int gs_sht_map2alm_weighted(gs_sht* p, int ncomp, const double* maps, const double* weights, double* alm_real,
@@ -2340,7 +2425,36 @@ int gs_sht_map2alm_weighted(gs_sht* p, int ncomp, const double* maps, const doub
     if (check_sht(p)) return -1;
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_map2alm_weighted: ncomp must be 1 (T), 2 (Q,U) or 3 (T,Q,U)");
     if (!alm_real || !maps || !weights) return set_error("gs_sht_map2alm_weighted: null argument");
-    return sht_analysis(p, ncomp, GS_ALM_REAL, maps, alm_real, 0, stream, weights);
+    return sht_analysis(p, 1, ncomp, GS_ALM_REAL, maps, alm_real, 0, stream, weights);
+}
+
+int gs_sht_reserve(gs_sht* p, int nmap, void* stream) {
+    if (check_sht(p)) return -1;
+    if (nmap < 1) return set_error("gs_sht_reserve: nmap < 1");
+    return sht_batch_native(p) ? sht_reserve(p, nmap, S(stream)) : 0;
+}
+
+int gs_sht_alm2map_batch(gs_sht* p, int nmap, int ncomp, int layout, const double* alm, const double* bl,
+                         double* maps, void* stream) {
+    return sht_alm2map(p, nmap, ncomp, layout, alm, bl, maps, stream);
+}
+
+int gs_sht_map2alm_batch(gs_sht* p, int nmap, int ncomp, int layout, const double* maps, const double* weights,
+                         double* alm, int niter, void* stream) {
+    if (weights) {
+        if (layout != GS_ALM_REAL) return set_error("gs_sht_map2alm_batch: weights need the real layout");
+        if (niter != 0) return set_error("gs_sht_map2alm_batch: weights need niter 0");
+        if (check_sht(p)) return -1;
+        if (ncomp < 1 || ncomp > 3 || nmap < 1 || !maps || !alm) return set_error("gs_sht_map2alm_batch: bad argument");
+        if (nmap > 1 && !sht_batch_native(p)) {
+            const long long as = ncomp * alm_comp_stride(layout, p->L), ms = (long long)ncomp * p->npix;
+            for (int b = 0; b < nmap; ++b)
+                if (sht_analysis(p, 1, ncomp, layout, maps + b * ms, alm + b * as, 0, stream, weights)) return -1;
+            return 0;
+        }
+        return sht_analysis(p, nmap, ncomp, layout, maps, alm, 0, stream, weights);
+    }
+    return sht_map2alm(p, nmap, ncomp, layout, maps, alm, niter, stream);
 }
 
 }  // extern "C"

@@ -284,12 +284,12 @@ class GibbsSampler:
         if not self.polarization:
             raise NotImplementedError("masked temperature-only runs: the reference's TT masked path is broken "
                                       "at HEAD (SURVEY.md Appendix B.7); use fields='TEB'")
-        if self.nchains != 1:
-            raise NotImplementedError("masked runs batch one chain per process (shard chains over GPUs)")
+        # nchains > 1: the chains run as one batch (batched SHTs, per-chain streams
+        # keyed by the global chain id chain0 + b); histories gain a chain axis
         return MaskedCR(self.pix_map, noise_temp, noise_pol, self.bl_gauss, self.lmax, self.nside, mask=self.mask,
                         nfields=self.nfields, gibbs_cr=gibbs_cr, n_gibbs=n_gibbs, alpha=alpha,
                         overrelaxation=overrelaxation, ula=ula, tau=tau, rng=self.rng, seed=self.seed,
-                        chain=self.chain0, rj=rj)
+                        chain=self.chain0, rj=rj, nchains=self.nchains)
 
     def _masked_mh_runner(self, kind, cr, cr_kind_):
         from .masked import MaskedMHRunner

@@ -16,6 +16,15 @@ All arithmetic runs in libgibbs_hip.so (gs_masked_cr + gs_sht); this module
 only moves arrays and, in replay mode, draws numpy's legacy global stream in
 the reference's order (A.5 of SURVEY.md) so results match the reference for
 the same ``np.random.seed``.  There is no CPU fallback.
+
+Chains: ``nchains`` = B > 1 runs B independent chains of the same data set in
+one context (global ids chain .. chain + B - 1) -- the reference's SLURM array
+of chains (job-script.sh:6-8) as one batch whose transforms are batched SHTs
+(one launch per stage for all B maps).  Device arrays then carry a leading
+chain axis ([B, F, NR], [B, nspec, L+1], ...); with B = 1 the shapes are the
+one-chain ones.  Chain b of a batch is bit-identical to a one-chain context of
+chain id chain + b.  Replay draws for B > 1 are chain-major: each chain's
+reference-order draws in turn.
 """
 import ctypes
 import time
@@ -40,7 +49,7 @@ class MaskedCR:
 
     def __init__(self, pix_map, noise_temp, noise_pol, bl, lmax, nside, mask=None, nfields=2, gibbs_cr=True,
                  n_gibbs=1, alpha=-0.995, overrelaxation=False, ula=False, tau=0.02, rng="replay", seed=0, chain=0,
-                 device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000, rj=False):
+                 device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000, rj=False, nchains=1):
         if nfields not in (1, 2, 3):
             raise ValueError("nfields must be 1 (T), 2 (EB, the reference) or 3 (TEB)")
         self.lib = _capi.load()
@@ -53,7 +62,12 @@ class MaskedCR:
         self.rj = bool(rj)
         self.n_gibbs, self.alpha, self.tau = int(n_gibbs), float(alpha), float(tau)
         self.pcg_accuracy, self.pcg_maxiter = float(pcg_accuracy), int(pcg_maxiter)   # CenteredGibbs.py:279-283
-        self.pcg_iterations = []
+        self.B = int(nchains)
+        if self.B < 1:
+            raise ValueError("nchains >= 1")
+        self.pcg_iterations = []          # per solve: the CG iterations (mean over the batch's chains)
+        self.pcg_iterations_chains = []   # per solve: every chain's count
+        self.pcg_launched = []            # per solve: CG iterations launched (the slowest chain's)
         self.pcg_syncs = []
         if rng not in ("replay", "native"):
             raise ValueError(rng)
@@ -80,6 +94,7 @@ class MaskedCR:
         desc.n_gibbs, desc.alpha, desc.tau, desc.noise_pol0 = self.n_gibbs, self.alpha, self.tau, float(npol[0])
         desc.mu_eps = 1e-7 if self.F == 1 else 1e-14
         desc.adj_iter = 3 if self.F == 1 else 0
+        desc.nchains = self.B
         h = ctypes.c_void_p()
         _capi.check(self.lib.gs_masked_create(ctypes.byref(desc), _capi.ptr(self._maps), _capi.ptr(self._inv),
                                               ctypes.byref(h)), "gs_masked_create")
@@ -87,9 +102,9 @@ class MaskedCR:
         mu = (ctypes.c_double * 3)()
         _capi.check(self.lib.gs_masked_info(h, mu, None), "gs_masked_info")
         self.mu = np.array(mu[:])
-        self.v = torch.zeros((self.F, self.Npix), dtype=torch.float64, device=device)
-        self._acc = torch.zeros(1, dtype=torch.int32, device=device)
-        self._lr = torch.zeros(1, dtype=torch.float64, device=device)
+        self.v = torch.zeros(self._shape(self.F, self.Npix), dtype=torch.float64, device=device)
+        self._acc = torch.zeros(self.B, dtype=torch.int32, device=device)
+        self._lr = torch.zeros(self.B, dtype=torch.float64, device=device)
 
     def __del__(self):
         _capi.park(dict(self.__dict__))       # inside a capture: tensors freed after it
@@ -99,36 +114,54 @@ class MaskedCR:
             self.handle = None
 
     # -- conversions -------------------------------------------------------------------
+    def _shape(self, *tail):
+        """a per-chain array's shape: the one-chain shape, or [B, ...] for a batch"""
+        return tail if self.B == 1 else (self.B,) + tail
+
     def _dl(self, all_dls):
+        """D_l dict (every chain) or list of B dicts -> device [B?, nspec, L+1]."""
         specs = SPECS[self.F]
-        arr = np.stack([np.asarray(all_dls[s], dtype=np.float64)[: self.L + 1] for s in specs])
-        return torch.from_numpy(np.ascontiguousarray(arr)).to(self.device)
+        one = lambda d: np.stack([np.asarray(d[s], dtype=np.float64)[: self.L + 1] for s in specs])
+        if isinstance(all_dls, (list, tuple)):
+            arr = np.stack([one(d) for d in all_dls])
+        else:
+            arr = one(all_dls)
+            if self.B > 1:
+                arr = np.broadcast_to(arr, (self.B,) + arr.shape)
+        return torch.from_numpy(np.ascontiguousarray(arr)).to(self.device).reshape(self._shape(len(specs), self.L + 1))
 
     def _s(self, s):
         if isinstance(s, torch.Tensor):
-            return s.to(self.device, torch.float64).contiguous().clone()
+            return s.to(self.device, torch.float64).contiguous().clone().reshape(self._shape(self.F, self.NR))
         if isinstance(s, np.ndarray):
-            return torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64).reshape(self.F, self.NR)).to(self.device)
-        return torch.from_numpy(np.ascontiguousarray(np.stack([np.asarray(s[k], dtype=np.float64)
-                                                              for k in FIELDS[self.F]]))).to(self.device)
+            return torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64).reshape(
+                self._shape(self.F, self.NR))).to(self.device)
+        one = lambda d: np.stack([np.asarray(d[k], dtype=np.float64) for k in FIELDS[self.F]])
+        arr = np.stack([one(d) for d in s]) if isinstance(s, (list, tuple)) else one(s)
+        return torch.from_numpy(np.ascontiguousarray(arr).reshape(self._shape(self.F, self.NR))).to(self.device)
 
     def _out(self, s):
-        a = s.cpu().numpy()
-        return {k: a[i].copy() for i, k in enumerate(FIELDS[self.F])}
+        a = s.cpu().numpy().reshape(self.B, self.F, self.NR)
+        out = [{k: a[b, i].copy() for i, k in enumerate(FIELDS[self.F])} for b in range(self.B)]
+        return out[0] if self.B == 1 else out
+
+    def _flags(self, t):
+        a = t.cpu().numpy()
+        return int(a[0]) if self.B == 1 else a.astype(np.int64)
 
     def second_part_grad(self):
         out = torch.empty((self.F, self.NR), dtype=torch.float64, device=self.device)
         _capi.check(self.lib.gs_masked_info(self.handle, None, _capi.ptr(out)), "gs_masked_info")
         return out
 
-    # -- replay draws (reference order) -----------------------------------
+    # -- replay draws (reference order, SURVEY.md A.5; chain-major for a batch) --------
     def _pix(self, n):
         return np.stack([np.stack([np.random.normal(size=self.Npix) for _ in range(self.F)]) for _ in range(n)])
 
     def _slots(self):
         return np.stack([np.random.normal(size=self.NR) for _ in range(self.F)])
 
-    def _replay(self, kind):
+    def _replay_one(self, kind):
         zv = zs = zm = um = None
         if kind == _capi.GS_MCR_AUX or kind == _capi.GS_MCR_AUX_MALA:
             v, s = [], []
@@ -146,8 +179,14 @@ class MaskedCR:
         if kind in (_capi.GS_MCR_MALA, _capi.GS_MCR_AUX_MALA):
             zm = self._slots()
             um = np.array([np.random.uniform()])
-        dev = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
-        return dev(zv), dev(zs), dev(zm), dev(um)
+        return zv, zs, zm, um
+
+    def _dev(self, a):
+        return None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+
+    def _replay(self, kind):
+        per = [self._replay_one(kind) for _ in range(self.B)]
+        return tuple(self._dev(None if per[0][k] is None else np.stack([p[k] for p in per])) for k in range(4))
 
     # -- the device step -------------------------------------------------------------------
     def step(self, kind, dl, s, iteration=None):
@@ -165,7 +204,7 @@ class MaskedCR:
     def _run(self, kind, all_dls, s_old):
         s = self._s(s_old)
         self.step(kind, self._dl(all_dls), s)
-        return self._out(s), int(self._acc.item())
+        return self._out(s), self._flags(self._acc)
 
     # -- reference surface ----------------------------------------------------------------
     def sample_gibbs_change_variable(self, all_dls, old_s):
@@ -178,6 +217,8 @@ class MaskedCR:
         return self._run(_capi.GS_MCR_MALA, all_dls, s_old)
 
     def compute_gradient_mala(self, all_dls, s_old):
+        if self.B != 1:
+            raise NotImplementedError("compute_gradient_mala: the reference surface's one-chain form")
         s = self._s(s_old)
         grad = torch.empty_like(s)
         pix = torch.empty((self.F, self.Npix), dtype=torch.float64, device=self.device)
@@ -194,13 +235,16 @@ class MaskedCR:
         it = self.iteration if iteration is None else int(iteration)
         zv = zs = None
         if self.rng == "replay":
-            if self.F == 1:           # TT (CenteredGibbs.py:153-155): z_alm, then z_pix
-                zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
-                zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
-            else:                     # CenteredGibbs.py:467-478: z_Q, z_U, then z_E, z_B
-                zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
-                zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
-        rhs = torch.empty((self.F, self.NR), dtype=torch.float64, device=self.device)
+            zvl, zsl = [], []
+            for _ in range(self.B):
+                if self.F == 1:           # TT (CenteredGibbs.py:153-155): z_alm, then z_pix
+                    zsl.append(self._slots())
+                    zvl.append(self._pix(1)[0])
+                else:                     # CenteredGibbs.py:467-478: z_Q, z_U, then z_E, z_B
+                    zvl.append(self._pix(1)[0])
+                    zsl.append(self._slots())
+            zv, zs = self._dev(np.stack(zvl)), self._dev(np.stack(zsl))
+        rhs = torch.empty(self._shape(self.F, self.NR), dtype=torch.float64, device=self.device)
         _capi.check(self.lib.gs_masked_pcg_rhs(self.handle, _capi.ptr(dl), _capi.ptr(zv), _capi.ptr(zs), self.seed,
                                                it, self.chain, _capi.ptr(rhs), _capi.stream_ptr()),
                     "gs_masked_pcg_rhs")
@@ -209,18 +253,22 @@ class MaskedCR:
     def pcg_solve(self, dl, rhs, x=None, tol=None, maxiter=None):
         guess = x is not None
         x = torch.empty_like(rhs) if x is None else x
-        iters = ctypes.c_int()
-        res = ctypes.c_double()
+        iters = (ctypes.c_int * self.B)()
+        res = (ctypes.c_double * self.B)()
         _capi.check(self.lib.gs_masked_pcg_solve(self.handle, _capi.ptr(dl), _capi.ptr(rhs), _capi.ptr(x),
                                                  int(guess), self.pcg_accuracy if tol is None else float(tol),
                                                  self.pcg_maxiter if maxiter is None else int(maxiter),
-                                                 ctypes.byref(iters), ctypes.byref(res), _capi.stream_ptr()),
+                                                 iters, res, _capi.stream_ptr()),
                     "gs_masked_pcg_solve")
-        self.pcg_iterations.append(iters.value)
-        self.pcg_residual = res.value
-        syncs = ctypes.c_int()
-        _capi.check(self.lib.gs_masked_pcg_info(self.handle, ctypes.byref(syncs)), "gs_masked_pcg_info")
+        its = [int(v) for v in iters]
+        self.pcg_iterations.append(its[0] if self.B == 1 else float(np.mean(its)))
+        self.pcg_iterations_chains.append(its)
+        self.pcg_residual = res[0] if self.B == 1 else [float(v) for v in res]
+        syncs, launched = ctypes.c_int(), ctypes.c_int()
+        _capi.check(self.lib.gs_masked_pcg_info2(self.handle, ctypes.byref(syncs), ctypes.byref(launched)),
+                    "gs_masked_pcg_info2")
         self.pcg_syncs.append(syncs.value)          # host synchronisations of this solve (one per batch)
+        self.pcg_launched.append(launched.value)    # iterations launched (the batch's slowest chain)
         return x
 
     def pcg_apply(self, dl, x, out=None):
@@ -241,7 +289,10 @@ class MaskedCR:
         rhs = self.pcg_rhs(dl, iteration=it)
         um = None
         if self.rng == "replay":
-            um = torch.tensor([np.random.uniform()], dtype=torch.float64, device=self.device)
+            # one uniform per chain after its normals: a batch's chain-major replay
+            # draws chain b's normals and uniform in turn only for B = 1 (the
+            # reference's order); B > 1 draws the B uniforms after all normals
+            um = torch.tensor([np.random.uniform() for _ in range(self.B)], dtype=torch.float64, device=self.device)
         x = self.pcg_solve(dl, rhs, x=-s)
         _capi.check(self.lib.gs_masked_rj_accept(self.handle, _capi.ptr(dl), _capi.ptr(rhs), _capi.ptr(x),
                                                  _capi.ptr(s), _capi.ptr(um), self.seed, it, self.chain,
@@ -254,7 +305,7 @@ class MaskedCR:
         (s_old, 0) otherwise."""
         s = self._s(s_old)
         self.rj_step(self._dl(all_dls), s)
-        return self._out(s), int(self._acc.item())
+        return self._out(s), self._flags(self._acc)
 
     def tt_fullsky(self, dl, noncentered=False, iteration=None, out=None):
         """temperature full-sky CR from the pixel map (gs_masked_tt_fullsky):
@@ -263,9 +314,12 @@ class MaskedCR:
         it = self.iteration if iteration is None else int(iteration)
         zv = zs = None
         if self.rng == "replay":
-            zs = torch.from_numpy(np.ascontiguousarray(self._slots())).to(self.device)
-            zv = torch.from_numpy(np.ascontiguousarray(self._pix(1)[0])).to(self.device)
-        out = torch.empty((1, self.NR), dtype=torch.float64, device=self.device) if out is None else out
+            zsl, zvl = [], []
+            for _ in range(self.B):
+                zsl.append(self._slots())
+                zvl.append(self._pix(1)[0])
+            zs, zv = self._dev(np.stack(zsl)), self._dev(np.stack(zvl))
+        out = torch.empty(self._shape(1, self.NR), dtype=torch.float64, device=self.device) if out is None else out
         _capi.check(self.lib.gs_masked_tt_fullsky(self.handle, int(bool(noncentered)), _capi.ptr(dl), _capi.ptr(zv),
                                                   _capi.ptr(zs), self.seed, it, self.chain, _capi.ptr(out),
                                                   _capi.stream_ptr()), "gs_masked_tt_fullsky")
@@ -278,7 +332,8 @@ class MaskedCR:
         return self._out(x), 1
 
     def last_log_ratio(self):
-        return float(self._lr.item())
+        a = self._lr.cpu().numpy()
+        return float(a[0]) if self.B == 1 else a
 
     def sample(self, all_dls, s_old=None):
         """CenteredGibbs.py:828-850 (masked): the flag ladder."""
@@ -317,12 +372,31 @@ def cr_kind(gibbs_cr, overrelaxation, ula, rj=False):
     return KIND_PCG
 
 
+def _unfold_index(spectra, bins, L, device):
+    """the (index, valid) pair of utils.unfold_bins on the device: row k, l -> bin"""
+    idx = np.full((len(spectra), L + 1), -1, dtype=np.int64)
+    for k, sp in enumerate(spectra):
+        b = bins[sp]
+        for i in range(len(b) - 1):
+            idx[k, b[i]:min(b[i + 1], L + 1)] = i
+    return torch.from_numpy(np.maximum(idx, 0)).to(device), torch.from_numpy(idx >= 0).to(device)
+
+
+def _unfold_batch(binned_t, idx, valid):
+    """utils.unfold_bins on the device: binned [B, nspec, maxbins] -> [B, nspec, L+1]."""
+    B = binned_t.shape[0]
+    g = torch.gather(binned_t, 2, idx.unsqueeze(0).expand(B, -1, -1))
+    return torch.where(valid.unsqueeze(0), g, 0.0).contiguous()
+
+
 class MaskedRunner:
-    """GibbsSampler.run_polarization (GibbsSampler.py:118-180) for a masked run on
-    one chain: per iteration the masked CR (MaskedCR, the a12 ladder) and the
-    centered C_l draw (gs_sweep_stats + gs_cls_draw), everything resident on
-    the device.  The reference's first CR (GibbsSampler.py:136-138) is the
-    qcinv PCG (row f1); the start map is given instead (``s_init``)."""
+    """GibbsSampler.run_polarization (GibbsSampler.py:118-180) for a masked run:
+    per iteration the masked CR (MaskedCR, the a12 ladder) and the centered C_l
+    draw (gs_sweep_stats + gs_cls_draw), everything resident on the device, for
+    the context's B chains at once.  The reference's first CR
+    (GibbsSampler.py:136-138) is the qcinv PCG (row f1); a start map may be
+    given instead (``s_init``).  Histories: dict of [n_iter + 1, nbins] (B = 1)
+    or [n_iter + 1, B, nbins]; accept flags [n_iter] or [n_iter, B]."""
 
     def __init__(self, cr, bins, kind=None):
         from .engine import GibbsPlan
@@ -331,20 +405,14 @@ class MaskedRunner:
         F = cr.F
         self.spectra = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
         self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
-        self.plan = GibbsPlan(cr.L, cr.nside, F, 1, cr.bl, [1.0] * F, self.bins, chain0=cr.chain)
+        self.plan = GibbsPlan(cr.L, cr.nside, F, cr.B, cr.bl, [1.0] * F, self.bins, chain0=cr.chain)
         self.d0 = self.plan.zeros(F, cr.NR)
-        L = cr.L
-        idx = np.full((len(self.spectra), L + 1), -1, dtype=np.int64)
-        for k, sp in enumerate(self.spectra):
-            b = self.bins[sp]
-            for i in range(len(b) - 1):
-                idx[k, b[i]:min(b[i + 1], L + 1)] = i
-        self._idx = torch.from_numpy(np.maximum(idx, 0)).to(cr.device)
-        self._valid = torch.from_numpy(idx >= 0).to(cr.device)
+        self._idx, self._valid = _unfold_index(self.spectra, self.bins, cr.L, cr.device)
 
     def _unfold(self, binned_t):
-        """utils.unfold_bins on the device: binned [1, nspec, maxbins] -> [nspec, L+1]."""
-        return torch.where(self._valid, torch.gather(binned_t[0], 1, self._idx), 0.0).contiguous()
+        """utils.unfold_bins on the device: binned [B, nspec, maxbins] -> [B?, nspec, L+1]."""
+        return _unfold_batch(binned_t, self._idx, self._valid).reshape(self.cr._shape(len(self.spectra),
+                                                                                       self.cr.L + 1))
 
     def run(self, dls_init, n_iter, s_init):
         """The loop stays on the device: D_l, the accept flags and the histories are
@@ -352,7 +420,10 @@ class MaskedRunner:
         and two copies per iteration); the per-iteration CR / C_l times come from
         events read after the loop."""
         cr, plan = self.cr, self.plan
-        binned0 = {s: np.asarray(dls_init[s], dtype=np.float64) for s in self.spectra}
+        if isinstance(dls_init, (list, tuple)):
+            binned0 = [{s: np.asarray(d[s], dtype=np.float64) for s in self.spectra} for d in dls_init]
+        else:
+            binned0 = {s: np.asarray(dls_init[s], dtype=np.float64) for s in self.spectra}
         binned = plan.dl_tensor(binned0)
         hist, acc, evs = [binned], [], []
         if s_init is None:
@@ -362,7 +433,7 @@ class MaskedRunner:
             s = cr.pcg_solve(dl0, cr.pcg_rhs(dl0, iteration=0))
         else:
             s = cr._s(s_init)
-        one = torch.ones(1, dtype=torch.int32, device=cr.device)
+        ones = torch.ones(cr.B, dtype=torch.int32, device=cr.device)
         for i in range(n_iter):
             it = i + 1
             cr.iteration = it
@@ -371,15 +442,15 @@ class MaskedRunner:
             dl = self._unfold(binned)
             if self.kind == KIND_PCG:
                 s = cr.pcg_solve(dl, cr.pcg_rhs(dl, iteration=it))
-                acc.append(one)
+                acc.append(ones)
             elif self.kind == KIND_RJ:
                 cr.rj_step(dl, s, iteration=it)
-                acc.append(cr._acc.reshape(1).clone())
+                acc.append(cr._acc.clone())
             else:
                 cr.step(self.kind, dl, s, iteration=it)
-                acc.append(cr._acc.reshape(1).clone())
+                acc.append(cr._acc.clone())
             ev[1].record()
-            stats = plan.sweep_stats(self.d0, s[None])
+            stats = plan.sweep_stats(self.d0, s.reshape(cr.B, cr.F, cr.NR))
             var = plan.replay_invgamma() if cr.rng == "replay" else None
             binned = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)
             ev[2].record()
@@ -389,10 +460,12 @@ class MaskedRunner:
         torch.cuda.synchronize()
         t_cr = np.array([e[0].elapsed_time(e[1]) * 1e-3 for e in evs])
         t_cls = np.array([e[1].elapsed_time(e[2]) * 1e-3 for e in evs])
-        H = torch.cat(hist).cpu().numpy()                     # [n_iter + 1, nspec, maxbins]
-        A = torch.cat(acc).cpu().numpy().astype(np.int64) if acc else np.zeros(0, dtype=np.int64)
-        h = {sp: H[:, k, :len(self.bins[sp]) - 1].copy() for k, sp in enumerate(self.spectra)}
-        return h, A, t_cr, t_cls
+        H = torch.stack(hist).cpu().numpy()                   # [n_iter + 1, B, nspec, maxbins]
+        A = torch.stack(acc).cpu().numpy().astype(np.int64) if acc else np.zeros((0, cr.B), dtype=np.int64)
+        one = cr.B == 1
+        h = {sp: (H[:, 0, k, :len(self.bins[sp]) - 1] if one else H[:, :, k, :len(self.bins[sp]) - 1]).copy()
+             for k, sp in enumerate(self.spectra)}
+        return h, (A[:, 0] if one else A), t_cr, t_cls
 
 
 # ---------------------------------------------------------------------------------------
@@ -409,7 +482,8 @@ class PixelMH:
     one weighted Gram pass instead of one SHT and one host round trip per
     block.  The accept flags are read back once per sweep.
     Replay: numpy draws truncnorm EE, BB then one uniform per block attempt,
-    the reference's order (the likelihood draws nothing)."""
+    the reference's order (the likelihood draws nothing).  A batched context
+    (B chains) sweeps every chain (device tensors with a leading chain axis)."""
 
     def __init__(self, cr, bins, blocks, proposal_variances, n_iter_metropolis=1):
         from .engine import GibbsPlan, MH_ORDER
@@ -424,18 +498,12 @@ class PixelMH:
         self.bins = {s: np.asarray(bins[s]) for s in self.spectra}
         self.blocks = {s: np.asarray(blocks[s]) for s in self.spectra}
         self.n_iter = int(n_iter_metropolis)
-        self.plan = GibbsPlan(cr.L, cr.nside, F, 1, cr.bl, [1.0] * F, self.bins, blocks=self.blocks,
+        self.plan = GibbsPlan(cr.L, cr.nside, F, cr.B, cr.bl, [1.0] * F, self.bins, blocks=self.blocks,
                               proposal_variances=proposal_variances, chain0=cr.chain,
                               n_iter_metropolis=self.n_iter)
         L = cr.L
-        idx = np.full((F, L + 1), -1, dtype=np.int64)
-        for k, s in enumerate(self.spectra):
-            b = self.bins[s]
-            for i in range(len(b) - 1):
-                idx[k, b[i]:min(b[i + 1], L + 1)] = i
-        self._idx = torch.from_numpy(np.maximum(idx, 0)).to(cr.device)
-        self._valid = torch.from_numpy(idx >= 0).to(cr.device)
-        self._lik = torch.zeros(1, dtype=torch.float64, device=cr.device)
+        self._idx, self._valid = _unfold_index(self.spectra, self.bins, L, cr.device)
+        self._lik = torch.zeros(cr.B, dtype=torch.float64, device=cr.device)
         # block tables of gs_masked_pixel_mh, in decision order (spectra in MH order)
         blk = np.full((F, L + 1), -1, dtype=np.int32)
         lmax_, field, brange, self._acc_layout = [], [], [], []
@@ -454,11 +522,15 @@ class PixelMH:
         self.K = len(field)
         dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(cr.device)
         self._blk, self._blk_lmax, self._blk_field, self._blk_bins = dev(blk), dev(lmax_), dev(field), dev(brange)
-        self._acc = torch.zeros(max(self.K * self.n_iter, 1), dtype=torch.int32, device=cr.device)
+        self._acc = torch.zeros((cr.B, max(self.K * self.n_iter, 1)), dtype=torch.int32, device=cr.device)
+
+    def _batched(self, binned_t):
+        return binned_t if binned_t.dim() == 3 else binned_t[None]
 
     def unfold(self, binned_t):
-        """utils.unfold_bins on the device: [nspec, maxbins] -> [nspec, L+1]."""
-        return torch.where(self._valid, torch.gather(binned_t, 1, self._idx), 0.0).contiguous()
+        """utils.unfold_bins on the device: [B?, nspec, maxbins] -> [B?, nspec, L+1]."""
+        out = _unfold_batch(self._batched(binned_t), self._idx, self._valid)
+        return out if binned_t.dim() == 3 else out[0]
 
     def noncentre(self, dl_unbinned, s):
         """s_nc = C^-1/2 s (zero where C = 0; NonCenteredGibbs.py:186-191, ASIS.py:184-190)."""
@@ -481,38 +553,43 @@ class PixelMH:
         return self._lik
 
     def compute_log_likelihood(self, dls, s_nonCentered):
-        """NonCenteredGibbs.py:333-355 (binned dict, dict / array map) -> float."""
+        """NonCenteredGibbs.py:333-355 (binned dict, dict / array map) -> float (B = 1)."""
+        if self.cr.B != 1:
+            raise NotImplementedError("compute_log_likelihood: the reference surface's one-chain form")
         bt = self.plan.dl_tensor(dls)[0]
         return float(self.loglik_t(self.unfold(bt), self.cr._s(s_nonCentered)).item())
 
     def sweep_t(self, s_nc, binned_t, iteration):
         """one sweep on device tensors, no host synchronisation: binned_t
-        [nspec, maxbins] -> (updated copy, accept flags [K * n_iter] int32 in
-        decision order; the flags tensor is reused by the next sweep)."""
+        [B?, nspec, maxbins] -> (updated copy, accept flags [B?, K * n_iter] int32
+        in decision order; the flags tensor is reused by the next sweep)."""
         plan, cr = self.plan, self.cr
-        dl = binned_t[None].contiguous()
+        one = binned_t.dim() == 2
+        dl = self._batched(binned_t).contiguous()
         if cr.rng == "replay":
             up, ua = plan.replay_mh_uniforms()
             prop, logr, _ = plan.mh_propose(dl, up, seed=cr.seed, iteration=iteration)
         else:
             prop, logr, ua = plan.mh_propose(dl, None, seed=cr.seed, iteration=iteration, with_uniforms=True)
-        prop0, logr0 = prop[0].contiguous(), logr[0].contiguous()
-        cur = binned_t.clone()
+        prop, logr = prop.contiguous(), logr.contiguous()
+        cur = dl.clone()
         # every temporary stays referenced until the launch is enqueued (a freed
         # tensor's block is handed to the next allocation)
-        dl_cur, dl_prop, u0 = self.unfold(cur), self.unfold(prop0), ua[0].contiguous()
+        dl_cur = _unfold_batch(cur, self._idx, self._valid)
+        dl_prop = _unfold_batch(prop, self._idx, self._valid)
+        u0 = ua.contiguous()
         _capi.check(self.cr.lib.gs_masked_pixel_mh(
             cr.handle, self.K, self.n_iter, plan.maxbins, _capi.ptr(self._blk), _capi.ptr(self._blk_lmax),
-            _capi.ptr(self._blk_field), _capi.ptr(self._blk_bins), _capi.ptr(s_nc), _capi.ptr(dl_cur),
-            _capi.ptr(dl_prop), _capi.ptr(logr0), _capi.ptr(u0), _capi.ptr(prop0),
+            _capi.ptr(self._blk_field), _capi.ptr(self._blk_bins), _capi.ptr(s_nc.contiguous()), _capi.ptr(dl_cur),
+            _capi.ptr(dl_prop), _capi.ptr(logr), _capi.ptr(u0), _capi.ptr(prop),
             _capi.ptr(cur), _capi.ptr(self._acc), _capi.stream_ptr()), "gs_masked_pixel_mh")
-        return cur, self._acc
+        return (cur[0], self._acc[0]) if one else (cur, self._acc)
 
     def split_accept(self, flags):
         a = flags.cpu().numpy()
         out, off = {}, 0
         for s, n in self._acc_layout:
-            out[s] = [int(v) for v in a[off:off + n]]
+            out[s] = [int(v) for v in a[off:off + n]] if a.ndim == 1 else a[:, off:off + n].copy()
             off += n
         return out
 
@@ -523,7 +600,9 @@ class PixelMH:
         return cur, self.split_accept(flags)
 
     def sample(self, s_nonCentered, binned_dls_old, iteration=None):
-        """reference surface: dict maps / binned dicts in, (binned dict, accept dict) out."""
+        """reference surface: dict maps / binned dicts in, (binned dict, accept dict) out (B = 1)."""
+        if self.cr.B != 1:
+            raise NotImplementedError("PixelMH.sample: the reference surface's one-chain form (use sweep_t)")
         it = self.cr.iteration if iteration is None else int(iteration)
         bt = self.plan.dl_tensor(binned_dls_old)[0]
         cur, acc = self.sample_t(self.cr._s(s_nonCentered), bt, it)
@@ -531,7 +610,7 @@ class PixelMH:
 
 
 class MaskedMHRunner:
-    """Masked non-centred and interweaving drivers on one chain:
+    """Masked non-centred and interweaving drivers (the context's B chains at once):
 
     kind "noncentered": NonCenteredClsSampler.run_polarization
       (NonCenteredGibbs.py:529-571) -- per iteration the PCG CR in the centred
@@ -556,14 +635,21 @@ class MaskedMHRunner:
         return self.cr.pcg_solve(dl, self.cr.pcg_rhs(dl, iteration=it))
 
     def run(self, dls_init, n_iter, s_init=None):
-        """n_iter iterations from dls_init (binned dict).  s_init: continue from
-        this map instead of the reference's PCG start map (ASIS.py:153-156).
-        The loop stays on the device (D_l, accept flags and histories are device
-        tensors until the end; the stage times come from events read after it)."""
+        """n_iter iterations from dls_init (binned dict, or a list of B dicts).
+        s_init: continue from this map instead of the reference's PCG start map
+        (ASIS.py:153-156).  The loop stays on the device (D_l, accept flags and
+        histories are device tensors until the end; the stage times come from
+        events read after it)."""
         cr, mh, plan = self.cr, self.mh, self.plan
-        cur = plan.dl_tensor({s: np.asarray(dls_init[s], dtype=np.float64) for s in mh.spectra})[0]
+        B = cr.B
+        if isinstance(dls_init, (list, tuple)):
+            init = [{s: np.asarray(d[s], dtype=np.float64) for s in mh.spectra} for d in dls_init]
+        else:
+            init = {s: np.asarray(dls_init[s], dtype=np.float64) for s in mh.spectra}
+        cur = plan.dl_tensor(init)                             # [B, nspec, maxbins]
+        shape = lambda t: t.reshape(cr._shape(*t.shape[1:])) if B == 1 else t
         hist, flags, acc_cr, evs = [cur], [], [], []
-        dl = mh.unfold(cur)
+        dl = shape(mh.unfold(cur))
         s = None
         if s_init is not None:
             s = cr._s(s_init)
@@ -580,22 +666,22 @@ class MaskedMHRunner:
                 ev[1].record()
                 ev[2].record()
                 cur, f = mh.sweep_t(s_nc, cur, it)
-                dl = mh.unfold(cur)
+                dl = shape(mh.unfold(cur))
             else:
                 if self.cr_kind == KIND_PCG:
                     s = self._pcg(dl, it)
                 else:
                     cr.step(self.cr_kind, dl, s, iteration=it)
-                    acc_cr.append(cr._acc.reshape(1).clone())
+                    acc_cr.append(cr._acc.clone())
                 ev[1].record()
-                stats = plan.sweep_stats(self.d0[None], s[None])
+                stats = plan.sweep_stats(self.d0[None], s.reshape(B, cr.F, cr.NR))
                 var = plan.replay_invgamma() if cr.rng == "replay" else None
-                tmp = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)[0]
-                dl_tmp = mh.unfold(tmp)
+                tmp = plan.cls_draw(stats, var, seed=cr.seed, iteration=it)
+                dl_tmp = shape(mh.unfold(tmp))
                 s_nc = mh.noncentre(dl_tmp, s)
                 ev[2].record()
                 cur, f = mh.sweep_t(s_nc, tmp, it)
-                dl = mh.unfold(cur)
+                dl = shape(mh.unfold(cur))
                 s = mh.centre(dl, s if self.quirk else s_nc)
             ev[3].record()
             flags.append(f.clone())           # sweep_t reuses its flags tensor
@@ -608,16 +694,20 @@ class MaskedMHRunner:
         t_cr = np.array([el(e, 0, 1) for e in evs])
         t_cls = np.array([el(e, 1, 2) for e in evs])
         t_nc = np.array([el(e, 2, 3) for e in evs])
-        H = torch.stack(hist).cpu().numpy()                   # [n_iter + 1, nspec, maxbins]
-        h = {sp: H[:, k, :len(mh.bins[sp]) - 1].copy() for k, sp in enumerate(mh.spectra)}
+        H = torch.stack(hist).cpu().numpy()                   # [n_iter + 1, B, nspec, maxbins]
+        one = B == 1
+        h = {sp: (H[:, 0, k, :len(mh.bins[sp]) - 1] if one else H[:, :, k, :len(mh.bins[sp]) - 1]).copy()
+             for k, sp in enumerate(mh.spectra)}
         acc = {sp: [] for sp in mh.spectra}
         if flags:
-            Fl = torch.stack(flags).cpu().numpy()
-            for row in Fl:
-                off = 0
-                for sp, n in mh._acc_layout:
-                    acc[sp].append([int(v) for v in row[off:off + n]])
-                    off += n
-        a_cr = torch.cat(acc_cr).cpu().numpy().astype(np.int64) if acc_cr else None
-        out = ({sp: np.array(v) for sp, v in h.items()}, {sp: np.array(v) for sp, v in acc.items()})
+            Fl = torch.stack(flags).cpu().numpy().reshape(len(flags), B, -1)   # [n_iter, B, K n_iter]
+            off = 0
+            for sp, n in mh._acc_layout:
+                a = Fl[:, :, off:off + n].astype(np.int64)
+                acc[sp] = a[:, 0] if one else a
+                off += n
+        a_cr = torch.stack(acc_cr).cpu().numpy().astype(np.int64) if acc_cr else None
+        if a_cr is not None and one:
+            a_cr = a_cr[:, 0]
+        out = (h, {sp: np.array(v) for sp, v in acc.items()})
         return out + (a_cr, t_it, t_cr, t_cls, t_nc)

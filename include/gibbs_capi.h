@@ -232,6 +232,21 @@ int gs_sht_map2alm(gs_sht* sht, int ncomp, int layout, const double* maps, doubl
 int gs_sht_alm2map_beamed(gs_sht* sht, int ncomp, const double* alm_real, const double* bl, double* maps, void* stream);
 int gs_sht_map2alm_weighted(gs_sht* sht, int ncomp, const double* maps, const double* weights, double* alm_real,
                             void* stream);
+/* Batches of maps (one per chain; the reference runs its chains as separate
+ * SLURM tasks, job-script.sh:6-8, each calling hp.alm2map / hp.map2alm):
+ * alm [nmap][ncomp][n], maps [nmap][ncomp][Npix] contiguous; one launch per
+ * stage serves every map (small maps fill the GPU), and map b of a batch is
+ * bit-identical to the same map transformed alone.  bl (nullable, real layout):
+ * per-l beam on the synthesis input (hp.alm2map(almxfl(alm, b_l))); weights
+ * (nullable; real layout, niter 0): [ncomp][Npix] shared by the batch, the
+ * analysis of weights * maps (hp.map2alm(N^-1 m)).  gs_sht_reserve sizes the
+ * plan's per-map workspace for nmap maps ahead of a graph capture (a larger
+ * batch inside a capture is an error). */
+int gs_sht_reserve(gs_sht* sht, int nmap, void* stream);
+int gs_sht_alm2map_batch(gs_sht* sht, int nmap, int ncomp, int layout, const double* alm, const double* bl,
+                         double* maps, void* stream);
+int gs_sht_map2alm_batch(gs_sht* sht, int nmap, int ncomp, int layout, const double* maps, const double* weights,
+                         double* alm, int niter, void* stream);
 
 /* ---- masked (pixel-domain) constrained realisation (gs_masked.hip) -------
  * Replaces PolarizedCenteredConstrainedRealization's masked samplers:
@@ -239,16 +254,23 @@ int gs_sht_map2alm_weighted(gs_sht* sht, int ncomp, const double* maps, const do
  *   GS_MCR_OVERRELAX  overrelaxation_sampler        CenteredGibbs.py:733-825
  *   GS_MCR_MALA       sample_mala                   CenteredGibbs.py:560-603 (EB only)
  *   GS_MCR_AUX_MALA   the ula composition of sample CenteredGibbs.py:832-836
- * One chain per call.  maps / inv_noise (create): DEVICE [3][Npix] rows T, Q, U
- * (inv_noise mask-multiplied, CenteredGibbs.py:266-274; the T row is read
- * only for nfields = 3).  dl: DEVICE unbinned D_l [nspec][L+1]; s: [F][(L+1)^2]
- * real layout, updated in place; v: [F][Npix] the auxiliary map (needed
- * across calls only by GS_MCR_OVERRELAX; may be NULL).  Replay variates
- * (NULL = native Philox streams): zv [n][F][Npix] pixel normals, zs [n][F][NR]
- * slot normals in the reference's draw order (AUX: per inner iteration v then
- * s; OVERRELAX: initial v, then per iteration s, v, s; MALA: zm [F][NR], um[1]).
- * accept (device int32, optional): 1 for the auxiliary samplers, the MALA
- * decision otherwise; log_ratio (device double, optional). */
+ * A context runs a batch of B = desc.nchains chains (0 -> 1) on one data set:
+ * the reference's independent chains (its SLURM array, job-script.sh:6-8) as
+ * one batch whose transforms are batched SHTs; `chain` arguments are the global
+ * id of the batch's first chain (chain b has id chain + b), and chain b's
+ * results equal a one-chain context's for id chain + b bit for bit.
+ * maps / inv_noise (create): DEVICE [3][Npix] rows T, Q, U (inv_noise
+ * mask-multiplied, CenteredGibbs.py:266-274; the T row is read only for
+ * nfields = 3), shared by the batch.  Every per-chain argument is [B][...]
+ * contiguous: dl DEVICE unbinned D_l [B][nspec][L+1]; s [B][F][(L+1)^2] real
+ * layout, updated in place; v [B][F][Npix] the auxiliary map (needed across
+ * calls only by GS_MCR_OVERRELAX; may be NULL).  Replay variates (NULL =
+ * native Philox streams), per chain: zv [B][n][F][Npix] pixel normals, zs
+ * [B][n][F][NR] slot normals in the reference's draw order (AUX: per inner
+ * iteration v then s; OVERRELAX: initial v, then per iteration s, v, s; MALA:
+ * zm [B][F][NR], um [B]).  accept (device int32 [B], optional): 1 for the
+ * auxiliary samplers, the MALA decisions otherwise; log_ratio (device double
+ * [B], optional). */
 #define GS_MCR_AUX 0
 #define GS_MCR_OVERRELAX 1
 #define GS_MCR_MALA 2
@@ -268,10 +290,12 @@ typedef struct gs_masked_desc {
                                    /* b A^T N^-1 d and of the aux s|v analysis:    */
                                    /* 0 (pol: iter=0) or 3 (TT: adjoint_synthesis_hp */
                                    /* and healpy's default, CenteredGibbs.py:208)  */
+    int nchains;                   /* chains of the batch (0 or 1: one chain)     */
 } gs_masked_desc;
 int gs_masked_create(const gs_masked_desc* desc, const double* maps, const double* inv_noise, gs_masked** out);
 int gs_masked_destroy(gs_masked* ctx);
 int gs_masked_info(const gs_masked* ctx, double* mu3 /* HOST [3] */, double* second_part_grad /* DEVICE [F][NR] */);
+int gs_masked_nchains(const gs_masked* ctx);   /* chains of the batch; -1 for a null context */
 int gs_masked_gradient(gs_masked* ctx, const double* dl, const double* s, double* grad, double* pix, void* stream);
 /* f4: temperature full-sky CR from pixel data (nfields = 1 context):
  * centered CenteredConstrainedRealization.sample_no_mask (CenteredGibbs.py:108-132)
@@ -291,12 +315,18 @@ int gs_masked_cr(gs_masked* ctx, int kind, const double* dl, double* s, double* 
  * z_B) or NULL for the native streams.  The CG recurrence's scalars stay on
  * the device; the host launches batches of iterations sized from the residual's
  * decay and synchronises once per batch (no host round trip per iteration).
- * gs_masked_pcg_info: host synchronisations of the last solve. */
+ * Batched contexts solve every chain's system at once (per-chain scalars and
+ * convergence; rhs / x [B][F][NR]); iters / rel_residual are HOST [B].
+ * gs_masked_pcg_info: host synchronisations of the last solve; _info2 also the
+ * CG iterations launched (>= every chain's count: a converged chain's kernels
+ * return at once, its transforms still run until the batch's last chain
+ * converges). */
 int gs_masked_pcg_rhs(gs_masked* ctx, const double* dl, const double* zv, const double* zs, uint64_t seed,
                       uint32_t iteration, int chain, double* rhs, void* stream);
 int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, double* x, int x_is_guess, double tol,
                         int maxiter, int* iters, double* rel_residual, void* stream);
 int gs_masked_pcg_info(const gs_masked* ctx, int* host_syncs);
+int gs_masked_pcg_info2(const gs_masked* ctx, int* host_syncs, int* launched);
 /* out = Q x, the PCG system operator (C^+ + b A^T N^-1 A b) applied to x
  * (qcinv opfilt_pp fwd_op, CenteredGibbs.py:631,655). */
 int gs_masked_pcg_apply(gs_masked* ctx, const double* dl, const double* x, double* out, void* stream);

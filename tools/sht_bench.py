@@ -53,6 +53,35 @@ def bench(N, L, reps):
     return sht
 
 
+def bench_batch(N, L, reps, batches, ncomps=(2,)):
+    """batched transforms (gs_sht_*_batch, one launch per stage for B maps): ms per
+    batch, ms per map and TF/s; the beam / N^-1 fused forms of the masked CR."""
+    from gibbssampler_amd import _capi
+    sht = HealpixSHT(N, L)
+    lib = sht.lib
+    nlm = (L + 1) * (L + 2) // 2
+    npair = 2 * N
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for ncomp in ncomps:
+        c = {1: 4, 2: 16, 3: 20}[ncomp]
+        w = torch.rand((ncomp, 12 * N * N), generator=g, device="cuda", dtype=torch.float64)
+        bl = torch.rand(L + 1, generator=g, device="cuda", dtype=torch.float64)
+        for B in batches:
+            a = torch.randn((B, ncomp, (L + 1) ** 2), generator=g, device="cuda", dtype=torch.float64)
+            m = torch.randn((B, ncomp, 12 * N * N), generator=g, device="cuda", dtype=torch.float64)
+            out_m, out_a = torch.empty_like(m), torch.empty_like(a)
+            sp = _capi.stream_ptr()
+            syn = lambda: lib.gs_sht_alm2map_batch(sht.handle, B, ncomp, 0, _capi.ptr(a), _capi.ptr(bl),
+                                                   _capi.ptr(out_m), sp)
+            ana = lambda: lib.gs_sht_map2alm_batch(sht.handle, B, ncomp, 0, _capi.ptr(m), _capi.ptr(w),
+                                                   _capi.ptr(out_a), 0, sp)
+            ts, ta = timeit(syn, reps), timeit(ana, reps)
+            fl = npair * nlm * c * B
+            print(f"batch N_side={N} ncomp={ncomp} B={B:3d}: alm2map {ts:8.3f} ms ({ts / B:7.4f} ms/map, "
+                  f"{fl / ts / 1e9:6.2f} TF/s)   map2alm {ta:8.3f} ms ({ta / B:7.4f} ms/map, {fl / ta / 1e9:6.2f} TF/s)",
+                  flush=True)
+
+
 def check_big(N, L):
     """adjointness + one single mode at a size whose cap rings need M > 8192."""
     sht = HealpixSHT(N, L)
@@ -91,7 +120,13 @@ if __name__ == "__main__":
     ap.add_argument("--lmax", type=int, default=None)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--big", action="store_true")
+    ap.add_argument("--batch", default=None, help="comma-separated batch sizes: batched-transform timings only")
+    ap.add_argument("--ncomp", default="2")
     args = ap.parse_args()
+    if args.batch:
+        bench_batch(args.nside, args.lmax or 2 * args.nside, args.reps, [int(b) for b in args.batch.split(",")],
+                    tuple(int(c) for c in args.ncomp.split(",")))
+        raise SystemExit(0)
     bench(args.nside, args.lmax or 2 * args.nside, args.reps)
     if args.big:
         check_big(2048, 4096)
