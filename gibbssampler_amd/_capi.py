@@ -57,6 +57,7 @@ class GsMaskedDesc(ctypes.Structure):
         ("mu_eps", ctypes.c_double),
         ("adj_iter", ctypes.c_int),
         ("nchains", ctypes.c_int),
+        ("sht_mode", ctypes.c_int),
     ]
 
 
@@ -117,6 +118,8 @@ _SIGS = [
     ("gs_sht_alm2map_beamed", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP]),
     ("gs_sht_map2alm_weighted", ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP]),
     ("gs_sht_reserve", ctypes.c_int, [_VP, ctypes.c_int, _VP]),
+    ("gs_sht_set_mfma", ctypes.c_int, [_VP, ctypes.c_int]),
+    ("gs_sht_mfma_info", ctypes.c_int, [_VP, c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
     ("gs_sht_alm2map_batch", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP]),
     ("gs_sht_map2alm_batch", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP,
                                             ctypes.c_int, _VP]),
@@ -124,6 +127,7 @@ _SIGS = [
     ("gs_masked_destroy", ctypes.c_int, [_VP]),
     ("gs_masked_info", ctypes.c_int, [_VP, c_double_p, _VP]),
     ("gs_masked_nchains", ctypes.c_int, [_VP]),
+    ("gs_masked_sht_tables", ctypes.c_int, [_VP]),
     ("gs_masked_gradient", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     ("gs_masked_pcg_rhs", ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, _VP,
                                          _VP]),

@@ -1313,6 +1313,7 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
         return set_error("gs_masked_create: nfields must be 1 (T), 2 (EB) or 3 (TEB)");
     if (desc->adj_iter < 0 || desc->adj_iter > 16) return set_error("gs_masked_create: adj_iter out of range");
     if (desc->nchains < 0 || desc->nchains > 4096) return set_error("gs_masked_create: nchains out of range");
+    if (desc->sht_mode < 0 || desc->sht_mode > 2) return set_error("gs_masked_create: sht_mode must be 0, 1 or 2");
     if (!desc->bl) return set_error("gs_masked_create: null beam");
     gs_masked* c = new gs_masked();
     c->L = desc->lmax; c->nside = desc->nside; c->F = desc->nfields;
@@ -1332,6 +1333,14 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     c->nblk = (int)std::min<long long>(512, nblocks(std::max(c->F * c->NR, c->F * c->npix), RED_BLOCK));
     if (gs_sht_create(c->nside, c->L, &c->sht)) { mc_free(c); return -1; }
     if (gs_sht_reserve(c->sht, c->B, nullptr)) { mc_free(c); return -1; }
+    // the Legendre stage: matrix-core tables for batches (auto: >= 4 chains,
+    // when the plan is a small-map one and the table fits its budget)
+    if (desc->sht_mode == 2 || (desc->sht_mode == 0 && c->B >= 4)) {
+        if (gs_sht_set_mfma(c->sht, 1)) {
+            if (desc->sht_mode == 2) { mc_free(c); return -1; }
+            (void)gs_last_error();          // auto: keep the on-the-fly kernels
+        }
+    }
     const long long FR = c->FR, FP = c->FP;
     const size_t B = (size_t)c->B;
     int rc = 0;
@@ -1423,6 +1432,13 @@ int gs_masked_info(const gs_masked* c, double* mu3, double* second_part_grad) {
 }
 
 int gs_masked_nchains(const gs_masked* c) { return c ? c->B : set_error("null masked context"); }
+
+int gs_masked_sht_tables(const gs_masked* c) {
+    if (!c) return set_error("null masked context");
+    int on = 0;
+    if (gs_sht_mfma_info(c->sht, &on, nullptr)) return -1;
+    return on;
+}
 
 int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, void* stream) {
     if (!c) return set_error("null masked context");

@@ -1711,6 +1711,421 @@ __global__ void k_sub_maps(long long n, const double* __restrict__ a, double* __
     if (g < n) b[g] = a[g] - b[g];
 }
 
+// ===========================================================================
+// Batched small maps: the Legendre stage as dense fp64 matrix-core contractions
+// ===========================================================================
+// For a batch of B maps the Legendre stage of one m is a matrix product whose
+// inner dimension is shared by every map:
+//   synthesis  Phi[ring][col] = sum_{l, F} G_F(l, ring) a_F(l, col)   (K = l)
+//   analysis   a[l][col]      = sum_{ring, F} G_F(l, ring) Phi_F(ring, col)  (K = rings)
+// with col = (map, output part) and G = lambda (spin 0) or the spin-2 F1 / F2,
+// the north / south parity folded as in the VALU kernels (output rows of one
+// l parity).  Here G comes from a plan-time table (MfTab) filled by the same
+// scaled recurrence the VALU kernels run -- a value the recurrence holds below
+// the representable range (k < 0) is stored as 0, exactly what they multiply --
+// so both transform kernels are v_mfma_f64_16x16x4_f64 streams whose K loop
+// reads the table once per transform for every map of the batch.  The table
+// costs 3 x 8 B x N_ringpair x N_lm (1.6 GB at N_side 256 / l_max 512), so it
+// is built for small maps only (large maps keep the on-the-fly recurrence).
+// Blocks of 16 l x 16 ring pairs; blocks wholly below the representable range
+// of a (m, 16-pair tile) are not stored (b0); planes lambda, F1, F2.
+constexpr int MF_TILE = 16;
+constexpr int MF_BLK = 3 * 256;                  // doubles per block (3 planes of 16 l x 16 pairs)
+
+struct MfTab {
+    const double* tab;       // blocks
+    const long long* off;    // [L+1][ntile] first stored block of (m, tile)
+    const int* b0;           // [L+1][ntile] first stored block index (l = m + 16 b)
+    int ntile;
+};
+
+// pass 1: first representable l of every (m, ring pair) -> per (m, 16-pair tile) b0
+__global__ __launch_bounds__(256) void k_mf_onset(ShtDev D, const double* __restrict__ lmm, const int* __restrict__ lmk,
+                                                  int* __restrict__ b0) {
+    const int L = D.L, npair = D.npair;
+    const int m = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    int lon = L + 1;
+    if (p < npair) {
+        const double x = D.geom[p].x;
+        const LegCoef* cf = D.coef + (cidx(L, m, m) - m);
+        double v1 = 0.0, v0 = lmm[(long long)m * npair + p];
+        int k = lmk[(long long)m * npair + p];
+        for (int l = m; l <= L; ++l) {
+            if (k == 0) { lon = l; break; }
+            if (l == L) break;
+            rec_step(cf[l + 1], x, v0, v1);
+            if (k < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
+        }
+    }
+    // min over the 16 pairs of the tile (lanes 16 t .. 16 t + 15 of the wave)
+    for (int o = 8; o > 0; o >>= 1) lon = min(lon, __shfl_xor(lon, o, 16));
+    if ((threadIdx.x & 15) == 0 && p < npair) {
+        const int nb = (L - m + MF_TILE) / MF_TILE;
+        b0[(long long)m * ((npair + MF_TILE - 1) / MF_TILE) + p / MF_TILE] = lon > L ? nb : (lon - m) / MF_TILE;
+    }
+}
+
+// pass 2: every (m, ring pair) walks its recurrence from m and writes lambda,
+// F1, F2 of the stored blocks (the VALU kernels' values: k < 0 -> 0)
+__global__ __launch_bounds__(256) void k_mf_fill(ShtDev D, const double* __restrict__ lmm, const int* __restrict__ lmk,
+                                                 MfTab T) {
+    const int L = D.L, npair = D.npair;
+    const int m = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npair) return;
+    const int t = p / MF_TILE, j = p % MF_TILE;
+    const long long ti = (long long)m * T.ntile + t;
+    const int b0 = T.b0[ti], nb = (L - m + MF_TILE) / MF_TILE;
+    if (b0 >= nb) return;
+    double* out = const_cast<double*>(T.tab) + T.off[ti] * MF_BLK;
+    const double x = D.geom[p].x, is2 = D.geom[p].is2, xis2 = x * is2;
+    const LegCoef* cf = D.coef + (cidx(L, m, m) - m);
+    double v1 = 0.0, v0 = lmm[(long long)m * npair + p];
+    int k = lmk[(long long)m * npair + p];
+    for (int l = m; l < m + nb * MF_TILE; ++l) {
+        const int b = (l - m) / MF_TILE, r = (l - m) % MF_TILE;
+        double lam = 0.0, f1 = 0.0, f2 = 0.0;
+        if (l <= L) {
+            const LegCoef c = cf[l];
+            const double w0 = k == 0 ? v0 : 0.0, w1 = k == 0 ? v1 : 0.0;
+            lam = w0;
+            f1 = fma(c.R * xis2, w1, -fma(c.P, is2, c.Q) * w0);
+            f2 = fma(c.Rm * is2, w1, -(c.T * xis2) * w0);
+            if (l < L) {
+                rec_step(cf[l + 1], x, v0, v1);
+                if (k < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
+            }
+        }
+        if (b >= b0) {
+            double* blk = out + (long long)(b - b0) * MF_BLK + r * MF_TILE + j;
+            blk[0] = lam;
+            blk[256] = f1;
+            blk[512] = f2;
+        }
+    }
+}
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// ---- synthesis: one wave per 16-pair tile, TPW tiles per workgroup ---------------
+// Spin 2 (E, B -> Q, U): per quad of l (l0 = m + 16 b + 4 q, l0 - m even) the
+// K entries of the "+" product are (l0, F1), (l0+1, F2), (l0+2, F1), (l0+3, F2)
+// and of the "-" product the other function at each l (F1 carries lambda's
+// parity, F2 the opposite one), so lane (g = lane / 16, j = lane % 16) holds A =
+// G(l0 + g, pair 16 t + j) and B = the a_lm row of (l0 + g, col j); col =
+// (map 4 cg + j / 4, part j % 4 = Q re, Q im, U re, U im):
+//   F1 row: (aE.x, aE.y, aB.x, aB.y)     F2 row: (-aB.y, aB.x, aE.y, -aE.x)
+// N = -(C+ + C-), S = -(C+ - C-).  Spin 0 (T): per octet the "+" K entries are
+// the even l (l0, l0+2, l0+4, l0+6) and the "-" the odd ones, lambda rows, col =
+// (map 8 cg + j / 2, re / im).  The a_lm of the workgroup's maps for MF_CH l are
+// staged in LDS (every tile of the m reads them).
+constexpr int MF_CH = 32;                          // l staged per chunk (two blocks)
+// the staged a_lm of one chunk: every thread moves MF_SITEMS entries; the next
+// chunk's are loaded into registers while this chunk's MFMAs run (issued after
+// the chunk's table loads, so waiting for those never waits for them)
+template <int SPIN, int CGW>
+__global__ __launch_bounds__(256) void k_sht_synth_mfma(ShtDev D, MfTab T, const double2* __restrict__ ain,
+                                                        double2* __restrict__ phi, int nmap, int ncm, int cbase) {
+    constexpr int CPG = SPIN == 2 ? 4 : 8;         // maps per 16-column group
+    constexpr int MPW = CGW * CPG;                 // maps per workgroup
+    constexpr int NCMP = SPIN == 2 ? 2 : 1;        // a_lm comps read
+    constexpr int NIT = MF_CH * MPW * NCMP;        // staged entries per chunk
+    constexpr int PER = (NIT + 255) / 256;         // per thread (block of 256)
+    __shared__ __attribute__((aligned(16))) double2 sa[MF_CH][MPW][NCMP];
+    const int L = D.L, npair = D.npair, nlm = D.nlm;
+    const int m = blockIdx.x;
+    const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t = blockIdx.y * (blockDim.x >> 6) + wave;
+    const int c0 = blockIdx.z * MPW;
+    const int nb = (L - m + MF_TILE) / MF_TILE;
+    const long long ti = (long long)m * T.ntile + min(t, T.ntile - 1);
+    const int b0 = t < T.ntile ? T.b0[ti] : nb;
+    const double* tab = T.tab + (t < T.ntile ? T.off[ti] : 0) * MF_BLK;
+    const long long base = cidx(L, m, m) - m;
+    auto fetch = [&](int cb, double2 (&pf)[PER]) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            const int cc = i % NCMP, mp = (i / NCMP) % MPW, lr = i / (NCMP * MPW);
+            const int l = m + cb * MF_TILE + lr, c = c0 + mp;
+            pf[k] = (i < NIT && l <= L && c < nmap) ? ain[((long long)c * ncm + cbase + cc) * nlm + base + l]
+                                                    : make_double2(0.0, 0.0);
+        }
+    };
+    f64x4 Cp[CGW], Cm[CGW];
+#pragma unroll
+    for (int c = 0; c < CGW; ++c) { Cp[c] = f64x4{0, 0, 0, 0}; Cm[c] = f64x4{0, 0, 0, 0}; }
+    double2 pf[PER];
+    fetch(0, pf);
+    const int o = j & 3;
+    const bool ox = o == 0 || o == 3;
+    for (int cb = 0; cb < nb; cb += MF_CH / MF_TILE) {
+        __syncthreads();                            // the previous chunk's readers are done
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            if (i < NIT) (&sa[0][0][0])[i] = pf[k];
+        }
+        __syncthreads();
+        const int bend = min(cb + MF_CH / MF_TILE, nb);
+        const int bst = max(cb, b0);
+        // this chunk's table values first (both blocks, every quad / octet) ...
+        constexpr int NQ = 2 * 4 * 2;               // blocks x quads x functions (spin 2); x octet halves (spin 0)
+        double gv[NQ];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int b = cb + bb;
+            const bool ok = b >= bst && b < bend;
+            const double* blk = tab + (long long)(ok ? b - b0 : 0) * MF_BLK;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if constexpr (SPIN == 2) {
+                    const int row = 4 * q + g;
+                    gv[(bb * 4 + q) * 2 + 0] = ok ? blk[256 + row * MF_TILE + j] : 0.0;
+                    gv[(bb * 4 + q) * 2 + 1] = ok ? blk[512 + row * MF_TILE + j] : 0.0;
+                } else {
+                    // q = 2 h + e: octet half h, even (e = 0) / odd row of lambda
+                    const int row = 8 * (q >> 1) + 2 * g + (q & 1);
+                    gv[(bb * 4 + q) * 2 + 0] = ok ? blk[row * MF_TILE + j] : 0.0;
+                    gv[(bb * 4 + q) * 2 + 1] = 0.0;
+                }
+            }
+        }
+        // ... then the next chunk's a_lm (their wait is the next iteration's)
+        if (cb + MF_CH / MF_TILE < nb) fetch(cb + MF_CH / MF_TILE, pf);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int b = cb + bb;
+            if (b < bst || b >= bend) continue;     // wave-uniform
+            const int lr0 = bb * MF_TILE;
+            if constexpr (SPIN == 2) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int row = 4 * q + g;
+                    const double f1 = gv[(bb * 4 + q) * 2 + 0], f2 = gv[(bb * 4 + q) * 2 + 1];
+                    const bool ev = (g & 1) == 0;
+                    const double ap = ev ? f1 : f2, am = ev ? f2 : f1;
+#pragma unroll
+                    for (int c = 0; c < CGW; ++c) {
+                        const int mp = c * 4 + (j >> 2);
+                        const double* e = reinterpret_cast<const double*>(&sa[lr0 + row][mp][0]);
+                        const double* bb2 = reinterpret_cast<const double*>(&sa[lr0 + row][mp][1]);
+                        // E part: x for Q re / U im cols (o 0, 3), y otherwise; B part the other
+                        const double ev_ = e[ox ? 0 : 1], bv = bb2[ox ? 1 : 0];
+                        // F1 row (aE.x, aE.y, aB.x, aB.y), F2 row (-aB.y, aB.x, aE.y, -aE.x)
+                        const double r1 = o < 2 ? ev_ : bv;
+                        const double r2 = (o == 0 || o == 3) ? -(o == 0 ? bv : ev_) : (o == 1 ? bv : ev_);
+                        Cp[c] = mfma64(ap, ev ? r1 : r2, Cp[c]);
+                        Cm[c] = mfma64(am, ev ? r2 : r1, Cm[c]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int re = 8 * h + 2 * g, ro = re + 1;
+                    const double ap = gv[(bb * 4 + 2 * h) * 2], am = gv[(bb * 4 + 2 * h + 1) * 2];
+#pragma unroll
+                    for (int c = 0; c < CGW; ++c) {
+                        const int mp = c * 8 + (j >> 1);
+                        const double* ae = reinterpret_cast<const double*>(&sa[lr0 + re][mp][0]);
+                        const double* ao = reinterpret_cast<const double*>(&sa[lr0 + ro][mp][0]);
+                        Cp[c] = mfma64(ap, ae[j & 1], Cp[c]);
+                        Cm[c] = mfma64(am, ao[j & 1], Cm[c]);
+                    }
+                }
+            }
+        }
+    }
+    if (t >= T.ntile) return;
+    // D layout: lane (g, j) holds rows g + 4 r (pairs 16 t + g + 4 r), col j
+    const long long plane = phi_plane(L, npair);
+#pragma unroll
+    for (int c = 0; c < CGW; ++c) {
+        const int mp = SPIN == 2 ? c * 4 + (j >> 2) : c * 8 + (j >> 1);
+        const int map = c0 + mp;
+        if (map >= nmap) continue;
+        const int comp = SPIN == 2 ? cbase + ((j & 3) >> 1) : cbase;
+        const int part = j & 1;
+        double* PN = reinterpret_cast<double*>(phi + (((long long)map * ncm + comp) * 2 + 0) * plane);
+        double* PS = reinterpret_cast<double*>(phi + (((long long)map * ncm + comp) * 2 + 1) * plane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int pr = MF_TILE * t + g + 4 * r;
+            if (pr >= npair) continue;
+            const double sp = Cp[c][r], sn = Cm[c][r];
+            const long long off = 2 * phi_at(m, pr, npair) + part;
+            if constexpr (SPIN == 2) { PN[off] = -(sp + sn); PS[off] = -(sp - sn); }
+            else { PN[off] = sp + sn; PS[off] = sp - sn; }
+        }
+    }
+}
+
+// ---- analysis: one wave per 32-l window (16 even + 16 odd l), all pair tiles ----
+// a^T[col][l] = sum_K Phi^T[col][K] G[K][l], K = 4 ring pairs of one function
+// per MFMA: A = Phi^T (lane: row = col j, k = pair 4 s + g), B = G (lane: k =
+// pair, col = l index j of the window's parity-p rows, l = lw + 2 j + p).  The
+// ring phases of each 16-pair tile are staged once per workgroup in LDS as the
+// parity-combined (N + S, N - S) of Q, U (spin 2) or T (spin 0), the next
+// tile's loaded into registers while this tile's MFMAs run.  Spin 2, even l
+// (p = 0; p = 1 swaps + and -), output parts o = (E re, E im, B re, B im):
+//   F1 coefficients (+Q.x, +Q.y, +U.x, +U.y)[o]
+//   F2 coefficients sign(o) (-)[3 - o] of (-Q.x, -Q.y, -U.x, -U.y), sign - for o = 0, 3
+// where + = N + S, - = N - S (ana_term of the recurrence kernels).  The tiles
+// are summed inside the accumulator in tile order (no cross-workgroup
+// reduction); the weight (spin 0: w, spin 2: -w) and the caller's layout are
+// applied on the store.
+template <int SPIN, int CGW>
+__global__ __launch_bounds__(512) void k_sht_anal_mfma(ShtDev D, MfTab T, const double2* __restrict__ phi, int nmap,
+                                                       int ncm, int cbase, double w, int layout, int acc,
+                                                       double* __restrict__ alm) {
+    constexpr int CPG = SPIN == 2 ? 4 : 8;
+    constexpr int MPW = CGW * CPG;
+    constexpr int NV = SPIN == 2 ? 8 : 4;          // staged doubles per (pair, map)
+    constexpr int NIT = MF_TILE * MPW;             // staged (pair, map) items per tile
+    constexpr int PER = (NIT + 511) / 512;
+    __shared__ __attribute__((aligned(16))) double sp[MF_TILE][MPW][NV];
+    const int L = D.L, npair = D.npair;
+    const int m = blockIdx.x;
+    // workgroups whose first window starts past L leave before any barrier
+    if (m + 32 * (int)(blockIdx.y * (blockDim.x >> 6)) > L) return;
+    const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int win = blockIdx.y * (blockDim.x >> 6) + wave;
+    const int lw = m + 32 * win;
+    const bool live = lw <= L;
+    const int c0 = blockIdx.z * MPW;
+    const int nb = (L - m + MF_TILE) / MF_TILE;
+    const int bw = 2 * win;                        // the window's first block
+    const long long plane = phi_plane(L, npair);
+    // the staged item of thread (k): N, S phases of (pair, map) -> registers
+    struct Ph { double2 a, b, c, d; };
+    auto fetch = [&](int t, Ph (&pf)[PER]) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 512 * k;
+            const int mp = i % MPW, jp = i / MPW;
+            const int pr = MF_TILE * t + jp, map = c0 + mp;
+            const double2 z = make_double2(0.0, 0.0);
+            pf[k] = Ph{z, z, z, z};
+            if (i < NIT && pr < npair && map < nmap) {
+                const long long off = phi_at(m, pr, npair);
+                const double2* P = phi + ((long long)map * ncm + cbase) * 2 * plane;
+                pf[k].a = P[off];
+                pf[k].b = P[plane + off];
+                if constexpr (SPIN == 2) {
+                    pf[k].c = P[2 * plane + off];
+                    pf[k].d = P[3 * plane + off];
+                }
+            }
+        }
+    };
+    f64x4 C[CGW][2];
+#pragma unroll
+    for (int c = 0; c < CGW; ++c) { C[c][0] = f64x4{0, 0, 0, 0}; C[c][1] = f64x4{0, 0, 0, 0}; }
+    Ph pf[PER];
+    fetch(0, pf);
+    const int o = j & 3;
+    const double s2 = (o == 0 || o == 3) ? -1.0 : 1.0;
+    for (int t = 0; t < T.ntile; ++t) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 512 * k;
+            if (i >= NIT) continue;
+            double* dst = sp[i / MPW][i % MPW];
+            const Ph& q = pf[k];
+            if constexpr (SPIN == 2) {          // a = Q north, b = Q south, c = U north, d = U south
+                dst[0] = q.a.x + q.b.x; dst[1] = q.a.y + q.b.y; dst[2] = q.c.x + q.d.x; dst[3] = q.c.y + q.d.y;
+                dst[4] = q.a.x - q.b.x; dst[5] = q.a.y - q.b.y; dst[6] = q.c.x - q.d.x; dst[7] = q.c.y - q.d.y;
+            } else {
+                dst[0] = q.a.x + q.b.x; dst[1] = q.a.y + q.b.y; dst[2] = q.a.x - q.b.x; dst[3] = q.a.y - q.b.y;
+            }
+        }
+        __syncthreads();
+        // this tile's table values first ...
+        const long long ti = (long long)m * T.ntile + t;
+        const int b0 = T.b0[ti];
+        const bool any = live && bw + 1 >= b0 && bw < nb;    // wave-uniform
+        const int bj = bw + (j >> 3);
+        const bool okb = any && bj >= b0 && bj < nb;
+        const double* blk = T.tab + (T.off[ti] + (okb ? bj - b0 : 0)) * MF_BLK;
+        constexpr int NF = SPIN == 2 ? 2 : 1;
+        double gv[4][2][NF];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int row = 2 * (j & 7) + p;
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+                    gv[s][p][f] = okb ? blk[(SPIN == 2 ? 256 * (f + 1) : 0) + row * MF_TILE + 4 * s + g] : 0.0;
+            }
+        // ... then the next tile's phases (their wait is the next iteration's)
+        if (t + 1 < T.ntile) fetch(t + 1, pf);
+        if (!any) continue;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int jp = 4 * s + g;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+#pragma unroll
+                for (int c = 0; c < CGW; ++c) {
+                    if constexpr (SPIN == 2) {
+                        const double* v = sp[jp][c * 4 + (j >> 2)];
+                        // F1 takes the parity-p combination (p = 0: +, 1: -), F2 the other
+                        const double a1 = v[4 * p + o];
+                        const double a2 = s2 * v[4 * (1 - p) + 3 - o];
+                        C[c][p] = mfma64(a1, gv[s][p][0], C[c][p]);
+                        C[c][p] = mfma64(a2, gv[s][p][NF - 1], C[c][p]);
+                    } else {
+                        const double* v = sp[jp][c * 8 + (j >> 1)];
+                        C[c][p] = mfma64(v[2 * p + (j & 1)], gv[s][p][0], C[c][p]);
+                    }
+                }
+            }
+        }
+    }
+    if (!live) return;
+    // D layout: lane (g, j) holds rows g + 4 r = col index, col j = l index:
+    // spin 2: map 4 c + r, part g (E re, E im, B re, B im); spin 0: map 8 c +
+    // (g + 4 r) / 2, part (g + 4 r) % 2
+    const double f = SPIN == 2 ? -w : w;
+    constexpr double SQ2 = 1.41421356237309504880;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int l = lw + 2 * j + p;
+        if (l > L) continue;
+        const long long ic = cidx(L, l, m);
+#pragma unroll
+        for (int c = 0; c < CGW; ++c) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = g + 4 * r;
+                const int map = SPIN == 2 ? c0 + c * 4 + r : c0 + c * 8 + row / 2;
+                const int comp = SPIN == 2 ? cbase + (g >> 1) : cbase;
+                const int part = SPIN == 2 ? (g & 1) : (row & 1);
+                if (map >= nmap) continue;
+                const double v = f * C[c][p][r];
+                double* out = alm + ((long long)map * ncm + comp) * alm_comp_stride(layout, L);
+                if (layout == GS_ALM_COMPLEX) {
+                    double* d = out + 2 * ic + part;
+                    *d = acc ? *d + v : v;
+                } else if (m == 0) {
+                    if (part == 0) { double* d = out + l; *d = acc ? *d + v : v; }
+                } else {
+                    double* d = out + 2 * ic - (L + 1) + part;
+                    *d = acc ? *d + SQ2 * v : SQ2 * v;
+                }
+            }
+        }
+    }
+}
+
 inline unsigned nblocks(long long n, int bs) { return (unsigned)std::max<long long>(1, (n + bs - 1) / bs); }
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
@@ -1750,6 +2165,16 @@ struct gs_sht {
     double* mapw = nullptr;      // [cap][3][npix] Jacobi residual maps
     double2* ain = nullptr;      // [cap][3][nlm] a_lm in healpy complex order
     int cap = 1;                 // maps of a batch the per-map workspace (phi, part, ain, mapw) holds
+    // batched small maps: the Legendre stage on the fp64 matrix cores from a
+    // plan-time table (gs_sht_set_mfma); mf = 1 routes every transform of the
+    // plan (any batch size: results do not depend on it) through it
+    int mf = 0;
+    double* mf_tab = nullptr;
+    long long* mf_off = nullptr;
+    int* mf_b0 = nullptr;
+    int mf_ntile = 0;
+    long long mf_bytes = 0;
+    MfTab mftab() const { return MfTab{mf_tab, mf_off, mf_b0, mf_ntile}; }
     // ring classes by FFT length
     std::vector<int> cls_M;      // M of each class
     std::vector<int> cls_n;      // pairs in the class
@@ -1791,7 +2216,7 @@ int sht_alloc(gs_sht* p, T** dst, size_t n) {
 
 void sht_free(gs_sht* p) {
     void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->sscr,
-                    p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs};
+                    p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs, p->mf_tab, p->mf_off, p->mf_b0};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (int* b : p->cls_pairs)
@@ -2254,6 +2679,109 @@ static int sht_reserve(gs_sht* p, int nmap, hipStream_t st) {
     return 0;
 }
 
+// ---- the matrix-core Legendre stage (plans with mf set) --------------------------
+constexpr int MF_CGW = 4;         // 16-column groups per workgroup (16 maps spin 2, 32 spin 0)
+
+static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
+    const ShtDev D = p->dev();
+    const MfTab T = p->mftab();
+    const unsigned ty = (unsigned)((p->mf_ntile + 3) / 4);
+    if (ncomp != 2) {               // T (spin 0): comp 0
+        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
+        hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW>), g, dim3(256), 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0);
+        GS_LAUNCH_CHECK("k_sht_synth_mfma<0>");
+    }
+    if (ncomp != 1) {               // E, B -> Q, U: comps ncomp - 2, ncomp - 1
+        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
+        hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW>), g, dim3(256), 0, st, D, T, p->ain, p->phi, nmap, ncomp,
+                           ncomp - 2);
+        GS_LAUNCH_CHECK("k_sht_synth_mfma<2>");
+    }
+    return 0;
+}
+
+static int sht_anal_mfma(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st) {
+    const ShtDev D = p->dev();
+    const MfTab T = p->mftab();
+    const double w = 4.0 * PI / (double)p->npix;
+    const int nwin = (p->L + 1 + 31) / 32;          // 32-l windows of m = 0
+    const unsigned ty = (unsigned)((nwin + 7) / 8);  // 8 windows (waves) per workgroup
+    if (ncomp != 2) {
+        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
+        hipLaunchKernelGGL((k_sht_anal_mfma<0, MF_CGW>), g, dim3(512), 0, st, D, T, p->phi, nmap, ncomp, 0, w, layout,
+                           acc, alm);
+        GS_LAUNCH_CHECK("k_sht_anal_mfma<0>");
+    }
+    if (ncomp != 1) {
+        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
+        hipLaunchKernelGGL((k_sht_anal_mfma<2, MF_CGW>), g, dim3(512), 0, st, D, T, p->phi, nmap, ncomp, ncomp - 2, w,
+                           layout, acc, alm);
+        GS_LAUNCH_CHECK("k_sht_anal_mfma<2>");
+    }
+    return 0;
+}
+
+// build (on = 1) or drop (0) the plan's Legendre tables
+static int sht_set_mfma(gs_sht* p, int on) {
+    if (!on) {
+        p->mf = 0;
+        return 0;
+    }
+    if (p->mf_tab) { p->mf = 1; return 0; }
+    const int L = p->L, npair = p->npair;
+    const int ntile = (npair + MF_TILE - 1) / MF_TILE;
+    double* lmm = nullptr;
+    int* lmk = nullptr;
+    int* b0d = nullptr;
+    auto fail = [&](const char* what) {
+        if (lmm) (void)hipFree(lmm);
+        if (lmk) (void)hipFree(lmk);
+        if (b0d) (void)hipFree(b0d);
+        return set_error(std::string("gs_sht_set_mfma: ") + what);
+    };
+    if (hipMalloc((void**)&lmm, (size_t)(L + 1) * npair * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&lmk, (size_t)(L + 1) * npair * sizeof(int)) != hipSuccess ||
+        hipMalloc((void**)&b0d, (size_t)(L + 1) * ntile * sizeof(int)) != hipSuccess)
+        return fail("out of device memory");
+    hipLaunchKernelGGL(k_sht_lmm, dim3(nblocks(npair, 64)), dim3(64), 0, 0, L, npair, p->geom, lmm, lmk);
+    hipLaunchKernelGGL(k_mf_onset, dim3(nblocks(npair, 256), L + 1), dim3(256), 0, 0, p->dev(), lmm, lmk, b0d);
+    std::vector<int> b0((size_t)(L + 1) * ntile);
+    if (hipMemcpy(b0.data(), b0d, b0.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail("onset pass failed");
+    std::vector<long long> off(b0.size());
+    long long nblk = 0;
+    for (int m = 0; m <= L; ++m) {
+        const int nb = (L - m + MF_TILE) / MF_TILE;
+        for (int t = 0; t < ntile; ++t) {
+            const size_t i = (size_t)m * ntile + t;
+            off[i] = nblk;
+            nblk += std::max(0, nb - b0[i]);
+        }
+    }
+    double* tab = nullptr;
+    long long* offd = nullptr;
+    if (hipMalloc((void**)&tab, (size_t)std::max(1LL, nblk) * MF_BLK * sizeof(double)) != hipSuccess)
+        return fail("out of device memory (table)");
+    if (hipMalloc((void**)&offd, off.size() * sizeof(long long)) != hipSuccess ||
+        hipMemcpy(offd, off.data(), off.size() * sizeof(long long), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(tab);
+        if (offd) (void)hipFree(offd);
+        return fail("offset upload failed");
+    }
+    p->mf_tab = tab; p->mf_off = offd; p->mf_b0 = b0d; p->mf_ntile = ntile;
+    b0d = nullptr;
+    hipLaunchKernelGGL(k_mf_fill, dim3(nblocks(npair, 256), L + 1), dim3(256), 0, 0, p->dev(), lmm, lmk, p->mftab());
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipFree(lmm);
+    (void)hipFree(lmk);
+    lmm = nullptr; lmk = nullptr;
+    if (e != hipSuccess || hipGetLastError() != hipSuccess) return set_error("gs_sht_set_mfma: table fill failed");
+    p->mf_bytes = nblk * MF_BLK * (long long)sizeof(double) + (long long)off.size() * 12;
+    p->bytes += p->mf_bytes;
+    p->mf = 1;
+    return 0;
+}
+
 // synthesis of B maps (alm [B][ncomp][n], maps [B][ncomp][Npix]); bl (real layout
 // only): the per-l beam applied on the input load
 static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double* alm, const double* bl, double* maps,
@@ -2276,6 +2804,10 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * ncomp, alm,
                        layout, p->ain, bl);
     GS_LAUNCH_CHECK("k_sht_alm_in");
+    if (p->mf) {
+        if (sht_synth_mfma(p, nmap, ncomp, S(stream))) return -1;
+        return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp);
+    }
     const int syn_nseg = p->syn_seg ? (p->L + p->syn_seg) / p->syn_seg : 1;
     if (p->syn_seg > 0 && p->syn_seg <= 64 && p->syn_sr == 1 && !p->syn_paired && syn_nseg <= 16) {
         // small maps: l-segmented synthesis, one wave per segment (<= 64 l: the
@@ -2316,6 +2848,7 @@ static int sht_analysis(gs_sht* p, int nmap, int ncomp, int layout, const double
     }
     if (sht_reserve(p, nmap, S(stream))) return -1;
     if (sht_rings(p, false, nmap * ncomp, maps, nullptr, stream, nullptr, nullptr, 1, wts, ncomp)) return -1;
+    if (p->mf) return sht_anal_mfma(p, nmap, ncomp, layout, acc, alm, S(stream));
     const int sr = p->ana_sr_nc[ncomp], sl = p->ana_seg_nc[ncomp];
     const int ntile = (p->ngroup + 4 * sr - 1) / (4 * sr);
     const int nsegz = sl ? (p->L + sl) / sl : 1;
@@ -2426,6 +2959,28 @@ int gs_sht_map2alm_weighted(gs_sht* p, int ncomp, const double* maps, const doub
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_map2alm_weighted: ncomp must be 1 (T), 2 (Q,U) or 3 (T,Q,U)");
     if (!alm_real || !maps || !weights) return set_error("gs_sht_map2alm_weighted: null argument");
     return sht_analysis(p, 1, ncomp, GS_ALM_REAL, maps, alm_real, 0, stream, weights);
+}
+
+int gs_sht_set_mfma(gs_sht* p, int on) {
+    if (check_sht(p)) return -1;
+    if (on && !sht_batch_native(p))
+        return set_error("gs_sht_set_mfma: the Legendre tables are for small maps (no split-ring FFT plan)");
+    if (on && !p->mf_tab) {
+        // 3 planes x 8 B per (l, m, ring pair), before the onset skip; budget
+        // GS_SHT_MFMA_MAX_GB (16 GB: N_side 512 / l_max 1024 takes 12.9 GB)
+        double gb = 16.0;
+        if (const char* e = std::getenv("GS_SHT_MFMA_MAX_GB")) gb = std::atof(e);
+        const double need = 24.0 * (double)p->npair * (double)p->nlm / 1e9;
+        if (need > gb) return set_error("gs_sht_set_mfma: the Legendre table exceeds GS_SHT_MFMA_MAX_GB");
+    }
+    return sht_set_mfma(p, on);
+}
+
+int gs_sht_mfma_info(const gs_sht* p, int* on, long long* table_bytes) {
+    if (check_sht(p)) return -1;
+    if (on) *on = p->mf;
+    if (table_bytes) *table_bytes = p->mf_bytes;
+    return 0;
 }
 
 int gs_sht_reserve(gs_sht* p, int nmap, void* stream) {

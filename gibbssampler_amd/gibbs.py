@@ -229,8 +229,7 @@ class GibbsSampler:
     def _tt_model(self, with_mh):
         from .tt import TTModel
         if self._tt is None:
-            if self.nchains != 1:
-                raise NotImplementedError("pixel-domain TT runs one chain per process (shard chains over GPUs)")
+            # nchains > 1: one batch (batched SHTs), histories with a chain axis
             pm = self.pix_map["TT"] if isinstance(self.pix_map, dict) else self.pix_map
             pv = blocks = None
             if with_mh:
@@ -240,7 +239,7 @@ class GibbsSampler:
                 blocks = blocks["TT"] if isinstance(blocks, dict) else blocks
             self._tt = TTModel(pm, self.noise, self.bl_gauss, self.lmax, self.nside, self.bins["TT"], mask=self.mask,
                                blocks=blocks, proposal_variances=pv, n_iter_metropolis=self.n_iter_metropolis,
-                               rng=self.rng, seed=self.seed, chain=self.chain0)
+                               rng=self.rng, seed=self.seed, chain=self.chain0, nchains=self.nchains)
         return self._tt
 
     # -- helpers of the reference base class --------------------------------------------

@@ -49,7 +49,7 @@ class MaskedCR:
 
     def __init__(self, pix_map, noise_temp, noise_pol, bl, lmax, nside, mask=None, nfields=2, gibbs_cr=True,
                  n_gibbs=1, alpha=-0.995, overrelaxation=False, ula=False, tau=0.02, rng="replay", seed=0, chain=0,
-                 device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000, rj=False, nchains=1):
+                 device="cuda", pcg_accuracy=1.0e-5, pcg_maxiter=4000, rj=False, nchains=1, sht_mode="auto"):
         if nfields not in (1, 2, 3):
             raise ValueError("nfields must be 1 (T), 2 (EB, the reference) or 3 (TEB)")
         self.lib = _capi.load()
@@ -95,6 +95,9 @@ class MaskedCR:
         desc.mu_eps = 1e-7 if self.F == 1 else 1e-14
         desc.adj_iter = 3 if self.F == 1 else 0
         desc.nchains = self.B
+        # the Legendre stage: "auto" (matrix-core tables for >= 4 chains on small
+        # maps), "recurrence" (on-the-fly VALU kernels) or "mfma"
+        desc.sht_mode = {"auto": 0, "recurrence": 1, "mfma": 2}[sht_mode]
         h = ctypes.c_void_p()
         _capi.check(self.lib.gs_masked_create(ctypes.byref(desc), _capi.ptr(self._maps), _capi.ptr(self._inv),
                                               ctypes.byref(h)), "gs_masked_create")
@@ -105,6 +108,11 @@ class MaskedCR:
         self.v = torch.zeros(self._shape(self.F, self.Npix), dtype=torch.float64, device=device)
         self._acc = torch.zeros(self.B, dtype=torch.int32, device=device)
         self._lr = torch.zeros(self.B, dtype=torch.float64, device=device)
+
+    @property
+    def sht_tables(self):
+        """True when the context's transforms run the matrix-core table path."""
+        return bool(self.lib.gs_masked_sht_tables(self.handle))
 
     def __del__(self):
         _capi.park(dict(self.__dict__))       # inside a capture: tensors freed after it

@@ -42,6 +42,48 @@ class HealpixSHT:
             _capi.release(self.lib.gs_sht_destroy, h)
             self.handle = None
 
+    def set_mfma(self, on=True):
+        """Route the Legendre stage through the fp64 matrix cores (plan-time
+        lambda / F1 / F2 table; small maps; gs_sht_set_mfma)."""
+        _capi.check(self.lib.gs_sht_set_mfma(self.handle, int(bool(on))), "gs_sht_set_mfma")
+        return self
+
+    @property
+    def mfma(self):
+        on, nb = ctypes.c_int(), ctypes.c_longlong()
+        _capi.check(self.lib.gs_sht_mfma_info(self.handle, ctypes.byref(on), ctypes.byref(nb)), "gs_sht_mfma_info")
+        return bool(on.value), nb.value
+
+    def alm2map_batch(self, alm, ncomp, bl=None, layout="real", out=None):
+        """alm [B, ncomp, n] -> maps [B, ncomp, Npix] in one batched transform
+        (optionally the per-l beam on the input load, real layout)."""
+        B = alm.shape[0]
+        a = alm.contiguous()
+        if layout == "complex":
+            a = torch.view_as_real(a)
+        if out is None:
+            out = torch.empty((B, ncomp, self.npix), dtype=torch.float64, device=alm.device)
+        _capi.check(self.lib.gs_sht_alm2map_batch(self.handle, B, ncomp, _LAYOUT[layout], _capi.ptr(a),
+                                                  _capi.ptr(None if bl is None else bl.contiguous()), _capi.ptr(out),
+                                                  _capi.stream_ptr()), "gs_sht_alm2map_batch")
+        return out
+
+    def map2alm_batch(self, maps, ncomp, iter=0, weights=None, layout="real", out=None):
+        """maps [B, ncomp, Npix] -> alm [B, ncomp, n] in one batched transform
+        (optionally of weights * maps, weights [ncomp, Npix] shared by the batch)."""
+        B = maps.shape[0]
+        maps = maps.contiguous()
+        if out is None:
+            if layout == "complex":
+                out = torch.empty((B, ncomp, self.ncomplex), dtype=torch.complex128, device=maps.device)
+            else:
+                out = torch.empty((B, ncomp, self.nreal), dtype=torch.float64, device=maps.device)
+        o = torch.view_as_real(out) if layout == "complex" else out
+        _capi.check(self.lib.gs_sht_map2alm_batch(self.handle, B, ncomp, _LAYOUT[layout], _capi.ptr(maps),
+                                                  _capi.ptr(None if weights is None else weights.contiguous()),
+                                                  _capi.ptr(o), int(iter), _capi.stream_ptr()), "gs_sht_map2alm_batch")
+        return out
+
     # -- shapes -----------------------------------------------------------------
     @property
     def nreal(self):

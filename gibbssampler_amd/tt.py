@@ -45,21 +45,26 @@ def _dl_from_var(var_cls, L):
 
 
 class TTModel:
-    """Device context of one TT chain: the masked-CR context (F = 1), the
-    C_l-draw plan and (for non-centred / ASIS runs) the pixel-likelihood MH."""
+    """Device context of the TT chains: the masked-CR context (F = 1), the
+    C_l-draw plan and (for non-centred / ASIS runs) the pixel-likelihood MH.
+    ``nchains`` = B > 1 runs B chains (global ids chain .. chain + B - 1) as one
+    batch (batched SHTs); the drivers' histories then carry a chain axis."""
 
     def __init__(self, pix_map, noise, bl, lmax, nside, bins, mask=None, blocks=None, proposal_variances=None,
-                 n_iter_metropolis=1, rng="native", seed=0, chain=0, pcg_accuracy=1.0e-6):
+                 n_iter_metropolis=1, rng="native", seed=0, chain=0, pcg_accuracy=1.0e-6, nchains=1,
+                 sht_mode="auto"):
         from .engine import GibbsPlan
         self.L, self.nside = int(lmax), int(nside)
         self.NR = (self.L + 1) ** 2
         self.bins = np.asarray(bins)
+        self.B = int(nchains)
         # TT PCG: 1e-6 relative, 4000 iterations (ConstrainedRealization.py:41)
         self.cr = MaskedCR(pix_map, noise, 1.0, bl, lmax, nside, mask=mask, nfields=1, gibbs_cr=True, n_gibbs=1,
-                           rng=rng, seed=seed, chain=chain, pcg_accuracy=pcg_accuracy)
+                           rng=rng, seed=seed, chain=chain, pcg_accuracy=pcg_accuracy, nchains=self.B,
+                           sht_mode=sht_mode)
         self.masked = mask is not None
         self.rng, self.seed = rng, int(seed)
-        self.plan = GibbsPlan(lmax, nside, 1, 1, self.cr.bl, [1.0], {"TT": self.bins}, chain0=chain)
+        self.plan = GibbsPlan(lmax, nside, 1, self.B, self.cr.bl, [1.0], {"TT": self.bins}, chain0=chain)
         self.d0 = self.plan.zeros(1, 1, self.NR)
         self.mh = None
         if proposal_variances is not None:
@@ -75,11 +80,18 @@ class TTModel:
 
     # -- device steps --------------------------------------------------------------------
     def unfold(self, binned_t):
-        """[1, maxbins] binned D -> [1, L+1] (utils.unfold_bins)."""
-        return torch.where(self._valid, torch.gather(binned_t, 1, self._idx), 0.0).contiguous()
+        """[B?, 1, maxbins] binned D -> [B?, 1, L+1] (utils.unfold_bins)."""
+        if binned_t.dim() == 2:
+            return torch.where(self._valid, torch.gather(binned_t, 1, self._idx), 0.0).contiguous()
+        B = binned_t.shape[0]
+        g = torch.gather(binned_t, 2, self._idx.unsqueeze(0).expand(B, -1, -1))
+        return torch.where(self._valid.unsqueeze(0), g, 0.0).contiguous()
 
     def binned_t(self, binned):
-        return self.plan.dl_tensor({"TT": np.asarray(binned, dtype=np.float64)})[0]
+        """binned D_l (one array for every chain, or [B, nbins]) -> [1, maxbins] (B = 1) / [B, 1, maxbins]"""
+        a = np.asarray(binned, dtype=np.float64)
+        t = self.plan.dl_tensor([{"TT": r} for r in a] if a.ndim == 2 else {"TT": a})
+        return t[0] if self.B == 1 else t
 
     def cr_centered(self, dl, it):
         """sample_no_mask (full sky) or sample_mask (PCG) in the centred parametrisation."""
@@ -104,16 +116,26 @@ class TTModel:
         return out
 
     def cls_draw(self, s, it):
-        stats = self.plan.sweep_stats(self.d0, s[None])
+        stats = self.plan.sweep_stats(self.d0, s.reshape(self.B, 1, self.NR))
         var = self.plan.replay_invgamma() if self.rng == "replay" else None
-        return self.plan.cls_draw(stats, var, seed=self.seed, iteration=it)[0]
+        out = self.plan.cls_draw(stats, var, seed=self.seed, iteration=it)
+        return out[0] if self.B == 1 else out
 
     def mh_sweep(self, s_nc, binned_t, it):
         cur, acc = self.mh.sample_t(s_nc, binned_t, it)
         return cur, acc["TT"]
 
     def host_binned(self, t):
-        return t[0, :len(self.bins) - 1].cpu().numpy().copy()
+        if self.B == 1:
+            return t[0, :len(self.bins) - 1].cpu().numpy().copy()
+        return t[:, 0, :len(self.bins) - 1].cpu().numpy().copy()
+
+    def _start(self, dls_init):
+        a = np.asarray(dls_init, dtype=np.float64).copy()
+        return a if self.B == 1 or a.ndim == 2 else np.broadcast_to(a, (self.B,) + a.shape).copy()
+
+    def _ones(self):
+        return 1 if self.B == 1 else np.ones(self.B, dtype=np.int64)
 
     # -- drivers -------------------------------------------------------------------------
     def run_centered(self, dls_init, n_iter):
@@ -121,13 +143,13 @@ class TTModel:
         cur = self.binned_t(dls_init)
         dl = self.unfold(cur)
         s = self.cr_centered(dl, 0)                  # the first CR (GibbsSampler.py:92)
-        h, acc, t = [np.asarray(dls_init, dtype=np.float64).copy()], [], []
+        h, acc, t = [self._start(dls_init)], [], []
         for i in range(n_iter):
             t0 = time.perf_counter()
             s = self.cr_centered(dl, i + 1)
             cur = self.cls_draw(s, i + 1)
             dl = self.unfold(cur)
-            acc.append(1)
+            acc.append(self._ones())
             h.append(self.host_binned(cur))
             t.append(time.perf_counter() - t0)
         self.s = s
@@ -156,7 +178,7 @@ class TTModel:
         cur = self.binned_t(dls_init)
         dl = self.unfold(cur)
         s = self.cr_centered(dl, 0)                  # ASIS.py:87
-        h, acc, acc_cr, t = [np.asarray(dls_init, dtype=np.float64).copy()], [], [], []
+        h, acc, acc_cr, t = [self._start(dls_init)], [], [], []
         for i in range(n_iter):
             it = i + 1
             t0 = time.perf_counter()
@@ -164,7 +186,7 @@ class TTModel:
                 s = self.cr_aux(dl, s, it)
             else:
                 s = self.cr_centered(dl, it)
-            acc_cr.append(1)
+            acc_cr.append(self._ones())
             tmp = self.cls_draw(s, it)
             s_nc = self.centre(self.unfold(tmp), s, -1)
             cur, a = self.mh_sweep(s_nc, tmp, it)

@@ -243,6 +243,15 @@ int gs_sht_map2alm_weighted(gs_sht* sht, int ncomp, const double* maps, const do
  * plan's per-map workspace for nmap maps ahead of a graph capture (a larger
  * batch inside a capture is an error). */
 int gs_sht_reserve(gs_sht* sht, int nmap, void* stream);
+/* on = 1: the plan's Legendre stage runs on the fp64 matrix cores from a
+ * plan-time table of lambda / F1 / F2 (3 x 8 B per (l, m, ring pair): 1.6 GB at
+ * N_side 256, 12.9 GB at N_side 512; budget GS_SHT_MFMA_MAX_GB, default 16) --
+ * a dense contraction per m whose inner dimension every map of a batch shares.
+ * Every transform of the plan then uses it (a map's result does not depend on
+ * the batch size); on = 0 returns to the on-the-fly recurrence kernels.
+ * Small maps only (plans without split-ring FFTs).  _info: state, table bytes. */
+int gs_sht_set_mfma(gs_sht* sht, int on);
+int gs_sht_mfma_info(const gs_sht* sht, int* on, long long* table_bytes);
 int gs_sht_alm2map_batch(gs_sht* sht, int nmap, int ncomp, int layout, const double* alm, const double* bl,
                          double* maps, void* stream);
 int gs_sht_map2alm_batch(gs_sht* sht, int nmap, int ncomp, int layout, const double* maps, const double* weights,
@@ -291,11 +300,16 @@ typedef struct gs_masked_desc {
                                    /* 0 (pol: iter=0) or 3 (TT: adjoint_synthesis_hp */
                                    /* and healpy's default, CenteredGibbs.py:208)  */
     int nchains;                   /* chains of the batch (0 or 1: one chain)     */
+    int sht_mode;                  /* Legendre stage: 0 auto (the matrix-core    */
+                                   /* table path for batches of >= 4 chains when  */
+                                   /* its table fits), 1 on-the-fly recurrence,   */
+                                   /* 2 the matrix-core table path                */
 } gs_masked_desc;
 int gs_masked_create(const gs_masked_desc* desc, const double* maps, const double* inv_noise, gs_masked** out);
 int gs_masked_destroy(gs_masked* ctx);
 int gs_masked_info(const gs_masked* ctx, double* mu3 /* HOST [3] */, double* second_part_grad /* DEVICE [F][NR] */);
 int gs_masked_nchains(const gs_masked* ctx);   /* chains of the batch; -1 for a null context */
+int gs_masked_sht_tables(const gs_masked* ctx); /* 1: the matrix-core table path is on, 0: off */
 int gs_masked_gradient(gs_masked* ctx, const double* dl, const double* s, double* grad, double* pix, void* stream);
 /* f4: temperature full-sky CR from pixel data (nfields = 1 context):
  * centered CenteredConstrainedRealization.sample_no_mask (CenteredGibbs.py:108-132)

@@ -104,11 +104,13 @@ def test_sht_batch_reserve_in_capture_errors():
 
 
 # ---- masked CR kinds -------------------------------------------------------------------
-def _crs(kind_kw, F=2, rng="native", **kw):
+def _crs(kind_kw, F=2, rng="native", sht_mode="recurrence", **kw):
     from gibbssampler_amd.masked import MaskedCR
     N, L, mask, maps, ntemp, npol, bl, dl, s0 = _problem()
     pix = {"T": maps[0], "Q": maps[1], "U": maps[2]}
-    args = dict(mask=mask, nfields=F, rng=rng, seed=4242, **kind_kw, **kw)
+    # the same Legendre stage for the batch and the one-chain contexts (the
+    # table path's summation order differs from the recurrence kernels')
+    args = dict(mask=mask, nfields=F, rng=rng, seed=4242, sht_mode=sht_mode, **kind_kw, **kw)
     batch = MaskedCR(pix, ntemp, npol, bl, L, N, chain=CHAIN0, nchains=B, **args)
     ones = [MaskedCR(pix, ntemp, npol, bl, L, N, chain=CHAIN0 + b, **args) for b in range(B)]
     rows = [1, 2] if F == 2 else [0, 1, 2]
@@ -123,15 +125,17 @@ def _dlt(cr, dl, nch):
     return torch.from_numpy(arr).cuda()
 
 
+@pytest.mark.parametrize("sht_mode", ["recurrence", "mfma"])
 @pytest.mark.parametrize("kind,F", [("aux", 2), ("aux", 3), ("over", 2), ("over", 3), ("mala", 2),
                                     ("aux_mala", 2)])
-def test_masked_cr_batch_equals_single(kind, F):
+def test_masked_cr_batch_equals_single(kind, F, sht_mode):
     from gibbssampler_amd import _capi
     kw = {"aux": dict(gibbs_cr=True, n_gibbs=2), "over": dict(gibbs_cr=True, overrelaxation=True, n_gibbs=2),
           "mala": dict(gibbs_cr=False, ula=True, tau=0.3), "aux_mala": dict(gibbs_cr=True, ula=True, tau=0.3)}[kind]
     code = {"aux": _capi.GS_MCR_AUX, "over": _capi.GS_MCR_OVERRELAX, "mala": _capi.GS_MCR_MALA,
             "aux_mala": _capi.GS_MCR_AUX_MALA}[kind]
-    batch, ones, dl, s0, L = _crs(kw, F=F)
+    batch, ones, dl, s0, L = _crs(kw, F=F, sht_mode=sht_mode)
+    assert batch.sht_tables == (sht_mode == "mfma")
     it = 7
     dlb = _dlt(batch, dl, B)
     sb = torch.from_numpy(np.ascontiguousarray(s0)).cuda()
@@ -148,11 +152,12 @@ def test_masked_cr_batch_equals_single(kind, F):
         assert len(set(acc_b.tolist())) >= 1
 
 
+@pytest.mark.parametrize("sht_mode", ["recurrence", "mfma"])
 @pytest.mark.parametrize("F", [2, 3])
-def test_pcg_batch_equals_single(F):
+def test_pcg_batch_equals_single(F, sht_mode):
     """the batched device CG (per-chain scalars and convergence) = each chain's
     own solve, bit for bit; iteration counts per chain equal."""
-    batch, ones, dl, s0, L = _crs(dict(gibbs_cr=False, ula=False), F=F, pcg_accuracy=1e-9)
+    batch, ones, dl, s0, L = _crs(dict(gibbs_cr=False, ula=False), F=F, pcg_accuracy=1e-9, sht_mode=sht_mode)
     it = 2
     dlb = _dlt(batch, dl, B)
     xb = batch.pcg_solve(dlb, batch.pcg_rhs(dlb, iteration=it))
@@ -211,11 +216,12 @@ def test_pixel_mh_batch_equals_single():
 
 
 # ---- drivers ---------------------------------------------------------------------------
-def test_masked_runner_batch_equals_single():
+@pytest.mark.parametrize("sht_mode", ["recurrence", "mfma"])
+def test_masked_runner_batch_equals_single(sht_mode):
     """MaskedRunner (the a12 ladder's aux + MALA composition, the C_l draw):
     chains 0 and B - 1 of a B-chain run equal one-chain runs."""
     from gibbssampler_amd.masked import MaskedRunner
-    batch, ones, dl, s0, L = _crs(dict(gibbs_cr=True, ula=True, n_gibbs=1), F=2)
+    batch, ones, dl, s0, L = _crs(dict(gibbs_cr=True, ula=True, n_gibbs=1), F=2, sht_mode=sht_mode)
     bins = {"EE": np.arange(L + 2), "BB": np.arange(L + 2)}
     init = {"EE": dl["EE"][:L + 1], "BB": dl["BB"][:L + 1]}
     hb, ab, _, _ = MaskedRunner(batch, bins).run(init, 3, s0)
@@ -226,14 +232,15 @@ def test_masked_runner_batch_equals_single():
         np.testing.assert_array_equal(ab[:, b], a1)
 
 
+@pytest.mark.parametrize("sht_mode", ["recurrence", "mfma"])
 @pytest.mark.parametrize("kind", ["asis", "noncentered"])
-def test_masked_mh_runner_batch_equals_single(kind):
+def test_masked_mh_runner_batch_equals_single(kind, sht_mode):
     """MaskedMHRunner: ASIS (over-relaxed aux CR + C_l draw + pixel MH +
     re-centring) and NC (PCG + pixel MH), chains 0 and B - 1 vs one-chain runs."""
     from gibbssampler_amd.masked import MaskedMHRunner, KIND_PCG, cr_kind
     kw = dict(gibbs_cr=True, overrelaxation=True, n_gibbs=2, ula=True) if kind == "asis" else \
         dict(gibbs_cr=False, ula=False)
-    batch, ones, dl, s0, L = _crs(kw, F=2, pcg_accuracy=1e-6)
+    batch, ones, dl, s0, L = _crs(kw, F=2, pcg_accuracy=1e-6, sht_mode=sht_mode)
     _, bins, blocks, pv = _mh_setup(batch, L)
     ck = cr_kind(True, True, True) if kind == "asis" else KIND_PCG
     start = {"EE": dl["EE"][:L + 1].copy(), "BB": np.array([np.mean(dl["BB"][bins["BB"][i]:bins["BB"][i + 1]])
@@ -264,3 +271,28 @@ def test_surface_masked_nchains():
     h1, _, _, _ = one.run(init)
     np.testing.assert_array_equal(h["EE"][:, 2], h1["EE"])
     np.testing.assert_array_equal(h["BB"][:, 2], h1["BB"])
+
+
+@pytest.mark.parametrize("driver", ["centered", "noncentered", "asis"])
+def test_tt_pixel_batch_equals_single(driver):
+    """the pixel-domain TT model (f4) batched: chains 0 and B - 1 of a B-chain
+    run equal one-chain runs (masked: PCG / aux CR, C_l draw, pixel MH)."""
+    from gibbssampler_amd.tt import TTModel
+    N, L, mask, maps, ntemp, npol, bl, dl, s0 = _problem()
+    bins = np.arange(L + 2)
+    pv = (0.05 * 1000.0) ** 2 * np.ones(L - 1)
+    kw = dict(mask=mask, rng="native", seed=21, blocks=np.arange(2, L + 2), proposal_variances=pv,
+              pcg_accuracy=1e-8, sht_mode="recurrence")
+    init = dl["TT"][:L + 1]
+
+    def go(m):
+        if driver == "centered":
+            return m.run_centered(init, 2)[0]
+        if driver == "noncentered":
+            return m.run_noncentered(init, 2)[0]
+        return m.run_asis(init, 2, gibbs_cr=True)[0]
+
+    hb = go(TTModel(maps[0], ntemp, bl, L, N, bins, chain=4, nchains=B, **kw))
+    for b in (0, B - 1):
+        h1 = go(TTModel(maps[0], ntemp, bl, L, N, bins, chain=4 + b, **kw))
+        np.testing.assert_array_equal(hb[:, b], h1, err_msg=f"chain {b}")

@@ -53,11 +53,16 @@ def bench(N, L, reps):
     return sht
 
 
-def bench_batch(N, L, reps, batches, ncomps=(2,)):
+def bench_batch(N, L, reps, batches, ncomps=(2,), mfma=False):
     """batched transforms (gs_sht_*_batch, one launch per stage for B maps): ms per
     batch, ms per map and TF/s; the beam / N^-1 fused forms of the masked CR."""
     from gibbssampler_amd import _capi
     sht = HealpixSHT(N, L)
+    if mfma:
+        t0 = time.time()
+        sht.set_mfma(True)
+        torch.cuda.synchronize()
+        print(f"Legendre tables: {sht.mfma[1] / 2**30:.2f} GiB, built in {time.time() - t0:.2f} s", flush=True)
     lib = sht.lib
     nlm = (L + 1) * (L + 2) // 2
     npair = 2 * N
@@ -122,10 +127,11 @@ if __name__ == "__main__":
     ap.add_argument("--big", action="store_true")
     ap.add_argument("--batch", default=None, help="comma-separated batch sizes: batched-transform timings only")
     ap.add_argument("--ncomp", default="2")
+    ap.add_argument("--mfma", action="store_true", help="batched timings on the matrix-core table path")
     args = ap.parse_args()
     if args.batch:
         bench_batch(args.nside, args.lmax or 2 * args.nside, args.reps, [int(b) for b in args.batch.split(",")],
-                    tuple(int(c) for c in args.ncomp.split(",")))
+                    tuple(int(c) for c in args.ncomp.split(",")), mfma=args.mfma)
         raise SystemExit(0)
     bench(args.nside, args.lmax or 2 * args.nside, args.reps)
     if args.big:
