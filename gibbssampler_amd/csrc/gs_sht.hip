@@ -65,6 +65,7 @@ constexpr int ANA_C = GS_ANA_C;             // l per reduction chunk (even)
 #define GS_SYN_PF 16
 #endif
 constexpr int LDS_FFT_MAX = 8192;           // complex points held in LDS
+constexpr int RING_MC_LDS_MAX = 160 * 1024;   // LDS of a multi-component ring workgroup
 constexpr double SC_UP = 0x1p768;
 constexpr double SC_DN = 0x1p-768;
 constexpr double SC_HI = 0x1p384;
@@ -1363,6 +1364,264 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
 }
 
 // ---------------------------------------------------------------------------
+// ring stage, NCB components per workgroup (batched small maps: the merged
+// launch, every ring's FFT in LDS, no split rings).  The components of one
+// ring pair share the workgroup's barriers, its LDS twiddle table and the
+// ring's Bluestein chirp / kernel loads; each FFT stage runs over all their
+// buffers (stride SB).  Per component the arithmetic is that of
+// k_sht_synth_ring / k_sht_anal_ring, so the results are bit-identical.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int ilog2d(int x) { return 31 - __clz(x); }
+
+template <int R, int NV>
+__device__ __forceinline__ void stockham_stage_mc(double2* buf, int SB, int nc, int lgM, int Ns, int dir,
+                                                  const double2* __restrict__ tw, int Mmax) {
+    constexpr int NBF = NV / R;
+    constexpr int LGR = R == 2 ? 1 : (R == 4 ? 2 : 3);
+    const int lgnb = lgM - LGR;
+    const int nb = 1 << lgnb;
+    const int nbt = nb * nc;
+    const int step = Mmax / (Ns * R);
+    double2 v[NBF][R];
+#pragma unroll
+    for (int b = 0; b < NBF; ++b) {
+        const int jj = threadIdx.x + b * blockDim.x;
+        if (jj < nbt) {
+            const int j = jj & (nb - 1);
+            const double2* B = buf + (jj >> lgnb) * SB;
+#pragma unroll
+            for (int k = 0; k < R; ++k) v[b][k] = B[j + k * nb];
+            if (Ns > 1) {
+                const int jm = j & (Ns - 1);
+#pragma unroll
+                for (int k = 1; k < R; ++k) v[b][k] = cmul(v[b][k], twid(jm * k * step, dir, tw, Mmax));
+            }
+            dft_reg<R>(v[b], dir);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NBF; ++b) {
+        const int jj = threadIdx.x + b * blockDim.x;
+        if (jj < nbt) {
+            const int j = jj & (nb - 1);
+            double2* B = buf + (jj >> lgnb) * SB;
+            const int jm = j & (Ns - 1);
+            const int base = (j - jm) * R + jm;
+#pragma unroll
+            for (int k = 0; k < R; ++k) B[base + k * Ns] = v[b][k];
+        }
+    }
+    __syncthreads();
+}
+
+template <int NV>
+__device__ __forceinline__ void fft_pow2_mc(double2* buf, int SB, int nc, int M, int dir,
+                                            const double2* __restrict__ tw, int Mmax) {
+    const int p = ilog2d(M);
+    int Ns = 1;
+    if (p % 3 == 1) { stockham_stage_mc<2, NV>(buf, SB, nc, p, 1, dir, tw, Mmax); Ns = 2; }
+    else if (p % 3 == 2) { stockham_stage_mc<4, NV>(buf, SB, nc, p, 1, dir, tw, Mmax); Ns = 4; }
+    for (; Ns < M; Ns *= 8) stockham_stage_mc<8, NV>(buf, SB, nc, p, Ns, dir, tw, Mmax);
+}
+
+template <int NV>
+__device__ __forceinline__ void bluestein_forward_mc(double2* buf, int SB, int nc, int n, int M,
+                                                     const double2* __restrict__ V, const double2* __restrict__ tw,
+                                                     int Mmax) {
+    const double2* __restrict__ C = V + M;
+    const int lgM = ilog2d(M);
+    for (int jj = threadIdx.x; jj < nc * M; jj += blockDim.x) {
+        const int j = jj & (M - 1);
+        double2* b = buf + (jj >> lgM) * SB + j;
+        *b = j < n ? cmul(*b, C[j]) : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    fft_pow2_mc<NV>(buf, SB, nc, M, -1, tw, Mmax);
+    for (int jj = threadIdx.x; jj < nc * M; jj += blockDim.x) {
+        const int j = jj & (M - 1);
+        double2* b = buf + (jj >> lgM) * SB + j;
+        *b = cmul(*b, V[j]);
+    }
+    __syncthreads();
+    fft_pow2_mc<NV>(buf, SB, nc, M, +1, tw, Mmax);
+    const double inv = 1.0 / M;
+    for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
+        const int c = jj / n, j = jj - c * n;
+        double2* b = buf + c * SB + j;
+        const double2 v = cmul(*b, C[j]);
+        *b = make_double2(v.x * inv, v.y * inv);
+    }
+    __syncthreads();
+}
+
+template <int NV>
+__device__ __forceinline__ void dft_mc(double2* buf, int SB, int nc, const PairGeom& g, int dir,
+                                       const double2* __restrict__ tw, int Mmax, const double2* __restrict__ bsk) {
+    if (g.bs_off < 0) { fft_pow2_mc<NV>(buf, SB, nc, g.M, dir, tw, Mmax); return; }
+    const int n = g.nphi;
+    if (dir > 0) {                                // conj(DFT(conj x))
+        for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) { const int c = jj / n; buf[c * SB + jj - c * n].y *= -1.0; }
+        __syncthreads();
+    }
+    bluestein_forward_mc<NV>(buf, SB, nc, n, g.M, bsk + g.bs_off, tw, Mmax);
+    if (dir > 0) {
+        for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) { const int c = jj / n; buf[c * SB + jj - c * n].y *= -1.0; }
+        __syncthreads();
+    }
+}
+
+// synthesis: grid (ring pairs, component groups of NCB); LDS NCB x SB + twiddles
+template <int NV>
+__global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, long long npix,
+                                                            const int* __restrict__ pairs,
+                                                            const PairGeom* __restrict__ geom,
+                                                            const double2* __restrict__ phi,
+                                                            const double2* __restrict__ tw, int Mmax,
+                                                            const double2* __restrict__ bsk, double* __restrict__ maps,
+                                                            int ncomp, int NCB, int SB, int twoff) {
+    extern __shared__ double2 lbuf[];
+    const int p = pairs[blockIdx.x];
+    const int c0 = blockIdx.y * NCB;
+    const int nc = min(NCB, ncomp - c0);
+    const PairGeom g = geom[p];
+    const int TC = blockDim.x / NCB;               // fold threads per component
+    const int cl = threadIdx.x / TC, tl = threadIdx.x - cl * TC;
+    const bool live = cl < nc;
+    int twM = Mmax;
+    const double2* twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
+    double2* buf = lbuf + cl * SB;
+    // fold reduction slots (J > 1: one pass) alias the component's own buffer
+    Fold4* red = reinterpret_cast<Fold4*>(buf);
+    const int n = g.nphi;
+    const long long plane = phi_plane(L, npair);
+    const double2* PN = phi + (2LL * (live ? c0 + cl : 0) + 0) * plane;
+    const double2* PS = PN + plane;
+    const bool eq = g.startS < 0;
+    const int K = n / 2 + 1;
+    const int J = K >= TC ? 1 : TC / K;
+    auto H = [&](const double2* P, int m, bool neg) {
+        const double2 v = P[phi_at(m, p, npair)];
+        const double cm = (m == 0 ? 1.0 : 2.0) * (neg ? -1.0 : 1.0);
+        return make_double2(cm * v.x, cm * v.y);
+    };
+    for (int s0 = 0; s0 < K * J; s0 += TC) {
+        const int sl = s0 + tl;
+        Fold4 f = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
+        const int k = sl % K, j0 = sl / K;
+        const int nk = (n - k) % n;
+        const bool on = live && sl < K * J;
+        if (on) {
+            for (int m = k + j0 * n, q = j0; m <= L; m += J * n, q += J) {
+                const bool neg = g.phi_half && (q & 1);
+                const double2 a = H(PN, m, neg);
+                f.nk.x += a.x; f.nk.y += a.y;
+                if (!eq) { const double2 b = H(PS, m, neg); f.sk.x += b.x; f.sk.y += b.y; }
+            }
+            if (nk != k)
+                for (int m = nk + j0 * n, q = j0; m <= L; m += J * n, q += J) {
+                    const bool neg = g.phi_half && (q & 1);
+                    const double2 a = H(PN, m, neg);
+                    f.nmk.x += a.x; f.nmk.y += a.y;
+                    if (!eq) { const double2 b = H(PS, m, neg); f.smk.x += b.x; f.smk.y += b.y; }
+                }
+        }
+        if (J > 1) {
+            if (live) red[tl] = f;
+            __syncthreads();
+            if (on && j0 == 0) {
+                for (int jj = 1; jj < J; ++jj) {
+                    const Fold4 o = red[tl + jj * K];
+                    f.nk.x += o.nk.x; f.nk.y += o.nk.y; f.nmk.x += o.nmk.x; f.nmk.y += o.nmk.y;
+                    f.sk.x += o.sk.x; f.sk.y += o.sk.y; f.smk.x += o.smk.x; f.smk.y += o.smk.y;
+                }
+            }
+            __syncthreads();
+        }
+        if (on && j0 == 0) {
+            if (g.phi_half) {
+                const double2 ek = expi_pi_u32(k, n);
+                const double2 enk = make_double2(-ek.x, ek.y);
+                f.nk = cmul(f.nk, ek);
+                f.sk = cmul(f.sk, ek);
+                f.nmk = cmul(f.nmk, enk);
+                f.smk = cmul(f.smk, enk);
+            }
+            if (nk == k) { f.nmk = f.nk; f.smk = f.sk; }
+            const double2 hn = make_double2(0.5 * (f.nk.x + f.nmk.x), 0.5 * (f.nk.y - f.nmk.y));
+            const double2 hs = make_double2(0.5 * (f.sk.x + f.smk.x), 0.5 * (f.sk.y - f.smk.y));
+            buf[k] = make_double2(hn.x - hs.y, hn.y + hs.x);
+            if (nk != k) {
+                const double2 hn2 = make_double2(hn.x, -hn.y), hs2 = make_double2(hs.x, -hs.y);
+                buf[nk] = make_double2(hn2.x - hs2.y, hn2.y + hs2.x);
+            }
+        }
+    }
+    __syncthreads();
+    dft_mc<NV>(lbuf, SB, nc, g, +1, twx, twM, bsk);
+    for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
+        const int c = jj / n, j = jj - c * n;
+        const double2 y = lbuf[c * SB + j];
+        double* mc = maps + (long long)(c0 + c) * npix;
+        mc[g.startN + j] = y.x;
+        if (!eq) mc[g.startS + j] = y.y;
+    }
+}
+
+// analysis: grid (ring pairs, component groups of NCB)
+template <int NV>
+__global__ __launch_bounds__(1024) void k_sht_anal_ring_mc(int L, int npair, long long npix,
+                                                           const int* __restrict__ pairs,
+                                                           const PairGeom* __restrict__ geom,
+                                                           const double* __restrict__ maps,
+                                                           const double2* __restrict__ tw, int Mmax,
+                                                           const double2* __restrict__ bsk, double2* __restrict__ phi,
+                                                           int ncomp, int NCB, int SB, int twoff,
+                                                           const double* __restrict__ wts, int wnc) {
+    extern __shared__ double2 lbuf[];
+    const int p = pairs[blockIdx.x];
+    const int c0 = blockIdx.y * NCB;
+    const int nc = min(NCB, ncomp - c0);
+    const PairGeom g = geom[p];
+    int twM = Mmax;
+    const double2* twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
+    const int n = g.nphi;
+    const bool eq = g.startS < 0;
+    for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
+        const int c = jj / n, j = jj - c * n;
+        const int comp = c0 + c;
+        const double* mc = maps + (long long)comp * npix;
+        const double* wc = wts ? wts + (long long)(comp % wnc) * npix : nullptr;
+        const long long iN = g.startN + j, iS = g.startS + j;
+        const double vn = wc ? wc[iN] * mc[iN] : mc[iN];
+        const double vs = eq ? 0.0 : (wc ? wc[iS] * mc[iS] : mc[iS]);
+        lbuf[c * SB + j] = make_double2(vn, vs);
+    }
+    __syncthreads();
+    dft_mc<NV>(lbuf, SB, nc, g, -1, twx, twM, bsk);
+    const long long plane = phi_plane(L, npair);
+    for (int jj = threadIdx.x; jj < nc * (L + 1); jj += blockDim.x) {
+        const int c = jj / (L + 1), m = jj - c * (L + 1);
+        const double2* buf = lbuf + c * SB;
+        double2* oN = phi + (2LL * (c0 + c) + 0) * plane;
+        double2* oS = oN + plane;
+        const int k = m % n;
+        const int nk = k == 0 ? 0 : n - k;
+        const double2 a = buf[k], b = buf[nk];
+        double2 xn = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+        double2 xs = make_double2(0.5 * (a.y + b.y), -0.5 * (a.x - b.x));
+        if (g.phi_half) {
+            const double2 e = expi_pi_neg_u32(m, n);
+            xn = cmul(xn, e);
+            xs = cmul(xs, e);
+        }
+        if (m == 0) { xn.y = 0.0; xs.y = 0.0; }
+        oN[phi_at(m, p, npair)] = xn;
+        oS[phi_at(m, p, npair)] = eq ? make_double2(0.0, 0.0) : xs;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // analysis: Legendre stage.  grid (m pairs or m, tiles of 4 ASR groups of 64 ring pairs)
 // out: part[tile][comp][nlm] (double2), unweighted sums
 //   T: sum lambda Phi_T ;  E: sum (Q F1 + i U F2) ;  B: sum (U F1 - i Q F2)
@@ -1728,7 +1987,8 @@ __global__ void k_sub_maps(long long n, const double* __restrict__ a, double* __
 // costs 3 x 8 B x N_ringpair x N_lm (1.6 GB at N_side 256 / l_max 512), so it
 // is built for small maps only (large maps keep the on-the-fly recurrence).
 // Blocks of 16 l x 16 ring pairs; blocks wholly below the representable range
-// of a (m, 16-pair tile) are not stored (b0); planes lambda, F1, F2.
+// of a (m, 16-pair tile) are not stored (b0); planes lambda, G+ (F1 at even
+// l - m, F2 at odd), G- (the other).
 constexpr int MF_TILE = 16;
 constexpr int MF_BLK = 3 * 256;                  // doubles per block (3 planes of 16 l x 16 pairs)
 
@@ -1798,12 +2058,28 @@ __global__ __launch_bounds__(256) void k_mf_fill(ShtDev D, const double* __restr
             }
         }
         if (b >= b0) {
+            // planes 1 / 2 = the function with lambda's parity ("+": F1 at even
+            // l - m, F2 at odd) and the other one ("-"), so the kernels' A
+            // operands need no per-lane select
             double* blk = out + (long long)(b - b0) * MF_BLK + r * MF_TILE + j;
+            const bool ev = (r & 1) == 0;
             blk[0] = lam;
-            blk[256] = f1;
-            blk[512] = f2;
+            blk[256] = ev ? f1 : f2;
+            blk[512] = ev ? f2 : f1;
         }
     }
+}
+
+// XCD-aware m order: blocks x, x + 8, x + 16, x + 24 of a grid row run on one
+// XCD (round-robin dispatch), so they take the 4 m of one PHI_MB block -- the
+// m that share every 128-B line of the phase planes meet in one L2 instead of
+// each XCD fetching (or writing back) the line for a quarter of it
+__device__ __forceinline__ int mf_m(int x, int L) {
+    static_assert(PHI_MB == 4, "mf_m groups 4 m per phase block");
+    const int full = (L + 1) / 32 * 32;
+    if (x >= full) return x;
+    const int slot = x >> 3;
+    return (slot >> 2) * 32 + (x & 7) * 4 + (slot & 3);
 }
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -1811,142 +2087,196 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// ---- synthesis: one wave per 16-pair tile, TPW tiles per workgroup ---------------
+// ---- synthesis: one wave per 16-pair tile, 4 tiles per workgroup ----------------
 // Spin 2 (E, B -> Q, U): per quad of l (l0 = m + 16 b + 4 q, l0 - m even) the
-// K entries of the "+" product are (l0, F1), (l0+1, F2), (l0+2, F1), (l0+3, F2)
-// and of the "-" product the other function at each l (F1 carries lambda's
-// parity, F2 the opposite one), so lane (g = lane / 16, j = lane % 16) holds A =
-// G(l0 + g, pair 16 t + j) and B = the a_lm row of (l0 + g, col j); col =
-// (map 4 cg + j / 4, part j % 4 = Q re, Q im, U re, U im):
+// "+" product takes G+ (F1 at even l - m, F2 at odd) and the "-" product G-,
+// so lane (g = lane / 16, j = lane % 16) holds A = G+-(l0 + g, pair 16 t + j)
+// and B = the matching a_lm row of (l0 + g, col j); col = (map 4 cg + j / 4,
+// part o = j % 4 = Q re, Q im, U re, U im):
 //   F1 row: (aE.x, aE.y, aB.x, aB.y)     F2 row: (-aB.y, aB.x, aE.y, -aE.x)
-// N = -(C+ + C-), S = -(C+ - C-).  Spin 0 (T): per octet the "+" K entries are
-// the even l (l0, l0+2, l0+4, l0+6) and the "-" the odd ones, lambda rows, col =
-// (map 8 cg + j / 2, re / im).  The a_lm of the workgroup's maps for MF_CH l are
-// staged in LDS (every tile of the m reads them).
+// N = -(C+ + C-), S = -(C+ - C-).  The rows are staged in LDS already permuted
+// ("+" row, "-" row per (l, map)), so the K loop is two LDS reads and two
+// MFMAs per quad and column group.  Spin 0 (T): per octet the "+" K entries
+// are the even l (l0, l0+2, l0+4, l0+6) and the "-" the odd ones, lambda rows,
+// col = (map 8 cg + j / 2, re / im).  The a_lm of the workgroup's maps for
+// MF_CH l are staged in LDS (every tile of the m reads them); the next chunk's
+// are loaded into registers while this chunk's MFMAs run, and each block's
+// table values are loaded one block ahead of their MFMAs.
+// GS_MF_EXP (timing experiments only, wrong results; default 0): bit 1 = table
+// loads from one cached block, bit 2 = no phase / a_lm global loads, bit 4 =
+// no barriers
+#ifndef GS_MF_EXP
+#define GS_MF_EXP 0
+#endif
+// optional occupancy targets (build-time A/B only: the default lets the
+// compiler keep every prefetched value in registers)
+#ifdef GS_MF_SYN_WPE
+#define GS_MF_SYN_ATTR __attribute__((amdgpu_waves_per_eu(GS_MF_SYN_WPE)))
+#else
+#define GS_MF_SYN_ATTR
+#endif
+#ifdef GS_MF_ANA_WPE
+#define GS_MF_ANA_ATTR __attribute__((amdgpu_waves_per_eu(GS_MF_ANA_WPE)))
+#else
+#define GS_MF_ANA_ATTR
+#endif
 constexpr int MF_CH = 32;                          // l staged per chunk (two blocks)
-// the staged a_lm of one chunk: every thread moves MF_SITEMS entries; the next
-// chunk's are loaded into registers while this chunk's MFMAs run (issued after
-// the chunk's table loads, so waiting for those never waits for them)
-template <int SPIN, int CGW>
-__global__ __launch_bounds__(256) void k_sht_synth_mfma(ShtDev D, MfTab T, const double2* __restrict__ ain,
+template <int SPIN, int CGW, int CPW>
+__global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_mfma(ShtDev D, MfTab T, const double2* __restrict__ ain,
                                                         double2* __restrict__ phi, int nmap, int ncm, int cbase) {
     constexpr int CPG = SPIN == 2 ? 4 : 8;         // maps per 16-column group
     constexpr int MPW = CGW * CPG;                 // maps per workgroup
-    constexpr int NCMP = SPIN == 2 ? 2 : 1;        // a_lm comps read
-    constexpr int NIT = MF_CH * MPW * NCMP;        // staged entries per chunk
-    constexpr int PER = (NIT + 255) / 256;         // per thread (block of 256)
-    __shared__ __attribute__((aligned(16))) double2 sa[MF_CH][MPW][NCMP];
-    const int L = D.L, npair = D.npair, nlm = D.nlm;
-    const int m = blockIdx.x;
+    constexpr int NIT = MF_CH * MPW;               // staged (l, map) items per chunk
+    constexpr int H = CGW / CPW;                   // waves per tile (column-group slices)
+    constexpr int NT = 256 * H;                    // 4 tiles per workgroup
+    constexpr int PER = (NIT + NT - 1) / NT;       // staged items per thread
+    constexpr int SW = SPIN == 2 ? 8 : 2;          // staged doubles per item
+    __shared__ __attribute__((aligned(16))) double sb[NIT * SW];
+    const int L = D.L, nlm = D.nlm, npair = D.npair;
+    const int m = mf_m(blockIdx.x, L);
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int t = blockIdx.y * (blockDim.x >> 6) + wave;
+    const int t = blockIdx.y * 4 + wave / H;
+    const int cg0 = (wave % H) * CPW;             // this wave's first column group
     const int c0 = blockIdx.z * MPW;
     const int nb = (L - m + MF_TILE) / MF_TILE;
     const long long ti = (long long)m * T.ntile + min(t, T.ntile - 1);
     const int b0 = t < T.ntile ? T.b0[ti] : nb;
     const double* tab = T.tab + (t < T.ntile ? T.off[ti] : 0) * MF_BLK;
     const long long base = cidx(L, m, m) - m;
-    auto fetch = [&](int cb, double2 (&pf)[PER]) {
+    // item i: l = chunk start + i % MF_CH, map c0 + i / MF_CH (consecutive
+    // threads read consecutive l of one map)
+    auto fetch = [&](int cb, double2 (&pf)[PER][SPIN == 2 ? 2 : 1]) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int i = threadIdx.x + 256 * k;
-            const int cc = i % NCMP, mp = (i / NCMP) % MPW, lr = i / (NCMP * MPW);
+            const int i = threadIdx.x + NT * k;
+            const int lr = i % MF_CH, mp = i / MF_CH;
             const int l = m + cb * MF_TILE + lr, c = c0 + mp;
-            pf[k] = (i < NIT && l <= L && c < nmap) ? ain[((long long)c * ncm + cbase + cc) * nlm + base + l]
-                                                    : make_double2(0.0, 0.0);
+            const bool ok = !(GS_MF_EXP & 2) && i < NIT && l <= L && c < nmap;
+            // clamped address: the load is unconditional, the value selected when
+            // staged (a select here would wait for the load)
+            const double2* src = ain + ((long long)(ok ? c : 0) * ncm + cbase) * nlm + base + (ok ? l : m);
+            pf[k][0] = src[0];
+            if constexpr (SPIN == 2) pf[k][1] = src[nlm];
         }
     };
-    f64x4 Cp[CGW], Cm[CGW];
-#pragma unroll
-    for (int c = 0; c < CGW; ++c) { Cp[c] = f64x4{0, 0, 0, 0}; Cm[c] = f64x4{0, 0, 0, 0}; }
-    double2 pf[PER];
-    fetch(0, pf);
-    const int o = j & 3;
-    const bool ox = o == 0 || o == 3;
-    for (int cb = 0; cb < nb; cb += MF_CH / MF_TILE) {
-        __syncthreads();                            // the previous chunk's readers are done
+    auto stage = [&](int cb, const double2 (&pf)[PER][SPIN == 2 ? 2 : 1]) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int i = threadIdx.x + 256 * k;
-            if (i < NIT) (&sa[0][0][0])[i] = pf[k];
-        }
-        __syncthreads();
-        const int bend = min(cb + MF_CH / MF_TILE, nb);
-        const int bst = max(cb, b0);
-        // this chunk's table values first (both blocks, every quad / octet) ...
-        constexpr int NQ = 2 * 4 * 2;               // blocks x quads x functions (spin 2); x octet halves (spin 0)
-        double gv[NQ];
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            const int b = cb + bb;
-            const bool ok = b >= bst && b < bend;
-            const double* blk = tab + (long long)(ok ? b - b0 : 0) * MF_BLK;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if constexpr (SPIN == 2) {
-                    const int row = 4 * q + g;
-                    gv[(bb * 4 + q) * 2 + 0] = ok ? blk[256 + row * MF_TILE + j] : 0.0;
-                    gv[(bb * 4 + q) * 2 + 1] = ok ? blk[512 + row * MF_TILE + j] : 0.0;
-                } else {
-                    // q = 2 h + e: octet half h, even (e = 0) / odd row of lambda
-                    const int row = 8 * (q >> 1) + 2 * g + (q & 1);
-                    gv[(bb * 4 + q) * 2 + 0] = ok ? blk[row * MF_TILE + j] : 0.0;
-                    gv[(bb * 4 + q) * 2 + 1] = 0.0;
-                }
-            }
-        }
-        // ... then the next chunk's a_lm (their wait is the next iteration's)
-        if (cb + MF_CH / MF_TILE < nb) fetch(cb + MF_CH / MF_TILE, pf);
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            const int b = cb + bb;
-            if (b < bst || b >= bend) continue;     // wave-uniform
-            const int lr0 = bb * MF_TILE;
+            const int i = threadIdx.x + NT * k;
+            if (i >= NIT) continue;
+            const int lr = i % MF_CH, mp = i / MF_CH;
+            const bool ok = m + cb * MF_TILE + lr <= L && c0 + mp < nmap;
             if constexpr (SPIN == 2) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int row = 4 * q + g;
-                    const double f1 = gv[(bb * 4 + q) * 2 + 0], f2 = gv[(bb * 4 + q) * 2 + 1];
-                    const bool ev = (g & 1) == 0;
-                    const double ap = ev ? f1 : f2, am = ev ? f2 : f1;
-#pragma unroll
-                    for (int c = 0; c < CGW; ++c) {
-                        const int mp = c * 4 + (j >> 2);
-                        const double* e = reinterpret_cast<const double*>(&sa[lr0 + row][mp][0]);
-                        const double* bb2 = reinterpret_cast<const double*>(&sa[lr0 + row][mp][1]);
-                        // E part: x for Q re / U im cols (o 0, 3), y otherwise; B part the other
-                        const double ev_ = e[ox ? 0 : 1], bv = bb2[ox ? 1 : 0];
-                        // F1 row (aE.x, aE.y, aB.x, aB.y), F2 row (-aB.y, aB.x, aE.y, -aE.x)
-                        const double r1 = o < 2 ? ev_ : bv;
-                        const double r2 = (o == 0 || o == 3) ? -(o == 0 ? bv : ev_) : (o == 1 ? bv : ev_);
-                        Cp[c] = mfma64(ap, ev ? r1 : r2, Cp[c]);
-                        Cm[c] = mfma64(am, ev ? r2 : r1, Cm[c]);
-                    }
-                }
+                const double ex = ok ? pf[k][0].x : 0.0, ey = ok ? pf[k][0].y : 0.0;
+                const double bx = ok ? pf[k][1].x : 0.0, by = ok ? pf[k][1].y : 0.0;
+                // F1 row (ex, ey, bx, by), F2 row (-by, bx, ey, -ex); "+" = F1 at even l - m
+                const bool ev = (lr & 1) == 0;     // l - m parity (chunks start at even l - m)
+                double2* P = reinterpret_cast<double2*>(sb + ((lr * 2 + 0) * MPW + mp) * 4);
+                double2* M = reinterpret_cast<double2*>(sb + ((lr * 2 + 1) * MPW + mp) * 4);
+                P[0] = make_double2(ev ? ex : -by, ev ? ey : bx);
+                P[1] = make_double2(ev ? bx : ey, ev ? by : -ex);
+                M[0] = make_double2(ev ? -by : ex, ev ? bx : ey);
+                M[1] = make_double2(ev ? ey : bx, ev ? -ex : by);
             } else {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int re = 8 * h + 2 * g, ro = re + 1;
-                    const double ap = gv[(bb * 4 + 2 * h) * 2], am = gv[(bb * 4 + 2 * h + 1) * 2];
-#pragma unroll
-                    for (int c = 0; c < CGW; ++c) {
-                        const int mp = c * 8 + (j >> 1);
-                        const double* ae = reinterpret_cast<const double*>(&sa[lr0 + re][mp][0]);
-                        const double* ao = reinterpret_cast<const double*>(&sa[lr0 + ro][mp][0]);
-                        Cp[c] = mfma64(ap, ae[j & 1], Cp[c]);
-                        Cm[c] = mfma64(am, ao[j & 1], Cm[c]);
-                    }
-                }
+                reinterpret_cast<double2*>(sb)[lr * MPW + mp] =
+                    make_double2(ok ? pf[k][0].x : 0.0, ok ? pf[k][0].y : 0.0);
             }
         }
+    };
+    // block b's table (a block outside [b0, nb) reads the table's first block
+    // instead -- always valid, never multiplied: mma skips it), so the loads
+    // carry no condition (a conditional load would make the compiler wait on
+    // the older loads at the join, the a_lm prefetch among them)
+    auto tblk = [&](int b) __attribute__((always_inline)) -> const double* {
+        const bool ok = b >= b0 && b < nb && !(GS_MF_EXP & 1);
+        return ok ? tab + (long long)(b - b0) * MF_BLK : T.tab;
+    };
+    // the table values of quad / octet-half q of a block
+    auto tload = [&](const double* blk, int q, double (&gv)[8]) __attribute__((always_inline)) {
+        if constexpr (SPIN == 2) {
+            const int row = 4 * q + g;
+            gv[2 * q + 0] = blk[256 + row * MF_TILE + j];
+            gv[2 * q + 1] = blk[512 + row * MF_TILE + j];
+        } else {
+            // q = 2 h + e: octet half h, even (e = 0) / odd row of lambda
+            const int row = 8 * (q >> 1) + 2 * g + (q & 1);
+            gv[q] = blk[row * MF_TILE + j];
+        }
+    };
+    f64x4 Cp[CPW], Cm[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) { Cp[c] = f64x4{0, 0, 0, 0}; Cm[c] = f64x4{0, 0, 0, 0}; }
+    const int o = j & 3;
+    // the staged B operands of quad / octet-half q (rows lr0 + ..): "+" and "-"
+    // per column group
+    // the lane's base in the staged rows; everything else is a compile-time
+    // offset (the ds_read immediate), so no per-read address registers
+    const double* sbl = SPIN == 2 ? sb + ((g * 2 * MPW) + cg0 * 4 + (j >> 2)) * 4 + o
+                                  : sb + ((2 * g * MPW) + cg0 * 8 + (j >> 1)) * 2 + (j & 1);
+    auto lds = [&](int lr0, int q, double (&bq)[2 * CPW]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+            if constexpr (SPIN == 2) {
+                const int r0 = lr0 + 4 * q;         // row = r0 + g
+                bq[2 * c + 0] = sbl[((r0 * 2 + 0) * MPW + c * 4) * 4];
+                bq[2 * c + 1] = sbl[((r0 * 2 + 1) * MPW + c * 4) * 4];
+            } else {
+                const int r0 = lr0 + 8 * q;         // even row = r0 + 2 g
+                bq[2 * c + 0] = sbl[(r0 * MPW + c * 8) * 2];
+                bq[2 * c + 1] = sbl[((r0 + 1) * MPW + c * 8) * 2];
+            }
+        }
+    };
+    // block b's MFMAs (staged rows lr0 ..): each quad's B operands read one quad
+    // ahead, its table registers refilled with block b + 1's values as soon as
+    // they are consumed (a block of MFMAs ahead of their use)
+    auto mma = [&](int b, int lr0, double (&gv)[8]) __attribute__((always_inline)) {
+        const double* nblk = tblk(b + 1);
+        if (b >= b0 && b < nb) {                    // wave-uniform; one straight-line body per block
+            constexpr int NQ = SPIN == 2 ? 4 : 2;
+            double bq[2][2 * CPW];                  // two rolling buffers
+            lds(lr0, 0, bq[0]);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (q + 1 < NQ) lds(lr0, q + 1, bq[(q + 1) & 1]);
+                // keep the order as written: the compiler's scheduler would sink the
+                // next quad's reads and the table refills behind the MFMAs
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int c = 0; c < CPW; ++c) {
+                    Cp[c] = mfma64(gv[2 * q], bq[q & 1][2 * c + 0], Cp[c]);
+                    Cm[c] = mfma64(gv[2 * q + 1], bq[q & 1][2 * c + 1], Cm[c]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (SPIN == 2) tload(nblk, q, gv);
+                else { tload(nblk, 2 * q, gv); tload(nblk, 2 * q + 1, gv); }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tload(nblk, q, gv);
+        }
+    };
+    double2 pf[PER][SPIN == 2 ? 2 : 1];
+    double gv[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tload(tblk(0), q, gv);
+    fetch(0, pf);
+    for (int cb = 0; cb < nb; cb += MF_CH / MF_TILE) {
+        if (!(GS_MF_EXP & 4)) __syncthreads();      // the previous chunk's readers are done
+        stage(cb, pf);
+        if (!(GS_MF_EXP & 4)) __syncthreads();
+        if (cb + MF_CH / MF_TILE < nb) fetch(cb + MF_CH / MF_TILE, pf);
+        mma(cb, 0, gv);
+        mma(cb + 1, MF_TILE, gv);
     }
     if (t >= T.ntile) return;
     // D layout: lane (g, j) holds rows g + 4 r (pairs 16 t + g + 4 r), col j
     const long long plane = phi_plane(L, npair);
 #pragma unroll
-    for (int c = 0; c < CGW; ++c) {
-        const int mp = SPIN == 2 ? c * 4 + (j >> 2) : c * 8 + (j >> 1);
+    for (int c = 0; c < CPW; ++c) {
+        const int mp = SPIN == 2 ? (cg0 + c) * 4 + (j >> 2) : (cg0 + c) * 8 + (j >> 1);
         const int map = c0 + mp;
         if (map >= nmap) continue;
         const int comp = SPIN == 2 ? cbase + ((j & 3) >> 1) : cbase;
@@ -1979,23 +2309,30 @@ __global__ __launch_bounds__(256) void k_sht_synth_mfma(ShtDev D, MfTab T, const
 // are summed inside the accumulator in tile order (no cross-workgroup
 // reduction); the weight (spin 0: w, spin 2: -w) and the caller's layout are
 // applied on the store.
-template <int SPIN, int CGW>
-__global__ __launch_bounds__(512) void k_sht_anal_mfma(ShtDev D, MfTab T, const double2* __restrict__ phi, int nmap,
+template <int SPIN, int CGW, int CPW, int NT>
+__global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, MfTab T, const double2* __restrict__ phi, int nmap,
                                                        int ncm, int cbase, double w, int layout, int acc,
                                                        double* __restrict__ alm) {
     constexpr int CPG = SPIN == 2 ? 4 : 8;
     constexpr int MPW = CGW * CPG;
     constexpr int NV = SPIN == 2 ? 8 : 4;          // staged doubles per (pair, map)
     constexpr int NIT = MF_TILE * MPW;             // staged (pair, map) items per tile
-    constexpr int PER = (NIT + 511) / 512;
-    __shared__ __attribute__((aligned(16))) double sp[MF_TILE][MPW][NV];
+    constexpr int PER = (NIT + NT - 1) / NT;
+    // rows padded by 16 B: the staging writes (consecutive threads =
+    // consecutive pairs = rows) spread over the banks
+    constexpr int RW = MPW * NV + 2;
+    __shared__ __attribute__((aligned(16))) double sp_[MF_TILE * RW];
+    auto sp = [&](int jp, int mp) __attribute__((always_inline)) -> double* { return sp_ + jp * RW + mp * NV; };
     const int L = D.L, npair = D.npair;
-    const int m = blockIdx.x;
+    const int m = mf_m(blockIdx.x, L);
     // workgroups whose first window starts past L leave before any barrier
-    if (m + 32 * (int)(blockIdx.y * (blockDim.x >> 6)) > L) return;
+    constexpr int H = CGW / CPW;                   // waves per window (column-group slices)
+    constexpr int WPG = NT / 64 / H;               // windows per workgroup
+    if (m + 32 * (int)(blockIdx.y * WPG) > L) return;
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int win = blockIdx.y * (blockDim.x >> 6) + wave;
+    const int win = blockIdx.y * WPG + wave / H;
+    const int cg0 = (wave % H) * CPW;             // this wave's first column group
     const int lw = m + 32 * win;
     const bool live = lw <= L;
     const int c0 = blockIdx.z * MPW;
@@ -2004,15 +2341,15 @@ __global__ __launch_bounds__(512) void k_sht_anal_mfma(ShtDev D, MfTab T, const 
     const long long plane = phi_plane(L, npair);
     // the staged item of thread (k): N, S phases of (pair, map) -> registers
     struct Ph { double2 a, b, c, d; };
-    auto fetch = [&](int t, Ph (&pf)[PER]) {
+    auto fetch = [&](int t, Ph (&pf)[PER]) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int i = threadIdx.x + 512 * k;
-            const int mp = i % MPW, jp = i / MPW;
+            const int i = threadIdx.x + NT * k;
+            const int jp = i % MF_TILE, mp = i / MF_TILE;     // lanes: consecutive pairs of one map
             const int pr = MF_TILE * t + jp, map = c0 + mp;
             const double2 z = make_double2(0.0, 0.0);
             pf[k] = Ph{z, z, z, z};
-            if (i < NIT && pr < npair && map < nmap) {
+            if (!(GS_MF_EXP & 2) && i < NIT && pr < npair && map < nmap) {
                 const long long off = phi_at(m, pr, npair);
                 const double2* P = phi + ((long long)map * ncm + cbase) * 2 * plane;
                 pf[k].a = P[off];
@@ -2024,20 +2361,48 @@ __global__ __launch_bounds__(512) void k_sht_anal_mfma(ShtDev D, MfTab T, const 
             }
         }
     };
-    f64x4 C[CGW][2];
+    f64x4 C[CPW][2];
 #pragma unroll
-    for (int c = 0; c < CGW; ++c) { C[c][0] = f64x4{0, 0, 0, 0}; C[c][1] = f64x4{0, 0, 0, 0}; }
-    Ph pf[PER];
-    fetch(0, pf);
+    for (int c = 0; c < CPW; ++c) { C[c][0] = f64x4{0, 0, 0, 0}; C[c][1] = f64x4{0, 0, 0, 0}; }
     const int o = j & 3;
     const double s2 = (o == 0 || o == 3) ? -1.0 : 1.0;
-    for (int t = 0; t < T.ntile; ++t) {
-        __syncthreads();
+    constexpr int NF = SPIN == 2 ? 2 : 1;
+    // the lane's bases in the staged phases (row jp = 4 s + g, map (cg0 + c) ..):
+    // spin 2 component o (a1) and 3 - o (a2), spin 0 re / im
+    const double* spo = SPIN == 2 ? sp_ + g * RW + (cg0 * 4 + (j >> 2)) * NV + o
+                                  : sp_ + g * RW + (cg0 * 8 + (j >> 1)) * NV + (j & 1);
+    const double* spr = sp_ + g * RW + (cg0 * 4 + (j >> 2)) * NV + 3 - o;
+    // tile t's window: false if it lies wholly below the tile's onset; bj / okb
+    // the lane's block and whether it is stored
+    struct Tw { const double* blk; bool any, okb; };
+    auto twin = [&](int t) __attribute__((always_inline)) -> Tw {
+        const long long ti = (long long)m * T.ntile + t;
+        const int b0 = T.b0[ti];
+        const bool any = live && bw + 1 >= b0 && bw < nb;    // wave-uniform
+        const int bj = bw + (j >> 3);
+        const bool okb = any && bj >= b0 && bj < nb;
+        return Tw{okb ? T.tab + (T.off[ti] + bj - b0) * MF_BLK : T.tab, any, okb};
+    };
+    // the table values of column slice s (pairs 4 s + g) of a tile, rows of
+    // parity p (l = lw + 2 j' + p); planes G+ / G-.  Unconditional loads (a lane
+    // whose block is not stored reads the first block; its values are zeroed
+    // where they are multiplied)
+    auto tload = [&](const Tw& w, int s, double (&gv)[4][2][NF]) __attribute__((always_inline)) {
+        const double* bp = (GS_MF_EXP & 1) ? T.tab : w.blk;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int row = 2 * (j & 7) + p;
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                gv[s][p][f] = bp[(SPIN == 2 ? 256 * (f + 1) : 0) + row * MF_TILE + 4 * s + g];
+        }
+    };
+    auto stage = [&](const Ph (&pf)[PER]) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int i = threadIdx.x + 512 * k;
+            const int i = threadIdx.x + NT * k;
             if (i >= NIT) continue;
-            double* dst = sp[i / MPW][i % MPW];
+            double* dst = sp(i % MF_TILE, i / MF_TILE);
             const Ph& q = pf[k];
             if constexpr (SPIN == 2) {          // a = Q north, b = Q south, c = U north, d = U south
                 dst[0] = q.a.x + q.b.x; dst[1] = q.a.y + q.b.y; dst[2] = q.c.x + q.d.x; dst[3] = q.c.y + q.d.y;
@@ -2046,49 +2411,71 @@ __global__ __launch_bounds__(512) void k_sht_anal_mfma(ShtDev D, MfTab T, const 
                 dst[0] = q.a.x + q.b.x; dst[1] = q.a.y + q.b.y; dst[2] = q.a.x - q.b.x; dst[3] = q.a.y - q.b.y;
             }
         }
-        __syncthreads();
-        // this tile's table values first ...
-        const long long ti = (long long)m * T.ntile + t;
-        const int b0 = T.b0[ti];
-        const bool any = live && bw + 1 >= b0 && bw < nb;    // wave-uniform
-        const int bj = bw + (j >> 3);
-        const bool okb = any && bj >= b0 && bj < nb;
-        const double* blk = T.tab + (T.off[ti] + (okb ? bj - b0 : 0)) * MF_BLK;
-        constexpr int NF = SPIN == 2 ? 2 : 1;
-        double gv[4][2][NF];
+    };
+    Ph pf[PER];
+    double gv[4][2][NF];
+    Tw cur = twin(0);
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 4; ++s) tload(cur, s, gv);
+    fetch(0, pf);
+    // tile t: stage its phases, issue tile t + 1's phases, then t's MFMAs; each
+    // slice's table registers are refilled with tile t + 1's values as soon as
+    // its MFMAs are issued (their latency hides behind the rest of the tile)
+    for (int t = 0; t < T.ntile; ++t) {
+        if (!(GS_MF_EXP & 4)) __syncthreads();
+        stage(pf);
+        if (!(GS_MF_EXP & 4)) __syncthreads();
+        const bool more = t + 1 < T.ntile;
+        if (more) fetch(t + 1, pf);
+        const Tw nxt = twin(more ? t + 1 : t);
+        if (cur.any) {                              // wave-uniform; one straight-line body per tile
+            // A operands of slice s (a1 / a2 per parity and column group), read one
+            // slice ahead of their MFMAs
+            double aq[2][2][CPW][NF];
+            auto ldsA = [&](int s, double (&a)[2][CPW][NF]) __attribute__((always_inline)) {
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const int row = 2 * (j & 7) + p;
+                for (int p = 0; p < 2; ++p)
 #pragma unroll
-                for (int f = 0; f < NF; ++f)
-                    gv[s][p][f] = okb ? blk[(SPIN == 2 ? 256 * (f + 1) : 0) + row * MF_TILE + 4 * s + g] : 0.0;
-            }
-        // ... then the next tile's phases (their wait is the next iteration's)
-        if (t + 1 < T.ntile) fetch(t + 1, pf);
-        if (!any) continue;
+                    for (int c = 0; c < CPW; ++c) {
+                        if constexpr (SPIN == 2) {
+                            a[p][c][0] = spo[s * 4 * RW + c * 4 * NV + 4 * p];
+                            a[p][c][1] = s2 * spr[s * 4 * RW + c * 4 * NV + 4 * (1 - p)];
+                        } else {
+                            a[p][c][0] = spo[s * 4 * RW + c * 8 * NV + 2 * p];
+                        }
+                    }
+            };
+            ldsA(0, aq[0]);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int jp = 4 * s + g;
+            for (int s = 0; s < 4; ++s) {
+                if (s + 1 < 4) ldsA(s + 1, aq[(s + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
+                for (int p = 0; p < 2; ++p) {
+                    double gz[NF];
 #pragma unroll
-                for (int c = 0; c < CGW; ++c) {
-                    if constexpr (SPIN == 2) {
-                        const double* v = sp[jp][c * 4 + (j >> 2)];
-                        // F1 takes the parity-p combination (p = 0: +, 1: -), F2 the other
-                        const double a1 = v[4 * p + o];
-                        const double a2 = s2 * v[4 * (1 - p) + 3 - o];
-                        C[c][p] = mfma64(a1, gv[s][p][0], C[c][p]);
-                        C[c][p] = mfma64(a2, gv[s][p][NF - 1], C[c][p]);
-                    } else {
-                        const double* v = sp[jp][c * 8 + (j >> 1)];
-                        C[c][p] = mfma64(v[2 * p + (j & 1)], gv[s][p][0], C[c][p]);
+                    for (int f = 0; f < NF; ++f) gz[f] = cur.okb ? gv[s][p][f] : 0.0;
+#pragma unroll
+                    for (int c = 0; c < CPW; ++c) {
+                        // F1 takes the parity-p combination (p = 0: +, 1: -), F2 the
+                        // other; F1 is plane G+ on even rows (p = 0), G- on odd
+                        if constexpr (SPIN == 2) {
+                            C[c][p] = mfma64(aq[s & 1][p][c][0], gz[p], C[c][p]);
+                            C[c][p] = mfma64(aq[s & 1][p][c][1], gz[1 - p], C[c][p]);
+                        } else {
+                            C[c][p] = mfma64(aq[s & 1][p][c][0], gz[0], C[c][p]);
+                        }
                     }
                 }
+                __builtin_amdgcn_sched_barrier(0);
+                tload(nxt, s, gv);                  // (the last tile reloads its own: harmless)
+                __builtin_amdgcn_sched_barrier(0);
             }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) tload(nxt, s, gv);
         }
+        cur = nxt;
     }
     if (!live) return;
     // D layout: lane (g, j) holds rows g + 4 r = col index, col j = l index:
@@ -2102,11 +2489,11 @@ __global__ __launch_bounds__(512) void k_sht_anal_mfma(ShtDev D, MfTab T, const 
         if (l > L) continue;
         const long long ic = cidx(L, l, m);
 #pragma unroll
-        for (int c = 0; c < CGW; ++c) {
+        for (int c = 0; c < CPW; ++c) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = g + 4 * r;
-                const int map = SPIN == 2 ? c0 + c * 4 + r : c0 + c * 8 + row / 2;
+                const int map = SPIN == 2 ? c0 + (cg0 + c) * 4 + r : c0 + (cg0 + c) * 8 + row / 2;
                 const int comp = SPIN == 2 ? cbase + (g >> 1) : cbase;
                 const int part = SPIN == 2 ? (g & 1) : (row & 1);
                 if (map >= nmap) continue;
@@ -2472,6 +2859,9 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       LDS_FFT_MAX * (int)sizeof(double2) + 64 * 4 * (int)sizeof(double2));
+        const void* mc[] = {(const void*)k_sht_synth_ring_mc<8>, (const void*)k_sht_anal_ring_mc<8>};
+        for (const void* f : mc)
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RING_MC_LDS_MAX);
         (void)hipGetLastError();
     }
     hipLaunchKernelGGL(k_sht_twiddles, dim3(nblocks(Mmax / 2, 256)), dim3(256), 0, 0, Mmax, p->tw);
@@ -2581,6 +2971,23 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
 // stream while the largest class runs on the caller's.
 // ncomp = every comp of the batch (maps b * wnc + c, contiguous); wts: wnc weight
 // maps shared by the batch's maps
+// components per ring workgroup in the merged launch (GS_SHT_RING_NC, default
+// 2 -- measured at N_side 256, 16 spin-2 maps: 1 / 2 / 4 = 401 / 326 / 358 us
+// synthesis ring stage; 1 = one component per workgroup, the k_sht_*_ring kernels): bounded by
+// the LDS (NCB buffers of the longest FFT + its twiddles) and by 1024 threads
+// at ring_block(M) threads (<= 8 values each) per component
+static int ring_mc_ncb(int M, int ncomp) {
+    static const int want = [] {
+        const char* e = getenv("GS_SHT_RING_NC");
+        return e ? std::max(1, atoi(e)) : 2;
+    }();
+    int ncb = std::min(want, ncomp);
+    ncb = std::min(ncb, 1024 / ring_block(M));
+    const int SB = std::max(M, 4 * ring_block(M));
+    while (ncb > 1 && (size_t)(ncb * SB + M / 2) * sizeof(double2) > (size_t)RING_MC_LDS_MAX) --ncb;
+    return ncb;
+}
+
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
                      const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1, const double* wts = nullptr,
                      int wnc = 3) {
@@ -2589,12 +2996,31 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
         // (shorter rings leave threads idle; their fold reduction uses the
         // J = block / K aliases per bin pair, as a short-ring class does)
         const int M = p->merged_M, bd = ring_block(M);
+        const double2* ph = phi ? phi : p->phi;
+        const int ncb = comp_lmax ? 1 : ring_mc_ncb(M, ncomp);
+        if (ncb > 1) {
+            // ring_block(M) threads per component, as the one-component kernels (the
+            // fold's alias split J, hence its summation order, is the same)
+            // (a component's buffer also holds its fold reduction: 4 per thread)
+            const int bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
+            const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
+            const dim3 gm(p->merged_n, (ncomp + ncb - 1) / ncb);
+            if (synth)
+                hipLaunchKernelGGL(k_sht_synth_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
+                                   p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, maps_out, ncomp, ncb, SB,
+                                   toff);
+            else
+                hipLaunchKernelGGL(k_sht_anal_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
+                                   p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, p->phi, ncomp, ncb, SB,
+                                   toff, wts, wnc);
+            GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring_mc" : "k_sht_anal_ring_mc");
+            return 0;
+        }
         const bool nb8 = M / 2 > 4 * bd;
         size_t lds = 0;
         int twoff = -1;
         ring_lds(M, bd, false, true, lds, twoff);
         const dim3 grid(p->merged_n, ncomp);
-        const double2* ph = phi ? phi : p->phi;
         if (synth) {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
@@ -2682,42 +3108,75 @@ static int sht_reserve(gs_sht* p, int nmap, hipStream_t st) {
 // ---- the matrix-core Legendre stage (plans with mf set) --------------------------
 constexpr int MF_CGW = 4;         // 16-column groups per workgroup (16 maps spin 2, 32 spin 0)
 
-static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
+// launch shapes (speed only; every shape gives the same bits): column groups
+// per wave in the synthesis (GS_SHT_MFS_CPW 4 / 2) and the analysis
+// (GS_SHT_MFA_CPW 4 / 2), analysis workgroup size (GS_SHT_MFA_NT 256 / 512).
+// Measured (N_side 256, 16 spin-2 maps, rocprofv3 averages): synthesis CPW 4 /
+// 2 = 580 / 597 us; analysis (CPW, NT) (4, 512) / (4, 256) / (2, 256) / (2,
+// 512) = 819 / 966 / 957 / 1090 us
+static int mf_env(const char* name, int a, int b, int dflt) {
+    const char* e = getenv(name);
+    if (!e) return dflt;
+    const int v = atoi(e);
+    return v == a || v == b ? v : dflt;
+}
+static int mfs_cpw() { static const int v = mf_env("GS_SHT_MFS_CPW", 2, 4, 4); return v; }
+static int mfa_cpw() { static const int v = mf_env("GS_SHT_MFA_CPW", 2, 4, 4); return v; }
+static int mfa_nt() { static const int v = mf_env("GS_SHT_MFA_NT", 256, 512, 512); return v; }
+
+extern "C++" {
+template <int CPW>
+static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
     const ShtDev D = p->dev();
     const MfTab T = p->mftab();
     const unsigned ty = (unsigned)((p->mf_ntile + 3) / 4);
+    const dim3 blk(256 * (MF_CGW / CPW));
     if (ncomp != 2) {               // T (spin 0): comp 0
         const dim3 g(p->L + 1, ty, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
-        hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW>), g, dim3(256), 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0);
-        GS_LAUNCH_CHECK("k_sht_synth_mfma<0>");
+        hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0);
     }
     if (ncomp != 1) {               // E, B -> Q, U: comps ncomp - 2, ncomp - 1
         const dim3 g(p->L + 1, ty, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
-        hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW>), g, dim3(256), 0, st, D, T, p->ain, p->phi, nmap, ncomp,
+        hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp,
                            ncomp - 2);
-        GS_LAUNCH_CHECK("k_sht_synth_mfma<2>");
     }
+}
+
+template <int CPW, int NT>
+static void sht_anal_mfma_v(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st) {
+    const ShtDev D = p->dev();
+    const MfTab T = p->mftab();
+    const double w = 4.0 * PI / (double)p->npix;
+    constexpr int WPG = NT / 64 / (MF_CGW / CPW);    // windows per workgroup
+    const int nwin = (p->L + 1 + 31) / 32;           // 32-l windows of m = 0
+    const unsigned ty = (unsigned)((nwin + WPG - 1) / WPG);
+    if (ncomp != 2) {
+        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
+        hipLaunchKernelGGL((k_sht_anal_mfma<0, MF_CGW, CPW, NT>), g, dim3(NT), 0, st, D, T, p->phi, nmap, ncomp, 0, w,
+                           layout, acc, alm);
+    }
+    if (ncomp != 1) {
+        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
+        hipLaunchKernelGGL((k_sht_anal_mfma<2, MF_CGW, CPW, NT>), g, dim3(NT), 0, st, D, T, p->phi, nmap, ncomp,
+                           ncomp - 2, w, layout, acc, alm);
+    }
+}
+}  // extern "C++"
+
+static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
+    if (mfs_cpw() == 2) sht_synth_mfma_v<2>(p, nmap, ncomp, st);
+    else sht_synth_mfma_v<4>(p, nmap, ncomp, st);
+    GS_LAUNCH_CHECK("k_sht_synth_mfma");
     return 0;
 }
 
 static int sht_anal_mfma(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st) {
-    const ShtDev D = p->dev();
-    const MfTab T = p->mftab();
-    const double w = 4.0 * PI / (double)p->npix;
-    const int nwin = (p->L + 1 + 31) / 32;          // 32-l windows of m = 0
-    const unsigned ty = (unsigned)((nwin + 7) / 8);  // 8 windows (waves) per workgroup
-    if (ncomp != 2) {
-        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
-        hipLaunchKernelGGL((k_sht_anal_mfma<0, MF_CGW>), g, dim3(512), 0, st, D, T, p->phi, nmap, ncomp, 0, w, layout,
-                           acc, alm);
-        GS_LAUNCH_CHECK("k_sht_anal_mfma<0>");
-    }
-    if (ncomp != 1) {
-        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
-        hipLaunchKernelGGL((k_sht_anal_mfma<2, MF_CGW>), g, dim3(512), 0, st, D, T, p->phi, nmap, ncomp, ncomp - 2, w,
-                           layout, acc, alm);
-        GS_LAUNCH_CHECK("k_sht_anal_mfma<2>");
-    }
+    const int cpw = mfa_cpw(), nt = mfa_nt();
+    if (cpw == 2 && nt == 512) sht_anal_mfma_v<2, 512>(p, nmap, ncomp, layout, acc, alm, st);
+    else if (cpw == 2) sht_anal_mfma_v<2, 256>(p, nmap, ncomp, layout, acc, alm, st);
+    else if (nt == 512) sht_anal_mfma_v<4, 512>(p, nmap, ncomp, layout, acc, alm, st);
+    else sht_anal_mfma_v<4, 256>(p, nmap, ncomp, layout, acc, alm, st);
+    GS_LAUNCH_CHECK("k_sht_anal_mfma");
     return 0;
 }
 
