@@ -2070,18 +2070,6 @@ __global__ __launch_bounds__(256) void k_mf_fill(ShtDev D, const double* __restr
     }
 }
 
-// XCD-aware m order: blocks x, x + 8, x + 16, x + 24 of a grid row run on one
-// XCD (round-robin dispatch), so they take the 4 m of one PHI_MB block -- the
-// m that share every 128-B line of the phase planes meet in one L2 instead of
-// each XCD fetching (or writing back) the line for a quarter of it
-__device__ __forceinline__ int mf_m(int x, int L) {
-    static_assert(PHI_MB == 4, "mf_m groups 4 m per phase block");
-    const int full = (L + 1) / 32 * 32;
-    if (x >= full) return x;
-    const int slot = x >> 3;
-    return (slot >> 2) * 32 + (x & 7) * 4 + (slot & 3);
-}
-
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -2133,10 +2121,14 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     constexpr int SW = SPIN == 2 ? 8 : 2;          // staged doubles per item
     __shared__ __attribute__((aligned(16))) double sb[NIT * SW];
     const int L = D.L, nlm = D.nlm, npair = D.npair;
-    const int m = mf_m(blockIdx.x, L);
+    // grid (tile group, m, map group): the 8 tile groups of one m are
+    // consecutive blocks -- one per XCD, at the same time, so m's a_lm come
+    // from HBM once (the other XCDs hit the infinity cache) -- and the 4 m of a
+    // phase block written by one tile group all land on that tile group's XCD
+    const int m = blockIdx.y;
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int t = blockIdx.y * 4 + wave / H;
+    const int t = blockIdx.x * 4 + wave / H;
     const int cg0 = (wave % H) * CPW;             // this wave's first column group
     const int c0 = blockIdx.z * MPW;
     const int nb = (L - m + MF_TILE) / MF_TILE;
@@ -2233,29 +2225,30 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // they are consumed (a block of MFMAs ahead of their use)
     auto mma = [&](int b, int lr0, double (&gv)[8]) __attribute__((always_inline)) {
         const double* nblk = tblk(b + 1);
-        if (b >= b0 && b < nb) {                    // wave-uniform; one straight-line body per block
-            constexpr int NQ = SPIN == 2 ? 4 : 2;
-            double bq[2][2 * CPW];                  // two rolling buffers
-            lds(lr0, 0, bq[0]);
+        // every load unconditional (a load in one arm of a branch makes the
+        // compiler's wait at the join cover the other arm's registers too); only
+        // the MFMAs sit under the wave-uniform block test
+        const bool on = b >= b0 && b < nb;
+        constexpr int NQ = SPIN == 2 ? 4 : 2;
+        double bq[2][2 * CPW];                      // two rolling buffers
+        lds(lr0, 0, bq[0]);
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                if (q + 1 < NQ) lds(lr0, q + 1, bq[(q + 1) & 1]);
-                // keep the order as written: the compiler's scheduler would sink the
-                // next quad's reads and the table refills behind the MFMAs
-                __builtin_amdgcn_sched_barrier(0);
+        for (int q = 0; q < NQ; ++q) {
+            if (q + 1 < NQ) lds(lr0, q + 1, bq[(q + 1) & 1]);
+            // keep the order as written: the scheduler would sink the next
+            // quad's reads and the table refills behind the MFMAs
+            __builtin_amdgcn_sched_barrier(0);
+            if (on) {
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
                     Cp[c] = mfma64(gv[2 * q], bq[q & 1][2 * c + 0], Cp[c]);
                     Cm[c] = mfma64(gv[2 * q + 1], bq[q & 1][2 * c + 1], Cm[c]);
                 }
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (SPIN == 2) tload(nblk, q, gv);
-                else { tload(nblk, 2 * q, gv); tload(nblk, 2 * q + 1, gv); }
-                __builtin_amdgcn_sched_barrier(0);
             }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tload(nblk, q, gv);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (SPIN == 2) tload(nblk, q, gv);
+            else { tload(nblk, 2 * q, gv); tload(nblk, 2 * q + 1, gv); }
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
     double2 pf[PER][SPIN == 2 ? 2 : 1];
@@ -2324,14 +2317,21 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     __shared__ __attribute__((aligned(16))) double sp_[MF_TILE * RW];
     auto sp = [&](int jp, int mp) __attribute__((always_inline)) -> double* { return sp_ + jp * RW + mp * NV; };
     const int L = D.L, npair = D.npair;
-    const int m = mf_m(blockIdx.x, L);
-    // workgroups whose first window starts past L leave before any barrier
+    // XCD-aware order (1-D grid over (m, window group)): blocks lin, lin + 8,
+    // ... run on one XCD, and each XCD takes whole phase blocks -- the 4 m x
+    // WGY window groups that read the same 128-B phase lines -- back to back,
+    // so those lines come from HBM once into that XCD's L2
     constexpr int H = CGW / CPW;                   // waves per window (column-group slices)
     constexpr int WPG = NT / 64 / H;               // windows per workgroup
-    if (m + 32 * (int)(blockIdx.y * WPG) > L) return;
+    const int WGY = ((L + 1 + 31) / 32 + WPG - 1) / WPG;   // window groups of m = 0
+    const int lin = blockIdx.x, slot = lin >> 3, per = PHI_MB * WGY;
+    const int m = ((slot / per) * 8 + (lin & 7)) * PHI_MB + (slot % per) / WGY;
+    const int wgy = (slot % per) % WGY;
+    // workgroups whose first window starts past L leave before any barrier
+    if (m > L || m + 32 * wgy * WPG > L) return;
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int win = blockIdx.y * WPG + wave / H;
+    const int win = wgy * WPG + wave / H;
     const int cg0 = (wave % H) * CPW;             // this wave's first column group
     const int lw = m + 32 * win;
     const bool live = lw <= L;
@@ -2428,28 +2428,29 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
         const bool more = t + 1 < T.ntile;
         if (more) fetch(t + 1, pf);
         const Tw nxt = twin(more ? t + 1 : t);
-        if (cur.any) {                              // wave-uniform; one straight-line body per tile
-            // A operands of slice s (a1 / a2 per parity and column group), read one
-            // slice ahead of their MFMAs
-            double aq[2][2][CPW][NF];
-            auto ldsA = [&](int s, double (&a)[2][CPW][NF]) __attribute__((always_inline)) {
+        // A operands of slice s (a1 / a2 per parity and column group), read one
+        // slice ahead of their MFMAs; every load unconditional, only the MFMAs
+        // under the wave-uniform window test (see the synthesis)
+        double aq[2][2][CPW][NF];
+        auto ldsA = [&](int s, double (&a)[2][CPW][NF]) __attribute__((always_inline)) {
 #pragma unroll
-                for (int p = 0; p < 2; ++p)
+            for (int p = 0; p < 2; ++p)
 #pragma unroll
-                    for (int c = 0; c < CPW; ++c) {
-                        if constexpr (SPIN == 2) {
-                            a[p][c][0] = spo[s * 4 * RW + c * 4 * NV + 4 * p];
-                            a[p][c][1] = s2 * spr[s * 4 * RW + c * 4 * NV + 4 * (1 - p)];
-                        } else {
-                            a[p][c][0] = spo[s * 4 * RW + c * 8 * NV + 2 * p];
-                        }
+                for (int c = 0; c < CPW; ++c) {
+                    if constexpr (SPIN == 2) {
+                        a[p][c][0] = spo[s * 4 * RW + c * 4 * NV + 4 * p];
+                        a[p][c][1] = spr[s * 4 * RW + c * 4 * NV + 4 * (1 - p)];
+                    } else {
+                        a[p][c][0] = spo[s * 4 * RW + c * 8 * NV + 2 * p];
                     }
-            };
-            ldsA(0, aq[0]);
+                }
+        };
+        ldsA(0, aq[0]);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                if (s + 1 < 4) ldsA(s + 1, aq[(s + 1) & 1]);
-                __builtin_amdgcn_sched_barrier(0);
+        for (int s = 0; s < 4; ++s) {
+            if (s + 1 < 4) ldsA(s + 1, aq[(s + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (cur.any) {
 #pragma unroll
                 for (int p = 0; p < 2; ++p) {
                     double gz[NF];
@@ -2461,19 +2462,16 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
                         // other; F1 is plane G+ on even rows (p = 0), G- on odd
                         if constexpr (SPIN == 2) {
                             C[c][p] = mfma64(aq[s & 1][p][c][0], gz[p], C[c][p]);
-                            C[c][p] = mfma64(aq[s & 1][p][c][1], gz[1 - p], C[c][p]);
+                            C[c][p] = mfma64(s2 * aq[s & 1][p][c][1], gz[1 - p], C[c][p]);
                         } else {
                             C[c][p] = mfma64(aq[s & 1][p][c][0], gz[0], C[c][p]);
                         }
                     }
                 }
-                __builtin_amdgcn_sched_barrier(0);
-                tload(nxt, s, gv);                  // (the last tile reloads its own: harmless)
-                __builtin_amdgcn_sched_barrier(0);
             }
-        } else {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) tload(nxt, s, gv);
+            __builtin_amdgcn_sched_barrier(0);
+            tload(nxt, s, gv);                      // (the last tile reloads its own: harmless)
+            __builtin_amdgcn_sched_barrier(0);
         }
         cur = nxt;
     }
@@ -3111,9 +3109,9 @@ constexpr int MF_CGW = 4;         // 16-column groups per workgroup (16 maps spi
 // launch shapes (speed only; every shape gives the same bits): column groups
 // per wave in the synthesis (GS_SHT_MFS_CPW 4 / 2) and the analysis
 // (GS_SHT_MFA_CPW 4 / 2), analysis workgroup size (GS_SHT_MFA_NT 256 / 512).
-// Measured (N_side 256, 16 spin-2 maps, rocprofv3 averages): synthesis CPW 4 /
-// 2 = 580 / 597 us; analysis (CPW, NT) (4, 512) / (4, 256) / (2, 256) / (2,
-// 512) = 819 / 966 / 957 / 1090 us
+// Measured (N_side 256, 16 spin-2 maps, rocprofv3 averages, XCD-aware
+// orders): synthesis CPW 4 / 2 = 550 / 598 us; analysis (CPW, NT) (4, 256) /
+// (4, 512) / (2, 512) = 737 / 825 / 1040 us
 static int mf_env(const char* name, int a, int b, int dflt) {
     const char* e = getenv(name);
     if (!e) return dflt;
@@ -3122,7 +3120,7 @@ static int mf_env(const char* name, int a, int b, int dflt) {
 }
 static int mfs_cpw() { static const int v = mf_env("GS_SHT_MFS_CPW", 2, 4, 4); return v; }
 static int mfa_cpw() { static const int v = mf_env("GS_SHT_MFA_CPW", 2, 4, 4); return v; }
-static int mfa_nt() { static const int v = mf_env("GS_SHT_MFA_NT", 256, 512, 512); return v; }
+static int mfa_nt() { static const int v = mf_env("GS_SHT_MFA_NT", 256, 512, 256); return v; }
 
 extern "C++" {
 template <int CPW>
@@ -3132,11 +3130,11 @@ static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
     const unsigned ty = (unsigned)((p->mf_ntile + 3) / 4);
     const dim3 blk(256 * (MF_CGW / CPW));
     if (ncomp != 2) {               // T (spin 0): comp 0
-        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
+        const dim3 g(ty, p->L + 1, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0);
     }
     if (ncomp != 1) {               // E, B -> Q, U: comps ncomp - 2, ncomp - 1
-        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
+        const dim3 g(ty, p->L + 1, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp,
                            ncomp - 2);
     }
@@ -3149,14 +3147,16 @@ static void sht_anal_mfma_v(gs_sht* p, int nmap, int ncomp, int layout, int acc,
     const double w = 4.0 * PI / (double)p->npix;
     constexpr int WPG = NT / 64 / (MF_CGW / CPW);    // windows per workgroup
     const int nwin = (p->L + 1 + 31) / 32;           // 32-l windows of m = 0
-    const unsigned ty = (unsigned)((nwin + WPG - 1) / WPG);
+    const int wgy = (nwin + WPG - 1) / WPG;
+    const int nmb = (p->L + 1 + PHI_MB - 1) / PHI_MB;   // phase blocks of 4 m, dealt to 8 XCDs
+    const unsigned nx = (unsigned)(((nmb + 7) / 8) * 8 * PHI_MB * wgy);
     if (ncomp != 2) {
-        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
+        const dim3 g(nx, 1, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_anal_mfma<0, MF_CGW, CPW, NT>), g, dim3(NT), 0, st, D, T, p->phi, nmap, ncomp, 0, w,
                            layout, acc, alm);
     }
     if (ncomp != 1) {
-        const dim3 g(p->L + 1, ty, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
+        const dim3 g(nx, 1, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_anal_mfma<2, MF_CGW, CPW, NT>), g, dim3(NT), 0, st, D, T, p->phi, nmap, ncomp,
                            ncomp - 2, w, layout, acc, alm);
     }
