@@ -7,15 +7,19 @@
 #   bench_<tag>_*.json        bench lines: default (with cpu_baseline), stored sky map, centered C2,
 #                             asis C4 (per GPU), the drop-in surface, masked C5, HEAD's masked modes
 #   prof_<tag>_<mode>         kernel stats of configs[1], the masked workloads, SHT at N_side 2048
-# usage (GPU box): bash tools/profile_round.sh <tag> [a|b|all]   (then python tools/summarize_profile.py <tag>)
+# usage (GPU box): bash tools/profile_round.sh <tag> [a|b|c|d|all]   (then python tools/summarize_profile.py <tag>)
 #   a: the harmonic trace, PMC passes and harmonic bench lines; b: the masked bench lines and the
-#   masked / configs[1] / SHT kernel stats (two gpurun calls stay within one call's time limit)
+#   masked / configs[1] / SHT kernel stats (two gpurun calls stay within one call's time limit);
+#   c (r04): the chain-batched SHT (N_side 256, 16 spin-2 maps, matrix-core Legendre tables) --
+#   kernel stats and FETCH_SIZE / WRITE_SIZE / SQ passes -- and the N_side 2048 recurrence kernels'
+#   PMC passes; d (r04): HEAD's masked modes at 16 chains per GPU (bench lines + kernel stats)
+#   (python tools/summarize_sht_pmc.py <tag> folds c's passes into profiles/pmc_traffic.json)
 set -e
 TAG=${1:-r03}
 PART=${2:-all}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
-if [ "$PART" != b ]; then
+if [ "$PART" = a ] || [ "$PART" = all ]; then
 rm -rf "$OUT"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
@@ -45,7 +49,39 @@ timeout -k 10 300 python3 bench.py --workload asis \
 timeout -k 10 300 python3 bench.py --workload surface_noncentered --no-cpu-baseline \
     > gpurun_out/bench_${TAG}_surface_C3.json 2> gpurun_out/bench_${TAG}_surface_C3.err
 fi
-if [ "$PART" != a ]; then
+if [ "$PART" = c ]; then
+O=gpurun_out/prof_${TAG}_shtb; rm -rf $O; mkdir -p $O
+A="tools/sht_bench.py --nside 256 --batch 16 --ncomp 2 --reps 5 --mfma"
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $A > $O/trace.log 2>&1
+for pass in "FETCH_SIZE" "WRITE_SIZE" \
+    "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
+    n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    timeout -s KILL 60 rocprofv3 --pmc $pass --kernel-include-regex "k_sht" -d $O/$n -o run --output-format csv \
+        -- python3 $A > $O/$n.log 2>&1
+done
+O=gpurun_out/prof_${TAG}_sht2048; rm -rf $O; mkdir -p $O
+A="tools/sht_bench.py --nside 2048 --reps 2"
+for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE"; do
+    n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-include-regex "k_sht_(anal|synth)_leg" -d $O/$n -o run \
+        --output-format csv -- python3 $A > $O/$n.log 2>&1
+done
+echo "profile $TAG c done"
+exit 0
+fi
+if [ "$PART" = d ]; then
+for m in masked_asis masked_centered_ula masked_centered_pcg masked_noncentered; do
+    timeout -k 10 300 python3 bench.py --workload $m --nchains 16 > gpurun_out/bench_${TAG}_${m}_b16.json \
+        2> gpurun_out/bench_${TAG}_${m}_b16.err
+done
+rm -rf "${OUT}_pcg_b16"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "${OUT}_pcg_b16" -o run --output-format csv -- \
+    python3 bench.py --workload masked_centered_pcg --nchains 16 --steps 2 --warmup 1 --no-cpu-baseline \
+    > "${OUT}_pcg_b16.log" 2>&1
+echo "profile $TAG d done"
+exit 0
+fi
+if [ "$PART" = b ] || [ "$PART" = all ]; then
 rm -rf "${OUT}_masked" "${OUT}_sht" "${OUT}_masked_asis" "${OUT}_c2"
 timeout -k 10 600 python3 bench.py --workload masked > gpurun_out/bench_${TAG}_masked_C5.json \
     2> gpurun_out/bench_${TAG}_masked_C5.err
