@@ -632,6 +632,11 @@ def run_masked_head(args, ctx, cpu=None):
                             "converged chains' update kernels return at once"}
     fl = n_sht * sht_flops(N, L, 16) * B
     achieved = fl / (elapsed / args.steps) / 1e12
+    # HBM bytes of the step's transforms from the PMC pass of the same batched
+    # transform (profiles/pmc_traffic.json; the SHT kernels are ~90 % of the step)
+    tprof = load_profile(args.profile_json, f"masked_sht_N{N}_L{L}_B{B}")
+    traffic = (int(n_sht * tprof["bytes_per_transform_per_map"] * B)
+               if tprof.get("bytes_per_transform_per_map") else None)
     return {
         "metric": METRIC % (N, L),
         "value": round(args.steps * B * ctx.world / elapsed, 4),
@@ -647,7 +652,9 @@ def run_masked_head(args, ctx, cpu=None):
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
         "roofline": {"bound": "fp64", "kernel": f"{n_sht:.1f} spin-2 SHT-equivalents per chain-iteration",
                      "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP64_VALU_PEAK_TFS, 4), "traffic": None,
+                     "frac": round(achieved / FP64_VALU_PEAK_TFS, 4), "traffic": traffic,
+                     "traffic_unit": "HBM bytes per step (the transforms', PMC)",
+                     "traffic_source": tprof.get("source"),
                      "algorithmic_flops_per_step": fl},
         "cpu_baseline": _finalize_cpu(cpu, pcg_info["cg_iterations_per_solve"] if pcg_info else None),
         "pcg": pcg_info,

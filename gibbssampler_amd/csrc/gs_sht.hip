@@ -1479,7 +1479,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
                                                             const double2* __restrict__ phi,
                                                             const double2* __restrict__ tw, int Mmax,
                                                             const double2* __restrict__ bsk, double* __restrict__ maps,
-                                                            int ncomp, int NCB, int SB, int twoff) {
+                                                            int ncomp, int NCB, int SB, int twoff,
+                                                            const int* __restrict__ comp_lmax, int comp_div) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int c0 = blockIdx.y * NCB;
@@ -1500,6 +1501,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
     const bool eq = g.startS < 0;
     const int K = n / 2 + 1;
     const int J = K >= TC ? 1 : TC / K;
+    // block syntheses (f2): comp c holds only m <= comp_lmax[c / comp_div]
+    const int Lc = comp_lmax && live ? comp_lmax[(c0 + cl) / comp_div] : L;
     auto H = [&](const double2* P, int m, bool neg) {
         const double2 v = P[phi_at(m, p, npair)];
         const double cm = (m == 0 ? 1.0 : 2.0) * (neg ? -1.0 : 1.0);
@@ -1512,14 +1515,14 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
         const int nk = (n - k) % n;
         const bool on = live && sl < K * J;
         if (on) {
-            for (int m = k + j0 * n, q = j0; m <= L; m += J * n, q += J) {
+            for (int m = k + j0 * n, q = j0; m <= Lc; m += J * n, q += J) {
                 const bool neg = g.phi_half && (q & 1);
                 const double2 a = H(PN, m, neg);
                 f.nk.x += a.x; f.nk.y += a.y;
                 if (!eq) { const double2 b = H(PS, m, neg); f.sk.x += b.x; f.sk.y += b.y; }
             }
             if (nk != k)
-                for (int m = nk + j0 * n, q = j0; m <= L; m += J * n, q += J) {
+                for (int m = nk + j0 * n, q = j0; m <= Lc; m += J * n, q += J) {
                     const bool neg = g.phi_half && (q & 1);
                     const double2 a = H(PN, m, neg);
                     f.nmk.x += a.x; f.nmk.y += a.y;
@@ -1979,18 +1982,25 @@ __global__ void k_sub_maps(long long n, const double* __restrict__ a, double* __
 //   analysis   a[l][col]      = sum_{ring, F} G_F(l, ring) Phi_F(ring, col)  (K = rings)
 // with col = (map, output part) and G = lambda (spin 0) or the spin-2 F1 / F2,
 // the north / south parity folded as in the VALU kernels (output rows of one
-// l parity).  Here G comes from a plan-time table (MfTab) filled by the same
+// l parity).  lambda comes from a plan-time table (MfTab) filled by the same
 // scaled recurrence the VALU kernels run -- a value the recurrence holds below
 // the representable range (k < 0) is stored as 0, exactly what they multiply --
-// so both transform kernels are v_mfma_f64_16x16x4_f64 streams whose K loop
-// reads the table once per transform for every map of the batch.  The table
-// costs 3 x 8 B x N_ringpair x N_lm (1.6 GB at N_side 256 / l_max 512), so it
-// is built for small maps only (large maps keep the on-the-fly recurrence).
-// Blocks of 16 l x 16 ring pairs; blocks wholly below the representable range
-// of a (m, 16-pair tile) are not stored (b0); planes lambda, G+ (F1 at even
-// l - m, F2 at odd), G- (the other).
+// and the spin-2 F1 / F2 are formed in the kernels from the table's lambda_l,
+// lambda_{l-1} and the per-l coefficients (the VALU kernels' expressions, a few
+// fp64 operations shared by every column group), so both transform kernels are
+// v_mfma_f64_16x16x4_f64 streams whose K loop reads the table once per
+// transform for every map of the batch.  The table costs 8 B x N_ringpair x
+// N_lm (0.54 GB at N_side 256 / l_max 512; r04 first stored lambda, F1 and F2:
+// three times the bytes, and the kernels ran at 3-4 TB/s of HBM reading it),
+// so it is built for small maps only (large maps keep the on-the-fly
+// recurrence).  Blocks of 16 l x 16 ring pairs; blocks wholly below the
+// representable range of a (m, 16-pair tile) are not stored (b0, chosen so the
+// stored blocks also hold the row above the first representable l).  At that
+// first l the recurrence's lambda_{l-1} is already rescaled while its own row
+// (k < 0) multiplies 0: the table keeps the rescaled value there (it enters the
+// sums at l - 1 with weight ~2^-384, far below the fp64 rounding of the sums).
 constexpr int MF_TILE = 16;
-constexpr int MF_BLK = 3 * 256;                  // doubles per block (3 planes of 16 l x 16 pairs)
+constexpr int MF_BLK = 256;                      // doubles per block (16 l x 16 pairs of lambda)
 
 struct MfTab {
     const double* tab;       // blocks
@@ -2022,12 +2032,16 @@ __global__ __launch_bounds__(256) void k_mf_onset(ShtDev D, const double* __rest
     for (int o = 8; o > 0; o >>= 1) lon = min(lon, __shfl_xor(lon, o, 16));
     if ((threadIdx.x & 15) == 0 && p < npair) {
         const int nb = (L - m + MF_TILE) / MF_TILE;
-        b0[(long long)m * ((npair + MF_TILE - 1) / MF_TILE) + p / MF_TILE] = lon > L ? nb : (lon - m) / MF_TILE;
+        // the stored blocks start at the one holding lon - 1 (the kernels read
+        // lambda_{lon-1} for F1 / F2 at lon)
+        b0[(long long)m * ((npair + MF_TILE - 1) / MF_TILE) + p / MF_TILE] =
+            lon > L ? nb : (max(lon - 1, m) - m) / MF_TILE;
     }
 }
 
-// pass 2: every (m, ring pair) walks its recurrence from m and writes lambda,
-// F1, F2 of the stored blocks (the VALU kernels' values: k < 0 -> 0)
+// pass 2: every (m, ring pair) walks its recurrence from m and writes lambda of
+// the stored blocks (the VALU kernels' values: k < 0 -> 0; at the first
+// representable l the row above takes the recurrence's rescaled lambda_{l-1})
 __global__ __launch_bounds__(256) void k_mf_fill(ShtDev D, const double* __restrict__ lmm, const int* __restrict__ lmk,
                                                  MfTab T) {
     const int L = D.L, npair = D.npair;
@@ -2039,34 +2053,26 @@ __global__ __launch_bounds__(256) void k_mf_fill(ShtDev D, const double* __restr
     const int b0 = T.b0[ti], nb = (L - m + MF_TILE) / MF_TILE;
     if (b0 >= nb) return;
     double* out = const_cast<double*>(T.tab) + T.off[ti] * MF_BLK;
-    const double x = D.geom[p].x, is2 = D.geom[p].is2, xis2 = x * is2;
+    const double x = D.geom[p].x;
     const LegCoef* cf = D.coef + (cidx(L, m, m) - m);
     double v1 = 0.0, v0 = lmm[(long long)m * npair + p];
     int k = lmk[(long long)m * npair + p];
+    bool was_on = false;
     for (int l = m; l < m + nb * MF_TILE; ++l) {
         const int b = (l - m) / MF_TILE, r = (l - m) % MF_TILE;
-        double lam = 0.0, f1 = 0.0, f2 = 0.0;
+        double lam = 0.0;
         if (l <= L) {
-            const LegCoef c = cf[l];
-            const double w0 = k == 0 ? v0 : 0.0, w1 = k == 0 ? v1 : 0.0;
-            lam = w0;
-            f1 = fma(c.R * xis2, w1, -fma(c.P, is2, c.Q) * w0);
-            f2 = fma(c.Rm * is2, w1, -(c.T * xis2) * w0);
+            const bool on = k == 0;
+            lam = on ? v0 : 0.0;
+            if (on && !was_on && l > m && (l - 1 - m) / MF_TILE >= b0)   // the onset's lambda_{l-1}
+                out[(long long)((l - 1 - m) / MF_TILE - b0) * MF_BLK + ((l - 1 - m) % MF_TILE) * MF_TILE + j] = v1;
+            was_on = on;
             if (l < L) {
                 rec_step(cf[l + 1], x, v0, v1);
                 if (k < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++k; }
             }
         }
-        if (b >= b0) {
-            // planes 1 / 2 = the function with lambda's parity ("+": F1 at even
-            // l - m, F2 at odd) and the other one ("-"), so the kernels' A
-            // operands need no per-lane select
-            double* blk = out + (long long)(b - b0) * MF_BLK + r * MF_TILE + j;
-            const bool ev = (r & 1) == 0;
-            blk[0] = lam;
-            blk[256] = ev ? f1 : f2;
-            blk[512] = ev ? f2 : f1;
-        }
+        if (b >= b0) out[(long long)(b - b0) * MF_BLK + r * MF_TILE + j] = lam;
     }
 }
 
@@ -2118,8 +2124,15 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     constexpr int H = CGW / CPW;                   // waves per tile (column-group slices)
     constexpr int NT = 256 * H;                    // 4 tiles per workgroup
     constexpr int PER = (NIT + NT - 1) / NT;       // staged items per thread
-    constexpr int SW = SPIN == 2 ? 8 : 2;          // staged doubles per item
-    __shared__ __attribute__((aligned(16))) double sb[NIT * SW];
+    // staged rows (spin 2: per l a "+" and a "-" row of MPW x 4 doubles; spin 0
+    // per l one row of MPW x 2), padded by 64 B: the four 16-lane groups of a
+    // wave read four consecutive l, and rows 128 B apart mod 256 B put the two
+    // groups of each half-wave on disjoint banks
+    constexpr int SR = SPIN == 2 ? MPW * 4 + 8 : MPW * 2 + 8;
+    constexpr int NROW = SPIN == 2 ? 2 * MF_CH : MF_CH;
+    __shared__ __attribute__((aligned(16))) double sb[NROW * SR];
+    // spin 2: the chunk's per-l coefficients (P, Q, R, T, Rm, 0) of F1 / F2
+    __shared__ __attribute__((aligned(16))) double sc[SPIN == 2 ? MF_CH * 6 : 2];
     const int L = D.L, nlm = D.nlm, npair = D.npair;
     // grid (tile group, m, map group): the 8 tile groups of one m are
     // consecutive blocks -- one per XCD, at the same time, so m's a_lm come
@@ -2136,6 +2149,32 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     const int b0 = t < T.ntile ? T.b0[ti] : nb;
     const double* tab = T.tab + (t < T.ntile ? T.off[ti] : 0) * MF_BLK;
     const long long base = cidx(L, m, m) - m;
+    // the lane's ring pair (F1 / F2 geometry)
+    const int pj = min(MF_TILE * min(t, T.ntile - 1) + j, npair - 1);
+    const double is2 = D.geom[pj].is2, xis2 = D.geom[pj].x * is2;
+    // per-l coefficients of the chunk (threads < MF_CH; spin 2)
+    const double2* cfb = reinterpret_cast<const double2*>(D.coef + base);
+    double2 pc[3];
+    auto fetchc = [&](int cb) __attribute__((always_inline)) {
+        if constexpr (SPIN == 2) {
+            // every thread loads (thread i the row i mod MF_CH: no branch around
+            // the loads, see tblk); threads < MF_CH stage them
+            const int l = min(m + cb * MF_TILE + (int)(threadIdx.x & (MF_CH - 1)), L);
+            pc[0] = cfb[4 * l + 1]; pc[1] = cfb[4 * l + 2]; pc[2] = cfb[4 * l + 3];   // (P, Q), (R, T), (Rm, -)
+        }
+    };
+    auto stagec = [&](int cb) __attribute__((always_inline)) {
+        if constexpr (SPIN == 2) {
+            if (threadIdx.x < MF_CH) {
+                const bool ok = m + cb * MF_TILE + (int)threadIdx.x <= L;
+                double2* d = reinterpret_cast<double2*>(sc + threadIdx.x * 6);
+                // (component selects: a select of double2 values goes through scratch)
+                d[0] = make_double2(ok ? pc[0].x : 0.0, ok ? pc[0].y : 0.0);
+                d[1] = make_double2(ok ? pc[1].x : 0.0, ok ? pc[1].y : 0.0);
+                d[2] = make_double2(ok ? pc[2].x : 0.0, 0.0);
+            }
+        }
+    };
     // item i: l = chunk start + i % MF_CH, map c0 + i / MF_CH (consecutive
     // threads read consecutive l of one map)
     auto fetch = [&](int cb, double2 (&pf)[PER][SPIN == 2 ? 2 : 1]) __attribute__((always_inline)) {
@@ -2164,14 +2203,14 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
                 const double bx = ok ? pf[k][1].x : 0.0, by = ok ? pf[k][1].y : 0.0;
                 // F1 row (ex, ey, bx, by), F2 row (-by, bx, ey, -ex); "+" = F1 at even l - m
                 const bool ev = (lr & 1) == 0;     // l - m parity (chunks start at even l - m)
-                double2* P = reinterpret_cast<double2*>(sb + ((lr * 2 + 0) * MPW + mp) * 4);
-                double2* M = reinterpret_cast<double2*>(sb + ((lr * 2 + 1) * MPW + mp) * 4);
+                double2* P = reinterpret_cast<double2*>(sb + (lr * 2 + 0) * SR + mp * 4);
+                double2* M = reinterpret_cast<double2*>(sb + (lr * 2 + 1) * SR + mp * 4);
                 P[0] = make_double2(ev ? ex : -by, ev ? ey : bx);
                 P[1] = make_double2(ev ? bx : ey, ev ? by : -ex);
                 M[0] = make_double2(ev ? -by : ex, ev ? bx : ey);
                 M[1] = make_double2(ev ? ey : bx, ev ? -ex : by);
             } else {
-                reinterpret_cast<double2*>(sb)[lr * MPW + mp] =
+                reinterpret_cast<double2*>(sb + lr * SR)[mp] =
                     make_double2(ok ? pf[k][0].x : 0.0, ok ? pf[k][0].y : 0.0);
             }
         }
@@ -2184,12 +2223,16 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         const bool ok = b >= b0 && b < nb && !(GS_MF_EXP & 1);
         return ok ? tab + (long long)(b - b0) * MF_BLK : T.tab;
     };
-    // the table values of quad / octet-half q of a block
-    auto tload = [&](const double* blk, int q, double (&gv)[8]) __attribute__((always_inline)) {
+    // the table values of quad / octet-half q of a block: spin 2 lambda_l and
+    // lambda_{l-1} (row 4 q + g and the row above; for the first row the
+    // previous block's last one, read only when that block is stored: mma
+    // zeroes it otherwise), spin 0 lambda
+    auto tload = [&](const double* blk, bool prev, int q, double (&gv)[8]) __attribute__((always_inline)) {
         if constexpr (SPIN == 2) {
             const int row = 4 * q + g;
-            gv[2 * q + 0] = blk[256 + row * MF_TILE + j];
-            gv[2 * q + 1] = blk[512 + row * MF_TILE + j];
+            gv[2 * q + 0] = blk[row * MF_TILE + j];
+            gv[2 * q + 1] = row > 0 ? blk[(row - 1) * MF_TILE + j]
+                                    : (prev ? blk - MF_BLK + 15 * MF_TILE + j : T.tab)[0];
         } else {
             // q = 2 h + e: octet half h, even (e = 0) / odd row of lambda
             const int row = 8 * (q >> 1) + 2 * g + (q & 1);
@@ -2204,19 +2247,19 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // per column group
     // the lane's base in the staged rows; everything else is a compile-time
     // offset (the ds_read immediate), so no per-read address registers
-    const double* sbl = SPIN == 2 ? sb + ((g * 2 * MPW) + cg0 * 4 + (j >> 2)) * 4 + o
-                                  : sb + ((2 * g * MPW) + cg0 * 8 + (j >> 1)) * 2 + (j & 1);
+    const double* sbl = SPIN == 2 ? sb + (g * 2) * SR + (cg0 * 4 + (j >> 2)) * 4 + o
+                                  : sb + (2 * g) * SR + (cg0 * 8 + (j >> 1)) * 2 + (j & 1);
     auto lds = [&](int lr0, int q, double (&bq)[2 * CPW]) __attribute__((always_inline)) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (SPIN == 2) {
                 const int r0 = lr0 + 4 * q;         // row = r0 + g
-                bq[2 * c + 0] = sbl[((r0 * 2 + 0) * MPW + c * 4) * 4];
-                bq[2 * c + 1] = sbl[((r0 * 2 + 1) * MPW + c * 4) * 4];
+                bq[2 * c + 0] = sbl[(r0 * 2 + 0) * SR + c * 16];
+                bq[2 * c + 1] = sbl[(r0 * 2 + 1) * SR + c * 16];
             } else {
                 const int r0 = lr0 + 8 * q;         // even row = r0 + 2 g
-                bq[2 * c + 0] = sbl[(r0 * MPW + c * 8) * 2];
-                bq[2 * c + 1] = sbl[((r0 + 1) * MPW + c * 8) * 2];
+                bq[2 * c + 0] = sbl[r0 * SR + c * 16];
+                bq[2 * c + 1] = sbl[(r0 + 1) * SR + c * 16];
             }
         }
     };
@@ -2225,42 +2268,71 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // they are consumed (a block of MFMAs ahead of their use)
     auto mma = [&](int b, int lr0, double (&gv)[8]) __attribute__((always_inline)) {
         const double* nblk = tblk(b + 1);
+        const bool nprev = b >= b0 && b + 1 < nb;    // blocks b and b + 1 stored (b + 1's row above)
+        const bool prev = b - 1 >= b0;               // block b's
         // every load unconditional (a load in one arm of a branch makes the
         // compiler's wait at the join cover the other arm's registers too); only
         // the MFMAs sit under the wave-uniform block test
         const bool on = b >= b0 && b < nb;
         constexpr int NQ = SPIN == 2 ? 4 : 2;
         double bq[2][2 * CPW];                      // two rolling buffers
+        double cv[2][5];                            // spin 2: (P, Q, R, T, Rm) of the lane's row
+        auto ldc = [&](int q, double (&c)[5]) __attribute__((always_inline)) {
+            if constexpr (SPIN == 2) {
+                const double* cq = sc + (lr0 + 4 * q + g) * 6;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) c[k] = cq[k];
+            }
+        };
         lds(lr0, 0, bq[0]);
+        ldc(0, cv[0]);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            if (q + 1 < NQ) lds(lr0, q + 1, bq[(q + 1) & 1]);
+            if (q + 1 < NQ) { lds(lr0, q + 1, bq[(q + 1) & 1]); ldc(q + 1, cv[(q + 1) & 1]); }
             // keep the order as written: the scheduler would sink the next
             // quad's reads and the table refills behind the MFMAs
             __builtin_amdgcn_sched_barrier(0);
             if (on) {
+                double ap, am;
+                if constexpr (SPIN == 2) {
+                    // F1 / F2 at l = m + 16 b + 4 q + g (the VALU kernels' expressions;
+                    // G+ = the one with lambda's parity: F1 at even l - m)
+                    const double w0 = gv[2 * q];
+                    const double w1 = (q > 0 || g > 0 || prev) ? gv[2 * q + 1] : 0.0;
+                    const int u = q & 1;
+                    const double f1 = fma(cv[u][2] * xis2, w1, -fma(cv[u][0], is2, cv[u][1]) * w0);
+                    const double f2 = fma(cv[u][4] * is2, w1, -(cv[u][3] * xis2) * w0);
+                    const bool ev = (g & 1) == 0;
+                    ap = ev ? f1 : f2;
+                    am = ev ? f2 : f1;
+                } else {
+                    ap = gv[2 * q];
+                    am = gv[2 * q + 1];
+                }
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
-                    Cp[c] = mfma64(gv[2 * q], bq[q & 1][2 * c + 0], Cp[c]);
-                    Cm[c] = mfma64(gv[2 * q + 1], bq[q & 1][2 * c + 1], Cm[c]);
+                    Cp[c] = mfma64(ap, bq[q & 1][2 * c + 0], Cp[c]);
+                    Cm[c] = mfma64(am, bq[q & 1][2 * c + 1], Cm[c]);
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (SPIN == 2) tload(nblk, q, gv);
-            else { tload(nblk, 2 * q, gv); tload(nblk, 2 * q + 1, gv); }
+            if constexpr (SPIN == 2) tload(nblk, nprev, q, gv);
+            else { tload(nblk, false, 2 * q, gv); tload(nblk, false, 2 * q + 1, gv); }
             __builtin_amdgcn_sched_barrier(0);
         }
     };
     double2 pf[PER][SPIN == 2 ? 2 : 1];
     double gv[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) tload(tblk(0), q, gv);
+    for (int q = 0; q < 4; ++q) tload(tblk(0), false, q, gv);
     fetch(0, pf);
+    fetchc(0);
     for (int cb = 0; cb < nb; cb += MF_CH / MF_TILE) {
         if (!(GS_MF_EXP & 4)) __syncthreads();      // the previous chunk's readers are done
         stage(cb, pf);
+        stagec(cb);
         if (!(GS_MF_EXP & 4)) __syncthreads();
-        if (cb + MF_CH / MF_TILE < nb) fetch(cb + MF_CH / MF_TILE, pf);
+        if (cb + MF_CH / MF_TILE < nb) { fetch(cb + MF_CH / MF_TILE, pf); fetchc(cb + MF_CH / MF_TILE); }
         mma(cb, 0, gv);
         mma(cb + 1, MF_TILE, gv);
     }
@@ -2311,11 +2383,13 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     constexpr int NV = SPIN == 2 ? 8 : 4;          // staged doubles per (pair, map)
     constexpr int NIT = MF_TILE * MPW;             // staged (pair, map) items per tile
     constexpr int PER = (NIT + NT - 1) / NT;
-    // rows padded by 16 B: the staging writes (consecutive threads =
-    // consecutive pairs = rows) spread over the banks
-    constexpr int RW = MPW * NV + 2;
+    // per ring pair jp a row [N + S | N - S] x [map] x [component] (HV = NV / 2
+    // components: Q.x Q.y U.x U.y or T.x T.y), so the 16 lanes of a group read
+    // 16 consecutive doubles; rows padded to 128 B mod 256 B, so the two groups
+    // of a half-wave (pairs 4 s + g, g = 0 / 1 and 2 / 3) use disjoint banks
+    constexpr int HV = NV / 2;
+    constexpr int RW = 2 * MPW * HV + 16;
     __shared__ __attribute__((aligned(16))) double sp_[MF_TILE * RW];
-    auto sp = [&](int jp, int mp) __attribute__((always_inline)) -> double* { return sp_ + jp * RW + mp * NV; };
     const int L = D.L, npair = D.npair;
     // XCD-aware order (1-D grid over (m, window group)): blocks lin, lin + 8,
     // ... run on one XCD, and each XCD takes whole phase blocks -- the 4 m x
@@ -2369,54 +2443,70 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     constexpr int NF = SPIN == 2 ? 2 : 1;
     // the lane's bases in the staged phases (row jp = 4 s + g, map (cg0 + c) ..):
     // spin 2 component o (a1) and 3 - o (a2), spin 0 re / im
-    const double* spo = SPIN == 2 ? sp_ + g * RW + (cg0 * 4 + (j >> 2)) * NV + o
-                                  : sp_ + g * RW + (cg0 * 8 + (j >> 1)) * NV + (j & 1);
-    const double* spr = sp_ + g * RW + (cg0 * 4 + (j >> 2)) * NV + 3 - o;
+    const double* spo = SPIN == 2 ? sp_ + g * RW + (cg0 * 4 + (j >> 2)) * HV + o
+                                  : sp_ + g * RW + (cg0 * 8 + (j >> 1)) * HV + (j & 1);
+    const double* spr = sp_ + g * RW + (cg0 * 4 + (j >> 2)) * HV + 3 - o;
     // tile t's window: false if it lies wholly below the tile's onset; bj / okb
     // the lane's block and whether it is stored
-    struct Tw { const double* blk; bool any, okb; };
+    // (prv: the row above the lane's first row -- the previous block's last --
+    // is stored; the lane's l for p = 0 is that block's row 2 (j & 7))
+    struct Tw { const double* blk; bool any, okb, prv; };
     auto twin = [&](int t) __attribute__((always_inline)) -> Tw {
         const long long ti = (long long)m * T.ntile + t;
         const int b0 = T.b0[ti];
         const bool any = live && bw + 1 >= b0 && bw < nb;    // wave-uniform
         const int bj = bw + (j >> 3);
         const bool okb = any && bj >= b0 && bj < nb;
-        return Tw{okb ? T.tab + (T.off[ti] + bj - b0) * MF_BLK : T.tab, any, okb};
+        return Tw{okb ? T.tab + (T.off[ti] + bj - b0) * MF_BLK : T.tab, any, okb, okb && bj - 1 >= b0};
     };
-    // the table values of column slice s (pairs 4 s + g) of a tile, rows of
-    // parity p (l = lw + 2 j' + p); planes G+ / G-.  Unconditional loads (a lane
-    // whose block is not stored reads the first block; its values are zeroed
-    // where they are multiplied)
-    auto tload = [&](const Tw& w, int s, double (&gv)[4][2][NF]) __attribute__((always_inline)) {
+    // the per-slice values of a tile (pairs 4 s + g): lambda at the lane's rows
+    // 2 (j & 7) + p, spin 2 also the row above p = 0's and the pair's geometry.
+    // Unconditional loads (a lane whose block is not stored reads the first
+    // block; its values are zeroed where they are used)
+    constexpr int NG = SPIN == 2 ? 5 : 2;
+    auto tload = [&](const Tw& w, int t, int s, double (&gv)[4][NG]) __attribute__((always_inline)) {
         const double* bp = (GS_MF_EXP & 1) ? T.tab : w.blk;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int row = 2 * (j & 7) + p;
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                gv[s][p][f] = bp[(SPIN == 2 ? 256 * (f + 1) : 0) + row * MF_TILE + 4 * s + g];
+        const int row = 2 * (j & 7);
+        gv[s][0] = bp[row * MF_TILE + 4 * s + g];
+        gv[s][1] = bp[(row + 1) * MF_TILE + 4 * s + g];
+        if constexpr (SPIN == 2) {
+            const double* up = (j & 7) ? bp + (row - 1) * MF_TILE : (w.prv ? bp - MF_BLK + 15 * MF_TILE : T.tab);
+            gv[s][2] = up[4 * s + g];
+            const PairGeom* ge = D.geom + min(MF_TILE * t + 4 * s + g, npair - 1);
+            gv[s][3] = ge->x;
+            gv[s][4] = ge->is2;
         }
     };
+    // spin 2: the lane's per-l coefficients of F1 / F2 (l = lw + 2 j + p)
+    double cP[2], cQ[2], cR[2], cT[2], cRm[2];
+    if constexpr (SPIN == 2) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const LegCoef c = D.coef[cidx(L, m, m) + min(lw + 2 * j + p, L) - m];
+            cP[p] = c.P; cQ[p] = c.Q; cR[p] = c.R; cT[p] = c.T; cRm[p] = c.Rm;
+        }
+    }
     auto stage = [&](const Ph (&pf)[PER]) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
             if (i >= NIT) continue;
-            double* dst = sp(i % MF_TILE, i / MF_TILE);
+            double* dp = sp_ + (i % MF_TILE) * RW + (i / MF_TILE) * HV;   // N + S
+            double* dm = dp + MPW * HV;                                      // N - S
             const Ph& q = pf[k];
             if constexpr (SPIN == 2) {          // a = Q north, b = Q south, c = U north, d = U south
-                dst[0] = q.a.x + q.b.x; dst[1] = q.a.y + q.b.y; dst[2] = q.c.x + q.d.x; dst[3] = q.c.y + q.d.y;
-                dst[4] = q.a.x - q.b.x; dst[5] = q.a.y - q.b.y; dst[6] = q.c.x - q.d.x; dst[7] = q.c.y - q.d.y;
+                dp[0] = q.a.x + q.b.x; dp[1] = q.a.y + q.b.y; dp[2] = q.c.x + q.d.x; dp[3] = q.c.y + q.d.y;
+                dm[0] = q.a.x - q.b.x; dm[1] = q.a.y - q.b.y; dm[2] = q.c.x - q.d.x; dm[3] = q.c.y - q.d.y;
             } else {
-                dst[0] = q.a.x + q.b.x; dst[1] = q.a.y + q.b.y; dst[2] = q.a.x - q.b.x; dst[3] = q.a.y - q.b.y;
+                dp[0] = q.a.x + q.b.x; dp[1] = q.a.y + q.b.y; dm[0] = q.a.x - q.b.x; dm[1] = q.a.y - q.b.y;
             }
         }
     };
     Ph pf[PER];
-    double gv[4][2][NF];
+    double gv[4][NG];
     Tw cur = twin(0);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) tload(cur, s, gv);
+    for (int s = 0; s < 4; ++s) tload(cur, 0, s, gv);
     fetch(0, pf);
     // tile t: stage its phases, issue tile t + 1's phases, then t's MFMAs; each
     // slice's table registers are refilled with tile t + 1's values as soon as
@@ -2438,10 +2528,10 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
                     if constexpr (SPIN == 2) {
-                        a[p][c][0] = spo[s * 4 * RW + c * 4 * NV + 4 * p];
-                        a[p][c][1] = spr[s * 4 * RW + c * 4 * NV + 4 * (1 - p)];
+                        a[p][c][0] = spo[s * 4 * RW + p * MPW * HV + c * 4 * HV];          // (N +- S)[o]
+                        a[p][c][1] = spr[s * 4 * RW + (1 - p) * MPW * HV + c * 4 * HV];    // (N -+ S)[3 - o]
                     } else {
-                        a[p][c][0] = spo[s * 4 * RW + c * 8 * NV + 2 * p];
+                        a[p][c][0] = spo[s * 4 * RW + p * MPW * HV + c * 8 * HV];
                     }
                 }
         };
@@ -2454,15 +2544,25 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
 #pragma unroll
                 for (int p = 0; p < 2; ++p) {
                     double gz[NF];
-#pragma unroll
-                    for (int f = 0; f < NF; ++f) gz[f] = cur.okb ? gv[s][p][f] : 0.0;
+                    if constexpr (SPIN == 2) {
+                        // F1 / F2 at (l = lw + 2 j + p, pair 16 t + 4 s + g): the VALU
+                        // kernels' expressions on the table's lambda_l, lambda_{l-1}
+                        const double w0 = gv[s][p];
+                        const double w1 = p ? gv[s][0] : (((j & 7) || cur.prv) ? gv[s][2] : 0.0);
+                        const double is2 = gv[s][4], xis2 = gv[s][3] * is2;
+                        const double f1 = fma(cR[p] * xis2, w1, -fma(cP[p], is2, cQ[p]) * w0);
+                        const double f2 = fma(cRm[p] * is2, w1, -(cT[p] * xis2) * w0);
+                        gz[0] = cur.okb ? f1 : 0.0;
+                        gz[1] = cur.okb ? f2 : 0.0;
+                    } else {
+                        gz[0] = cur.okb ? gv[s][p] : 0.0;
+                    }
 #pragma unroll
                     for (int c = 0; c < CPW; ++c) {
-                        // F1 takes the parity-p combination (p = 0: +, 1: -), F2 the
-                        // other; F1 is plane G+ on even rows (p = 0), G- on odd
+                        // F1 takes the parity-p combination (p = 0: +, 1: -), F2 the other
                         if constexpr (SPIN == 2) {
-                            C[c][p] = mfma64(aq[s & 1][p][c][0], gz[p], C[c][p]);
-                            C[c][p] = mfma64(s2 * aq[s & 1][p][c][1], gz[1 - p], C[c][p]);
+                            C[c][p] = mfma64(aq[s & 1][p][c][0], gz[0], C[c][p]);
+                            C[c][p] = mfma64(s2 * aq[s & 1][p][c][1], gz[1], C[c][p]);
                         } else {
                             C[c][p] = mfma64(aq[s & 1][p][c][0], gz[0], C[c][p]);
                         }
@@ -2470,7 +2570,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
-            tload(nxt, s, gv);                      // (the last tile reloads its own: harmless)
+            tload(nxt, more ? t + 1 : t, s, gv);    // (the last tile reloads its own: harmless)
             __builtin_amdgcn_sched_barrier(0);
         }
         cur = nxt;
@@ -2995,7 +3095,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
         // J = block / K aliases per bin pair, as a short-ring class does)
         const int M = p->merged_M, bd = ring_block(M);
         const double2* ph = phi ? phi : p->phi;
-        const int ncb = comp_lmax ? 1 : ring_mc_ncb(M, ncomp);
+        const int ncb = ring_mc_ncb(M, ncomp);
         if (ncb > 1) {
             // ring_block(M) threads per component, as the one-component kernels (the
             // fold's alias split J, hence its summation order, is the same)
@@ -3006,7 +3106,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             if (synth)
                 hipLaunchKernelGGL(k_sht_synth_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, maps_out, ncomp, ncb, SB,
-                                   toff);
+                                   toff, comp_lmax, comp_div);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, p->phi, ncomp, ncb, SB,
@@ -3429,7 +3529,7 @@ int gs_sht_set_mfma(gs_sht* p, int on) {
         // GS_SHT_MFMA_MAX_GB (16 GB: N_side 512 / l_max 1024 takes 12.9 GB)
         double gb = 16.0;
         if (const char* e = std::getenv("GS_SHT_MFMA_MAX_GB")) gb = std::atof(e);
-        const double need = 24.0 * (double)p->npair * (double)p->nlm / 1e9;
+        const double need = 8.0 * (double)p->npair * (double)p->nlm / 1e9;
         if (need > gb) return set_error("gs_sht_set_mfma: the Legendre table exceeds GS_SHT_MFMA_MAX_GB");
     }
     return sht_set_mfma(p, on);

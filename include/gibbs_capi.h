@@ -244,9 +244,10 @@ int gs_sht_map2alm_weighted(gs_sht* sht, int ncomp, const double* maps, const do
  * batch inside a capture is an error). */
 int gs_sht_reserve(gs_sht* sht, int nmap, void* stream);
 /* on = 1: the plan's Legendre stage runs on the fp64 matrix cores from a
- * plan-time table of lambda / F1 / F2 (3 x 8 B per (l, m, ring pair): 1.6 GB at
- * N_side 256, 12.9 GB at N_side 512; budget GS_SHT_MFMA_MAX_GB, default 16) --
- * a dense contraction per m whose inner dimension every map of a batch shares.
+ * plan-time table of lambda (8 B per (l, m, ring pair): 0.54 GB at N_side 256,
+ * 4.3 GB at N_side 512; budget GS_SHT_MFMA_MAX_GB, default 16; the spin-2 F1 /
+ * F2 are formed in the kernels) -- a dense contraction per m whose inner
+ * dimension every map of a batch shares.
  * Every transform of the plan then uses it (a map's result does not depend on
  * the batch size); on = 0 returns to the on-the-fly recurrence kernels.
  * Small maps only (plans without split-ring FFTs).  _info: state, table bytes. */
