@@ -1471,7 +1471,21 @@ __device__ __forceinline__ void dft_mc(double2* buf, int SB, int nc, const PairG
     }
 }
 
-// synthesis: grid (ring pairs, component groups of NCB); LDS NCB x SB + twiddles
+// XCD-aware 1-D order of the multi-component ring launches: blocks lin, lin +
+// 8, ... run on one XCD, which takes two consecutive ring entries (pairs p, p +
+// 1 share every 128-B line of the phase planes) with all their component
+// groups back to back (the ring's Bluestein tables then come from HBM into
+// that XCD's L2 once).  Returns false past the last ring.
+__device__ __forceinline__ bool ring_mc_slot(int nring, int ncg, int& idx, int& cg) {
+    const int lin = blockIdx.x, xcd = lin & 7, slot = lin >> 3;
+    const int j = slot / (2 * ncg), rem = slot - j * 2 * ncg;
+    idx = 2 * (8 * j + xcd) + rem / ncg;
+    cg = rem % ncg;
+    return idx < nring;
+}
+
+// synthesis: 1-D grid over (ring pair, component group of NCB) (ring_mc_slot);
+// LDS NCB x SB + twiddles
 template <int NV>
 __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, long long npix,
                                                             const int* __restrict__ pairs,
@@ -1480,10 +1494,13 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
                                                             const double2* __restrict__ tw, int Mmax,
                                                             const double2* __restrict__ bsk, double* __restrict__ maps,
                                                             int ncomp, int NCB, int SB, int twoff,
-                                                            const int* __restrict__ comp_lmax, int comp_div) {
+                                                            const int* __restrict__ comp_lmax, int comp_div,
+                                                            int nring) {
     extern __shared__ double2 lbuf[];
-    const int p = pairs[blockIdx.x];
-    const int c0 = blockIdx.y * NCB;
+    int idx, cg;
+    if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
+    const int p = pairs[idx];
+    const int c0 = cg * NCB;
     const int nc = min(NCB, ncomp - c0);
     const PairGeom g = geom[p];
     const int TC = blockDim.x / NCB;               // fold threads per component
@@ -1571,7 +1588,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
     }
 }
 
-// analysis: grid (ring pairs, component groups of NCB)
+// analysis: 1-D grid over (ring pair, component group of NCB) (ring_mc_slot)
 template <int NV>
 __global__ __launch_bounds__(1024) void k_sht_anal_ring_mc(int L, int npair, long long npix,
                                                            const int* __restrict__ pairs,
@@ -1580,10 +1597,12 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring_mc(int L, int npair, lon
                                                            const double2* __restrict__ tw, int Mmax,
                                                            const double2* __restrict__ bsk, double2* __restrict__ phi,
                                                            int ncomp, int NCB, int SB, int twoff,
-                                                           const double* __restrict__ wts, int wnc) {
+                                                           const double* __restrict__ wts, int wnc, int nring) {
     extern __shared__ double2 lbuf[];
-    const int p = pairs[blockIdx.x];
-    const int c0 = blockIdx.y * NCB;
+    int idx, cg;
+    if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
+    const int p = pairs[idx];
+    const int c0 = cg * NCB;
     const int nc = min(NCB, ncomp - c0);
     const PairGeom g = geom[p];
     int twM = Mmax;
@@ -3102,15 +3121,16 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             // (a component's buffer also holds its fold reduction: 4 per thread)
             const int bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
             const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
-            const dim3 gm(p->merged_n, (ncomp + ncb - 1) / ncb);
+            const int ncg = (ncomp + ncb - 1) / ncb;
+            const dim3 gm((unsigned)(8 * ((p->merged_n + 15) / 16) * 2 * ncg));
             if (synth)
                 hipLaunchKernelGGL(k_sht_synth_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, maps_out, ncomp, ncb, SB,
-                                   toff, comp_lmax, comp_div);
+                                   toff, comp_lmax, comp_div, p->merged_n);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, p->phi, ncomp, ncb, SB,
-                                   toff, wts, wnc);
+                                   toff, wts, wnc, p->merged_n);
             GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring_mc" : "k_sht_anal_ring_mc");
             return 0;
         }
