@@ -102,8 +102,6 @@ _SIGS = [
     ("gs_nc_finish", ctypes.c_int, [_VP, _VP]),
     ("gs_nc_decide", ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP]),
     ("gs_nc_decide_fused", ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP, ctypes.c_int, _VP]),
-    ("gs_nc_decide_chain", ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.c_uint32, _VP, _VP, ctypes.c_int,
-                                          ctypes.c_int, _VP]),
     ("gs_step_asis", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
                                     _VP, _VP, ctypes.c_int, _VP]),
     ("gs_iteration_counter", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_uint32]),

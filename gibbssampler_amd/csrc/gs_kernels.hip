@@ -1063,22 +1063,6 @@ __device__ __forceinline__ double wave_sum(double v) {
 // proposals (NonCenteredGibbs.py:292-309) and per-bin log proposal ratios
 // (313-330, 410-413): one thread per (chain, spectrum, bin)
 template <int F>
-__device__ __forceinline__ void mh_propose_val(int sp, int b, double old, double sd, const Key& key,
-                                               const double* u, uint32_t iter, double& p, double& lr) {
-    if (F == 3 && sp == 3) {
-        // TE: symmetric normal proposal (build spec; no positivity constraint)
-        const double y = u ? normcdfinv(*u) : normal1(key, b, sp, TAG_TN, iter);
-        p = old + sd * y;
-        lr = 0.0;
-    } else {
-        const double a = -old / sd;
-        const double q = u ? *u : uniform1(key, b, sp, TAG_TN, iter);
-        p = old + sd * tn_ppf(q, a);
-        lr = log_ndtr(old / sd) - log_ndtr(p / sd);
-    }
-}
-
-template <int F>
 __device__ __forceinline__ void mh_propose_at(long long g, int nchains, int maxbins, const int* __restrict__ nbins_arr,
                                               const double* __restrict__ prop_sd, const double* __restrict__ dl,
                                               double* __restrict__ prop, double* __restrict__ logr,
@@ -1092,8 +1076,20 @@ __device__ __forceinline__ void mh_propose_at(long long g, int nchains, int maxb
     const int chain = (int)(g / ((long long)maxbins * NSP));
     if (b < 2 || b >= nbins_arr[sp]) return;
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
+    const double sd = prop_sd[sp * maxbins + b];
+    const double old = dl[g];
     double p, lr;
-    mh_propose_val<F>(sp, b, dl[g], prop_sd[sp * maxbins + b], key, u_prop ? u_prop + g : nullptr, iter, p, lr);
+    if (F == 3 && sp == 3) {
+        // TE: symmetric normal proposal (build spec; no positivity constraint)
+        const double y = u_prop ? normcdfinv(u_prop[g]) : normal1(key, b, sp, TAG_TN, iter);
+        p = old + sd * y;
+        lr = 0.0;
+    } else {
+        const double a = -old / sd;
+        const double q = u_prop ? u_prop[g] : uniform1(key, b, sp, TAG_TN, iter);
+        p = old + sd * tn_ppf(q, a);
+        lr = log_ndtr(old / sd) - log_ndtr(p / sd);
+    }
     prop[g] = p;
     logr[g] = lr;
 }
@@ -1275,21 +1271,6 @@ struct MhPhases {
 // so the ticket is race-free).  (Computing the next step's prologue here as
 // well was measured slower: it puts that wide, latency-bound work on one
 // workgroup per chain.)
-// the next iteration's non-centred prologue drawn by the MH launch (on = 1):
-// each chain's workgroup, after its decisions, makes that chain's proposals
-// from its new D_l, the next step's accept uniforms and (params != null) the
-// CR block parameters -- k_nc_prologue's work for iteration + 1, the same
-// values -- so the next step launches no prologue
-struct NcNext {
-    double* prop;
-    double* logr;
-    double* u_out;
-    double* params;         // nullable (the sweep computes them per lane)
-    const double* prop_sd;
-    int nspec;
-    int on;
-};
-
 struct MhEpi {
     double* trace;          // nullable: trace[(it-1) % cap][chain][nspec][maxbins]
     int cap;
@@ -1620,7 +1601,7 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
                                             const double* __restrict__ prop, const double* __restrict__ logr,
                                             const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
                                             uint32_t iter, int chain0, int32_t* __restrict__ accept_out,
-                                            double* smem, const NcNext& nx) {
+                                            double* smem) {
     (void)tl_on;
     GS_TL(0);
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
@@ -1824,34 +1805,6 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
     }
     for (int k = tid; k < nrow; k += blockDim.x) D[k] = Ds[k];
     GS_TL(20);
-    if (nx.on) {
-        // the next iteration's prologue from Ds (this chain's new D_l, in LDS:
-        // the workgroup's last writes to it were before the phase loop's final
-        // barrier)
-        const uint32_t nit = iter + 1;
-        for (int k = tid; k < nrow; k += blockDim.x) {
-            const int sp = k / maxbins, b = k - sp * maxbins;
-            if (b < 2 || b >= meta[sp]) continue;
-            double pv, lr;
-            mh_propose_val<F>(sp, b, Ds[k], nx.prop_sd[sp * maxbins + b], key, nullptr, nit, pv, lr);
-            nx.prop[(long long)chain * nrow + k] = pv;
-            nx.logr[(long long)chain * nrow + k] = lr;
-        }
-        for (int k = tid; k < nacc; k += blockDim.x)
-            mh_uniform_at((long long)chain * nacc + k, chain + 1, nx.nspec, meta, nacc, n_iter_mh, seed_lo, seed_hi,
-                          nit, chain0, nx.u_out);
-        if (nx.params) {
-            constexpr int NW = F == 3 ? gs_block::NP : 2 * F;
-            for (int ell = tid; ell < Lp1; ell += blockDim.x) {
-                double dq[NSP], pp[gs_block::NP];
-                block_params_load<F>(0, ell, L, maxbins, Ds, ell2bin, dq);
-                block_params_from<F, 1>(ell, bl[ell], dq, k0, k1, k2, pp);
-                double* o = nx.params + ((long long)chain * Lp1 + ell) * gs_block::NP;
-#pragma unroll
-                for (int q = 0; q < NW; ++q) o[q] = pp[q];
-            }
-        }
-    }
 }
 
 template <int F>
@@ -1867,13 +1820,13 @@ __global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, M
                                                            const double* __restrict__ logr,
                                                            const double* __restrict__ u_acc, uint32_t seed_lo,
                                                            uint32_t seed_hi, IterArg itarg, int chain0,
-                                                           int32_t* __restrict__ accept_out, MhEpi epi, NcNext nx) {
+                                                           int32_t* __restrict__ accept_out, MhEpi epi) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const uint32_t iter = itarg.get();
     const int chain = blockIdx.x;
     mh_reg_body<F>(chain, chain == 0, L, maxbins, ph, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
                    ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
-                   smem, nx);
+                   smem);
     mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x);
 }
 
@@ -2489,8 +2442,7 @@ int gs_cls_draw(gs_plan* p, const double* stats, const double* variates, uint64_
 }
 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
-                     uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi = nullptr,
-                     const NcNext* nx = nullptr);
+                     uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi = nullptr);
 
 int gs_mh_propose(gs_plan* p, const double* dl, const double* u_prop, uint64_t seed, uint32_t iteration,
                   double* prop_out, double* logr_out, double* u_acc_out, void* stream) {
@@ -2535,13 +2487,8 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
 
 // the MH phases proper (proposals already in p->prop / p->logr)
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
-                     uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi, const NcNext* nx) {
+                     uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi) {
     int maxnb = 0;
-    const NcNext nx_none{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
-    const NcNext NX = nx ? *nx : nx_none;
-    // the next prologue rides only in the one-workgroup-per-chain form; the
-    // other forms return 1 (not drawn: the caller launches gs_nc_prologue)
-    const int nd = NX.on ? 1 : 0;
     const MhEpi none{nullptr, 1, nullptr, p->nchains, 0};
     const MhEpi E = epi ? *epi : none;
     MhPhases ph{};
@@ -2572,7 +2519,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
         hipLaunchKernelGGL((k_mh_reg<FF>), dim3(p->nchains), dim3(MH_REG_THREADS), lds_reg, S(stream), p->L,           \
                            p->maxbins, ph, ntab, p->phase_tab, p->phase_rng, p->meta, p->nacc, p->n_iter_mh, p->ell2blk,     \
                            p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop, p->logr,      \
-                           u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out, E, NX); } while (0)
+                           u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out, E); } while (0)
         if (p->F == 1) GS_MR(1); else if (p->F == 2) GS_MR(2); else GS_MR(3);
 #undef GS_MR
         GS_LAUNCH_CHECK("k_mh_reg");
@@ -2592,7 +2539,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
 #undef GS_MF2
 #undef GS_MF
         GS_LAUNCH_CHECK("k_mh_fused");
-        return nd;
+        return 0;
     }
     if (epi) return set_error("mh_decide: the fused epilogue needs the single-launch MH (l_max too large)");
     // very large l_max: two launches per phase (terms in HBM, one wave per block)
@@ -2616,7 +2563,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
 #undef GS_MA
         GS_LAUNCH_CHECK("k_mh_accept");
     }
-    return nd;
+    return 0;
 }
 
 int gs_stats_to_noncentered(gs_plan* p, const double* dl, double* stats, void* stream) {
@@ -2775,27 +2722,6 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv};
     return mh_decide(p, p->stats, dl, p->u_nat_ready ? p->u_nat : nullptr, slo, shi, it, accept_out, stream, &epi);
-}
-
-int gs_nc_decide_chain(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32_t* accept_out, double* trace,
-                       int capacity, int next_prologue, void* stream) {
-    if (check_plan(p)) return -1;
-    if (!p->has_mh) return set_error("gs_nc_decide_chain: plan has no MH blocks / proposal variances");
-    if (!dl) return set_error("gs_nc_decide_chain: null argument");
-    if (trace && capacity < 1) return set_error("gs_nc_decide_chain: capacity < 1");
-    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv};
-    const bool can = next_prologue && p->nacc > 0 && !getenv("GS_MH_INKERNEL_UNIFORMS");
-    const NcNext nx{p->prop, p->logr, p->u_nat, p->inkernel_params ? nullptr : p->params, p->prop_sd, p->nspec,
-                    can ? 1 : 0};
-    const int rc = mh_decide(p, p->stats, dl, p->u_nat_ready ? p->u_nat : nullptr, slo, shi, it, accept_out, stream,
-                             &epi, &nx);
-    if (rc < 0) return rc;
-    if (can && rc == 0) {
-        p->u_nat_ready = true;       // the next step's decide reads the uniforms drawn here
-        return 0;
-    }
-    return 1;
 }
 
 int gs_step_noncentered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,

@@ -1476,7 +1476,15 @@ __device__ __forceinline__ void dft_mc(double2* buf, int SB, int nc, const PairG
 // 1 share every 128-B line of the phase planes) with all their component
 // groups back to back (the ring's Bluestein tables then come from HBM into
 // that XCD's L2 once).  Returns false past the last ring.
+#ifndef GS_RING_XCD
+#define GS_RING_XCD 1
+#endif
 __device__ __forceinline__ bool ring_mc_slot(int nring, int ncg, int& idx, int& cg) {
+    if (!GS_RING_XCD) {                            // A/B: ring-major, ring fastest
+        idx = blockIdx.x % nring;
+        cg = blockIdx.x / nring;
+        return cg < ncg;
+    }
     const int lin = blockIdx.x, xcd = lin & 7, slot = lin >> 3;
     const int j = slot / (2 * ncg), rem = slot - j * 2 * ncg;
     idx = 2 * (8 * j + xcd) + rem / ncg;
@@ -2133,6 +2141,13 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #else
 #define GS_MF_ANA_ATTR
 #endif
+// LDS row padding (doubles) of the synthesis / analysis staging (A/B: 0)
+#ifndef GS_MF_SPAD
+#define GS_MF_SPAD 8
+#endif
+#ifndef GS_MF_APAD
+#define GS_MF_APAD 16
+#endif
 constexpr int MF_CH = 32;                          // l staged per chunk (two blocks)
 template <int SPIN, int CGW, int CPW>
 __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_mfma(ShtDev D, MfTab T, const double2* __restrict__ ain,
@@ -2147,7 +2162,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // per l one row of MPW x 2), padded by 64 B: the four 16-lane groups of a
     // wave read four consecutive l, and rows 128 B apart mod 256 B put the two
     // groups of each half-wave on disjoint banks
-    constexpr int SR = SPIN == 2 ? MPW * 4 + 8 : MPW * 2 + 8;
+    constexpr int SR = SPIN == 2 ? MPW * 4 + GS_MF_SPAD : MPW * 2 + GS_MF_SPAD;
     constexpr int NROW = SPIN == 2 ? 2 * MF_CH : MF_CH;
     __shared__ __attribute__((aligned(16))) double sb[NROW * SR];
     // spin 2: the chunk's per-l coefficients (P, Q, R, T, Rm, 0) of F1 / F2
@@ -2407,7 +2422,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     // 16 consecutive doubles; rows padded to 128 B mod 256 B, so the two groups
     // of a half-wave (pairs 4 s + g, g = 0 / 1 and 2 / 3) use disjoint banks
     constexpr int HV = NV / 2;
-    constexpr int RW = 2 * MPW * HV + 16;
+    constexpr int RW = 2 * MPW * HV + GS_MF_APAD;
     __shared__ __attribute__((aligned(16))) double sp_[MF_TILE * RW];
     const int L = D.L, npair = D.npair;
     // XCD-aware order (1-D grid over (m, window group)): blocks lin, lin + 8,

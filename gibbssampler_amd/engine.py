@@ -265,14 +265,6 @@ class GibbsPlan:
         C.check(self.lib.gs_nc_decide(self._h, C.ptr(dl), C.ptr(u_acc), int(seed), int(iteration), C.ptr(accept),
                                       self._s()), "gs_nc_decide")
 
-    def nc_decide_chain(self, dl, seed=0, iteration=0, accept=None, trace=None, capacity=0, next_prologue=True):
-        """nc_decide_fused that also draws the next iteration's prologue (True
-        when drawn: the next step skips nc_prologue)"""
-        rc = self.lib.gs_nc_decide_chain(self._h, C.ptr(dl), int(seed), int(iteration), C.ptr(accept), C.ptr(trace),
-                                         int(capacity), int(bool(next_prologue)), self._s())
-        C.check(min(rc, 0), "gs_nc_decide_chain")
-        return rc == 0
-
     def nc_decide_fused(self, dl, seed=0, iteration=0, accept=None, trace=None, capacity=0):
         C.check(self.lib.gs_nc_decide_fused(self._h, C.ptr(dl), int(seed), int(iteration), C.ptr(accept),
                                             C.ptr(trace), int(capacity), self._s()), "gs_nc_decide_fused")

@@ -221,14 +221,11 @@ class BatchedRunner:
                     # accept_trace [nsteps, nchains, nacc]: step i writes its own slot
                     acc = self.accept if accept_trace is None else accept_trace[i]
                     if self.kind == "noncentered":
-                        # the previous step's MH launch drew this step's prologue
-                        # (proposals, accept uniforms, block parameters) when it could
-                        if i == 0 or not drawn:
-                            p.nc_prologue(self.dl, seed=self.seed)
+                        p.nc_prologue(self.dl, seed=self.seed)
                         p.nc_sweep(self.d, self.dl, self.s, seed=self.seed, finish=False)
                         p.nc_finish()
-                        drawn = p.nc_decide_chain(self.dl, seed=self.seed, accept=acc, trace=trace,
-                                                  capacity=trace_capacity or 0, next_prologue=i + 1 < nsteps)
+                        p.nc_decide_fused(self.dl, seed=self.seed, accept=acc, trace=trace,
+                                          capacity=trace_capacity or 0)
                     elif self.kind == "centered":
                         p.step_centered_fused(self.d, self.dl, self.s, seed=self.seed, trace=trace,
                                               capacity=trace_capacity or 0)

@@ -174,15 +174,6 @@ int gs_nc_decide(gs_plan* plan, double* dl_binned, const double* u_accept_replay
  * workgroup read it at its start). */
 int gs_nc_decide_fused(gs_plan* plan, double* dl_binned, uint64_t seed, uint32_t iteration, int32_t* accept_out,
                        double* trace, int capacity, void* stream);
-/* gs_nc_decide_fused that, with next_prologue = 1, also draws the NEXT
- * iteration's prologue (gs_nc_prologue's proposals from the new D_l, accept
- * uniforms and block parameters for iteration + 1: the same values) in the
- * same launch, so a graph-captured run launches one prologue per replay
- * instead of one per step (NonCenteredGibbs.py:401-445 then 292-330).  Returns
- * 0 when drawn, 1 when this plan's MH form cannot (the caller launches
- * gs_nc_prologue before the next step), < 0 on error.  Native RNG only. */
-int gs_nc_decide_chain(gs_plan* plan, double* dl_binned, uint64_t seed, uint32_t iteration, int32_t* accept_out,
-                       double* trace, int capacity, int next_prologue, void* stream);
 /* dl_tmp_out: nullable, receives the centered draw; recentre: 0 lazy (s_out keeps the
  * centered CR draw), 1 materialise the re-centred map in s_out */
 int gs_step_asis(gs_plan* plan, const double* d_alm, double* dl_binned, double* s_out,
