@@ -1476,8 +1476,10 @@ __device__ __forceinline__ void dft_mc(double2* buf, int SB, int nc, const PairG
 // 1 share every 128-B line of the phase planes) with all their component
 // groups back to back (the ring's Bluestein tables then come from HBM into
 // that XCD's L2 once).  Returns false past the last ring.
+// measured: the XCD order 332 / 350 us against 318 / 340 us ring-major
+// (synthesis / analysis ring stage, 16 spin-2 maps, same box): off
 #ifndef GS_RING_XCD
-#define GS_RING_XCD 1
+#define GS_RING_XCD 0
 #endif
 __device__ __forceinline__ bool ring_mc_slot(int nring, int ncg, int& idx, int& cg) {
     if (!GS_RING_XCD) {                            // A/B: ring-major, ring fastest
@@ -2141,6 +2143,21 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #else
 #define GS_MF_ANA_ATTR
 #endif
+// synthesis staging item order: 1 = consecutive threads take consecutive maps
+// at one l (LDS rows written contiguously; each quarter-wave's global reads
+// touch 16 lines), 0 = consecutive l of one map (coalesced global reads; the
+// LDS writes then step a row per thread, 16-way bank conflicts)
+#ifndef GS_MF_SMAP
+#define GS_MF_SMAP 1
+#endif
+// analysis staging item order: 1 = consecutive threads take consecutive maps
+// of one ring pair (LDS rows written contiguously), 0 = consecutive pairs of
+// one map (phase reads in 64-B runs; LDS writes a row apart per thread).
+// Measured (16 spin-2 maps, same box): 0 = 651 us, 1 = 805 us; the synthesis'
+// GS_MF_SMAP 1 / 0 = 567 / 591 us
+#ifndef GS_MF_AMAP
+#define GS_MF_AMAP 0
+#endif
 // LDS row padding (doubles) of the synthesis / analysis staging (A/B: 0)
 #ifndef GS_MF_SPAD
 #define GS_MF_SPAD 8
@@ -2209,13 +2226,12 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
             }
         }
     };
-    // item i: l = chunk start + i % MF_CH, map c0 + i / MF_CH (consecutive
-    // threads read consecutive l of one map)
+    // item i: (l, map) in the GS_MF_SMAP order
     auto fetch = [&](int cb, double2 (&pf)[PER][SPIN == 2 ? 2 : 1]) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
-            const int lr = i % MF_CH, mp = i / MF_CH;
+            const int lr = GS_MF_SMAP ? i / MPW : i % MF_CH, mp = GS_MF_SMAP ? i % MPW : i / MF_CH;
             const int l = m + cb * MF_TILE + lr, c = c0 + mp;
             const bool ok = !(GS_MF_EXP & 2) && i < NIT && l <= L && c < nmap;
             // clamped address: the load is unconditional, the value selected when
@@ -2230,7 +2246,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
             if (i >= NIT) continue;
-            const int lr = i % MF_CH, mp = i / MF_CH;
+            const int lr = GS_MF_SMAP ? i / MPW : i % MF_CH, mp = GS_MF_SMAP ? i % MPW : i / MF_CH;
             const bool ok = m + cb * MF_TILE + lr <= L && c0 + mp < nmap;
             if constexpr (SPIN == 2) {
                 const double ex = ok ? pf[k][0].x : 0.0, ey = ok ? pf[k][0].y : 0.0;
@@ -2453,7 +2469,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
-            const int jp = i % MF_TILE, mp = i / MF_TILE;     // lanes: consecutive pairs of one map
+            const int jp = GS_MF_AMAP ? i / MPW : i % MF_TILE, mp = GS_MF_AMAP ? i % MPW : i / MF_TILE;
             const int pr = MF_TILE * t + jp, map = c0 + mp;
             const double2 z = make_double2(0.0, 0.0);
             pf[k] = Ph{z, z, z, z};
@@ -2525,7 +2541,8 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
             if (i >= NIT) continue;
-            double* dp = sp_ + (i % MF_TILE) * RW + (i / MF_TILE) * HV;   // N + S
+            const int jp = GS_MF_AMAP ? i / MPW : i % MF_TILE, mp = GS_MF_AMAP ? i % MPW : i / MF_TILE;
+            double* dp = sp_ + jp * RW + mp * HV;                            // N + S
             double* dm = dp + MPW * HV;                                      // N - S
             const Ph& q = pf[k];
             if constexpr (SPIN == 2) {          // a = Q north, b = Q south, c = U north, d = U south
