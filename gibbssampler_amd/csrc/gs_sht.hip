@@ -2143,6 +2143,10 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #else
 #define GS_MF_ANA_ATTR
 #endif
+// (measured, 16 spin-2 maps, same box: 0 = 563 us, 1 = 544 us)
+#ifndef GS_MF_SYN_XCD
+#define GS_MF_SYN_XCD 1
+#endif
 // synthesis staging item order: 1 = consecutive threads take consecutive maps
 // at one l (LDS rows written contiguously; each quarter-wave's global reads
 // touch 16 lines), 0 = consecutive l of one map (coalesced global reads; the
@@ -2185,14 +2189,25 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // spin 2: the chunk's per-l coefficients (P, Q, R, T, Rm, 0) of F1 / F2
     __shared__ __attribute__((aligned(16))) double sc[SPIN == 2 ? MF_CH * 6 : 2];
     const int L = D.L, nlm = D.nlm, npair = D.npair;
-    // grid (tile group, m, map group): the 8 tile groups of one m are
-    // consecutive blocks -- one per XCD, at the same time, so m's a_lm come
-    // from HBM once (the other XCDs hit the infinity cache) -- and the 4 m of a
-    // phase block written by one tile group all land on that tile group's XCD
-    const int m = blockIdx.y;
+    // GS_MF_SYN_XCD 0: grid (tile group, m, map group): the tile groups of one
+    // m are consecutive blocks -- one per XCD, at the same time, so m's a_lm
+    // come from HBM once (the other XCDs hit the infinity cache) -- and the 4 m
+    // of a phase block written by one tile group land on that tile group's XCD.
+    // 1: a 1-D grid in which each XCD takes whole phase blocks (4 m x every
+    // tile group) back to back: a_lm and phase lines both stay in one L2.
+    int m, tg;
+    if (GS_MF_SYN_XCD) {
+        const int ty = (T.ntile + 3) / 4, lin = blockIdx.x, slot = lin >> 3, per = PHI_MB * ty;
+        m = ((slot / per) * 8 + (lin & 7)) * PHI_MB + (slot % per) / ty;
+        tg = (slot % per) % ty;
+        if (m > L) return;
+    } else {
+        m = blockIdx.y;
+        tg = blockIdx.x;
+    }
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int t = blockIdx.x * 4 + wave / H;
+    const int t = tg * 4 + wave / H;
     const int cg0 = (wave % H) * CPW;             // this wave's first column group
     const int c0 = blockIdx.z * MPW;
     const int nb = (L - m + MF_TILE) / MF_TILE;
@@ -3281,12 +3296,16 @@ static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
     const MfTab T = p->mftab();
     const unsigned ty = (unsigned)((p->mf_ntile + 3) / 4);
     const dim3 blk(256 * (MF_CGW / CPW));
+    // (GS_MF_SYN_XCD 1: 1-D over whole phase blocks)
+    const int nmb = (p->L + 1 + PHI_MB - 1) / PHI_MB;
+    const unsigned gx = GS_MF_SYN_XCD ? (unsigned)(((nmb + 7) / 8) * 8 * PHI_MB * ty) : ty;
+    const unsigned gy = GS_MF_SYN_XCD ? 1u : (unsigned)(p->L + 1);
     if (ncomp != 2) {               // T (spin 0): comp 0
-        const dim3 g(ty, p->L + 1, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
+        const dim3 g(gx, gy, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0);
     }
     if (ncomp != 1) {               // E, B -> Q, U: comps ncomp - 2, ncomp - 1
-        const dim3 g(ty, p->L + 1, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
+        const dim3 g(gx, gy, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp,
                            ncomp - 2);
     }
