@@ -121,6 +121,7 @@ _SIGS = [
     ("gs_sht_set_mfma", ctypes.c_int, [_VP, ctypes.c_int]),
     ("gs_sht_mfma_info", ctypes.c_int, [_VP, c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
     ("gs_sht_alm2map_batch", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP]),
+    ("gs_sht_apply_weighted_batch", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP]),
     ("gs_sht_map2alm_batch", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP,
                                             ctypes.c_int, _VP]),
     ("gs_masked_create", ctypes.c_int, [ctypes.POINTER(GsMaskedDesc), _VP, _VP, ctypes.POINTER(_VP)]),

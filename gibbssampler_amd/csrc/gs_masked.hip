@@ -1451,8 +1451,9 @@ int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* 
 // per-block p . Q p of every chain
 static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, double* partial, int nb,
                      const PcgState* state, hipStream_t st) {
-    if (mc_synth(c, c->B, x, c->pix0, st)) return -1;
-    if (gs_sht_map2alm_batch(c->sht, c->B, c->F, GS_ALM_REAL, c->pix0, c->ninv, c->r, 0, st)) return -1;
+    // r = map2alm(N^-1 A b x): one fused operator pass (the maps stay in LDS on
+    // the table path; bit-identical to alm2map_beamed + map2alm_weighted)
+    if (gs_sht_apply_weighted_batch(c->sht, c->B, c->F, x, c->bl, c->ninv, c->pix0, c->r, st)) return -1;
     const dim3 g(partial ? nb : nblocks(c->nlm, RED_BLOCK), c->B), b(RED_BLOCK);
     const double iw = 1.0 / c->w;
     if (c->F == 1) hipLaunchKernelGGL(k_pcg_qdot<1>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);

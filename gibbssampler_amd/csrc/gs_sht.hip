@@ -1653,6 +1653,130 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring_mc(int L, int npair, lon
     }
 }
 
+// weighted operator ring stage (the masked PCG's A^T N^-1 A): per ring pair the
+// synthesis ring work (fold, inverse DFT), the pixel weights, and the analysis
+// ring work (forward DFT, unfold) in one workgroup, the pixels never leaving
+// LDS: the same arithmetic as k_sht_synth_ring_mc, a map stored and reloaded,
+// and k_sht_anal_ring_mc on weights x map (bit-identical), phases updated in
+// place (each pair's phases are read and written by its own workgroup only)
+template <int NV>
+__global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, long long npix,
+                                                            const int* __restrict__ pairs,
+                                                            const PairGeom* __restrict__ geom, double2* phi,
+                                                            const double2* __restrict__ tw, int Mmax,
+                                                            const double2* __restrict__ bsk, int ncomp, int NCB, int SB,
+                                                            int twoff, const double* __restrict__ wts, int wnc,
+                                                            int nring) {
+    extern __shared__ double2 lbuf[];
+    int idx, cg;
+    if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
+    const int p = pairs[idx];
+    const int c0 = cg * NCB;
+    const int nc = min(NCB, ncomp - c0);
+    const PairGeom g = geom[p];
+    const int TC = blockDim.x / NCB;
+    const int cl = threadIdx.x / TC, tl = threadIdx.x - cl * TC;
+    const bool live = cl < nc;
+    int twM = Mmax;
+    const double2* twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
+    double2* buf = lbuf + cl * SB;
+    Fold4* red = reinterpret_cast<Fold4*>(buf);
+    const int n = g.nphi;
+    const long long plane = phi_plane(L, npair);
+    const double2* PN = phi + (2LL * (live ? c0 + cl : 0) + 0) * plane;
+    const double2* PS = PN + plane;
+    const bool eq = g.startS < 0;
+    const int K = n / 2 + 1;
+    const int J = K >= TC ? 1 : TC / K;
+    auto H = [&](const double2* P, int m, bool neg) {
+        const double2 v = P[phi_at(m, p, npair)];
+        const double cm = (m == 0 ? 1.0 : 2.0) * (neg ? -1.0 : 1.0);
+        return make_double2(cm * v.x, cm * v.y);
+    };
+    for (int s0 = 0; s0 < K * J; s0 += TC) {
+        const int sl = s0 + tl;
+        Fold4 f = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
+        const int k = sl % K, j0 = sl / K;
+        const int nk = (n - k) % n;
+        const bool on = live && sl < K * J;
+        if (on) {
+            for (int m = k + j0 * n, q = j0; m <= L; m += J * n, q += J) {
+                const bool neg = g.phi_half && (q & 1);
+                const double2 a = H(PN, m, neg);
+                f.nk.x += a.x; f.nk.y += a.y;
+                if (!eq) { const double2 b = H(PS, m, neg); f.sk.x += b.x; f.sk.y += b.y; }
+            }
+            if (nk != k)
+                for (int m = nk + j0 * n, q = j0; m <= L; m += J * n, q += J) {
+                    const bool neg = g.phi_half && (q & 1);
+                    const double2 a = H(PN, m, neg);
+                    f.nmk.x += a.x; f.nmk.y += a.y;
+                    if (!eq) { const double2 b = H(PS, m, neg); f.smk.x += b.x; f.smk.y += b.y; }
+                }
+        }
+        if (J > 1) {
+            if (live) red[tl] = f;
+            __syncthreads();
+            if (on && j0 == 0) {
+                for (int jj = 1; jj < J; ++jj) {
+                    const Fold4 o = red[tl + jj * K];
+                    f.nk.x += o.nk.x; f.nk.y += o.nk.y; f.nmk.x += o.nmk.x; f.nmk.y += o.nmk.y;
+                    f.sk.x += o.sk.x; f.sk.y += o.sk.y; f.smk.x += o.smk.x; f.smk.y += o.smk.y;
+                }
+            }
+            __syncthreads();
+        }
+        if (on && j0 == 0) {
+            if (g.phi_half) {
+                const double2 ek = expi_pi_u32(k, n);
+                const double2 enk = make_double2(-ek.x, ek.y);
+                f.nk = cmul(f.nk, ek);
+                f.sk = cmul(f.sk, ek);
+                f.nmk = cmul(f.nmk, enk);
+                f.smk = cmul(f.smk, enk);
+            }
+            if (nk == k) { f.nmk = f.nk; f.smk = f.sk; }
+            const double2 hn = make_double2(0.5 * (f.nk.x + f.nmk.x), 0.5 * (f.nk.y - f.nmk.y));
+            const double2 hs = make_double2(0.5 * (f.sk.x + f.smk.x), 0.5 * (f.sk.y - f.smk.y));
+            buf[k] = make_double2(hn.x - hs.y, hn.y + hs.x);
+            if (nk != k) {
+                const double2 hn2 = make_double2(hn.x, -hn.y), hs2 = make_double2(hs.x, -hs.y);
+                buf[nk] = make_double2(hn2.x - hs2.y, hn2.y + hs2.x);
+            }
+        }
+    }
+    __syncthreads();
+    dft_mc<NV>(lbuf, SB, nc, g, +1, twx, twM, bsk);
+    // the ring's pixels (north .x, south .y) times the weights: the analysis input
+    for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
+        const int c = jj / n, j = jj - c * n;
+        const double* wc = wts + (long long)((c0 + c) % wnc) * npix;
+        const double2 y = lbuf[c * SB + j];
+        lbuf[c * SB + j] = make_double2(wc[g.startN + j] * y.x, eq ? 0.0 : wc[g.startS + j] * y.y);
+    }
+    __syncthreads();
+    dft_mc<NV>(lbuf, SB, nc, g, -1, twx, twM, bsk);
+    for (int jj = threadIdx.x; jj < nc * (L + 1); jj += blockDim.x) {
+        const int c = jj / (L + 1), m = jj - c * (L + 1);
+        const double2* b2 = lbuf + c * SB;
+        double2* oN = phi + (2LL * (c0 + c) + 0) * plane;
+        double2* oS = oN + plane;
+        const int k = m % n;
+        const int nk = k == 0 ? 0 : n - k;
+        const double2 a = b2[k], b = b2[nk];
+        double2 xn = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+        double2 xs = make_double2(0.5 * (a.y + b.y), -0.5 * (a.x - b.x));
+        if (g.phi_half) {
+            const double2 e = expi_pi_neg_u32(m, n);
+            xn = cmul(xn, e);
+            xs = cmul(xs, e);
+        }
+        if (m == 0) { xn.y = 0.0; xs.y = 0.0; }
+        oN[phi_at(m, p, npair)] = xn;
+        oS[phi_at(m, p, npair)] = eq ? make_double2(0.0, 0.0) : xs;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // analysis: Legendre stage.  grid (m pairs or m, tiles of 4 ASR groups of 64 ring pairs)
 // out: part[tile][comp][nlm] (double2), unweighted sums
@@ -3023,7 +3147,8 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       LDS_FFT_MAX * (int)sizeof(double2) + 64 * 4 * (int)sizeof(double2));
-        const void* mc[] = {(const void*)k_sht_synth_ring_mc<8>, (const void*)k_sht_anal_ring_mc<8>};
+        const void* mc[] = {(const void*)k_sht_synth_ring_mc<8>, (const void*)k_sht_anal_ring_mc<8>,
+                            (const void*)k_sht_apply_ring_mc<8>};
         for (const void* f : mc)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RING_MC_LDS_MAX);
         (void)hipGetLastError();
@@ -3622,6 +3747,40 @@ int gs_sht_reserve(gs_sht* p, int nmap, void* stream) {
 int gs_sht_alm2map_batch(gs_sht* p, int nmap, int ncomp, int layout, const double* alm, const double* bl,
                          double* maps, void* stream) {
     return sht_alm2map(p, nmap, ncomp, layout, alm, bl, maps, stream);
+}
+
+// alm_out = map2alm(weights x alm2map(bl x alm_in)) (real layout): on the
+// table path with the multi-component ring stage the maps never leave LDS
+// (k_sht_apply_ring_mc); otherwise the two transforms through maps_scratch
+int gs_sht_apply_weighted_batch(gs_sht* p, int nmap, int ncomp, const double* alm_in, const double* bl,
+                                const double* weights, double* maps_scratch, double* alm_out, void* stream) {
+    if (check_sht(p)) return -1;
+    if (ncomp < 1 || ncomp > 3 || nmap < 1 || !alm_in || !weights || !alm_out)
+        return set_error("gs_sht_apply_weighted_batch: bad argument");
+    const int M = p->merged_M;
+    const int ncb = (p->mf && p->merged_n > 0) ? ring_mc_ncb(M, nmap * ncomp) : 1;
+    if (ncb < 2 || std::getenv("GS_SHT_NO_FUSED_APPLY")) {
+        if (!maps_scratch) return set_error("gs_sht_apply_weighted_batch: this plan needs maps_scratch");
+        if (sht_alm2map(p, nmap, ncomp, GS_ALM_REAL, alm_in, bl, maps_scratch, stream)) return -1;
+        return gs_sht_map2alm_batch(p, nmap, ncomp, GS_ALM_REAL, maps_scratch, weights, alm_out, 0, stream);
+    }
+    if (sht_reserve(p, nmap, S(stream))) return -1;
+    const long long nin = (long long)nmap * ncomp * p->nlm;
+    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * ncomp,
+                       alm_in, GS_ALM_REAL, p->ain, bl);
+    GS_LAUNCH_CHECK("k_sht_alm_in");
+    if (sht_synth_mfma(p, nmap, ncomp, S(stream))) return -1;
+    {
+        const int bd = ring_block(M), bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
+        const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
+        const int nc = nmap * ncomp, ncg = (nc + ncb - 1) / ncb;
+        const dim3 gm((unsigned)(8 * ((p->merged_n + 15) / 16) * 2 * ncg));
+        hipLaunchKernelGGL(k_sht_apply_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
+                           p->merged_pairs, p->geom, p->phi, p->tw, p->Mmax, p->bsk, nc, ncb, SB, toff, weights, ncomp,
+                           p->merged_n);
+        GS_LAUNCH_CHECK("k_sht_apply_ring_mc");
+    }
+    return sht_anal_mfma(p, nmap, ncomp, GS_ALM_REAL, 0, alm_out, S(stream));
 }
 
 int gs_sht_map2alm_batch(gs_sht* p, int nmap, int ncomp, int layout, const double* maps, const double* weights,

@@ -84,6 +84,22 @@ class HealpixSHT:
                                                   _capi.ptr(o), int(iter), _capi.stream_ptr()), "gs_sht_map2alm_batch")
         return out
 
+    def apply_weighted_batch(self, alm, ncomp, weights, bl=None, out=None):
+        """alm [B, ncomp, n] (real layout) -> map2alm(weights * alm2map(bl x alm)):
+        the masked PCG operator's transform pair (CenteredGibbs.py:448-491), the
+        maps kept on chip on the table path (gs_sht_apply_weighted_batch)."""
+        B = alm.shape[0]
+        a = alm.contiguous()
+        w = weights.contiguous()
+        if out is None:
+            out = torch.empty((B, ncomp, self.nreal), dtype=torch.float64, device=alm.device)
+        scratch = torch.empty((B, ncomp, self.npix), dtype=torch.float64, device=alm.device)
+        _capi.check(self.lib.gs_sht_apply_weighted_batch(self.handle, B, ncomp, _capi.ptr(a),
+                                                         _capi.ptr(None if bl is None else bl.contiguous()),
+                                                         _capi.ptr(w), _capi.ptr(scratch), _capi.ptr(out),
+                                                         _capi.stream_ptr()), "gs_sht_apply_weighted_batch")
+        return out
+
     # -- shapes -----------------------------------------------------------------
     @property
     def nreal(self):

@@ -255,6 +255,16 @@ int gs_sht_set_mfma(gs_sht* sht, int on);
 int gs_sht_mfma_info(const gs_sht* sht, int* on, long long* table_bytes);
 int gs_sht_alm2map_batch(gs_sht* sht, int nmap, int ncomp, int layout, const double* alm, const double* bl,
                          double* maps, void* stream);
+/* the masked PCG operator's transform pair in one call: alm_out =
+ * map2alm(weights x alm2map(bl x alm_in)), real layout, niter 0 (the
+ * reference's hp.map2alm(N^-1 hp.alm2map(almxfl(s, b_l))) of its PCG fwd_op,
+ * CenteredGibbs.py:448-491).  On the matrix-core table path with the
+ * multi-component ring stage the per-ring synthesis, weighting and analysis run
+ * in one workgroup and the maps never reach HBM (bit-identical to the two
+ * calls); otherwise the two calls through maps_scratch ([nmap][ncomp][Npix],
+ * may be NULL only on the fused path). */
+int gs_sht_apply_weighted_batch(gs_sht* sht, int nmap, int ncomp, const double* alm_in, const double* bl,
+                                const double* weights, double* maps_scratch, double* alm_out, void* stream);
 int gs_sht_map2alm_batch(gs_sht* sht, int nmap, int ncomp, int layout, const double* maps, const double* weights,
                          double* alm, int niter, void* stream);
 

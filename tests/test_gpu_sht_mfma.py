@@ -132,6 +132,26 @@ def test_mfma_batch_bit_identical(ncomp):
         assert torch.equal(ab[b], one[0]), f"map2alm map {b}"
 
 
+@pytest.mark.parametrize("mfma", [True, False])
+@pytest.mark.parametrize("ncomp,N,L,B", [(2, 16, 37, 5), (1, 16, 37, 3), (3, 8, 20, 2), (2, 64, 128, 4)])
+def test_apply_weighted_equals_two_transforms(mfma, ncomp, N, L, B):
+    """the fused operator pass (maps on chip) = alm2map(beamed) then the weighted
+    map2alm, bit for bit, on the table path and on the recurrence path"""
+    from gibbssampler_amd.sht import HealpixSHT
+    sht = HealpixSHT(N, L).set_mfma(mfma)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    npix = 12 * N * N
+    alm = torch.randn((B, ncomp, (L + 1) ** 2), dtype=torch.float64, device="cuda", generator=g)
+    w = torch.rand((ncomp, npix), dtype=torch.float64, device="cuda", generator=g)
+    w[:, : npix // 7] = 0.0
+    bl = torch.linspace(1.0, 0.3, L + 1, dtype=torch.float64, device="cuda")
+    want = sht.map2alm_batch(sht.alm2map_batch(alm, ncomp, bl=bl), ncomp, weights=w)
+    got = sht.apply_weighted_batch(alm, ncomp, w, bl=bl)
+    assert torch.equal(got, want)
+    for b in (0, B - 1):
+        assert torch.equal(sht.apply_weighted_batch(alm[b:b + 1], ncomp, w, bl=bl)[0], got[b]), b
+
+
 def test_mfma_round_trip_and_adjoint_nside256():
     """band-limited round trip (iter 3) and exact adjointness on the table path"""
     from gibbssampler_amd.sht import HealpixSHT
