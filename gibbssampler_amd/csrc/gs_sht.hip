@@ -1494,6 +1494,50 @@ __device__ __forceinline__ bool ring_mc_slot(int nring, int ncg, int& idx, int& 
     return idx < nring;
 }
 
+// a ring pair without weight (pflag 0): its analysis phases are exact zeros
+// (0 x pixel, transformed) and are written as such, no ring work
+__device__ __forceinline__ void ring_zero_phases(int L, int npair, int p, double2* phi, int c0, int nc) {
+    const long long plane = phi_plane(L, npair);
+    for (int jj = threadIdx.x; jj < nc * (L + 1); jj += blockDim.x) {
+        const int c = jj / (L + 1), m = jj - c * (L + 1);
+        double2* oN = phi + (2LL * (c0 + c) + 0) * plane;
+        oN[phi_at(m, p, npair)] = make_double2(0.0, 0.0);
+        oN[plane + phi_at(m, p, npair)] = make_double2(0.0, 0.0);
+    }
+}
+
+// the support of a weighted analysis: pflag[p] = 1 when a pixel of either ring
+// of pair p has a nonzero weight in some component (one workgroup per pair).
+// A pair without weight contributes exact zeros to the analysis (0 x pixel),
+// so the ring stage writes its phases as zeros and the matrix-core Legendre
+// stages skip 16-pair tiles without weight -- the same bits, less work (a
+// galactic cut in galactic coordinates removes whole equatorial rings; the
+// bench's |cos theta| > 0.2 band 15 % of the pairs, 4 of 32 tiles)
+__global__ __launch_bounds__(256) void k_pair_support(long long npix, const PairGeom* __restrict__ geom,
+                                                      const double* __restrict__ wts, int wnc, int* __restrict__ pflag) {
+    const int p = blockIdx.x;
+    const PairGeom g = geom[p];
+    const int n = g.nphi;
+    const bool eq = g.startS < 0;
+    int any = 0;
+    for (int i = threadIdx.x; i < wnc * n; i += blockDim.x) {
+        const int c = i / n, j = i - c * n;
+        const double* wc = wts + (long long)c * npix;
+        any |= wc[g.startN + j] != 0.0;
+        if (!eq) any |= wc[g.startS + j] != 0.0;
+    }
+    any = __syncthreads_or(any);
+    if (threadIdx.x == 0) pflag[p] = any;
+}
+
+// tile t (pairs 16 t ..) has weight: any of its pair flags
+__device__ __forceinline__ bool tile_support(const int* __restrict__ pflag, int t, int npair) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) any |= 16 * t + k < npair && pflag[min(16 * t + k, npair - 1)] != 0;
+    return any;
+}
+
 // synthesis: 1-D grid over (ring pair, component group of NCB) (ring_mc_slot);
 // LDS NCB x SB + twiddles
 template <int NV>
@@ -1607,13 +1651,15 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring_mc(int L, int npair, lon
                                                            const double2* __restrict__ tw, int Mmax,
                                                            const double2* __restrict__ bsk, double2* __restrict__ phi,
                                                            int ncomp, int NCB, int SB, int twoff,
-                                                           const double* __restrict__ wts, int wnc, int nring) {
+                                                           const double* __restrict__ wts, int wnc, int nring,
+                                                           const int* __restrict__ pflag) {
     extern __shared__ double2 lbuf[];
     int idx, cg;
     if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
     const int p = pairs[idx];
     const int c0 = cg * NCB;
     const int nc = min(NCB, ncomp - c0);
+    if (pflag && !pflag[p]) { ring_zero_phases(L, npair, p, phi, c0, nc); return; }
     const PairGeom g = geom[p];
     int twM = Mmax;
     const double2* twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
@@ -1666,13 +1712,14 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
                                                             const double2* __restrict__ tw, int Mmax,
                                                             const double2* __restrict__ bsk, int ncomp, int NCB, int SB,
                                                             int twoff, const double* __restrict__ wts, int wnc,
-                                                            int nring) {
+                                                            int nring, const int* __restrict__ pflag) {
     extern __shared__ double2 lbuf[];
     int idx, cg;
     if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
     const int p = pairs[idx];
     const int c0 = cg * NCB;
     const int nc = min(NCB, ncomp - c0);
+    if (pflag && !pflag[p]) { ring_zero_phases(L, npair, p, phi, c0, nc); return; }
     const PairGeom g = geom[p];
     const int TC = blockDim.x / NCB;
     const int cl = threadIdx.x / TC, tl = threadIdx.x - cl * TC;
@@ -2293,10 +2340,17 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #ifndef GS_MF_APAD
 #define GS_MF_APAD 16
 #endif
+// table prefetch distance of the synthesis in blocks (1: the block after the
+// one being multiplied; 2: two blocks ahead, a second register set)
+#ifndef GS_MF_TPF
+#define GS_MF_TPF 2
+#endif
 constexpr int MF_CH = 32;                          // l staged per chunk (two blocks)
+constexpr int MF_TL_MAX = 256;                     // tiles of a support-skipping analysis (N_side <= 2048)
 template <int SPIN, int CGW, int CPW>
 __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_mfma(ShtDev D, MfTab T, const double2* __restrict__ ain,
-                                                        double2* __restrict__ phi, int nmap, int ncm, int cbase) {
+                                                        double2* __restrict__ phi, int nmap, int ncm, int cbase,
+                                                        const int* __restrict__ pflag) {
     constexpr int CPG = SPIN == 2 ? 4 : 8;         // maps per 16-column group
     constexpr int MPW = CGW * CPG;                 // maps per workgroup
     constexpr int NIT = MF_CH * MPW;               // staged (l, map) items per chunk
@@ -2329,14 +2383,22 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         m = blockIdx.y;
         tg = blockIdx.x;
     }
+    // pflag (the fused weighted operator): tiles without weight need no phases
+    // (the ring stage writes zeros there); a tile group without any leaves
+    if (pflag) {
+        bool any = false;
+        for (int k = 0; k < 4; ++k) any |= tg * 4 + k < T.ntile && tile_support(pflag, tg * 4 + k, D.npair);
+        if (!any) return;
+    }
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int t = tg * 4 + wave / H;
+    const bool tlive = t < T.ntile && (!pflag || tile_support(pflag, t, D.npair));
     const int cg0 = (wave % H) * CPW;             // this wave's first column group
     const int c0 = blockIdx.z * MPW;
     const int nb = (L - m + MF_TILE) / MF_TILE;
     const long long ti = (long long)m * T.ntile + min(t, T.ntile - 1);
-    const int b0 = t < T.ntile ? T.b0[ti] : nb;
+    const int b0 = tlive ? T.b0[ti] : nb;
     const double* tab = T.tab + (t < T.ntile ? T.off[ti] : 0) * MF_BLK;
     const long long base = cidx(L, m, m) - m;
     // the lane's ring pair (F1 / F2 geometry)
@@ -2456,8 +2518,10 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // ahead, its table registers refilled with block b + 1's values as soon as
     // they are consumed (a block of MFMAs ahead of their use)
     auto mma = [&](int b, int lr0, double (&gv)[8]) __attribute__((always_inline)) {
-        const double* nblk = tblk(b + 1);
-        const bool nprev = b >= b0 && b + 1 < nb;    // blocks b and b + 1 stored (b + 1's row above)
+        // refill with block b + GS_MF_TPF (its row above: block b + GS_MF_TPF - 1's
+        // last row, read when both blocks are stored)
+        const double* nblk = tblk(b + GS_MF_TPF);
+        const bool nprev = b + GS_MF_TPF - 1 >= b0 && b + GS_MF_TPF < nb;
         const bool prev = b - 1 >= b0;               // block b's
         // every load unconditional (a load in one arm of a branch makes the
         // compiler's wait at the join cover the other arm's registers too); only
@@ -2511,9 +2575,19 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         }
     };
     double2 pf[PER][SPIN == 2 ? 2 : 1];
-    double gv[8];
+    double gv[8], gw[8];
+    auto tload4 = [&](int b, double (&g)[8]) __attribute__((always_inline)) {
+        const bool pv = b - 1 >= b0 && b < nb;
+        if constexpr (SPIN == 2) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) tload(tblk(0), false, q, gv);
+            for (int q = 0; q < 4; ++q) tload(tblk(b), pv, q, g);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tload(tblk(b), false, q, g);
+        }
+    };
+    tload4(0, gv);
+    if (GS_MF_TPF == 2) tload4(1, gw);
     fetch(0, pf);
     fetchc(0);
     for (int cb = 0; cb < nb; cb += MF_CH / MF_TILE) {
@@ -2523,9 +2597,9 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         if (!(GS_MF_EXP & 4)) __syncthreads();
         if (cb + MF_CH / MF_TILE < nb) { fetch(cb + MF_CH / MF_TILE, pf); fetchc(cb + MF_CH / MF_TILE); }
         mma(cb, 0, gv);
-        mma(cb + 1, MF_TILE, gv);
+        mma(cb + 1, MF_TILE, GS_MF_TPF == 2 ? gw : gv);
     }
-    if (t >= T.ntile) return;
+    if (!tlive) return;
     // D layout: lane (g, j) holds rows g + 4 r (pairs 16 t + g + 4 r), col j
     const long long plane = phi_plane(L, npair);
 #pragma unroll
@@ -2566,7 +2640,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
 template <int SPIN, int CGW, int CPW, int NT>
 __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, MfTab T, const double2* __restrict__ phi, int nmap,
                                                        int ncm, int cbase, double w, int layout, int acc,
-                                                       double* __restrict__ alm) {
+                                                       double* __restrict__ alm, const int* __restrict__ pflag) {
     constexpr int CPG = SPIN == 2 ? 4 : 8;
     constexpr int MPW = CGW * CPG;
     constexpr int NV = SPIN == 2 ? 8 : 4;          // staged doubles per (pair, map)
@@ -2579,6 +2653,8 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     constexpr int HV = NV / 2;
     constexpr int RW = 2 * MPW * HV + GS_MF_APAD;
     __shared__ __attribute__((aligned(16))) double sp_[MF_TILE * RW];
+    __shared__ int tl_[MF_TL_MAX];                 // pflag: the tiles with weight, in order
+    __shared__ int ntl_;
     const int L = D.L, npair = D.npair;
     // XCD-aware order (1-D grid over (m, window group)): blocks lin, lin + 8,
     // ... run on one XCD, and each XCD takes whole phase blocks -- the 4 m x
@@ -2692,22 +2768,45 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
             }
         }
     };
+    // the tiles summed: all, or (pflag) those with weight -- a tile without
+    // adds exact zeros, so skipping it leaves every bit of the sums
+    int ntl = T.ntile;
+    if (pflag) {
+        if (threadIdx.x < 64) {
+            int cnt = 0;
+            for (int b = 0; b < T.ntile; b += 64) {
+                const bool f = b + lane < T.ntile && tile_support(pflag, b + lane, npair);
+                const unsigned long long msk = __ballot(f);
+                if (f) tl_[cnt + __popcll(msk & ((1ull << lane) - 1))] = b + lane;
+                cnt += __popcll(msk);
+            }
+            if (lane == 0) ntl_ = cnt;
+        }
+        __syncthreads();
+        ntl = ntl_;
+    }
+    auto tile = [&](int i) __attribute__((always_inline)) {
+        return pflag ? __builtin_amdgcn_readfirstlane(tl_[i]) : i;
+    };
     Ph pf[PER];
     double gv[4][NG];
-    Tw cur = twin(0);
+    const int t0 = ntl > 0 ? tile(0) : 0;
+    Tw cur = twin(t0);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) tload(cur, 0, s, gv);
-    fetch(0, pf);
-    // tile t: stage its phases, issue tile t + 1's phases, then t's MFMAs; each
-    // slice's table registers are refilled with tile t + 1's values as soon as
-    // its MFMAs are issued (their latency hides behind the rest of the tile)
-    for (int t = 0; t < T.ntile; ++t) {
+    for (int s = 0; s < 4; ++s) tload(cur, t0, s, gv);
+    fetch(t0, pf);
+    // tile t: stage its phases, issue the next tile's phases, then t's MFMAs;
+    // each slice's table registers are refilled with the next tile's values as
+    // soon as its MFMAs are issued (their latency hides behind the rest of the tile)
+    for (int i = 0; i < ntl; ++i) {
+        const int t = tile(i);
         if (!(GS_MF_EXP & 4)) __syncthreads();
         stage(pf);
         if (!(GS_MF_EXP & 4)) __syncthreads();
-        const bool more = t + 1 < T.ntile;
-        if (more) fetch(t + 1, pf);
-        const Tw nxt = twin(more ? t + 1 : t);
+        const bool more = i + 1 < ntl;
+        const int tn = more ? tile(i + 1) : t;
+        if (more) fetch(tn, pf);
+        const Tw nxt = twin(tn);
         // A operands of slice s (a1 / a2 per parity and column group), read one
         // slice ahead of their MFMAs; every load unconditional, only the MFMAs
         // under the wave-uniform window test (see the synthesis)
@@ -2760,7 +2859,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
-            tload(nxt, more ? t + 1 : t, s, gv);    // (the last tile reloads its own: harmless)
+            tload(nxt, tn, s, gv);                  // (the last tile reloads its own: harmless)
             __builtin_amdgcn_sched_barrier(0);
         }
         cur = nxt;
@@ -2859,6 +2958,8 @@ struct gs_sht {
     // launch per length class; 0 pairs = per-class launches
     int* merged_pairs = nullptr;
     int merged_n = 0, merged_M = 0;
+    // ring-pair support of the current weighted analysis (k_pair_support)
+    int* support = nullptr;
     // the short-ring classes run on a side stream beside the largest class
     // (fork / join by events, graph-capturable); 0 = all on the caller's stream
     hipStream_t side = nullptr;
@@ -2891,7 +2992,7 @@ int sht_alloc(gs_sht* p, T** dst, size_t n) {
 
 void sht_free(gs_sht* p) {
     void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->sscr,
-                    p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs, p->mf_tab, p->mf_off, p->mf_b0};
+                    p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs, p->mf_tab, p->mf_off, p->mf_b0, p->support};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (int* b : p->cls_pairs)
@@ -3120,6 +3221,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
             p->merged_M = mmax;
         }
     }
+    if (sht_alloc(p, &p->support, (size_t)p->npair)) { sht_free(p); return -1; }
     if (p->nsplit) {
         int nmax = 0;
         for (auto& g : geom) if (g.split) nmax = std::max(nmax, g.nphi);
@@ -3279,7 +3381,7 @@ static int ring_mc_ncb(int M, int ncomp) {
 
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
                      const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1, const double* wts = nullptr,
-                     int wnc = 3) {
+                     int wnc = 3, const int* pflag = nullptr) {
     if (p->merged_n > 0) {
         // all ring pairs in one launch: the block size and LDS of the longest FFT
         // (shorter rings leave threads idle; their fold reduction uses the
@@ -3302,7 +3404,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             else
                 hipLaunchKernelGGL(k_sht_anal_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, p->phi, ncomp, ncb, SB,
-                                   toff, wts, wnc, p->merged_n);
+                                   toff, wts, wnc, p->merged_n, pflag);
             GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring_mc" : "k_sht_anal_ring_mc");
             return 0;
         }
@@ -3416,7 +3518,7 @@ static int mfa_nt() { static const int v = mf_env("GS_SHT_MFA_NT", 256, 512, 256
 
 extern "C++" {
 template <int CPW>
-static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
+static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st, const int* pflag) {
     const ShtDev D = p->dev();
     const MfTab T = p->mftab();
     const unsigned ty = (unsigned)((p->mf_ntile + 3) / 4);
@@ -3427,17 +3529,19 @@ static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
     const unsigned gy = GS_MF_SYN_XCD ? 1u : (unsigned)(p->L + 1);
     if (ncomp != 2) {               // T (spin 0): comp 0
         const dim3 g(gx, gy, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
-        hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0);
+        hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0,
+                           pflag);
     }
     if (ncomp != 1) {               // E, B -> Q, U: comps ncomp - 2, ncomp - 1
         const dim3 g(gx, gy, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp,
-                           ncomp - 2);
+                           ncomp - 2, pflag);
     }
 }
 
 template <int CPW, int NT>
-static void sht_anal_mfma_v(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st) {
+static void sht_anal_mfma_v(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st,
+                            const int* pflag) {
     const ShtDev D = p->dev();
     const MfTab T = p->mftab();
     const double w = 4.0 * PI / (double)p->npix;
@@ -3449,31 +3553,44 @@ static void sht_anal_mfma_v(gs_sht* p, int nmap, int ncomp, int layout, int acc,
     if (ncomp != 2) {
         const dim3 g(nx, 1, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_anal_mfma<0, MF_CGW, CPW, NT>), g, dim3(NT), 0, st, D, T, p->phi, nmap, ncomp, 0, w,
-                           layout, acc, alm);
+                           layout, acc, alm, pflag);
     }
     if (ncomp != 1) {
         const dim3 g(nx, 1, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
         hipLaunchKernelGGL((k_sht_anal_mfma<2, MF_CGW, CPW, NT>), g, dim3(NT), 0, st, D, T, p->phi, nmap, ncomp,
-                           ncomp - 2, w, layout, acc, alm);
+                           ncomp - 2, w, layout, acc, alm, pflag);
     }
 }
 }  // extern "C++"
 
-static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st) {
-    if (mfs_cpw() == 2) sht_synth_mfma_v<2>(p, nmap, ncomp, st);
-    else sht_synth_mfma_v<4>(p, nmap, ncomp, st);
+static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st, const int* pflag = nullptr) {
+    if (mfs_cpw() == 2) sht_synth_mfma_v<2>(p, nmap, ncomp, st, pflag);
+    else sht_synth_mfma_v<4>(p, nmap, ncomp, st, pflag);
     GS_LAUNCH_CHECK("k_sht_synth_mfma");
     return 0;
 }
 
-static int sht_anal_mfma(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st) {
+static int sht_anal_mfma(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st,
+                         const int* pflag = nullptr) {
     const int cpw = mfa_cpw(), nt = mfa_nt();
-    if (cpw == 2 && nt == 512) sht_anal_mfma_v<2, 512>(p, nmap, ncomp, layout, acc, alm, st);
-    else if (cpw == 2) sht_anal_mfma_v<2, 256>(p, nmap, ncomp, layout, acc, alm, st);
-    else if (nt == 512) sht_anal_mfma_v<4, 512>(p, nmap, ncomp, layout, acc, alm, st);
-    else sht_anal_mfma_v<4, 256>(p, nmap, ncomp, layout, acc, alm, st);
+    if (cpw == 2 && nt == 512) sht_anal_mfma_v<2, 512>(p, nmap, ncomp, layout, acc, alm, st, pflag);
+    else if (cpw == 2) sht_anal_mfma_v<2, 256>(p, nmap, ncomp, layout, acc, alm, st, pflag);
+    else if (nt == 512) sht_anal_mfma_v<4, 512>(p, nmap, ncomp, layout, acc, alm, st, pflag);
+    else sht_anal_mfma_v<4, 256>(p, nmap, ncomp, layout, acc, alm, st, pflag);
     GS_LAUNCH_CHECK("k_sht_anal_mfma");
     return 0;
+}
+
+// the ring-pair support flags of a weighted analysis on the table path, or
+// nullptr: no skipping (GS_SHT_SUPPORT_SKIP=0, or more tiles than the
+// analysis' list holds)
+static const int* sht_support(gs_sht* p, const double* wts, int wnc, hipStream_t st) {
+    static const bool on = [] { const char* e = getenv("GS_SHT_SUPPORT_SKIP"); return !e || atoi(e) != 0; }();
+    const int nt = (p->npair + 15) / 16;
+    if (!on || !p->mf || !wts || nt > MF_TL_MAX || nt != p->mf_ntile) return nullptr;
+    hipLaunchKernelGGL(k_pair_support, dim3(p->npair), dim3(256), 0, st, p->npix, p->geom, wts, wnc, p->support);
+    if (hipGetLastError() != hipSuccess) return nullptr;
+    return p->support;
 }
 
 // build (on = 1) or drop (0) the plan's Legendre tables
@@ -3602,8 +3719,10 @@ static int sht_analysis(gs_sht* p, int nmap, int ncomp, int layout, const double
         return 0;
     }
     if (sht_reserve(p, nmap, S(stream))) return -1;
-    if (sht_rings(p, false, nmap * ncomp, maps, nullptr, stream, nullptr, nullptr, 1, wts, ncomp)) return -1;
-    if (p->mf) return sht_anal_mfma(p, nmap, ncomp, layout, acc, alm, S(stream));
+    const int* sup = sht_support(p, wts, ncomp, S(stream));
+    if (sht_rings(p, false, nmap * ncomp, maps, nullptr, stream, nullptr, nullptr, 1, wts, ncomp, sup))
+        return -1;
+    if (p->mf) return sht_anal_mfma(p, nmap, ncomp, layout, acc, alm, S(stream), sup);
     const int sr = p->ana_sr_nc[ncomp], sl = p->ana_seg_nc[ncomp];
     const int ntile = (p->ngroup + 4 * sr - 1) / (4 * sr);
     const int nsegz = sl ? (p->L + sl) / sl : 1;
@@ -3769,7 +3888,9 @@ int gs_sht_apply_weighted_batch(gs_sht* p, int nmap, int ncomp, const double* al
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * ncomp,
                        alm_in, GS_ALM_REAL, p->ain, bl);
     GS_LAUNCH_CHECK("k_sht_alm_in");
-    if (sht_synth_mfma(p, nmap, ncomp, S(stream))) return -1;
+    // pairs / tiles without weight: no synthesis, zero phases, skipped in the analysis
+    const int* sup = sht_support(p, weights, ncomp, S(stream));
+    if (sht_synth_mfma(p, nmap, ncomp, S(stream), sup)) return -1;
     {
         const int bd = ring_block(M), bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
         const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
@@ -3777,10 +3898,10 @@ int gs_sht_apply_weighted_batch(gs_sht* p, int nmap, int ncomp, const double* al
         const dim3 gm((unsigned)(8 * ((p->merged_n + 15) / 16) * 2 * ncg));
         hipLaunchKernelGGL(k_sht_apply_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                            p->merged_pairs, p->geom, p->phi, p->tw, p->Mmax, p->bsk, nc, ncb, SB, toff, weights, ncomp,
-                           p->merged_n);
+                           p->merged_n, sup);
         GS_LAUNCH_CHECK("k_sht_apply_ring_mc");
     }
-    return sht_anal_mfma(p, nmap, ncomp, GS_ALM_REAL, 0, alm_out, S(stream));
+    return sht_anal_mfma(p, nmap, ncomp, GS_ALM_REAL, 0, alm_out, S(stream), sup);
 }
 
 int gs_sht_map2alm_batch(gs_sht* p, int nmap, int ncomp, int layout, const double* maps, const double* weights,

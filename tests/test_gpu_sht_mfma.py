@@ -133,19 +133,33 @@ def test_mfma_batch_bit_identical(ncomp):
 
 
 @pytest.mark.parametrize("mfma", [True, False])
-@pytest.mark.parametrize("ncomp,N,L,B", [(2, 16, 37, 5), (1, 16, 37, 3), (3, 8, 20, 2), (2, 64, 128, 4)])
-def test_apply_weighted_equals_two_transforms(mfma, ncomp, N, L, B):
+@pytest.mark.parametrize("ncomp,N,L,B,zero", [(2, 16, 37, 5, "cap"), (1, 16, 37, 3, "cap"), (3, 8, 20, 2, "cap"),
+                                              (2, 64, 128, 4, "cap"), (2, 64, 128, 3, "band"), (1, 64, 128, 2, "band"),
+                                              (2, 32, 64, 2, "none"), (2, 32, 64, 2, "all")])
+def test_apply_weighted_equals_two_transforms(mfma, ncomp, N, L, B, zero):
     """the fused operator pass (maps on chip) = alm2map(beamed) then the weighted
-    map2alm, bit for bit, on the table path and on the recurrence path"""
+    map2alm = the analysis of the pre-weighted maps, bit for bit, on the table
+    path and on the recurrence path.  Zero weights on the polar caps / an
+    equatorial band (whole ring pairs and 16-pair tiles without weight, which
+    the table path skips) / nowhere / everywhere."""
+    from gibbssampler_amd.data import pixel_cos_theta
     from gibbssampler_amd.sht import HealpixSHT
     sht = HealpixSHT(N, L).set_mfma(mfma)
     g = torch.Generator(device="cuda").manual_seed(11)
     npix = 12 * N * N
     alm = torch.randn((B, ncomp, (L + 1) ** 2), dtype=torch.float64, device="cuda", generator=g)
     w = torch.rand((ncomp, npix), dtype=torch.float64, device="cuda", generator=g)
-    w[:, : npix // 7] = 0.0
+    if zero == "cap":
+        w[:, : npix // 7] = 0.0
+    elif zero == "band":
+        w[:, torch.from_numpy(np.abs(pixel_cos_theta(N)) <= 0.2).cuda()] = 0.0
+    elif zero == "all":
+        w.zero_()
     bl = torch.linspace(1.0, 0.3, L + 1, dtype=torch.float64, device="cuda")
-    want = sht.map2alm_batch(sht.alm2map_batch(alm, ncomp, bl=bl), ncomp, weights=w)
+    maps = sht.alm2map_batch(alm, ncomp, bl=bl)
+    want = sht.map2alm_batch(maps, ncomp, weights=w)
+    pre = sht.map2alm_batch(maps * w, ncomp)          # no weights: nothing skipped
+    assert torch.equal(want, pre)
     got = sht.apply_weighted_batch(alm, ncomp, w, bl=bl)
     assert torch.equal(got, want)
     for b in (0, B - 1):
