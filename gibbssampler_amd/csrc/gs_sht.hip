@@ -2347,10 +2347,15 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #endif
 constexpr int MF_CH = 32;                          // l staged per chunk (two blocks)
 constexpr int MF_TL_MAX = 256;                     // tiles of a support-skipping analysis (N_side <= 2048)
-template <int SPIN, int CGW, int CPW>
+// RIN: the input is the caller's real-layout a_lm (areal, comp stride
+// (L + 1)^2) with the optional beam bl, read and scaled while staging exactly as
+// k_sht_alm_in would have (no separate input pass); otherwise the plan's
+// complex-layout ain
+template <int SPIN, int CGW, int CPW, bool RIN>
 __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_mfma(ShtDev D, MfTab T, const double2* __restrict__ ain,
                                                         double2* __restrict__ phi, int nmap, int ncm, int cbase,
-                                                        const int* __restrict__ pflag) {
+                                                        const int* __restrict__ pflag, const double* __restrict__ areal,
+                                                        const double* __restrict__ bl) {
     constexpr int CPG = SPIN == 2 ? 4 : 8;         // maps per 16-column group
     constexpr int MPW = CGW * CPG;                 // maps per workgroup
     constexpr int NIT = MF_CH * MPW;               // staged (l, map) items per chunk
@@ -2428,6 +2433,8 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         }
     };
     // item i: (l, map) in the GS_MF_SMAP order
+    const long long NR = (long long)(L + 1) * (L + 1);
+    double pb[PER];                                // RIN: the items' beam factors
     auto fetch = [&](int cb, double2 (&pf)[PER][SPIN == 2 ? 2 : 1]) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
@@ -2437,10 +2444,27 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
             const bool ok = !(GS_MF_EXP & 2) && i < NIT && l <= L && c < nmap;
             // clamped address: the load is unconditional, the value selected when
             // staged (a select here would wait for the load)
-            const double2* src = ain + ((long long)(ok ? c : 0) * ncm + cbase) * nlm + base + (ok ? l : m);
-            pf[k][0] = src[0];
-            if constexpr (SPIN == 2) pf[k][1] = src[nlm];
+            if constexpr (RIN) {
+                // real layout: m = 0 at [l] (the next double is read and dropped),
+                // m > 0 (re, im) at 2 cidx(l, m) - (L + 1)
+                const int lq = ok ? l : m;
+                const long long r = m == 0 ? lq : 2 * (base + lq) - (L + 1);
+                const double* a = areal + ((long long)(ok ? c : 0) * ncm + cbase) * NR + r;
+                pf[k][0] = make_double2(a[0], a[1]);
+                if constexpr (SPIN == 2) pf[k][1] = make_double2(a[NR], a[NR + 1]);
+                pb[k] = bl ? bl[lq] : 1.0;
+            } else {
+                const double2* src = ain + ((long long)(ok ? c : 0) * ncm + cbase) * nlm + base + (ok ? l : m);
+                pf[k][0] = src[0];
+                if constexpr (SPIN == 2) pf[k][1] = src[nlm];
+            }
         }
+    };
+    // RIN: k_sht_alm_in's scaling of an item (m = 0: b a; m > 0: (b a) / sqrt 2)
+    auto rin = [&](double2 v, double b) __attribute__((always_inline)) -> double2 {
+        constexpr double IS2 = 0.70710678118654752440;
+        if (m == 0) return make_double2(b * v.x, 0.0);
+        return make_double2((b * v.x) * IS2, (b * v.y) * IS2);
     };
     auto stage = [&](int cb, const double2 (&pf)[PER][SPIN == 2 ? 2 : 1]) __attribute__((always_inline)) {
 #pragma unroll
@@ -2449,9 +2473,12 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
             if (i >= NIT) continue;
             const int lr = GS_MF_SMAP ? i / MPW : i % MF_CH, mp = GS_MF_SMAP ? i % MPW : i / MF_CH;
             const bool ok = m + cb * MF_TILE + lr <= L && c0 + mp < nmap;
+            double2 v0 = pf[k][0];
+            double2 v1 = SPIN == 2 ? pf[k][SPIN == 2 ? 1 : 0] : v0;
+            if constexpr (RIN) { v0 = rin(v0, pb[k]); v1 = rin(v1, pb[k]); }
             if constexpr (SPIN == 2) {
-                const double ex = ok ? pf[k][0].x : 0.0, ey = ok ? pf[k][0].y : 0.0;
-                const double bx = ok ? pf[k][1].x : 0.0, by = ok ? pf[k][1].y : 0.0;
+                const double ex = ok ? v0.x : 0.0, ey = ok ? v0.y : 0.0;
+                const double bx = ok ? v1.x : 0.0, by = ok ? v1.y : 0.0;
                 // F1 row (ex, ey, bx, by), F2 row (-by, bx, ey, -ex); "+" = F1 at even l - m
                 const bool ev = (lr & 1) == 0;     // l - m parity (chunks start at even l - m)
                 double2* P = reinterpret_cast<double2*>(sb + (lr * 2 + 0) * SR + mp * 4);
@@ -2461,8 +2488,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
                 M[0] = make_double2(ev ? -by : ex, ev ? bx : ey);
                 M[1] = make_double2(ev ? ey : bx, ev ? -ex : by);
             } else {
-                reinterpret_cast<double2*>(sb + lr * SR)[mp] =
-                    make_double2(ok ? pf[k][0].x : 0.0, ok ? pf[k][0].y : 0.0);
+                reinterpret_cast<double2*>(sb + lr * SR)[mp] = make_double2(ok ? v0.x : 0.0, ok ? v0.y : 0.0);
             }
         }
     };
@@ -3517,8 +3543,9 @@ static int mfa_cpw() { static const int v = mf_env("GS_SHT_MFA_CPW", 2, 4, 4); r
 static int mfa_nt() { static const int v = mf_env("GS_SHT_MFA_NT", 256, 512, 256); return v; }
 
 extern "C++" {
-template <int CPW>
-static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st, const int* pflag) {
+template <int CPW, bool RIN>
+static void sht_synth_mfma_r(gs_sht* p, int nmap, int ncomp, hipStream_t st, const int* pflag, const double* areal,
+                             const double* bl) {
     const ShtDev D = p->dev();
     const MfTab T = p->mftab();
     const unsigned ty = (unsigned)((p->mf_ntile + 3) / 4);
@@ -3529,13 +3556,13 @@ static void sht_synth_mfma_v(gs_sht* p, int nmap, int ncomp, hipStream_t st, con
     const unsigned gy = GS_MF_SYN_XCD ? 1u : (unsigned)(p->L + 1);
     if (ncomp != 2) {               // T (spin 0): comp 0
         const dim3 g(gx, gy, (unsigned)((nmap + 8 * MF_CGW - 1) / (8 * MF_CGW)));
-        hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp, 0,
-                           pflag);
+        hipLaunchKernelGGL((k_sht_synth_mfma<0, MF_CGW, CPW, RIN>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp,
+                           0, pflag, areal, bl);
     }
     if (ncomp != 1) {               // E, B -> Q, U: comps ncomp - 2, ncomp - 1
         const dim3 g(gx, gy, (unsigned)((nmap + 4 * MF_CGW - 1) / (4 * MF_CGW)));
-        hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW, CPW>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp,
-                           ncomp - 2, pflag);
+        hipLaunchKernelGGL((k_sht_synth_mfma<2, MF_CGW, CPW, RIN>), g, blk, 0, st, D, T, p->ain, p->phi, nmap, ncomp,
+                           ncomp - 2, pflag, areal, bl);
     }
 }
 
@@ -3563,9 +3590,18 @@ static void sht_anal_mfma_v(gs_sht* p, int nmap, int ncomp, int layout, int acc,
 }
 }  // extern "C++"
 
-static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st, const int* pflag = nullptr) {
-    if (mfs_cpw() == 2) sht_synth_mfma_v<2>(p, nmap, ncomp, st, pflag);
-    else sht_synth_mfma_v<4>(p, nmap, ncomp, st, pflag);
+// areal: the caller's real-layout a_lm (and beam bl) read by the kernel itself
+// instead of the plan's ain (filled by k_sht_alm_in)
+static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st, const int* pflag = nullptr,
+                          const double* areal = nullptr, const double* bl = nullptr) {
+    const bool two = mfs_cpw() == 2;
+    if (areal) {
+        if (two) sht_synth_mfma_r<2, true>(p, nmap, ncomp, st, pflag, areal, bl);
+        else sht_synth_mfma_r<4, true>(p, nmap, ncomp, st, pflag, areal, bl);
+    } else {
+        if (two) sht_synth_mfma_r<2, false>(p, nmap, ncomp, st, pflag, nullptr, nullptr);
+        else sht_synth_mfma_r<4, false>(p, nmap, ncomp, st, pflag, nullptr, nullptr);
+    }
     GS_LAUNCH_CHECK("k_sht_synth_mfma");
     return 0;
 }
@@ -3671,6 +3707,11 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
         return 0;
     }
     if (sht_reserve(p, nmap, S(stream))) return -1;
+    if (p->mf && layout == GS_ALM_REAL) {
+        // the table kernel reads the real layout (and the beam) itself
+        if (sht_synth_mfma(p, nmap, ncomp, S(stream), nullptr, alm, bl)) return -1;
+        return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp);
+    }
     const long long nin = (long long)nmap * ncomp * p->nlm;
     // the batch's comps are contiguous: the input pass sees B * ncomp comps
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * ncomp, alm,
@@ -3884,13 +3925,9 @@ int gs_sht_apply_weighted_batch(gs_sht* p, int nmap, int ncomp, const double* al
         return gs_sht_map2alm_batch(p, nmap, ncomp, GS_ALM_REAL, maps_scratch, weights, alm_out, 0, stream);
     }
     if (sht_reserve(p, nmap, S(stream))) return -1;
-    const long long nin = (long long)nmap * ncomp * p->nlm;
-    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * ncomp,
-                       alm_in, GS_ALM_REAL, p->ain, bl);
-    GS_LAUNCH_CHECK("k_sht_alm_in");
     // pairs / tiles without weight: no synthesis, zero phases, skipped in the analysis
     const int* sup = sht_support(p, weights, ncomp, S(stream));
-    if (sht_synth_mfma(p, nmap, ncomp, S(stream), sup)) return -1;
+    if (sht_synth_mfma(p, nmap, ncomp, S(stream), sup, alm_in, bl)) return -1;
     {
         const int bd = ring_block(M), bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
         const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);

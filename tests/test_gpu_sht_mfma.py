@@ -166,6 +166,37 @@ def test_apply_weighted_equals_two_transforms(mfma, ncomp, N, L, B, zero):
         assert torch.equal(sht.apply_weighted_batch(alm[b:b + 1], ncomp, w, bl=bl)[0], got[b]), b
 
 
+@pytest.mark.parametrize("ncomp,beam", [(1, False), (2, True), (3, True), (2, False)])
+def test_mfma_real_input_equals_complex_input(ncomp, beam):
+    """the table synthesis reading the real layout (and beam) itself = the same
+    coefficients given in the complex layout (the separate input pass), bit for
+    bit: m = 0 (b a_l0, 0), m > 0 ((b a_re) / sqrt 2, (b a_im) / sqrt 2)"""
+    from gibbssampler_amd.sht import HealpixSHT
+    N, L, B = 16, 37, 5
+    sht = HealpixSHT(N, L).set_mfma(True)
+    g = torch.Generator(device="cuda").manual_seed(21)
+    a = torch.randn((B, ncomp, (L + 1) ** 2), dtype=torch.float64, device="cuda", generator=g)
+    bl = torch.linspace(1.0, 0.2, L + 1, dtype=torch.float64, device="cuda") if beam else None
+    ls, ms = np.meshgrid(np.arange(L + 1), np.arange(L + 1), indexing="ij")
+    keep = ls >= ms
+    ls, ms = ls[keep], ms[keep]
+    ci = ms * (2 * L + 1 - ms) // 2 + ls                  # complex (healpy) index
+    order = np.argsort(ci)
+    ls, ms, ci = ls[order], ms[order], ci[order]
+    r = np.where(ms == 0, ls, 2 * ci - (L + 1))
+    re = a[..., torch.from_numpy(r).cuda()]
+    im = a[..., torch.from_numpy(np.where(ms == 0, 0, r + 1)).cuda()]
+    b = bl[torch.from_numpy(ls).cuda()] if beam else torch.ones(len(ls), dtype=torch.float64, device="cuda")
+    m0 = torch.from_numpy(ms == 0).cuda()
+    IS2 = 0.70710678118654752440
+    cre = torch.where(m0, b * re, (b * re) * IS2)
+    cim = torch.where(m0, torch.zeros_like(im), (b * im) * IS2)
+    ac = torch.complex(cre, cim).contiguous()
+    want = sht.alm2map_batch(ac, ncomp, layout="complex")
+    got = sht.alm2map_batch(a, ncomp, bl=bl)
+    assert torch.equal(got, want)
+
+
 def test_mfma_round_trip_and_adjoint_nside256():
     """band-limited round trip (iter 3) and exact adjointness on the table path"""
     from gibbssampler_amd.sht import HealpixSHT

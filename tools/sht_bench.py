@@ -53,7 +53,7 @@ def bench(N, L, reps):
     return sht
 
 
-def bench_batch(N, L, reps, batches, ncomps=(2,), mfma=False, apply=False):
+def bench_batch(N, L, reps, batches, ncomps=(2,), mfma=False, apply=False, band=0.2):
     """batched transforms (gs_sht_*_batch, one launch per stage for B maps): ms per
     batch, ms per map and TF/s; the beam / N^-1 fused forms of the masked CR."""
     from gibbssampler_amd import _capi
@@ -89,11 +89,11 @@ def bench_batch(N, L, reps, batches, ncomps=(2,), mfma=False, apply=False):
                 # the masked PCG operator: map2alm(N^-1 alm2map(b a)) with the bench's
                 # 80% band mask in N^-1 (gs_sht_apply_weighted_batch)
                 from gibbssampler_amd.data import band_mask
-                wm = w * torch.from_numpy(band_mask(N)).cuda()
+                wm = w * torch.from_numpy(band_mask(N, band)).cuda()
                 op = lambda: lib.gs_sht_apply_weighted_batch(sht.handle, B, ncomp, _capi.ptr(a), _capi.ptr(bl),
                                                              _capi.ptr(wm), _capi.ptr(out_m), _capi.ptr(out_a), sp)
                 to = timeit(op, reps)
-                print(f"batch N_side={N} ncomp={ncomp} B={B:3d}: weighted operator (band mask) {to:8.3f} ms "
+                print(f"batch N_side={N} ncomp={ncomp} B={B:3d}: weighted operator (|cos| > {band}) {to:8.3f} ms "
                       f"({to / B:7.4f} ms/map)", flush=True)
 
 
@@ -139,10 +139,11 @@ if __name__ == "__main__":
     ap.add_argument("--ncomp", default="2")
     ap.add_argument("--mfma", action="store_true", help="batched timings on the matrix-core table path")
     ap.add_argument("--apply", action="store_true", help="also the fused weighted operator (masked PCG)")
+    ap.add_argument("--band", type=float, default=0.2, help="--apply: zero weight where |cos theta| <= band")
     args = ap.parse_args()
     if args.batch:
         bench_batch(args.nside, args.lmax or 2 * args.nside, args.reps, [int(b) for b in args.batch.split(",")],
-                    tuple(int(c) for c in args.ncomp.split(",")), mfma=args.mfma, apply=args.apply)
+                    tuple(int(c) for c in args.ncomp.split(",")), mfma=args.mfma, apply=args.apply, band=args.band)
         raise SystemExit(0)
     bench(args.nside, args.lmax or 2 * args.nside, args.reps)
     if args.big:
