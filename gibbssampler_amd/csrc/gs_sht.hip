@@ -2296,12 +2296,6 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 // MF_CH l are staged in LDS (every tile of the m reads them); the next chunk's
 // are loaded into registers while this chunk's MFMAs run, and each block's
 // table values are loaded one block ahead of their MFMAs.
-// GS_MF_EXP (timing experiments only, wrong results; default 0): bit 1 = table
-// loads from one cached block, bit 2 = no phase / a_lm global loads, bit 4 =
-// no barriers
-#ifndef GS_MF_EXP
-#define GS_MF_EXP 0
-#endif
 // optional occupancy targets (build-time A/B only: the default lets the
 // compiler keep every prefetched value in registers)
 #ifdef GS_MF_SYN_WPE
@@ -2441,7 +2435,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
             const int i = threadIdx.x + NT * k;
             const int lr = GS_MF_SMAP ? i / MPW : i % MF_CH, mp = GS_MF_SMAP ? i % MPW : i / MF_CH;
             const int l = m + cb * MF_TILE + lr, c = c0 + mp;
-            const bool ok = !(GS_MF_EXP & 2) && i < NIT && l <= L && c < nmap;
+            const bool ok = i < NIT && l <= L && c < nmap;
             // clamped address: the load is unconditional, the value selected when
             // staged (a select here would wait for the load)
             if constexpr (RIN) {
@@ -2497,7 +2491,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // carry no condition (a conditional load would make the compiler wait on
     // the older loads at the join, the a_lm prefetch among them)
     auto tblk = [&](int b) __attribute__((always_inline)) -> const double* {
-        const bool ok = b >= b0 && b < nb && !(GS_MF_EXP & 1);
+        const bool ok = b >= b0 && b < nb;
         return ok ? tab + (long long)(b - b0) * MF_BLK : T.tab;
     };
     // the table values of quad / octet-half q of a block: spin 2 lambda_l and
@@ -2617,10 +2611,10 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     fetch(0, pf);
     fetchc(0);
     for (int cb = 0; cb < nb; cb += MF_CH / MF_TILE) {
-        if (!(GS_MF_EXP & 4)) __syncthreads();      // the previous chunk's readers are done
+        __syncthreads();                            // the previous chunk's readers are done
         stage(cb, pf);
         stagec(cb);
-        if (!(GS_MF_EXP & 4)) __syncthreads();
+        __syncthreads();
         if (cb + MF_CH / MF_TILE < nb) { fetch(cb + MF_CH / MF_TILE, pf); fetchc(cb + MF_CH / MF_TILE); }
         mma(cb, 0, gv);
         mma(cb + 1, MF_TILE, GS_MF_TPF == 2 ? gw : gv);
@@ -2714,7 +2708,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
             const int pr = MF_TILE * t + jp, map = c0 + mp;
             const double2 z = make_double2(0.0, 0.0);
             pf[k] = Ph{z, z, z, z};
-            if (!(GS_MF_EXP & 2) && i < NIT && pr < npair && map < nmap) {
+            if (i < NIT && pr < npair && map < nmap) {
                 const long long off = phi_at(m, pr, npair);
                 const double2* P = phi + ((long long)map * ncm + cbase) * 2 * plane;
                 pf[k].a = P[off];
@@ -2756,7 +2750,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     // block; its values are zeroed where they are used)
     constexpr int NG = SPIN == 2 ? 5 : 2;
     auto tload = [&](const Tw& w, int t, int s, double (&gv)[4][NG]) __attribute__((always_inline)) {
-        const double* bp = (GS_MF_EXP & 1) ? T.tab : w.blk;
+        const double* bp = w.blk;
         const int row = 2 * (j & 7);
         gv[s][0] = bp[row * MF_TILE + 4 * s + g];
         gv[s][1] = bp[(row + 1) * MF_TILE + 4 * s + g];
@@ -2826,9 +2820,9 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     // soon as its MFMAs are issued (their latency hides behind the rest of the tile)
     for (int i = 0; i < ntl; ++i) {
         const int t = tile(i);
-        if (!(GS_MF_EXP & 4)) __syncthreads();
+        __syncthreads();
         stage(pf);
-        if (!(GS_MF_EXP & 4)) __syncthreads();
+        __syncthreads();
         const bool more = i + 1 < ntl;
         const int tn = more ? tile(i + 1) : t;
         if (more) fetch(tn, pf);
