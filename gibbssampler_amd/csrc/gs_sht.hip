@@ -1519,14 +1519,19 @@ __global__ __launch_bounds__(256) void k_pair_support(long long npix, const Pair
     const PairGeom g = geom[p];
     const int n = g.nphi;
     const bool eq = g.startS < 0;
+    // chunk by chunk until a nonzero weight is seen (a live pair: usually the
+    // first chunk; a pair without weight: every pixel)
     int any = 0;
-    for (int i = threadIdx.x; i < wnc * n; i += blockDim.x) {
-        const int c = i / n, j = i - c * n;
-        const double* wc = wts + (long long)c * npix;
-        any |= wc[g.startN + j] != 0.0;
-        if (!eq) any |= wc[g.startS + j] != 0.0;
+    for (int i0 = 0; i0 < wnc * n && !any; i0 += blockDim.x) {
+        const int i = i0 + threadIdx.x;
+        int f = 0;
+        if (i < wnc * n) {
+            const int c = i / n, j = i - c * n;
+            const double* wc = wts + (long long)c * npix;
+            f = wc[g.startN + j] != 0.0 || (!eq && wc[g.startS + j] != 0.0);
+        }
+        any = __syncthreads_or(f);
     }
-    any = __syncthreads_or(any);
     if (threadIdx.x == 0) pflag[p] = any;
 }
 
