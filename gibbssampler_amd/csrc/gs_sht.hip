@@ -2339,6 +2339,24 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #ifndef GS_MF_APAD
 #define GS_MF_APAD 16
 #endif
+#ifndef GS_MF_ADB
+#define GS_MF_ADB 1
+#endif
+#ifndef GS_MF_SDB
+#define GS_MF_SDB 0
+#endif
+#ifndef GS_MF_XNS
+#define GS_MF_XNS 0
+#endif
+#ifndef GS_MF_XSC
+#define GS_MF_XSC 0
+#endif
+#ifndef GS_MF_XF
+#define GS_MF_XF 0
+#endif
+#ifndef GS_MF_SPF
+#define GS_MF_SPF 0
+#endif
 // table prefetch distance of the synthesis in blocks (1: the block after the
 // one being multiplied; 2: two blocks ahead, a second register set)
 #ifndef GS_MF_TPF
@@ -2367,9 +2385,14 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // groups of each half-wave on disjoint banks
     constexpr int SR = SPIN == 2 ? MPW * 4 + GS_MF_SPAD : MPW * 2 + GS_MF_SPAD;
     constexpr int NROW = SPIN == 2 ? 2 * MF_CH : MF_CH;
-    __shared__ __attribute__((aligned(16))) double sb[NROW * SR];
+    // GS_MF_SDB: two staging buffers (the next chunk staged while this one is
+    // multiplied: one barrier per chunk instead of two)
+    constexpr int NBUF = GS_MF_SDB ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) double sb[NBUF * NROW * SR];
     // spin 2: the chunk's per-l coefficients (P, Q, R, T, Rm, 0) of F1 / F2
-    __shared__ __attribute__((aligned(16))) double sc[SPIN == 2 ? MF_CH * 6 : 2];
+    __shared__ __attribute__((aligned(16))) double sc[NBUF * (SPIN == 2 ? MF_CH * 6 : 2)];
+    constexpr int SCN = SPIN == 2 ? MF_CH * 6 : 2;
+    int bsel = 0;                                  // the buffer the chunk's MFMAs read
     const int L = D.L, nlm = D.nlm, npair = D.npair;
     // GS_MF_SYN_XCD 0: grid (tile group, m, map group): the tile groups of one
     // m are consecutive blocks -- one per XCD, at the same time, so m's a_lm
@@ -2419,11 +2442,11 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
             pc[0] = cfb[4 * l + 1]; pc[1] = cfb[4 * l + 2]; pc[2] = cfb[4 * l + 3];   // (P, Q), (R, T), (Rm, -)
         }
     };
-    auto stagec = [&](int cb) __attribute__((always_inline)) {
+    auto stagec = [&](int cb, int bf) __attribute__((always_inline)) {
         if constexpr (SPIN == 2) {
             if (threadIdx.x < MF_CH) {
                 const bool ok = m + cb * MF_TILE + (int)threadIdx.x <= L;
-                double2* d = reinterpret_cast<double2*>(sc + threadIdx.x * 6);
+                double2* d = reinterpret_cast<double2*>(sc + bf * SCN + threadIdx.x * 6);
                 // (component selects: a select of double2 values goes through scratch)
                 d[0] = make_double2(ok ? pc[0].x : 0.0, ok ? pc[0].y : 0.0);
                 d[1] = make_double2(ok ? pc[1].x : 0.0, ok ? pc[1].y : 0.0);
@@ -2439,7 +2462,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
             const int lr = GS_MF_SMAP ? i / MPW : i % MF_CH, mp = GS_MF_SMAP ? i % MPW : i / MF_CH;
-            const int l = m + cb * MF_TILE + lr, c = c0 + mp;
+            const int l = m + (GS_MF_XSC ? 0 : cb) * MF_TILE + lr, c = c0 + mp;
             const bool ok = i < NIT && l <= L && c < nmap;
             // clamped address: the load is unconditional, the value selected when
             // staged (a select here would wait for the load)
@@ -2465,7 +2488,8 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         if (m == 0) return make_double2(b * v.x, 0.0);
         return make_double2((b * v.x) * IS2, (b * v.y) * IS2);
     };
-    auto stage = [&](int cb, const double2 (&pf)[PER][SPIN == 2 ? 2 : 1]) __attribute__((always_inline)) {
+    auto stage = [&](int cb, const double2 (&pf)[PER][SPIN == 2 ? 2 : 1], int bf) __attribute__((always_inline)) {
+        double* sbf = sb + bf * (NROW * SR);
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
@@ -2480,14 +2504,14 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
                 const double bx = ok ? v1.x : 0.0, by = ok ? v1.y : 0.0;
                 // F1 row (ex, ey, bx, by), F2 row (-by, bx, ey, -ex); "+" = F1 at even l - m
                 const bool ev = (lr & 1) == 0;     // l - m parity (chunks start at even l - m)
-                double2* P = reinterpret_cast<double2*>(sb + (lr * 2 + 0) * SR + mp * 4);
-                double2* M = reinterpret_cast<double2*>(sb + (lr * 2 + 1) * SR + mp * 4);
+                double2* P = reinterpret_cast<double2*>(sbf + (lr * 2 + 0) * SR + mp * 4);
+                double2* M = reinterpret_cast<double2*>(sbf + (lr * 2 + 1) * SR + mp * 4);
                 P[0] = make_double2(ev ? ex : -by, ev ? ey : bx);
                 P[1] = make_double2(ev ? bx : ey, ev ? by : -ex);
                 M[0] = make_double2(ev ? -by : ex, ev ? bx : ey);
                 M[1] = make_double2(ev ? ey : bx, ev ? -ex : by);
             } else {
-                reinterpret_cast<double2*>(sb + lr * SR)[mp] = make_double2(ok ? v0.x : 0.0, ok ? v0.y : 0.0);
+                reinterpret_cast<double2*>(sbf + lr * SR)[mp] = make_double2(ok ? v0.x : 0.0, ok ? v0.y : 0.0);
             }
         }
     };
@@ -2523,9 +2547,10 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     // per column group
     // the lane's base in the staged rows; everything else is a compile-time
     // offset (the ds_read immediate), so no per-read address registers
-    const double* sbl = SPIN == 2 ? sb + (g * 2) * SR + (cg0 * 4 + (j >> 2)) * 4 + o
-                                  : sb + (2 * g) * SR + (cg0 * 8 + (j >> 1)) * 2 + (j & 1);
+    const double* sbl0 = SPIN == 2 ? sb + (g * 2) * SR + (cg0 * 4 + (j >> 2)) * 4 + o
+                                   : sb + (2 * g) * SR + (cg0 * 8 + (j >> 1)) * 2 + (j & 1);
     auto lds = [&](int lr0, int q, double (&bq)[2 * CPW]) __attribute__((always_inline)) {
+        const double* sbl = sbl0 + bsel * (NROW * SR);
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (SPIN == 2) {
@@ -2554,43 +2579,72 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         const bool on = b >= b0 && b < nb;
         constexpr int NQ = SPIN == 2 ? 4 : 2;
         double bq[2][2 * CPW];                      // two rolling buffers
-        double cv[2][5];                            // spin 2: (P, Q, R, T, Rm) of the lane's row
+        // spin 2: (P, Q, R, T, Rm) of the lane's row, GS_MF_SPF: read two quads
+        // ahead (three buffers), else one (two)
+        constexpr int NCV = GS_MF_SPF ? 3 : 2;
+        double cv[NCV][5];
         auto ldc = [&](int q, double (&c)[5]) __attribute__((always_inline)) {
             if constexpr (SPIN == 2) {
-                const double* cq = sc + (lr0 + 4 * q + g) * 6;
+                const double* cq = sc + bsel * SCN + (lr0 + 4 * q + g) * 6;
 #pragma unroll
                 for (int k = 0; k < 5; ++k) c[k] = cq[k];
             }
         };
+        // F1 / F2 at l = m + 16 b + 4 q + g (the VALU kernels' expressions; G+ =
+        // the one with lambda's parity: F1 at even l - m); spin 0: lambda rows
+        auto fq = [&](int q, const double (&c)[5], double& ap, double& am) __attribute__((always_inline)) {
+            if constexpr (SPIN == 2) {
+                const double w0 = gv[2 * q];
+                const double w1 = (q > 0 || g > 0 || prev) ? gv[2 * q + 1] : 0.0;
+                const double f1 = fma(c[2] * xis2, w1, -fma(c[0], is2, c[1]) * w0);
+                const double f2 = fma(c[4] * is2, w1, -(c[3] * xis2) * w0);
+                const bool ev = (g & 1) == 0;
+                ap = ev ? f1 : f2;
+                am = ev ? f2 : f1;
+                if (GS_MF_XF) { ap = w0; am = gv[2 * q + 1]; }
+            } else {
+                ap = gv[2 * q];
+                am = gv[2 * q + 1];
+            }
+        };
         lds(lr0, 0, bq[0]);
         ldc(0, cv[0]);
+        // GS_MF_SPF (spin 2): the next quad's F values are formed while this
+        // quad's MFMAs run (interleaved: the matrix pipe is not left idle for
+        // the VALU chain between quads)
+        double apn = 0.0, amn = 0.0;
+        if (GS_MF_SPF && SPIN == 2) {
+            ldc(1, cv[1]);
+            if (on) fq(0, cv[0], apn, amn);
+        }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            if (q + 1 < NQ) { lds(lr0, q + 1, bq[(q + 1) & 1]); ldc(q + 1, cv[(q + 1) & 1]); }
+            if (GS_MF_SPF && SPIN == 2) {
+                if (q + 1 < NQ) lds(lr0, q + 1, bq[(q + 1) & 1]);
+                if (q + 2 < NQ) ldc(q + 2, cv[(q + 2) % NCV]);
+            } else if (q + 1 < NQ) {
+                lds(lr0, q + 1, bq[(q + 1) & 1]);
+                ldc(q + 1, cv[(q + 1) % NCV]);
+            }
             // keep the order as written: the scheduler would sink the next
             // quad's reads and the table refills behind the MFMAs
             __builtin_amdgcn_sched_barrier(0);
             if (on) {
                 double ap, am;
-                if constexpr (SPIN == 2) {
-                    // F1 / F2 at l = m + 16 b + 4 q + g (the VALU kernels' expressions;
-                    // G+ = the one with lambda's parity: F1 at even l - m)
-                    const double w0 = gv[2 * q];
-                    const double w1 = (q > 0 || g > 0 || prev) ? gv[2 * q + 1] : 0.0;
-                    const int u = q & 1;
-                    const double f1 = fma(cv[u][2] * xis2, w1, -fma(cv[u][0], is2, cv[u][1]) * w0);
-                    const double f2 = fma(cv[u][4] * is2, w1, -(cv[u][3] * xis2) * w0);
-                    const bool ev = (g & 1) == 0;
-                    ap = ev ? f1 : f2;
-                    am = ev ? f2 : f1;
-                } else {
-                    ap = gv[2 * q];
-                    am = gv[2 * q + 1];
-                }
+                if (GS_MF_SPF && SPIN == 2) { ap = apn; am = amn; }
+                else fq(q, cv[q % NCV], ap, am);
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
                     Cp[c] = mfma64(ap, bq[q & 1][2 * c + 0], Cp[c]);
                     Cm[c] = mfma64(am, bq[q & 1][2 * c + 1], Cm[c]);
+                }
+                if (GS_MF_SPF && SPIN == 2 && q + 1 < NQ) {
+                    fq(q + 1, cv[(q + 1) % NCV], apn, amn);
+#pragma unroll
+                    for (int k = 0; k < 2 * CPW; ++k) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                    }
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -2615,16 +2669,36 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     if (GS_MF_TPF == 2) tload4(1, gw);
     fetch(0, pf);
     fetchc(0);
-    for (int cb = 0; cb < nb; cb += MF_CH / MF_TILE) {
-        __syncthreads();                            // the previous chunk's readers are done
-        stage(cb, pf);
-        stagec(cb);
+    constexpr int CS = MF_CH / MF_TILE;              // blocks per chunk
+    if (GS_MF_SDB) {
+        // chunk 0 staged up front, chunk 1 in registers
+        stage(0, pf, 0);
+        stagec(0, 0);
+        if (CS < nb) { fetch(CS, pf); fetchc(CS); }
         __syncthreads();
-        if (cb + MF_CH / MF_TILE < nb) { fetch(cb + MF_CH / MF_TILE, pf); fetchc(cb + MF_CH / MF_TILE); }
+    }
+    for (int cb = 0; cb < nb; cb += CS) {
+        if (GS_MF_SDB) {
+            // this chunk was staged during the last one (buffer bsel); the next is
+            // staged now into the other buffer and the one after loaded; one
+            // barrier ends the chunk (the staging visible, this buffer read by
+            // every wave before it is written again)
+            bsel = (cb / CS) & 1;
+            if (cb + CS < nb) { stage(cb + CS, pf, bsel ^ 1); stagec(cb + CS, bsel ^ 1); }
+            if (cb + 2 * CS < nb) { fetch(cb + 2 * CS, pf); fetchc(cb + 2 * CS); }
+        } else {
+            __syncthreads();                        // the previous chunk's readers are done
+            stage(cb, pf, 0);
+            stagec(cb, 0);
+            __syncthreads();
+            if (cb + CS < nb) { fetch(cb + CS, pf); fetchc(cb + CS); }
+        }
         mma(cb, 0, gv);
         mma(cb + 1, MF_TILE, GS_MF_TPF == 2 ? gw : gv);
+        if (GS_MF_SDB) __syncthreads();
     }
     if (!tlive) return;
+    if (GS_MF_XNS && Cp[0][0] != 1234.5678) return;
     // D layout: lane (g, j) holds rows g + 4 r (pairs 16 t + g + 4 r), col j
     const long long plane = phi_plane(L, npair);
 #pragma unroll
@@ -2677,7 +2751,9 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     // of a half-wave (pairs 4 s + g, g = 0 / 1 and 2 / 3) use disjoint banks
     constexpr int HV = NV / 2;
     constexpr int RW = 2 * MPW * HV + GS_MF_APAD;
-    __shared__ __attribute__((aligned(16))) double sp_[MF_TILE * RW];
+    // GS_MF_ADB: two staging buffers (the next tile staged while this one is
+    // multiplied: one barrier per tile instead of two)
+    __shared__ __attribute__((aligned(16))) double sp_[(GS_MF_ADB ? 2 : 1) * MF_TILE * RW];
     __shared__ int tl_[MF_TL_MAX];                 // pflag: the tiles with weight, in order
     __shared__ int ntl_;
     const int L = D.L, npair = D.npair;
@@ -2776,13 +2852,13 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
             cP[p] = c.P; cQ[p] = c.Q; cR[p] = c.R; cT[p] = c.T; cRm[p] = c.Rm;
         }
     }
-    auto stage = [&](const Ph (&pf)[PER]) __attribute__((always_inline)) {
+    auto stage = [&](const Ph (&pf)[PER], double* sbuf) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
             if (i >= NIT) continue;
             const int jp = GS_MF_AMAP ? i / MPW : i % MF_TILE, mp = GS_MF_AMAP ? i % MPW : i / MF_TILE;
-            double* dp = sp_ + jp * RW + mp * HV;                            // N + S
+            double* dp = sbuf + jp * RW + mp * HV;                           // N + S
             double* dm = dp + MPW * HV;                                      // N - S
             const Ph& q = pf[k];
             if constexpr (SPIN == 2) {          // a = Q north, b = Q south, c = U north, d = U south
@@ -2820,17 +2896,35 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
 #pragma unroll
     for (int s = 0; s < 4; ++s) tload(cur, t0, s, gv);
     fetch(t0, pf);
+    if (GS_MF_ADB) {
+        if (ntl > 0) stage(pf, sp_);
+        if (ntl > 1) fetch(tile(1), pf);
+        __syncthreads();
+    }
     // tile t: stage its phases, issue the next tile's phases, then t's MFMAs;
     // each slice's table registers are refilled with the next tile's values as
-    // soon as its MFMAs are issued (their latency hides behind the rest of the tile)
+    // soon as its MFMAs are issued (their latency hides behind the rest of the
+    // tile).  GS_MF_ADB: tile i's phases were staged during tile i - 1 (buffer
+    // i & 1); tile i + 1's are staged now into the other buffer and tile i + 2's
+    // loaded, and one barrier ends the tile (the staging visible, the buffer
+    // read by every wave before it is written again)
     for (int i = 0; i < ntl; ++i) {
         const int t = tile(i);
-        __syncthreads();
-        stage(pf);
-        __syncthreads();
         const bool more = i + 1 < ntl;
         const int tn = more ? tile(i + 1) : t;
-        if (more) fetch(tn, pf);
+        int bo = 0;
+        if (GS_MF_ADB) {
+            bo = (i & 1) * (MF_TILE * RW);
+            if (more) stage(pf, sp_ + (MF_TILE * RW - bo));
+            if (i + 2 < ntl) fetch(tile(i + 2), pf);
+        } else {
+            __syncthreads();
+            stage(pf, sp_);
+            __syncthreads();
+            if (more) fetch(tn, pf);
+        }
+        const double* so = spo + bo;
+        const double* sr = spr + bo;
         const Tw nxt = twin(tn);
         // A operands of slice s (a1 / a2 per parity and column group), read one
         // slice ahead of their MFMAs; every load unconditional, only the MFMAs
@@ -2842,10 +2936,10 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
                     if constexpr (SPIN == 2) {
-                        a[p][c][0] = spo[s * 4 * RW + p * MPW * HV + c * 4 * HV];          // (N +- S)[o]
-                        a[p][c][1] = spr[s * 4 * RW + (1 - p) * MPW * HV + c * 4 * HV];    // (N -+ S)[3 - o]
+                        a[p][c][0] = so[s * 4 * RW + p * MPW * HV + c * 4 * HV];           // (N +- S)[o]
+                        a[p][c][1] = sr[s * 4 * RW + (1 - p) * MPW * HV + c * 4 * HV];     // (N -+ S)[3 - o]
                     } else {
-                        a[p][c][0] = spo[s * 4 * RW + p * MPW * HV + c * 8 * HV];
+                        a[p][c][0] = so[s * 4 * RW + p * MPW * HV + c * 8 * HV];
                     }
                 }
         };
@@ -2888,6 +2982,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
             __builtin_amdgcn_sched_barrier(0);
         }
         cur = nxt;
+        if (GS_MF_ADB) __syncthreads();
     }
     if (!live) return;
     // D layout: lane (g, j) holds rows g + 4 r = col index, col j = l index:
