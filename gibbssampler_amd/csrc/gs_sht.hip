@@ -2345,18 +2345,6 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #ifndef GS_MF_SDB
 #define GS_MF_SDB 0
 #endif
-#ifndef GS_MF_XNS
-#define GS_MF_XNS 0
-#endif
-#ifndef GS_MF_XSC
-#define GS_MF_XSC 0
-#endif
-#ifndef GS_MF_XF
-#define GS_MF_XF 0
-#endif
-#ifndef GS_MF_SPF
-#define GS_MF_SPF 0
-#endif
 // table prefetch distance of the synthesis in blocks (1: the block after the
 // one being multiplied; 2: two blocks ahead, a second register set)
 #ifndef GS_MF_TPF
@@ -2462,7 +2450,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         for (int k = 0; k < PER; ++k) {
             const int i = threadIdx.x + NT * k;
             const int lr = GS_MF_SMAP ? i / MPW : i % MF_CH, mp = GS_MF_SMAP ? i % MPW : i / MF_CH;
-            const int l = m + (GS_MF_XSC ? 0 : cb) * MF_TILE + lr, c = c0 + mp;
+            const int l = m + cb * MF_TILE + lr, c = c0 + mp;
             const bool ok = i < NIT && l <= L && c < nmap;
             // clamped address: the load is unconditional, the value selected when
             // staged (a select here would wait for the load)
@@ -2579,10 +2567,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         const bool on = b >= b0 && b < nb;
         constexpr int NQ = SPIN == 2 ? 4 : 2;
         double bq[2][2 * CPW];                      // two rolling buffers
-        // spin 2: (P, Q, R, T, Rm) of the lane's row, GS_MF_SPF: read two quads
-        // ahead (three buffers), else one (two)
-        constexpr int NCV = GS_MF_SPF ? 3 : 2;
-        double cv[NCV][5];
+        double cv[2][5];                            // spin 2: (P, Q, R, T, Rm) of the lane's row
         auto ldc = [&](int q, double (&c)[5]) __attribute__((always_inline)) {
             if constexpr (SPIN == 2) {
                 const double* cq = sc + bsel * SCN + (lr0 + 4 * q + g) * 6;
@@ -2590,61 +2575,35 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
                 for (int k = 0; k < 5; ++k) c[k] = cq[k];
             }
         };
-        // F1 / F2 at l = m + 16 b + 4 q + g (the VALU kernels' expressions; G+ =
-        // the one with lambda's parity: F1 at even l - m); spin 0: lambda rows
-        auto fq = [&](int q, const double (&c)[5], double& ap, double& am) __attribute__((always_inline)) {
-            if constexpr (SPIN == 2) {
-                const double w0 = gv[2 * q];
-                const double w1 = (q > 0 || g > 0 || prev) ? gv[2 * q + 1] : 0.0;
-                const double f1 = fma(c[2] * xis2, w1, -fma(c[0], is2, c[1]) * w0);
-                const double f2 = fma(c[4] * is2, w1, -(c[3] * xis2) * w0);
-                const bool ev = (g & 1) == 0;
-                ap = ev ? f1 : f2;
-                am = ev ? f2 : f1;
-                if (GS_MF_XF) { ap = w0; am = gv[2 * q + 1]; }
-            } else {
-                ap = gv[2 * q];
-                am = gv[2 * q + 1];
-            }
-        };
         lds(lr0, 0, bq[0]);
         ldc(0, cv[0]);
-        // GS_MF_SPF (spin 2): the next quad's F values are formed while this
-        // quad's MFMAs run (interleaved: the matrix pipe is not left idle for
-        // the VALU chain between quads)
-        double apn = 0.0, amn = 0.0;
-        if (GS_MF_SPF && SPIN == 2) {
-            ldc(1, cv[1]);
-            if (on) fq(0, cv[0], apn, amn);
-        }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            if (GS_MF_SPF && SPIN == 2) {
-                if (q + 1 < NQ) lds(lr0, q + 1, bq[(q + 1) & 1]);
-                if (q + 2 < NQ) ldc(q + 2, cv[(q + 2) % NCV]);
-            } else if (q + 1 < NQ) {
-                lds(lr0, q + 1, bq[(q + 1) & 1]);
-                ldc(q + 1, cv[(q + 1) % NCV]);
-            }
+            if (q + 1 < NQ) { lds(lr0, q + 1, bq[(q + 1) & 1]); ldc(q + 1, cv[(q + 1) & 1]); }
             // keep the order as written: the scheduler would sink the next
             // quad's reads and the table refills behind the MFMAs
             __builtin_amdgcn_sched_barrier(0);
             if (on) {
                 double ap, am;
-                if (GS_MF_SPF && SPIN == 2) { ap = apn; am = amn; }
-                else fq(q, cv[q % NCV], ap, am);
+                if constexpr (SPIN == 2) {
+                    // F1 / F2 at l = m + 16 b + 4 q + g (the VALU kernels' expressions;
+                    // G+ = the one with lambda's parity: F1 at even l - m)
+                    const double w0 = gv[2 * q];
+                    const double w1 = (q > 0 || g > 0 || prev) ? gv[2 * q + 1] : 0.0;
+                    const int u = q & 1;
+                    const double f1 = fma(cv[u][2] * xis2, w1, -fma(cv[u][0], is2, cv[u][1]) * w0);
+                    const double f2 = fma(cv[u][4] * is2, w1, -(cv[u][3] * xis2) * w0);
+                    const bool ev = (g & 1) == 0;
+                    ap = ev ? f1 : f2;
+                    am = ev ? f2 : f1;
+                } else {
+                    ap = gv[2 * q];
+                    am = gv[2 * q + 1];
+                }
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
                     Cp[c] = mfma64(ap, bq[q & 1][2 * c + 0], Cp[c]);
                     Cm[c] = mfma64(am, bq[q & 1][2 * c + 1], Cm[c]);
-                }
-                if (GS_MF_SPF && SPIN == 2 && q + 1 < NQ) {
-                    fq(q + 1, cv[(q + 1) % NCV], apn, amn);
-#pragma unroll
-                    for (int k = 0; k < 2 * CPW; ++k) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                    }
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -2698,7 +2657,6 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
         if (GS_MF_SDB) __syncthreads();
     }
     if (!tlive) return;
-    if (GS_MF_XNS && Cp[0][0] != 1234.5678) return;
     // D layout: lane (g, j) holds rows g + 4 r (pairs 16 t + g + 4 r), col j
     const long long plane = phi_plane(L, npair);
 #pragma unroll
