@@ -59,6 +59,16 @@ for pass in "FETCH_SIZE" "WRITE_SIZE" \
     timeout -s KILL 60 rocprofv3 --pmc $pass --kernel-include-regex "k_sht" -d $O/$n -o run --output-format csv \
         -- python3 $A > $O/$n.log 2>&1
 done
+# the fused PCG operator's ring stage (tools/sht_bench.py --apply: band-masked weights)
+O=gpurun_out/prof_${TAG}_shta; rm -rf $O; mkdir -p $O
+A="tools/sht_bench.py --nside 256 --batch 16 --ncomp 2 --reps 5 --mfma --apply"
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $A > $O/trace.log 2>&1
+for pass in "FETCH_SIZE" "WRITE_SIZE" \
+    "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
+    n=$(echo $pass | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    timeout -s KILL 60 rocprofv3 --pmc $pass --kernel-include-regex "k_sht_apply_ring|k_pair_support" -d $O/$n -o run \
+        --output-format csv -- python3 $A > $O/$n.log 2>&1
+done
 O=gpurun_out/prof_${TAG}_sht2048; rm -rf $O; mkdir -p $O
 A="tools/sht_bench.py --nside 2048 --reps 2"
 for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE"; do

@@ -103,13 +103,17 @@ def main():
     b = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_shtb")
     dur = durations(os.path.join(b, "trace", "run_kernel_stats.csv"))
     out["sht_N256_L512_B16_spin2_mfma"] = summarize(b, dur)
+    ba = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_shta")
+    if os.path.isdir(ba):
+        out["sht_N256_L512_B16_spin2_apply_band"] = summarize(ba, durations(os.path.join(ba, "trace",
+                                                                                        "run_kernel_stats.csv")))
     b2 = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_sht2048")
     out["sht_N2048_L4096_TEB_recurrence"] = summarize(b2, durations(os.path.join(ROOT, "profiles",
                                                                                  "r03_sht_kernel_stats.csv")))
     dst = os.path.join(ROOT, "profiles", f"{tag}_sht_pmc.json")
     json.dump(out, open(dst, "w"), indent=1)
     print("wrote", dst)
-    for name, sub in (("shtb", b), ("sht2048", b2)):
+    for name, sub in (("shtb", b), ("shta", ba), ("sht2048", b2)):
         for d in ("fetch_size", "write_size", "sq_wave_cycles", "sq_insts_valu"):
             src = os.path.join(sub, d, "run_counter_collection.csv")
             if os.path.exists(src):
