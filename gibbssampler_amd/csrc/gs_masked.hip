@@ -12,7 +12,9 @@
 // kernel carries the chain in blockIdx.y, and each transform is ONE batched SHT
 // over the B maps (gs_sht_*_batch) -- so B small-map chains fill the GPU that
 // one leaves mostly idle.  Chain b of a batch does exactly the arithmetic of a
-// one-chain context with chain id chain0 + b (bit-identical; tested).  The MALA
+// one-chain context with chain id chain0 + b (bit-identical for the same
+// resolved sht_mode -- the table and recurrence Legendre stages agree to
+// ~1e-12, not bit for bit -- tested).  The MALA
 // accept test reduces its eight sums in a fixed order (bitwise reproducible).
 //
 // Per-pixel arrays are [F][Npix] over the field rows (F = 2: Q, U; F = 3:

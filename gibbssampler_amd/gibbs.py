@@ -146,8 +146,13 @@ class GibbsSampler:
                  gibbs_cr=False, rj_step=False, ula=False, *, nchains=1, rng="native", seed=0, fields=None,
                  chain0=0, reference_quirks=True, noise_pol=None, proposal_variances=None,
                  metropolis_blocks=None, n_iter_metropolis=1, mask_path=None, distributed=False,
-                 dist_backend=None, keep_skymap=False):
+                 dist_backend=None, keep_skymap=False, sht_mode="auto"):
         self.shard = None
+        # masked / pixel-TT runs: the Legendre stage of their transforms ("auto":
+        # matrix-core tables from 4 chains on small maps, else the recurrence;
+        # "recurrence"; "mfma").  Chain b of a batch equals a one-chain run of
+        # the same chain id bit for bit only for the same resolved mode.
+        self.sht_mode = sht_mode
         self.keep_skymap = bool(keep_skymap)
         if distributed:
             # one process per GPU under torchrun: this rank runs global chains
@@ -239,7 +244,8 @@ class GibbsSampler:
                 blocks = blocks["TT"] if isinstance(blocks, dict) else blocks
             self._tt = TTModel(pm, self.noise, self.bl_gauss, self.lmax, self.nside, self.bins["TT"], mask=self.mask,
                                blocks=blocks, proposal_variances=pv, n_iter_metropolis=self.n_iter_metropolis,
-                               rng=self.rng, seed=self.seed, chain=self.chain0, nchains=self.nchains)
+                               rng=self.rng, seed=self.seed, chain=self.chain0, nchains=self.nchains,
+                               sht_mode=self.sht_mode)
         return self._tt
 
     # -- helpers of the reference base class --------------------------------------------
@@ -288,7 +294,7 @@ class GibbsSampler:
         return MaskedCR(self.pix_map, noise_temp, noise_pol, self.bl_gauss, self.lmax, self.nside, mask=self.mask,
                         nfields=self.nfields, gibbs_cr=gibbs_cr, n_gibbs=n_gibbs, alpha=alpha,
                         overrelaxation=overrelaxation, ula=ula, tau=tau, rng=self.rng, seed=self.seed,
-                        chain=self.chain0, rj=rj, nchains=self.nchains)
+                        chain=self.chain0, rj=rj, nchains=self.nchains, sht_mode=self.sht_mode)
 
     def _masked_mh_runner(self, kind, cr, cr_kind_):
         from .masked import MaskedMHRunner

@@ -23,8 +23,12 @@ of chains (job-script.sh:6-8) as one batch whose transforms are batched SHTs
 (one launch per stage for all B maps).  Device arrays then carry a leading
 chain axis ([B, F, NR], [B, nspec, L+1], ...); with B = 1 the shapes are the
 one-chain ones.  Chain b of a batch is bit-identical to a one-chain context of
-chain id chain + b.  Replay draws for B > 1 are chain-major: each chain's
-reference-order draws in turn.
+chain id chain + b that runs the same Legendre stage: ``sht_mode="auto"``
+resolves to the matrix-core tables for B >= 4 on small maps and to the
+recurrence otherwise (the two agree to ~1e-12 relative, not bit for bit), so
+pass "recurrence" or "mfma" explicitly when a batch must reproduce a one-chain
+run; ``sht_tables`` reports the resolved path.  Replay draws for B > 1 are
+chain-major: each chain's reference-order draws in turn.
 """
 import ctypes
 import time
@@ -238,20 +242,22 @@ class MaskedCR:
         return (*[g[i] for i in range(self.F)], *[p[i] for i in range(self.F)])
 
     # -- f1: PCG ------------------------------------------------------------------------
-    def pcg_rhs(self, dl, iteration=None):
-        """right-hand side b A^T N^-1 d + fluctuations (device tensor [F, NR])."""
+    def _rhs_draws_one(self):
+        """one chain's PCG fluctuation normals in the reference's order -> (z_pix, z_slot)"""
+        if self.F == 1:                   # TT (CenteredGibbs.py:153-155): z_alm, then z_pix
+            zs = self._slots()
+            return self._pix(1)[0], zs
+        zv = self._pix(1)[0]              # CenteredGibbs.py:467-478: z_Q, z_U, then z_E, z_B
+        return zv, self._slots()
+
+    def pcg_rhs(self, dl, iteration=None, draws=None):
+        """right-hand side b A^T N^-1 d + fluctuations (device tensor [F, NR]).
+        draws: replay normals already drawn, a list of B (z_pix, z_slot) pairs."""
         it = self.iteration if iteration is None else int(iteration)
         zv = zs = None
         if self.rng == "replay":
-            zvl, zsl = [], []
-            for _ in range(self.B):
-                if self.F == 1:           # TT (CenteredGibbs.py:153-155): z_alm, then z_pix
-                    zsl.append(self._slots())
-                    zvl.append(self._pix(1)[0])
-                else:                     # CenteredGibbs.py:467-478: z_Q, z_U, then z_E, z_B
-                    zvl.append(self._pix(1)[0])
-                    zsl.append(self._slots())
-            zv, zs = self._dev(np.stack(zvl)), self._dev(np.stack(zsl))
+            per = draws if draws is not None else [self._rhs_draws_one() for _ in range(self.B)]
+            zv, zs = self._dev(np.stack([p[0] for p in per])), self._dev(np.stack([p[1] for p in per]))
         rhs = torch.empty(self._shape(self.F, self.NR), dtype=torch.float64, device=self.device)
         _capi.check(self.lib.gs_masked_pcg_rhs(self.handle, _capi.ptr(dl), _capi.ptr(zv), _capi.ptr(zs), self.seed,
                                                it, self.chain, _capi.ptr(rhs), _capi.stream_ptr()),
@@ -292,15 +298,17 @@ class MaskedCR:
         (the draws of sample_mask, :622-643), the solve started from -s (:645-650),
         then log_proba = -sum (rhs - Q x) . (s - x) and log u < log_proba on the
         device (:652-672).  Replay: the uniform is np.random.uniform() after the
-        normals, the reference's order."""
+        normals, the reference's order; a batch draws chain b's normals and then
+        its uniform before chain b + 1's (chain-major like every replay draw)."""
         it = self.iteration if iteration is None else int(iteration)
-        rhs = self.pcg_rhs(dl, iteration=it)
-        um = None
+        um = per = None
         if self.rng == "replay":
-            # one uniform per chain after its normals: a batch's chain-major replay
-            # draws chain b's normals and uniform in turn only for B = 1 (the
-            # reference's order); B > 1 draws the B uniforms after all normals
-            um = torch.tensor([np.random.uniform() for _ in range(self.B)], dtype=torch.float64, device=self.device)
+            per, us = [], []
+            for _ in range(self.B):
+                per.append(self._rhs_draws_one())
+                us.append(np.random.uniform())
+            um = torch.tensor(us, dtype=torch.float64, device=self.device)
+        rhs = self.pcg_rhs(dl, iteration=it, draws=per)
         x = self.pcg_solve(dl, rhs, x=-s)
         _capi.check(self.lib.gs_masked_rj_accept(self.handle, _capi.ptr(dl), _capi.ptr(rhs), _capi.ptr(x),
                                                  _capi.ptr(s), _capi.ptr(um), self.seed, it, self.chain,

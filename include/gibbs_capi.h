@@ -278,7 +278,11 @@ int gs_sht_map2alm_batch(gs_sht* sht, int nmap, int ncomp, int layout, const dou
  * the reference's independent chains (its SLURM array, job-script.sh:6-8) as
  * one batch whose transforms are batched SHTs; `chain` arguments are the global
  * id of the batch's first chain (chain b has id chain + b), and chain b's
- * results equal a one-chain context's for id chain + b bit for bit.
+ * results equal a one-chain context's for id chain + b bit for bit when both
+ * contexts run the same Legendre stage (desc.sht_mode resolved to the same
+ * path: "auto" = 0 picks the matrix-core tables from 4 chains on small maps and
+ * the recurrence otherwise, so pass 1 or 2 explicitly to compare a batch with a
+ * one-chain run; the two paths agree to ~1e-12 relative).
  * maps / inv_noise (create): DEVICE [3][Npix] rows T, Q, U (inv_noise
  * mask-multiplied, CenteredGibbs.py:266-274; the T row is read only for
  * nfields = 3), shared by the batch.  Every per-chain argument is [B][...]

@@ -273,6 +273,33 @@ def test_surface_masked_nchains():
     np.testing.assert_array_equal(h["BB"][:, 2], h1["BB"])
 
 
+def test_surface_default_mode_batch_equals_single_of_resolved_mode():
+    """with the default sht_mode ("auto") a 4-chain batch resolves to
+    the matrix-core tables and a one-chain run to the recurrence, so the batch
+    reproduces a one-chain run of the same chain id only when that run is given
+    the batch's resolved mode -- passed through the drop-in class (sht_mode=)."""
+    from gibbssampler_amd.gibbs import CenteredGibbs
+    N, L, mask, maps, ntemp, npol, bl, dl, s0 = _problem()
+    init = {"EE": dl["EE"][:L + 1], "BB": dl["BB"][:L + 1]}
+    kw = dict(mask_path=mask, polarization=True, n_iter=2, gibbs_cr=True, ula=True, rng="native", seed=9)
+    cg = CenteredGibbs({"Q": maps[1], "U": maps[2]}, ntemp, npol, 4.0, N, L, 12 * N * N, nchains=4, chain0=1,
+                       skymap_init=s0[:4, 1:], **kw)
+    assert cg.constrained_sampler.sht_tables          # auto at B = 4: tables
+    h, acc, _, _ = cg.run(init)
+    for mode, tables in (("auto", False), ("mfma", True)):
+        one = CenteredGibbs({"Q": maps[1], "U": maps[2]}, ntemp, npol, 4.0, N, L, 12 * N * N, nchains=1, chain0=3,
+                            skymap_init=s0[2, 1:], sht_mode=mode, **kw)
+        assert one.constrained_sampler.sht_tables == tables
+        h1, a1, _, _ = one.run(init)
+        if tables:
+            np.testing.assert_array_equal(h["EE"][:, 2], h1["EE"])
+            np.testing.assert_array_equal(h["BB"][:, 2], h1["BB"])
+            np.testing.assert_array_equal(acc[:, 2], a1)
+        else:                                          # the other Legendre stage: ~1e-12 apart
+            np.testing.assert_allclose(h["EE"][:, 2], h1["EE"], rtol=1e-8)
+            np.testing.assert_allclose(h["BB"][:, 2], h1["BB"], rtol=1e-8)
+
+
 @pytest.mark.parametrize("driver", ["centered", "noncentered", "asis"])
 def test_tt_pixel_batch_equals_single(driver):
     """the pixel-domain TT model (f4) batched: chains 0 and B - 1 of a B-chain
