@@ -126,6 +126,7 @@ _SIGS = [
                                             ctypes.c_int, _VP]),
     ("gs_masked_create", ctypes.c_int, [ctypes.POINTER(GsMaskedDesc), _VP, _VP, ctypes.POINTER(_VP)]),
     ("gs_masked_destroy", ctypes.c_int, [_VP]),
+    ("gs_masked_ring_classes", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int)]),
     ("gs_masked_info", ctypes.c_int, [_VP, c_double_p, _VP]),
     ("gs_masked_nchains", ctypes.c_int, [_VP]),
     ("gs_masked_sht_tables", ctypes.c_int, [_VP]),

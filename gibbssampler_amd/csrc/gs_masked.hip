@@ -40,8 +40,12 @@
 
 // library-internal SHT entry points (gs_sht.hip)
 extern "C" long long gs_sht_phi_plane(const gs_sht* p);
-extern "C" int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int* blk, int K,
-                                   const int* blk_lmax, double* phib, double* maps, void* stream);
+extern "C" int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real, const int* blk, int K,
+                                   const int* blk_lmax, double* phib, double* maps, void* stream, int parseval);
+extern "C" int gs_sht_register_weights(gs_sht* p, const double* weights, int wnc, void* stream);
+extern "C" int gs_sht_blocks_parseval(const gs_sht* p, int nfield, int ncomp_total);
+extern "C" int gs_sht_parseval_maps(gs_sht* p, int ncomp, double* maps, void* stream);
+extern "C" int gs_sht_ring_class_counts(const gs_sht* p, int counts[3]);
 
 using namespace gs;
 using gs_detail::set_error;
@@ -906,14 +910,21 @@ constexpr int F2_RMAX = 176;         // rows (blocks + residual) per Gram pass
 constexpr size_t F2_DECIDE_LDS = 160 * 1024 - (2 * sizeof(double) + 3 * sizeof(int)) * F2_RMAX - 64;
 constexpr long long F2_CHUNK = 2048; // elements per Gram workgroup
 
-// delta a (real layout) of blocks [k0, k0 + kn) and their local block table
+// delta a (real layout) of blocks [k0, k0 + kn) and their local block table;
+// blockIdx.y = chain (per-chain D_l [F][L+1], s_nc / da [F][(L+1)^2]; chain 0's
+// threads write the shared local table)
 template <int F>
 __global__ void k_f2_delta(int L, int k0, int kn, const int* __restrict__ blk, const double* __restrict__ dl_cur,
                            const double* __restrict__ dl_prop, const double* __restrict__ bl,
                            const double* __restrict__ s_nc, double* __restrict__ da, int* __restrict__ blk_local) {
     const long long NR = (long long)(L + 1) * (L + 1);
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g <= L) {
+    const int b = blockIdx.y;
+    dl_cur += (long long)b * F * (L + 1);
+    dl_prop += (long long)b * F * (L + 1);
+    s_nc += (long long)b * F * NR;
+    da += (long long)b * F * NR;
+    if (g <= L && b == 0) {
 #pragma unroll
         for (int f = 0; f < F; ++f) {
             const int b = blk[f * (L + 1) + g];
@@ -937,10 +948,19 @@ __global__ void k_f2_delta(int L, int k0, int kn, const int* __restrict__ blk, c
     }
 }
 
+// r = d - m per chain (blockIdx.y; d shared)
 __global__ void k_f2_resid(long long n, const double* __restrict__ d, const double* __restrict__ m,
                            double* __restrict__ r) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g < n) r[g] = d[g] - m[g];
+    const long long o = blockIdx.y * n;
+    if (g < n) r[o + g] = d[g] - m[o + g];
+}
+
+// each chain's copy of the group's block l_max (the batched ring stage indexes
+// its comps chain-major)
+__global__ void k_f2_rep_lmax(int nb, int kn, const int* __restrict__ lmax, int* __restrict__ out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < nb * kn) out[g] = lmax[g % kn];
 }
 
 // Lower triangle of the R x R weighted Gram matrix of rows 0..R-2 = Y, R-1 = r,
@@ -968,6 +988,11 @@ template <int T>
 __global__ __launch_bounds__(256) void k_f2_gram_mfma(int R, long long n, const double* __restrict__ Y,
                                                       const double* __restrict__ r, const double* __restrict__ w,
                                                       double* __restrict__ partial) {
+    // chain blockIdx.y: rows Y + y (R - 1) n, residual r + y n, partials after the
+    // gridDim.x chunks of each earlier chain (w shared)
+    Y += (long long)blockIdx.y * (R - 1) * n;
+    r += (long long)blockIdx.y * n;
+    partial += (long long)blockIdx.y * gridDim.x * (((R + 3) / 4) * ((R + 3) / 4 + 1) / 2) * 16;
     constexpr int SROW = F2_RMAX + 6;
     static_assert(16 * F2_TMAX <= SROW, "tile rows exceed the staged column");
     constexpr int NPAIR = T * (T + 1) / 2;
@@ -1047,17 +1072,18 @@ __global__ __launch_bounds__(256) void k_f2_gram_mfma(int R, long long n, const 
 }
 
 template <int T>
-void launch_gram_mfma_t(int Tr, unsigned nchunk, hipStream_t st, int R, long long n, const double* Y,
+void launch_gram_mfma_t(int Tr, unsigned nchunk, unsigned nch, hipStream_t st, int R, long long n, const double* Y,
                         const double* r, const double* w, double* part) {
     if constexpr (T <= F2_TMAX) {
         if (Tr == T) {
-            hipLaunchKernelGGL(k_f2_gram_mfma<T>, dim3(nchunk), dim3(256), 0, st, R, n, Y, r, w, part);
+            hipLaunchKernelGGL(k_f2_gram_mfma<T>, dim3(nchunk, nch), dim3(256), 0, st, R, n, Y, r, w, part);
             return;
         }
-        launch_gram_mfma_t<T + 1>(Tr, nchunk, st, R, n, Y, r, w, part);
+        launch_gram_mfma_t<T + 1>(Tr, nchunk, nch, st, R, n, Y, r, w, part);
     }
 }
 
+// chain blockIdx.y: its partials (nchunk chunks) -> G + y R R
 __global__ void k_f2_gram_finish(int R, int nchunk, const double* __restrict__ partial, double* __restrict__ G) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= R * R) return;
@@ -1065,6 +1091,8 @@ __global__ void k_f2_gram_finish(int R, int nchunk, const double* __restrict__ p
     if (j > i) return;
     const int nb4 = (R + 3) / 4;
     const int nblk4 = nb4 * (nb4 + 1) / 2;
+    partial += (long long)blockIdx.y * nchunk * nblk4 * 16;
+    G += (long long)blockIdx.y * R * R;
     const int b = (i / 4) * (i / 4 + 1) / 2 + j / 4;
     const double* pp = partial + (long long)b * 16 + (i % 4) * 4 + (j % 4);
     const long long cs = (long long)nblk4 * 16;
@@ -1092,13 +1120,26 @@ __global__ void k_f2_gram_finish(int R, int nchunk, const double* __restrict__ p
 // log accept uniforms -- is staged in LDS in parallel first, so the serial
 // chain of decisions touches LDS only (it was a chain of global-memory
 // latencies per block: 236 us for 135 blocks at N_side 256).
+// One workgroup per chain (blockIdx.x; per-chain G [R][R], spectra [F][maxbins],
+// uniforms / flags [K][n_iter] with K = kacc blocks, taken [kn]): the chains'
+// serial decision chains run side by side
 __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* __restrict__ G, int k0, int n_iter,
                                                    const int* __restrict__ blk_field,
                                                    const int* __restrict__ blk_bins, int maxbins,
                                                    const double* __restrict__ logr, const double* __restrict__ u_acc,
                                                    const double* __restrict__ prop, double* __restrict__ binned,
                                                    int32_t* __restrict__ accept_out, double* __restrict__ taken_out,
-                                                   int lu_lds) {
+                                                   int lu_lds, int nspec, int kacc) {
+    {
+        const long long b = blockIdx.x;
+        G += b * R * R;
+        logr += b * nspec * maxbins;
+        prop += b * nspec * maxbins;
+        binned += b * nspec * maxbins;
+        u_acc += b * kacc * n_iter;
+        accept_out += b * kacc * n_iter;
+        taken_out += b * kn;
+    }
     extern __shared__ __attribute__((aligned(16))) double Gl[];      // [R (R + 1) / 2] lower triangle,
                                                                      // then (lu_lds) [kn][n_iter] log u
     __shared__ double corr[F2_RMAX];
@@ -1162,10 +1203,14 @@ __global__ __launch_bounds__(256) void k_f2_decide(int kn, int R, const double* 
     }
 }
 
-// r -= sum over accepted blocks of y_k (before the next group of blocks)
+// r -= sum over accepted blocks of y_k (before the next group of blocks); chain
+// blockIdx.y (Y [kn][n], taken [kn], r [n] per chain)
 __global__ void k_f2_update(long long n, int kn, const double* __restrict__ Y, const double* __restrict__ taken,
                             double* __restrict__ r) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    Y += (long long)blockIdx.y * kn * n;
+    taken += (long long)blockIdx.y * kn;
+    r += (long long)blockIdx.y * n;
     if (g >= n) return;
     double v = r[g];
     for (int k = 0; k < kn; ++k)
@@ -1205,11 +1250,12 @@ struct gs_masked {
     double* pcgs = nullptr;          // PcgState [B] of the device CG
     int pcg_syncs = 0;               // host synchronisations of the last solve
     int pcg_launched = 0;            // CG iterations launched by the last solve (>= every chain's count)
-    // f2 block MH workspace (one chain at a time; allocated on first use, grown as needed)
+    // f2 block MH workspace (f2_nb chains at a time; allocated on first use, grown as needed)
     double *f2_da = nullptr, *f2_r = nullptr, *f2_Y = nullptr, *f2_phib = nullptr, *f2_part = nullptr,
            *f2_G = nullptr, *f2_taken = nullptr;
-    int* f2_blk = nullptr;
-    int f2_cap = 0;                  // blocks the Y / phib buffers hold
+    int *f2_blk = nullptr, *f2_lmaxb = nullptr;
+    int f2_cap = 0;                  // blocks per chain the Y / phib buffers hold
+    int f2_nb = 0;                   // chains the buffers hold
 };
 
 namespace {
@@ -1225,6 +1271,7 @@ void mc_free(gs_masked* c) {
     if (c->ell2bin) (void)hipFree(c->ell2bin);
     if (c->accd) (void)hipFree(c->accd);
     if (c->f2_blk) (void)hipFree(c->f2_blk);
+    if (c->f2_lmaxb) (void)hipFree(c->f2_lmaxb);
     delete c;
 }
 
@@ -1398,6 +1445,9 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
         }
     }
     if (!ok) { mc_free(c); return set_error("gs_masked_create: copy failed"); }
+    // N^-1 never changes for the context: its ring classes are computed once
+    // (support skip, constant-ring operator and f2 Parseval forms)
+    if (gs_sht_register_weights(c->sht, c->ninv, c->F, nullptr)) { mc_free(c); return -1; }
     // second_part_grad = b * complex_to_real(map2alm(N^-1 d)) * Npix/(4 pi)  (CenteredGibbs.py:298-306)
     const long long n = c->F * c->npix;
     hipLaunchKernelGGL(k_mc_mul, dim3(nblocks(n, 256)), dim3(256), 0, 0, n, c->ninv, c->dpix, c->y);
@@ -1417,6 +1467,11 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     }
     *out = c;
     return 0;
+}
+
+int gs_masked_ring_classes(const gs_masked* c, int* counts) {
+    if (!c || !counts) return set_error("gs_masked_ring_classes: null argument");
+    return gs_sht_ring_class_counts(c->sht, counts);
 }
 
 int gs_masked_destroy(gs_masked* c) {
@@ -1685,24 +1740,52 @@ static int f2_group(const gs_masked* c) {
     return (int)std::max(1LL, std::min<long long>(F2_RMAX - 1, budget / std::max(per, 1LL)));
 }
 
-// one chain's sweep (pointers at that chain's slices; chain-0-relative scratch)
-static int pixel_mh_one(gs_masked* c, int K, int n_iter, int maxbins, const int* blk, const int* blk_lmax,
-                        const int* blk_field, const int* blk_bins, const double* s_nc, const double* dl_cur,
-                        const double* dl_prop, const double* logr, const double* u_acc, const double* prop_binned,
-                        double* binned, int32_t* accept_out, hipStream_t st) {
+// chains per f2 pass: every chain of a pass holds its block group's phase planes,
+// maps and Gram partials at once (GS_F2_BATCH_BYTES, default 64 GiB, of which
+// each chain takes f2_chain_bytes); the passes run in chain order
+static long long f2_chain_bytes(const gs_masked* c, int kcap) {
+    const long long nco = c->F == 1 ? 1 : 2;
+    const long long n = (long long)c->F * c->npix;
+    const long long nchunk = (n + F2_CHUNK - 1) / F2_CHUNK;
+    const long long nb4 = (kcap + 1 + 3) / 4;
+    return (long long)kcap * (nco * 2 * gs_sht_phi_plane(c->sht) * 16 + n * 8) + nchunk * nb4 * (nb4 + 1) / 2 * 128 +
+           (long long)(kcap + 1) * (kcap + 1) * 8 + n * 8 + (long long)c->F * c->NR * 8;
+}
+
+static int f2_chains_per_pass(const gs_masked* c, int kcap) {
+    long long budget = 64LL << 30;
+    if (const char* e = getenv("GS_F2_BATCH_BYTES")) budget = std::max(1LL, atoll(e));
+    return (int)std::max(1LL, std::min<long long>(c->B, budget / std::max(1LL, f2_chain_bytes(c, kcap))));
+}
+
+// one pass over nb chains (pointers at the pass's first chain; chain-0-relative
+// scratch): every launch carries the pass's chains in its grid, each chain's
+// arithmetic that of a one-chain sweep (bit-identical)
+static int pixel_mh_pass(gs_masked* c, int nb, int K, int n_iter, int maxbins, const int* blk, const int* blk_lmax,
+                         const int* blk_field, const int* blk_bins, const double* s_nc, const double* dl_cur,
+                         const double* dl_prop, const double* logr, const double* u_acc, const double* prop_binned,
+                         double* binned, int32_t* accept_out, hipStream_t st) {
     const int F = c->F;
     const int KG = f2_group(c);
     const long long n = (long long)F * c->npix;
     const long long nchunk = (n + F2_CHUNK - 1) / F2_CHUNK;
+    // the rows on constant-weight ring pairs in Parseval coordinates (their
+    // weighted sums over pixels are those over the coordinates; no ring DFT for
+    // the block maps there): decided per plan and block grouping, not per batch,
+    // so a chain's sums do not depend on how many chains share its pass
+    const int nco = F == 1 ? 1 : 2;
+    const int kn_last = K - KG * ((K - 1) / KG);
+    const int pv = kn_last * nco >= 2 ? gs_sht_blocks_parseval(c->sht, F, kn_last * nco) : 0;
     // residual of the current state: r = d - A b C_cur^1/2 s_nc
-    if (masked_center(c, 1, dl_cur, +1, s_nc, c->snew, st)) return -1;
-    if (mc_synth(c, 1, c->snew, c->pix1, st)) return -1;
-    hipLaunchKernelGGL(k_f2_resid, dim3(nblocks(n, 256)), dim3(256), 0, st, n, c->dpix, c->pix1, c->f2_r);
+    if (masked_center(c, nb, dl_cur, +1, s_nc, c->snew, st)) return -1;
+    if (mc_synth(c, nb, c->snew, c->pix1, st)) return -1;
+    hipLaunchKernelGGL(k_f2_resid, dim3(nblocks(n, 256), nb), dim3(256), 0, st, n, c->dpix, c->pix1, c->f2_r);
     GS_LAUNCH_CHECK("k_f2_resid");
+    if (pv && gs_sht_parseval_maps(c->sht, nb * F, c->f2_r, st)) return -1;
     for (int k0 = 0; k0 < K; k0 += KG) {
         const int kn = std::min(KG, K - k0);
         const int R = kn + 1;
-        const dim3 gd(nblocks(std::max<long long>(c->NR, c->L + 1), 256)), bd(256);
+        const dim3 gd(nblocks(std::max<long long>(c->NR, c->L + 1), 256), nb), bd(256);
         if (F == 1)
             hipLaunchKernelGGL(k_f2_delta<1>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
                                c->f2_blk);
@@ -1710,12 +1793,16 @@ static int pixel_mh_one(gs_masked* c, int K, int n_iter, int maxbins, const int*
             hipLaunchKernelGGL(k_f2_delta<2>, gd, bd, 0, st, c->L, k0, kn, blk, dl_cur, dl_prop, c->bl, s_nc, c->f2_da,
                                c->f2_blk);
         GS_LAUNCH_CHECK("k_f2_delta");
-        if (gs_sht_synth_blocks(c->sht, F, c->f2_da, c->f2_blk, kn, blk_lmax + k0, c->f2_phib, c->f2_Y, st))
+        hipLaunchKernelGGL(k_f2_rep_lmax, dim3(nblocks((long long)nb * kn, 256)), dim3(256), 0, st, nb, kn,
+                           blk_lmax + k0, c->f2_lmaxb);
+        GS_LAUNCH_CHECK("k_f2_rep_lmax");
+        if (gs_sht_synth_blocks(c->sht, nb, F, c->f2_da, c->f2_blk, kn, c->f2_lmaxb, c->f2_phib, c->f2_Y, st, pv))
             return -1;
-        launch_gram_mfma_t<1>((R + 15) / 16, (unsigned)nchunk, st, R, n, c->f2_Y, c->f2_r, c->ninv, c->f2_part);
+        launch_gram_mfma_t<1>((R + 15) / 16, (unsigned)nchunk, (unsigned)nb, st, R, n, c->f2_Y, c->f2_r, c->ninv,
+                              c->f2_part);
         GS_LAUNCH_CHECK("k_f2_gram_mfma");
-        hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256)), dim3(256), 0, st, R, (int)nchunk,
-                           c->f2_part, c->f2_G);
+        hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256), nb), dim3(256), 0, st, R,
+                           (int)nchunk, c->f2_part, c->f2_G);
         GS_LAUNCH_CHECK("k_f2_gram_finish");
         // dynamic LDS: G's lower triangle (<= 124.6 KB at F2_RMAX rows), plus the
         // log uniforms when they fit in what the static arrays leave of 160 KB
@@ -1730,11 +1817,11 @@ static int pixel_mh_one(gs_masked* c, int K, int n_iter, int maxbins, const int*
             (void)hipGetLastError();
             return set_error("gs_masked_pixel_mh: cannot raise k_f2_decide's dynamic LDS limit");
         }
-        hipLaunchKernelGGL(k_f2_decide, dim3(1), dim3(256), dlds, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
-                           maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken, lu_lds);
+        hipLaunchKernelGGL(k_f2_decide, dim3(nb), dim3(256), dlds, st, kn, R, c->f2_G, k0, n_iter, blk_field, blk_bins,
+                           maxbins, logr, u_acc, prop_binned, binned, accept_out, c->f2_taken, lu_lds, F, K);
         GS_LAUNCH_CHECK("k_f2_decide");
         if (k0 + kn < K) {
-            hipLaunchKernelGGL(k_f2_update, dim3(nblocks(n, 256)), dim3(256), 0, st, n, kn, c->f2_Y, c->f2_taken,
+            hipLaunchKernelGGL(k_f2_update, dim3(nblocks(n, 256), nb), dim3(256), 0, st, n, kn, c->f2_Y, c->f2_taken,
                                c->f2_r);
             GS_LAUNCH_CHECK("k_f2_update");
         }
@@ -1742,8 +1829,8 @@ static int pixel_mh_one(gs_masked* c, int K, int n_iter, int maxbins, const int*
     return 0;
 }
 
-// the batch: one sweep per chain (each chain's block synthesis, Gram pass and
-// decisions are whole-GPU launches already), the chains in order on one stream
+// the batch: passes of f2_chains_per_pass chains (one pass for a whole batch
+// whose workspace fits the budget), each launch of a pass serving all its chains
 int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* blk, const int* blk_lmax,
                        const int* blk_field, const int* blk_bins, const double* s_nc, const double* dl_cur,
                        const double* dl_prop, const double* logr, const double* u_acc, const double* prop_binned,
@@ -1764,34 +1851,39 @@ int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* 
     const long long n = (long long)F * c->npix;
     const long long nchunk = (n + F2_CHUNK - 1) / F2_CHUNK;
     const int nb4max = (kcap + 1 + 3) / 4;
-    if (c->f2_cap < kcap) {
-        double* bufs[] = {c->f2_Y, c->f2_phib, c->f2_part, c->f2_G, c->f2_taken};
+    const int NB = f2_chains_per_pass(c, kcap);
+    if (c->f2_cap < kcap || c->f2_nb < NB) {
+        double* bufs[] = {c->f2_Y, c->f2_phib, c->f2_part, c->f2_G, c->f2_taken, c->f2_da, c->f2_r};
         for (double* b : bufs)
             if (b) (void)hipFree(b);
-        c->f2_Y = c->f2_phib = c->f2_part = c->f2_G = c->f2_taken = nullptr;
+        if (c->f2_lmaxb) (void)hipFree(c->f2_lmaxb);
+        c->f2_Y = c->f2_phib = c->f2_part = c->f2_G = c->f2_taken = c->f2_da = c->f2_r = nullptr;
+        c->f2_lmaxb = nullptr;
         c->f2_cap = 0;
+        c->f2_nb = 0;
+        const size_t nb = (size_t)NB;
         int rc = 0;
-        rc |= mc_alloc(&c->f2_Y, (size_t)kcap * n);
-        rc |= mc_alloc(&c->f2_phib, (size_t)kcap * nco * 2 * gs_sht_phi_plane(c->sht) * 2);
-        rc |= mc_alloc(&c->f2_part, (size_t)nchunk * (nb4max * (nb4max + 1) / 2) * 16);
-        rc |= mc_alloc(&c->f2_G, (size_t)(kcap + 1) * (kcap + 1));
-        rc |= mc_alloc(&c->f2_taken, (size_t)kcap);
+        rc |= mc_alloc(&c->f2_Y, nb * kcap * n);
+        rc |= mc_alloc(&c->f2_phib, nb * kcap * nco * 2 * gs_sht_phi_plane(c->sht) * 2);
+        rc |= mc_alloc(&c->f2_part, nb * nchunk * (nb4max * (nb4max + 1) / 2) * 16);
+        rc |= mc_alloc(&c->f2_G, nb * (kcap + 1) * (kcap + 1));
+        rc |= mc_alloc(&c->f2_taken, nb * kcap);
+        rc |= mc_alloc(&c->f2_da, nb * F * c->NR);
+        rc |= mc_alloc(&c->f2_r, nb * n);
+        rc |= mc_alloc(&c->f2_lmaxb, nb * kcap);
         if (rc) return -1;
         c->f2_cap = kcap;
+        c->f2_nb = NB;
     }
-    if (!c->f2_da) {
-        int rc = 0;
-        rc |= mc_alloc(&c->f2_da, (size_t)F * c->NR);
-        rc |= mc_alloc(&c->f2_r, (size_t)n);
-        rc |= mc_alloc(&c->f2_blk, (size_t)F * (c->L + 1));
-        if (rc) return -1;
-    }
+    if (!c->f2_blk && mc_alloc(&c->f2_blk, (size_t)F * (c->L + 1))) return -1;
     const long long dls = (long long)F * (c->L + 1), bins = (long long)F * maxbins, acc = (long long)K * n_iter;
-    for (int b = 0; b < c->B; ++b)
-        if (pixel_mh_one(c, K, n_iter, maxbins, blk, blk_lmax, blk_field, blk_bins, s_nc + b * c->FR,
-                         dl_cur + b * dls, dl_prop + b * dls, logr + b * bins, u_acc + b * acc,
-                         prop_binned + b * bins, binned + b * bins, accept_out + b * acc, st))
+    for (int b = 0; b < c->B; b += NB) {
+        const int nb = std::min(NB, c->B - b);
+        if (pixel_mh_pass(c, nb, K, n_iter, maxbins, blk, blk_lmax, blk_field, blk_bins, s_nc + b * c->FR,
+                          dl_cur + b * dls, dl_prop + b * dls, logr + b * bins, u_acc + b * acc,
+                          prop_binned + b * bins, binned + b * bins, accept_out + b * acc, st))
             return -1;
+    }
     return 0;
 }
 

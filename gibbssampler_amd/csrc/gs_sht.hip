@@ -722,15 +722,21 @@ __device__ __forceinline__ void blk_accumulate(BlkAcc& A, int f, const LegCoef& 
 // STG: the m's recurrence coefficients, a_lm and block indices (l = m..L) are
 // staged in LDS by coalesced loads once per m (small l_max: <= 64 KB), instead
 // of wave-uniform scalar loads -- one memory latency -- per l step
+// A batch of chains (blockIdx.z = chain): chain z's inputs at ain + z NF nlm, its
+// planes at phib + z chain_stride (the block table is shared: every chain of a
+// batch sweeps the same blocks); each chain's arithmetic is the one-chain one.
 template <int NC, int SR, bool STG>
 __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const LegCoef* __restrict__ coef,
                                                                 const double2* __restrict__ ain,
                                                                 const int* __restrict__ blk,
-                                                                double2* __restrict__ phib, int paired) {
+                                                                double2* __restrict__ phib, int paired,
+                                                                long long chain_stride) {
     extern __shared__ __attribute__((aligned(16))) double2 bstage[];
     constexpr int NF = NC;                      // input fields
     constexpr int NCO = NC == 1 ? 1 : 2;        // output comps per block
     const int L = D.L, npair = D.npair, nlm = D.nlm;
+    ain += (long long)blockIdx.z * NF * nlm;
+    phib += (long long)blockIdx.z * chain_stride;
     // XCD-aware remap (bijective): workgroups are dealt round-robin over the 8
     // XCDs; give each XCD a contiguous range of (tile, m) items, m fastest, so
     // the four m of one [m/4] group of the phase planes are written by
@@ -1535,6 +1541,39 @@ __global__ __launch_bounds__(256) void k_pair_support(long long npix, const Pair
     if (threadIdx.x == 0) pflag[p] = any;
 }
 
+// the registered weights' ring classes (gs_sht_register_weights), one workgroup
+// per pair: pflag[p] = 0 (no weight on either ring), 1 (weighted), 3 (weighted
+// and every weight row constant on each ring of the pair -- e.g. isotropic noise
+// on rings the mask leaves whole); wconst[p][c] = (north, south) constants of row c
+// (south 0 for the equatorial ring).  A constant ring's inverse DFT, pixel
+// weight and forward DFT collapse to n w (the unnormalised round trip times the
+// constant), and its pixel vector's weighted inner products are those of its
+// Fourier coordinates (Parseval): the ring stages use both (k_sht_apply_ring_mc,
+// k_sht_synth_ring_mc's Parseval mode).
+__global__ __launch_bounds__(256) void k_ring_classes(long long npix, const PairGeom* __restrict__ geom,
+                                                      const double* __restrict__ wts, int wnc,
+                                                      int* __restrict__ pflag, double2* __restrict__ wconst) {
+    const int p = blockIdx.x;
+    const PairGeom g = geom[p];
+    const int n = g.nphi;
+    const bool eq = g.startS < 0;
+    int any = 0, cst = 1;
+    for (int c = 0; c < wnc; ++c) {
+        const double* wc = wts + (long long)c * npix;
+        const double vn = wc[g.startN], vs = eq ? 0.0 : wc[g.startS];
+        int a = 0, d = 0;
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            const double xn = wc[g.startN + j], xs = eq ? 0.0 : wc[g.startS + j];
+            a |= xn != 0.0 || xs != 0.0;
+            d |= xn != vn || xs != vs;
+        }
+        any |= __syncthreads_or(a);
+        cst &= !__syncthreads_or(d);
+        if (threadIdx.x == 0) wconst[(long long)p * wnc + c] = make_double2(vn, vs);
+    }
+    if (threadIdx.x == 0) pflag[p] = any ? (1 | (cst << 1)) : 0;
+}
+
 // tile t (pairs 16 t ..) has weight: any of its pair flags
 __device__ __forceinline__ bool tile_support(const int* __restrict__ pflag, int t, int npair) {
     bool any = false;
@@ -1543,8 +1582,39 @@ __device__ __forceinline__ bool tile_support(const int* __restrict__ pflag, int 
     return any;
 }
 
+// Parseval coordinates of a constant-weight ring pair (k_ring_classes): from the
+// packed spectrum a_q = s (Z^N_q + i Z^S_q) of the pair (Z the coefficients of
+// y_j = sum_q Z_q e^{2 pi i q j / n}, both rings real) the n real coordinates u
+// of each ring with sum_j y_j^2 = sum_j u_j^2: u_0 = sqrt(n) Z_0, (u_{2q-1}, u_{2q})
+// = sqrt(2n) (Re, Im) Z_q for 0 < q < n / 2, u_{n-1} = sqrt(n) Z_{n/2} (n even,
+// as every HEALPix ring).  Written over the rings' pixel slots: on such a ring
+// the weight is one number, so the f2 Gram pass's weighted sums over these
+// coordinates equal those over the pixels (its rows of block maps, residual).
+__device__ __forceinline__ void parseval_store(const double2* buf, int SB, int nc, int n, double s,
+                                               const PairGeom& g, double* maps, long long npix, int c0) {
+    const bool eq = g.startS < 0;
+    const double r1 = sqrt((double)n) * s, r2 = sqrt(2.0 * n) * s;
+    for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
+        const int c = jj / n, j = jj - c * n;
+        const double2* b = buf + c * SB;
+        const int q = (j + 1) >> 1;
+        const double2 a = b[q], bb = b[(n - q) % n];
+        const double2 zn = make_double2(0.5 * (a.x + bb.x), 0.5 * (a.y - bb.y));
+        const double2 zs = make_double2(0.5 * (a.y + bb.y), -0.5 * (a.x - bb.x));
+        double un, us;
+        if (j == 0 || 2 * q == n) { un = r1 * zn.x; us = r1 * zs.x; }
+        else if (j & 1) { un = r2 * zn.x; us = r2 * zs.x; }
+        else { un = r2 * zn.y; us = r2 * zs.y; }
+        double* mc = maps + (long long)(c0 + c) * npix;
+        mc[g.startN + j] = un;
+        if (!eq) mc[g.startS + j] = us;
+    }
+}
+
 // synthesis: 1-D grid over (ring pair, component group of NCB) (ring_mc_slot);
-// LDS NCB x SB + twiddles
+// LDS NCB x SB + twiddles.  pconst (f2 block maps only; nullptr otherwise): a
+// pair of class 0 (no weight) writes zeros, of class 3 (constant weights) its
+// Parseval coordinates instead of its pixels (parseval_store)
 template <int NV>
 __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, long long npix,
                                                             const int* __restrict__ pairs,
@@ -1554,7 +1624,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
                                                             const double2* __restrict__ bsk, double* __restrict__ maps,
                                                             int ncomp, int NCB, int SB, int twoff,
                                                             const int* __restrict__ comp_lmax, int comp_div,
-                                                            int nring) {
+                                                            int nring, const int* __restrict__ pconst) {
     extern __shared__ double2 lbuf[];
     int idx, cg;
     if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
@@ -1562,6 +1632,17 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
     const int c0 = cg * NCB;
     const int nc = min(NCB, ncomp - c0);
     const PairGeom g = geom[p];
+    const int cls = pconst ? pconst[p] : 1;
+    if (cls == 0) {                                // no weight: the Gram pass multiplies by 0
+        const bool eqz = g.startS < 0;
+        for (int jj = threadIdx.x; jj < nc * g.nphi; jj += blockDim.x) {
+            const int c = jj / g.nphi, j = jj - c * g.nphi;
+            double* mc = maps + (long long)(c0 + c) * npix;
+            mc[g.startN + j] = 0.0;
+            if (!eqz) mc[g.startS + j] = 0.0;
+        }
+        return;
+    }
     const int TC = blockDim.x / NCB;               // fold threads per component
     const int cl = threadIdx.x / TC, tl = threadIdx.x - cl * TC;
     const bool live = cl < nc;
@@ -1637,6 +1718,10 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
         }
     }
     __syncthreads();
+    if (cls & 2) {                                 // constant weights: Parseval coordinates
+        parseval_store(lbuf, SB, nc, n, 1.0, g, maps, npix, c0);
+        return;
+    }
     dft_mc<NV>(lbuf, SB, nc, g, +1, twx, twM, bsk);
     for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
         const int c = jj / n, j = jj - c * n;
@@ -1645,6 +1730,38 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
         mc[g.startN + j] = y.x;
         if (!eq) mc[g.startS + j] = y.y;
     }
+}
+
+// the Parseval coordinates of maps on the constant-weight pairs (class 3 of
+// pconst), in place: forward DFT of each such pair's two rings, Z = DFT / n,
+// parseval_store; other pairs keep their pixels.  1-D grid as the ring stages.
+template <int NV>
+__global__ __launch_bounds__(1024) void k_sht_parseval_ring_mc(long long npix, const int* __restrict__ pairs,
+                                                               const PairGeom* __restrict__ geom,
+                                                               const double2* __restrict__ tw, int Mmax,
+                                                               const double2* __restrict__ bsk, double* maps,
+                                                               int ncomp, int NCB, int SB, int twoff, int nring,
+                                                               const int* __restrict__ pconst) {
+    extern __shared__ double2 lbuf[];
+    int idx, cg;
+    if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
+    const int p = pairs[idx];
+    if (!(pconst[p] & 2)) return;
+    const int c0 = cg * NCB;
+    const int nc = min(NCB, ncomp - c0);
+    const PairGeom g = geom[p];
+    int twM = Mmax;
+    const double2* twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
+    const int n = g.nphi;
+    const bool eq = g.startS < 0;
+    for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
+        const int c = jj / n, j = jj - c * n;
+        const double* mc = maps + (long long)(c0 + c) * npix;
+        lbuf[c * SB + j] = make_double2(mc[g.startN + j], eq ? 0.0 : mc[g.startS + j]);
+    }
+    __syncthreads();
+    dft_mc<NV>(lbuf, SB, nc, g, -1, twx, twM, bsk);
+    parseval_store(lbuf, SB, nc, n, 1.0 / n, g, maps, npix, c0);
 }
 
 // analysis: 1-D grid over (ring pair, component group of NCB) (ring_mc_slot)
@@ -1717,7 +1834,8 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
                                                             const double2* __restrict__ tw, int Mmax,
                                                             const double2* __restrict__ bsk, int ncomp, int NCB, int SB,
                                                             int twoff, const double* __restrict__ wts, int wnc,
-                                                            int nring, const int* __restrict__ pflag) {
+                                                            int nring, const int* __restrict__ pflag,
+                                                            const double2* __restrict__ wconst) {
     extern __shared__ double2 lbuf[];
     int idx, cg;
     if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
@@ -1725,6 +1843,8 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
     const int c0 = cg * NCB;
     const int nc = min(NCB, ncomp - c0);
     if (pflag && !pflag[p]) { ring_zero_phases(L, npair, p, phi, c0, nc); return; }
+    // registered constant-weight pair (k_ring_classes): no DFTs, see below
+    const bool cring = wconst && (pflag[p] & 2);
     const PairGeom g = geom[p];
     const int TC = blockDim.x / NCB;
     const int cl = threadIdx.x / TC, tl = threadIdx.x - cl * TC;
@@ -1798,16 +1918,34 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
         }
     }
     __syncthreads();
-    dft_mc<NV>(lbuf, SB, nc, g, +1, twx, twM, bsk);
-    // the ring's pixels (north .x, south .y) times the weights: the analysis input
-    for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
-        const int c = jj / n, j = jj - c * n;
-        const double* wc = wts + (long long)((c0 + c) % wnc) * npix;
-        const double2 y = lbuf[c * SB + j];
-        lbuf[c * SB + j] = make_double2(wc[g.startN + j] * y.x, eq ? 0.0 : wc[g.startS + j] * y.y);
+    if (cring) {
+        // weights c_N / c_S constant on the rings: inverse DFT (unnormalised),
+        // weight, forward DFT = n (c_N Z^N_k + i c_S Z^S_k) per bin of the packed
+        // spectrum a_k = Z^N_k + i Z^S_k, i.e. n ((c_N + c_S) / 2 a_k + (c_N - c_S) / 2
+        // conj a_{n-k}) -- the two DFTs skipped (the same sums up to rounding)
+        const int nh = n / 2 + 1;
+        for (int jj = threadIdx.x; jj < nc * nh; jj += blockDim.x) {
+            const int c = jj / nh, k = jj - c * nh, nk = (n - k) % n;
+            const double2 wcv = wconst[(long long)p * wnc + (c0 + c) % wnc];
+            const double hp = 0.5 * (wcv.x + wcv.y) * n, hm = 0.5 * (wcv.x - wcv.y) * n;
+            double2* bb = lbuf + c * SB;
+            const double2 a = bb[k], b = bb[nk];
+            bb[k] = make_double2(hp * a.x + hm * b.x, hp * a.y - hm * b.y);
+            if (nk != k) bb[nk] = make_double2(hp * b.x + hm * a.x, hp * b.y - hm * a.y);
+        }
+        __syncthreads();
+    } else {
+        dft_mc<NV>(lbuf, SB, nc, g, +1, twx, twM, bsk);
+        // the ring's pixels (north .x, south .y) times the weights: the analysis input
+        for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
+            const int c = jj / n, j = jj - c * n;
+            const double* wc = wts + (long long)((c0 + c) % wnc) * npix;
+            const double2 y = lbuf[c * SB + j];
+            lbuf[c * SB + j] = make_double2(wc[g.startN + j] * y.x, eq ? 0.0 : wc[g.startS + j] * y.y);
+        }
+        __syncthreads();
+        dft_mc<NV>(lbuf, SB, nc, g, -1, twx, twM, bsk);
     }
-    __syncthreads();
-    dft_mc<NV>(lbuf, SB, nc, g, -1, twx, twM, bsk);
     for (int jj = threadIdx.x; jj < nc * (L + 1); jj += blockDim.x) {
         const int c = jj / (L + 1), m = jj - c * (L + 1);
         const double2* b2 = lbuf + c * SB;
@@ -3038,6 +3176,13 @@ struct gs_sht {
     int merged_n = 0, merged_M = 0;
     // ring-pair support of the current weighted analysis (k_pair_support)
     int* support = nullptr;
+    // registered weights (gs_sht_register_weights): their pair classes (k_ring_classes)
+    // and per-(pair, row) ring constants, computed once and reused by every
+    // weighted transform given the same pointer
+    const double* wreg = nullptr;
+    int wreg_nc = 0;
+    int* wsup = nullptr;
+    double2* wconst = nullptr;
     // the short-ring classes run on a side stream beside the largest class
     // (fork / join by events, graph-capturable); 0 = all on the caller's stream
     hipStream_t side = nullptr;
@@ -3070,7 +3215,8 @@ int sht_alloc(gs_sht* p, T** dst, size_t n) {
 
 void sht_free(gs_sht* p) {
     void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->sscr,
-                    p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs, p->mf_tab, p->mf_off, p->mf_b0, p->support};
+                    p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs, p->mf_tab, p->mf_off, p->mf_b0, p->support,
+                    p->wsup, p->wconst};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (int* b : p->cls_pairs)
@@ -3328,7 +3474,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       LDS_FFT_MAX * (int)sizeof(double2) + 64 * 4 * (int)sizeof(double2));
         const void* mc[] = {(const void*)k_sht_synth_ring_mc<8>, (const void*)k_sht_anal_ring_mc<8>,
-                            (const void*)k_sht_apply_ring_mc<8>};
+                            (const void*)k_sht_apply_ring_mc<8>, (const void*)k_sht_parseval_ring_mc<8>};
         for (const void* f : mc)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RING_MC_LDS_MAX);
         (void)hipGetLastError();
@@ -3459,7 +3605,7 @@ static int ring_mc_ncb(int M, int ncomp) {
 
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
                      const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1, const double* wts = nullptr,
-                     int wnc = 3, const int* pflag = nullptr) {
+                     int wnc = 3, const int* pflag = nullptr, const int* pconst = nullptr) {
     if (p->merged_n > 0) {
         // all ring pairs in one launch: the block size and LDS of the longest FFT
         // (shorter rings leave threads idle; their fold reduction uses the
@@ -3478,7 +3624,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             if (synth)
                 hipLaunchKernelGGL(k_sht_synth_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, maps_out, ncomp, ncb, SB,
-                                   toff, comp_lmax, comp_div, p->merged_n);
+                                   toff, comp_lmax, comp_div, p->merged_n, pconst);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, p->phi, ncomp, ncb, SB,
@@ -3486,6 +3632,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring_mc" : "k_sht_anal_ring_mc");
             return 0;
         }
+        if (pconst) return set_error("sht_rings: Parseval block maps need the multi-component ring stage");
         const bool nb8 = M / 2 > 4 * bd;
         size_t lds = 0;
         int twoff = -1;
@@ -3513,6 +3660,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
         GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring (merged)" : "k_sht_anal_ring (merged)");
         return 0;
     }
+    if (pconst) return set_error("sht_rings: Parseval block maps need the merged ring stage");
     const size_t ncls = p->cls_M.size();
     size_t big = 0;
     for (size_t c = 1; c < ncls; ++c)
@@ -3672,13 +3820,30 @@ static int sht_anal_mfma(gs_sht* p, int nmap, int ncomp, int layout, int acc, do
 // the ring-pair support flags of a weighted analysis on the table path, or
 // nullptr: no skipping (GS_SHT_SUPPORT_SKIP=0, or more tiles than the
 // analysis' list holds)
-static const int* sht_support(gs_sht* p, const double* wts, int wnc, hipStream_t st) {
+// (the registered weights' classes when wts is the registered array: computed
+// once; otherwise k_pair_support for this call)
+// *out = nullptr: no skipping.  A failed launch is an error (the sticky error
+// is reported, not cleared).
+static int sht_support(gs_sht* p, const double* wts, int wnc, hipStream_t st, const int** out) {
     static const bool on = [] { const char* e = getenv("GS_SHT_SUPPORT_SKIP"); return !e || atoi(e) != 0; }();
+    *out = nullptr;
     const int nt = (p->npair + 15) / 16;
-    if (!on || !p->mf || !wts || nt > MF_TL_MAX || nt != p->mf_ntile) return nullptr;
+    if (!on || !p->mf || !wts || nt > MF_TL_MAX || nt != p->mf_ntile) return 0;
+    if (wts == p->wreg && wnc == p->wreg_nc && p->wsup) { *out = p->wsup; return 0; }
     hipLaunchKernelGGL(k_pair_support, dim3(p->npair), dim3(256), 0, st, p->npix, p->geom, wts, wnc, p->support);
-    if (hipGetLastError() != hipSuccess) return nullptr;
-    return p->support;
+    GS_LAUNCH_CHECK("k_pair_support");
+    *out = p->support;
+    return 0;
+}
+
+// the registered ring constants for these weights (nullptr: not registered, or
+// the constant-ring forms turned off by GS_SHT_CONST_RINGS=0)
+static bool const_rings_on() {                     // read per call: tests A/B it in one process
+    const char* e = getenv("GS_SHT_CONST_RINGS");
+    return !e || atoi(e) != 0;
+}
+static const double2* sht_wconst(const gs_sht* p, const double* wts, int wnc) {
+    return const_rings_on() && wts && wts == p->wreg && wnc == p->wreg_nc ? p->wconst : nullptr;
 }
 
 // build (on = 1) or drop (0) the plan's Legendre tables
@@ -3812,7 +3977,8 @@ static int sht_analysis(gs_sht* p, int nmap, int ncomp, int layout, const double
         return 0;
     }
     if (sht_reserve(p, nmap, S(stream))) return -1;
-    const int* sup = sht_support(p, wts, ncomp, S(stream));
+    const int* sup = nullptr;
+    if (sht_support(p, wts, ncomp, S(stream), &sup)) return -1;
     if (sht_rings(p, false, nmap * ncomp, maps, nullptr, stream, nullptr, nullptr, 1, wts, ncomp, sup))
         return -1;
     if (p->mf) return sht_anal_mfma(p, nmap, ncomp, layout, acc, alm, S(stream), sup);
@@ -3844,17 +4010,37 @@ static int sht_analysis(gs_sht* p, int nmap, int ncomp, int layout, const double
 
 long long gs_sht_phi_plane(const gs_sht* p) { return p ? phi_plane(p->L, p->npair) : 0; }
 
-int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int* blk, int K, const int* blk_lmax,
-                        double* phib, double* maps, void* stream) {
+// nmap chains (batch-native plans; others one chain per pass): alm_real
+// [nmap][nfield][(L+1)^2], phib [nmap][K NCO][2][plane], maps [nmap][K NCO][Npix],
+// blk_lmax [nmap][K] (each chain's copy of the blocks' largest l)
+int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real, const int* blk, int K,
+                        const int* blk_lmax, double* phib, double* maps, void* stream, int parseval) {
     if (check_sht(p)) return -1;
     if (nfield != 1 && nfield != 2) return set_error("gs_sht_synth_blocks: nfield must be 1 (T) or 2 (E,B)");
-    if (K < 1 || !alm_real || !blk || !blk_lmax || !phib || !maps) return set_error("gs_sht_synth_blocks: null argument");
-    const long long nin = (long long)nfield * p->nlm;
-    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nfield, alm_real,
-                       GS_ALM_REAL, p->ain, nullptr);
+    if (K < 1 || nmap < 1 || !alm_real || !blk || !blk_lmax || !phib || !maps)
+        return set_error("gs_sht_synth_blocks: null argument");
+    const int nco = nfield == 1 ? 1 : 2;
+    const long long plane = phi_plane(p->L, p->npair);
+    if (nmap > 1 && !sht_batch_native(p)) {
+        for (int b = 0; b < nmap; ++b)
+            if (gs_sht_synth_blocks(p, 1, nfield, alm_real + (long long)b * nfield * (p->L + 1) * (p->L + 1), blk, K,
+                                    blk_lmax + (long long)b * K, phib + (long long)b * K * nco * 2 * plane * 2,
+                                    maps + (long long)b * K * nco * p->npix, stream, parseval))
+                return -1;
+        return 0;
+    }
+    if (nmap > 1 && sht_reserve(p, nmap, S(stream))) return -1;
+    const long long nin = (long long)nmap * nfield * p->nlm;
+    hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * nfield,
+                       alm_real, GS_ALM_REAL, p->ain, nullptr);
     GS_LAUNCH_CHECK("k_sht_alm_in");
     double2* ph = reinterpret_cast<double2*>(phib);
-    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr));
+    const long long cst = (long long)K * nco * 2 * plane;
+    // one launch per chain: the planes are written 16 B per lane at a 64-B stride,
+    // each 64-B run completed by the workgroups of its four m, which one chain's
+    // launch keeps co-resident (all chains in one grid measured 24.4 against 19.1
+    // ms for 16 chains at N_side 256: the runs' pieces then reach L2 too far apart)
+    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr), 1);
     // staged variant when m = 0's coefficients, a_lm and block indices fit 64 KB
     // of LDS (GS_SHT_BLK_STAGE=0 turns it off: tests)
     const size_t stg = (size_t)(p->L + 1) * (4 * sizeof(double2) + nfield * (sizeof(double2) + sizeof(int)));
@@ -3862,24 +4048,25 @@ int gs_sht_synth_blocks(gs_sht* p, int nfield, const double* alm_real, const int
     const bool stage_off = stg_env && atoi(stg_env) == 0;
     const bool use_stg = stg <= 64 * 1024 && !stage_off;
 #define GS_SB(NF, SR) do { if (use_stg) hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR, true>), grid, dim3(LEG_BLOCK), \
-                                         stg, S(stream), p->dev(), p->coef, p->ain, blk, ph, p->syn_paired); \
+                                         stg, S(stream), p->dev(), p->coef, p->ain + b * nfield * p->nlm, blk, \
+                                         ph + b * cst, p->syn_paired, cst); \
     else hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
-                            p->coef, p->ain, blk, ph, p->syn_paired); } while (0)
-    if (nfield == 1) { if (p->syn_sr == 2) GS_SB(1, 2); else GS_SB(1, 1); }
-    else { if (p->syn_sr == 2) GS_SB(2, 2); else GS_SB(2, 1); }
+                            p->coef, p->ain + b * nfield * p->nlm, blk, ph + b * cst, p->syn_paired, cst); } while (0)
+    for (long long b = 0; b < nmap; ++b) {
+        if (nfield == 1) { if (p->syn_sr == 2) GS_SB(1, 2); else GS_SB(1, 1); }
+        else { if (p->syn_sr == 2) GS_SB(2, 2); else GS_SB(2, 1); }
+    }
 #undef GS_SB
     GS_LAUNCH_CHECK("k_sht_synth_blocks");
     // ring stage: the plan's FFT scratch (global / split rings) holds three comps,
     // so rings that need it run three comps per launch
-    const int nco = nfield == 1 ? 1 : 2;
-    const int ncomp = K * nco;
+    const int ncomp = nmap * K * nco;
     const bool scratch = p->gscr != nullptr || p->nsplit > 0;
     const int chunk = scratch ? nco * (3 / nco) : ncomp;    // whole blocks per launch
-    const long long plane = phi_plane(p->L, p->npair);
     for (int c0 = 0; c0 < ncomp; c0 += chunk) {
         const int nc = std::min(chunk, ncomp - c0);
         if (sht_rings(p, true, nc, nullptr, maps + (long long)c0 * p->npix, stream, ph + (long long)c0 * 2 * plane,
-                      blk_lmax + c0 / nco, nco))
+                      blk_lmax + c0 / nco, nco, nullptr, 3, nullptr, parseval ? p->wsup : nullptr))
             return -1;
     }
     return 0;
@@ -3926,6 +4113,65 @@ int gs_sht_map2alm_weighted(gs_sht* p, int ncomp, const double* maps, const doub
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_map2alm_weighted: ncomp must be 1 (T), 2 (Q,U) or 3 (T,Q,U)");
     if (!alm_real || !maps || !weights) return set_error("gs_sht_map2alm_weighted: null argument");
     return sht_analysis(p, 1, ncomp, GS_ALM_REAL, maps, alm_real, 0, stream, weights);
+}
+
+// register a weights array [wnc][Npix] (the masked context's N^-1, fixed for its
+// lifetime): its pair support and constant-ring classes are computed once
+// (k_ring_classes) and used by every weighted transform given the same pointer
+// -- the support skip without a per-call pass, and the constant-ring forms of
+// the fused operator (k_sht_apply_ring_mc).  The caller must not change the
+// array while it is registered; weights = nullptr unregisters.
+int gs_sht_register_weights(gs_sht* p, const double* weights, int wnc, void* stream) {
+    if (check_sht(p)) return -1;
+    p->wreg = nullptr;
+    p->wreg_nc = 0;
+    if (!weights) return 0;
+    if (wnc < 1 || wnc > 3) return set_error("gs_sht_register_weights: wnc must be 1..3");
+    if (!p->wsup && sht_alloc(p, &p->wsup, (size_t)p->npair)) return -1;
+    if (!p->wconst && sht_alloc(p, &p->wconst, (size_t)p->npair * 3)) return -1;
+    hipLaunchKernelGGL(k_ring_classes, dim3(p->npair), dim3(256), 0, S(stream), p->npix, p->geom, weights, wnc,
+                       p->wsup, p->wconst);
+    GS_LAUNCH_CHECK("k_ring_classes");
+    p->wreg = weights;
+    p->wreg_nc = wnc;
+    return 0;
+}
+
+// the registered weights' pair classes: counts of class 0 (no weight), 1
+// (weighted, varying on a ring) and 3 (constant on both rings)
+int gs_sht_ring_class_counts(const gs_sht* p, int counts[3]) {
+    if (check_sht(p)) return -1;
+    counts[0] = counts[1] = counts[2] = 0;
+    if (!p->wreg) return 0;
+    std::vector<int> h((size_t)p->npair);
+    GS_CHECK(hipMemcpy(h.data(), p->wsup, h.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (int v : h) ++counts[v == 0 ? 0 : (v & 2 ? 2 : 1)];
+    return 0;
+}
+
+// f2 block maps in Parseval coordinates on the registered weights' constant
+// pairs: available when the block ring stage runs the merged multi-component
+// kernels (small maps) with registered weights of nfield rows
+int gs_sht_blocks_parseval(const gs_sht* p, int nfield, int ncomp_total) {
+    if (!p || !const_rings_on() || !p->wreg || p->wreg_nc != nfield || p->merged_n <= 0) return 0;
+    return ring_mc_ncb(p->merged_M, ncomp_total) > 1 ? 1 : 0;
+}
+
+// maps [ncomp][Npix] -> Parseval coordinates on the registered constant pairs, in
+// place (the f2 residual, to match block maps made with parseval = 1)
+int gs_sht_parseval_maps(gs_sht* p, int ncomp, double* maps, void* stream) {
+    if (check_sht(p)) return -1;
+    if (!p->wreg || p->merged_n <= 0 || !maps || ncomp < 1) return set_error("gs_sht_parseval_maps: not available");
+    const int M = p->merged_M, bd = ring_block(M);
+    const int ncb = std::max(1, ring_mc_ncb(M, ncomp));
+    const int bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
+    const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
+    const int ncg = (ncomp + ncb - 1) / ncb;
+    const dim3 gm((unsigned)(8 * ((p->merged_n + 15) / 16) * 2 * ncg));
+    hipLaunchKernelGGL(k_sht_parseval_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->npix, p->merged_pairs, p->geom,
+                       p->tw, p->Mmax, p->bsk, maps, ncomp, ncb, SB, toff, p->merged_n, p->wsup);
+    GS_LAUNCH_CHECK("k_sht_parseval_ring_mc");
+    return 0;
 }
 
 int gs_sht_set_mfma(gs_sht* p, int on) {
@@ -3978,16 +4224,18 @@ int gs_sht_apply_weighted_batch(gs_sht* p, int nmap, int ncomp, const double* al
     }
     if (sht_reserve(p, nmap, S(stream))) return -1;
     // pairs / tiles without weight: no synthesis, zero phases, skipped in the analysis
-    const int* sup = sht_support(p, weights, ncomp, S(stream));
+    const int* sup = nullptr;
+    if (sht_support(p, weights, ncomp, S(stream), &sup)) return -1;
     if (sht_synth_mfma(p, nmap, ncomp, S(stream), sup, alm_in, bl)) return -1;
     {
         const int bd = ring_block(M), bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
         const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
         const int nc = nmap * ncomp, ncg = (nc + ncb - 1) / ncb;
         const dim3 gm((unsigned)(8 * ((p->merged_n + 15) / 16) * 2 * ncg));
+        const double2* wc = sup && sup == p->wsup ? sht_wconst(p, weights, ncomp) : nullptr;
         hipLaunchKernelGGL(k_sht_apply_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
                            p->merged_pairs, p->geom, p->phi, p->tw, p->Mmax, p->bsk, nc, ncb, SB, toff, weights, ncomp,
-                           p->merged_n, sup);
+                           p->merged_n, sup, wc);
         GS_LAUNCH_CHECK("k_sht_apply_ring_mc");
     }
     return sht_anal_mfma(p, nmap, ncomp, GS_ALM_REAL, 0, alm_out, S(stream), sup);

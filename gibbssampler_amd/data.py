@@ -41,6 +41,35 @@ def band_mask(nside, cut=0.2):
     return (np.abs(pixel_cos_theta(nside)) > cut).astype(np.float64)
 
 
+def pixel_phi(nside):
+    """phi of every HEALPix RING pixel (healpy pix2ang: polar ring i at (j + 1/2)
+    pi / (2 i), equatorial ring i at (j + 1/2 [i + N even]) pi / (2 N))."""
+    N = int(nside)
+    out = []
+    for i in range(1, 4 * N):
+        ip = i if i < N else (4 * N - i if i > 3 * N else N)
+        n = 4 * ip
+        j = np.arange(n, dtype=np.float64)
+        if i < N or i > 3 * N:
+            out.append((j + 0.5) * np.pi / (2 * ip))
+        else:
+            out.append((j + (0.5 if (i + N) % 2 == 0 else 0.0)) * np.pi / (2 * N))
+    return np.concatenate(out)
+
+
+def galactic_mask(nside, cut=0.2, wave=(0.12, 0.06)):
+    """a galactic-plane-like 80% mask whose edge is not a ring: keep |cos theta| >
+    cut + wave[0] sin(2 phi) + wave[1] cos(3 phi + 1) (f_sky 0.8 on average).  A
+    galactic cut in galactic coordinates leaves the polar caps whole and cuts
+    the rings near the plane along a wavy edge: the rings that cross it have
+    varying weights, the others a constant one (the ring classes of
+    gs_sht_register_weights) -- the realistic counterpart of band_mask, whose
+    every ring is whole or cut."""
+    z, ph = pixel_cos_theta(nside), pixel_phi(nside)
+    edge = cut + wave[0] * np.sin(2.0 * ph) + wave[1] * np.cos(3.0 * ph + 1.0)
+    return (np.abs(z) > edge).astype(np.float64)
+
+
 def _beams(lmax, fwhm_rad, nfields):
     sigma = fwhm_rad / math.sqrt(8.0 * math.log(2.0))
     ell = np.arange(lmax + 1, dtype=np.float64)

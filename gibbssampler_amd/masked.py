@@ -118,7 +118,17 @@ class MaskedCR:
         """True when the context's transforms run the matrix-core table path."""
         return bool(self.lib.gs_masked_sht_tables(self.handle))
 
+    @property
+    def ring_classes(self):
+        """(pairs without weight, pairs with varying ring weights, pairs with one
+        weight per ring) of the context's N^-1 (gs_masked_ring_classes)."""
+        c = (ctypes.c_int * 3)()
+        _capi.check(self.lib.gs_masked_ring_classes(self.handle, c), "gs_masked_ring_classes")
+        return tuple(int(v) for v in c)
+
     def __del__(self):
+        if getattr(_capi, "park", None) is None:    # interpreter teardown: the driver frees everything
+            return
         _capi.park(dict(self.__dict__))       # inside a capture: tensors freed after it
         h = getattr(self, "handle", None)
         if h is not None and h.value:

@@ -322,6 +322,12 @@ typedef struct gs_masked_desc {
 } gs_masked_desc;
 int gs_masked_create(const gs_masked_desc* desc, const double* maps, const double* inv_noise, gs_masked** out);
 int gs_masked_destroy(gs_masked* ctx);
+/* Diagnostic (no reference counterpart): the context's N^-1 ring-pair classes,
+ * computed once at create -- counts[0] pairs without weight, counts[1] pairs
+ * with a ring whose weights vary, counts[2] pairs whose weights are one number
+ * per ring (isotropic noise on rings the mask leaves whole: the PCG operator's
+ * ring stage and the f2 Gram pass take their constant-ring forms there). */
+int gs_masked_ring_classes(const gs_masked* ctx, int* counts /* HOST [3] */);
 int gs_masked_info(const gs_masked* ctx, double* mu3 /* HOST [3] */, double* second_part_grad /* DEVICE [F][NR] */);
 int gs_masked_nchains(const gs_masked* ctx);   /* chains of the batch; -1 for a null context */
 int gs_masked_sht_tables(const gs_masked* ctx); /* 1: the matrix-core table path is on, 0: off */
