@@ -221,11 +221,26 @@ def capturing():
         return False
 
 
+def _drain():
+    """Run the deferred releases (no capture open).  Also reached from release /
+    park outside any capture, so entries parked during a capture that this
+    package did not open (torch.cuda.graph used directly: end_capture never
+    runs) are freed at the next teardown instead of living forever."""
+    while _GRAVEYARD:
+        fn, h = _GRAVEYARD.pop()
+        if fn is not None:
+            try:
+                fn(h)
+            except Exception:
+                pass
+
+
 def release(fn, handle):
     """Call fn(handle) now, or after the open capture ends."""
     if capturing():
         _GRAVEYARD.append((fn, handle))
     else:
+        _drain()
         fn(handle)
 
 
@@ -235,6 +250,7 @@ def park(obj):
     if capturing():
         _GRAVEYARD.append((None, obj))
         return True
+    _drain()
     return False
 
 
@@ -245,14 +261,8 @@ def begin_capture():
 def end_capture():
     """Leave a capture; after the outermost one, run the deferred releases."""
     _CAPTURE_DEPTH[0] = max(0, _CAPTURE_DEPTH[0] - 1)
-    if _CAPTURE_DEPTH[0] == 0:
-        while _GRAVEYARD:
-            fn, h = _GRAVEYARD.pop()
-            if fn is not None:
-                try:
-                    fn(h)
-                except Exception:
-                    pass
+    if _CAPTURE_DEPTH[0] == 0 and not capturing():
+        _drain()
 
 
 def graveyard_size():

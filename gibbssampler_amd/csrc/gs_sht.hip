@@ -2350,7 +2350,16 @@ struct MfTab {
     const long long* off;    // [L+1][ntile] first stored block of (m, tile)
     const int* b0;           // [L+1][ntile] first stored block index (l = m + 16 b)
     int ntile;
+    long long nblk;          // stored blocks (the GS_DEBUG bounds check of every table read)
 };
+
+// GS_DEBUG tripwire: every table address the matrix-core
+// kernels load lies inside the table (a read before its start faulted an r04
+// experiment build); compiled out otherwise
+__device__ __forceinline__ const double* mf_chk(const MfTab& T, const double* a) {
+    GS_ASSERT(a >= T.tab && a < T.tab + T.nblk * MF_BLK);
+    return a;
+}
 
 // pass 1: first representable l of every (m, ring pair) -> per (m, 16-pair tile) b0
 __global__ __launch_bounds__(256) void k_mf_onset(ShtDev D, const double* __restrict__ lmm, const int* __restrict__ lmk,
@@ -2656,13 +2665,13 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     auto tload = [&](const double* blk, bool prev, int q, double (&gv)[8]) __attribute__((always_inline)) {
         if constexpr (SPIN == 2) {
             const int row = 4 * q + g;
-            gv[2 * q + 0] = blk[row * MF_TILE + j];
-            gv[2 * q + 1] = row > 0 ? blk[(row - 1) * MF_TILE + j]
-                                    : (prev ? blk - MF_BLK + 15 * MF_TILE + j : T.tab)[0];
+            gv[2 * q + 0] = *mf_chk(T, blk + row * MF_TILE + j);
+            gv[2 * q + 1] = *mf_chk(T, row > 0 ? blk + (row - 1) * MF_TILE + j
+                                               : (prev ? blk - MF_BLK + 15 * MF_TILE + j : T.tab));
         } else {
             // q = 2 h + e: octet half h, even (e = 0) / odd row of lambda
             const int row = 8 * (q >> 1) + 2 * g + (q & 1);
-            gv[q] = blk[row * MF_TILE + j];
+            gv[q] = *mf_chk(T, blk + row * MF_TILE + j);
         }
     };
     f64x4 Cp[CPW], Cm[CPW];
@@ -2818,6 +2827,188 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     }
 }
 
+// ---- f2 block synthesis on the matrix cores (tables; spin 2: E, B -> Q, U) -------
+// The maps y_k = A(delta a_k) of a group's Metropolis blocks for a batch of
+// chains (NonCenteredGibbs.py:333-355 scores every block with one of them):
+// per (m, ring pair) the sums of k_sht_synth_mfma restricted to each block's l
+// range.  Every (field, l) belongs to at most one block, so the columns carry
+// one source field at a time (blockIdx.z = 2 chain group + field; a pass stages
+// only its field's delta a: F1 row (ex, ey, 0, 0) / F2 row (0, 0, ey, -ex) for E,
+// (0, 0, bx, by) / (-by, bx, 0, 0) for B).
+// The planes are the cost (1.1 GB per chain at N_side 256, l_max 512 against
+// ~2 GFLOP of MFMA), so a workgroup owns one 16-pair tile and the 4 m of one
+// phase block (wave w: m = 4 mq + w): the blocks are walked in l order, each
+// wave adds the block's rows of its m (a quad that straddles a block edge runs
+// with the other rows' B operands zeroed), and at the block's end the four
+// waves' sums go through LDS and out as whole 64-B runs (4 m x one pair), 1 KB
+// contiguous per (chain, component, N / S).  Writing 16 B per lane at the
+// planes' 64-B stride instead ran at 0.7 TB/s (27.7 ms for 16 chains against
+// 2.7 ms with the stores removed).  Blocks below a tile's representable onset
+// get zero planes.  da: [nmap][2][(L+1)^2] real layout (the beam folded in by
+// k_f2_delta); blk: [2][L+1] local block ids (-1: none); phib [nmap][K][2
+// comps][N, S][plane].
+template <int CGW>
+__global__ __launch_bounds__(256) void k_sht_blocks_mfma(ShtDev D, MfTab T, const double* __restrict__ da, int nmap,
+                                                         const int* __restrict__ blk, int K,
+                                                         double2* __restrict__ phib) {
+    constexpr int CPG = 4;                          // chains per 16-column group
+    constexpr int MPW = CGW * CPG;                  // chains per workgroup
+    constexpr int CH = MF_TILE;                     // l staged per chunk (one table block)
+    constexpr int NIT = CH * MPW;                   // staged (l, chain) items per wave and chunk
+    constexpr int PER = (NIT + 63) / 64;
+    constexpr int SR = MPW * 4 + GS_MF_SPAD;
+    constexpr int NROW = 2 * CH;
+    constexpr int NCOL = MPW * 4;                   // columns: chain x (Q re, Q im, U re, U im)
+    __shared__ __attribute__((aligned(16))) double sb[4 * NROW * SR];      // per wave
+    __shared__ __attribute__((aligned(16))) double sc[4 * CH * 6];         // per wave
+    __shared__ __attribute__((aligned(16))) double fb[4 * MF_TILE * NCOL * 2];
+    extern __shared__ int sblk[];                   // the field's block ids, l = 0 .. L
+    const int L = D.L, npair = D.npair;
+    const int fld = blockIdx.z & 1;
+    const int c0 = (blockIdx.z >> 1) * MPW;
+    const int t = blockIdx.x;
+    const int m0 = 4 * blockIdx.y;
+    const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = m0 + w;                           // this wave's m
+    const bool mlive = m <= L;
+    for (int l = threadIdx.x; l <= L; l += blockDim.x) sblk[l] = blk[fld * (L + 1) + l];
+    const int mc = min(m, L);
+    const int nb = (L - mc + MF_TILE) / MF_TILE;
+    const long long ti = (long long)mc * T.ntile + t;
+    const int b0 = mlive ? T.b0[ti] : nb;
+    const double* tab = T.tab + T.off[ti] * MF_BLK;
+    const long long base = cidx(L, mc, mc) - mc;
+    const int pj = min(MF_TILE * t + j, npair - 1);
+    const double is2 = D.geom[pj].is2, xis2 = D.geom[pj].x * is2;
+    const double2* cfb = reinterpret_cast<const double2*>(D.coef + base);
+    const long long NR = (long long)(L + 1) * (L + 1);
+    double* sbw = sb + w * NROW * SR;
+    double* scw = sc + w * CH * 6;
+    // stage table block / chunk ch of this wave's m (wave-local LDS; rows past L zero)
+    int staged = -1;
+    auto stage = [&](int ch) __attribute__((always_inline)) {
+        constexpr double IS2 = 0.70710678118654752440;
+        double2 v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = lane + 64 * k;
+            const int lr = i / MPW, mp = i % MPW;
+            const int l = mc + ch * CH + lr, c = c0 + mp;
+            const bool ok = i < NIT && l <= L && c < nmap && mlive;
+            const int lq = ok ? l : mc;
+            const long long r = mc == 0 ? lq : 2 * (base + lq) - (L + 1);
+            const double* a = da + ((long long)(ok ? c : 0) * 2 + fld) * NR + r;
+            const double2 x = make_double2(a[0], a[1]);
+            v[k] = !ok ? make_double2(0.0, 0.0)
+                       : (mc == 0 ? make_double2(x.x, 0.0) : make_double2(x.x * IS2, x.y * IS2));
+        }
+        double2 pc[3];
+        {
+            const int lr = lane & (CH - 1);
+            const int l = min(mc + ch * CH + lr, L);
+            pc[0] = cfb[4 * l + 1]; pc[1] = cfb[4 * l + 2]; pc[2] = cfb[4 * l + 3];
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = lane + 64 * k;
+            if (i >= NIT) continue;
+            const int lr = i / MPW, mp = i % MPW;
+            const double ex = fld == 0 ? v[k].x : 0.0, ey = fld == 0 ? v[k].y : 0.0;
+            const double bx = fld == 1 ? v[k].x : 0.0, by = fld == 1 ? v[k].y : 0.0;
+            const bool ev = (lr & 1) == 0;
+            double2* P = reinterpret_cast<double2*>(sbw + (lr * 2 + 0) * SR + mp * 4);
+            double2* M = reinterpret_cast<double2*>(sbw + (lr * 2 + 1) * SR + mp * 4);
+            P[0] = make_double2(ev ? ex : -by, ev ? ey : bx);
+            P[1] = make_double2(ev ? bx : ey, ev ? by : -ex);
+            M[0] = make_double2(ev ? -by : ex, ev ? bx : ey);
+            M[1] = make_double2(ev ? ey : bx, ev ? -ex : by);
+        }
+        if (lane < CH) {
+            const bool ok = mc + ch * CH + lane <= L;
+            double2* d = reinterpret_cast<double2*>(scw + lane * 6);
+            d[0] = make_double2(ok ? pc[0].x : 0.0, ok ? pc[0].y : 0.0);
+            d[1] = make_double2(ok ? pc[1].x : 0.0, ok ? pc[1].y : 0.0);
+            d[2] = make_double2(ok ? pc[2].x : 0.0, 0.0);
+        }
+        // the wave's own LDS writes complete before its lanes read them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        staged = ch;
+    };
+    f64x4 Cp[CGW], Cm[CGW];
+#pragma unroll
+    for (int c = 0; c < CGW; ++c) { Cp[c] = f64x4{0, 0, 0, 0}; Cm[c] = f64x4{0, 0, 0, 0}; }
+    const int o = j & 3;
+    // rows [lo, hi) of this wave's m (block k's part of it)
+    auto accumulate = [&](int lo, int hi) __attribute__((always_inline)) {
+        lo = max(lo, m);
+        if (!mlive || hi <= lo) return;
+        for (int i0 = (lo - m) & ~3; m + i0 < hi; i0 += 4) {
+            const int ch = i0 / CH, rr0 = i0 % CH;
+            if (ch != staged) stage(ch);
+            if (ch < b0 || ch >= nb) continue;          // below the onset: lambda = 0 (wave-uniform)
+            const double* bp = tab + (long long)(ch - b0) * MF_BLK;
+            const int rr = rr0 + g;
+            const double w0 = *mf_chk(T, bp + rr * MF_TILE + j);
+            double w1 = 0.0;
+            if (rr > 0) w1 = *mf_chk(T, bp + (rr - 1) * MF_TILE + j);
+            else if (ch - 1 >= b0) w1 = *mf_chk(T, bp - MF_BLK + 15 * MF_TILE + j);
+            const double* cq = scw + rr * 6;
+            const double f1 = fma(cq[2] * xis2, w1, -fma(cq[0], is2, cq[1]) * w0);
+            const double f2 = fma(cq[4] * is2, w1, -(cq[3] * xis2) * w0);
+            const bool ev = (g & 1) == 0;
+            const double ap = ev ? f1 : f2, am = ev ? f2 : f1;
+            const int l = m + i0 + g;
+            const bool mine = l >= lo && l < hi;
+            const double* sbl = sbw + (rr * 2) * SR + (j >> 2) * 4 + o;
+#pragma unroll
+            for (int c = 0; c < CGW; ++c) {
+                const double bqp = mine ? sbl[c * 16] : 0.0;
+                const double bqm = mine ? sbl[SR + c * 16] : 0.0;
+                Cp[c] = mfma64(ap, bqp, Cp[c]);
+                Cm[c] = mfma64(am, bqm, Cm[c]);
+            }
+        }
+    };
+    const long long plane = phi_plane(L, npair);
+    __syncthreads();                                // sblk visible
+    for (int l = m0; l <= L;) {
+        const int k = sblk[l];
+        int le = l + 1;
+        while (le <= L && sblk[le] == k) ++le;
+        if (k >= 0) {
+            accumulate(l, le);
+            // block k's sums of the 4 m -> LDS -> whole 64-B runs of the planes
+            __syncthreads();                        // (the previous flush's readers are done)
+#pragma unroll
+            for (int c = 0; c < CGW; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int pl = g + 4 * r, col = c * 16 + j;
+                    const double sp = Cp[c][r], sn = Cm[c][r];
+                    double* f = fb + ((w * MF_TILE + pl) * NCOL + col) * 2;
+                    f[0] = -(sp + sn);
+                    f[1] = -(sp - sn);
+                }
+#pragma unroll
+            for (int c = 0; c < CGW; ++c) { Cp[c] = f64x4{0, 0, 0, 0}; Cm[c] = f64x4{0, 0, 0, 0}; }
+            __syncthreads();
+            constexpr int NPC = MPW * 2 * 2 * MF_TILE * 4;     // 16-B pieces: chain, comp, N/S, pair, m
+            for (int pc = threadIdx.x; pc < NPC; pc += blockDim.x) {
+                const int wm = pc & 3, pl = (pc >> 2) & (MF_TILE - 1), rest = pc >> 6;
+                const int h = rest & 1, q = (rest >> 1) & 1, cc = rest >> 2;
+                const int pr = MF_TILE * t + pl, mm = m0 + wm;
+                if (c0 + cc >= nmap || pr >= npair || mm > L) continue;
+                const double* f = fb + ((wm * MF_TILE + pl) * NCOL + cc * 4 + q * 2) * 2 + h;
+                phib[((((long long)(c0 + cc) * K + k) * 2 + q) * 2 + h) * plane + phi_at(mm, pr, npair)] =
+                    make_double2(f[0], f[2]);
+            }
+        }
+        l = le;
+    }
+}
+
 // ---- analysis: one wave per 32-l window (16 even + 16 odd l), all pair tiles ----
 // a^T[col][l] = sum_K Phi^T[col][K] G[K][l], K = 4 ring pairs of one function
 // per MFMA: A = Phi^T (lane: row = col j, k = pair 4 s + g), B = G (lane: k =
@@ -2929,11 +3120,11 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     auto tload = [&](const Tw& w, int t, int s, double (&gv)[4][NG]) __attribute__((always_inline)) {
         const double* bp = w.blk;
         const int row = 2 * (j & 7);
-        gv[s][0] = bp[row * MF_TILE + 4 * s + g];
-        gv[s][1] = bp[(row + 1) * MF_TILE + 4 * s + g];
+        gv[s][0] = *mf_chk(T, bp + row * MF_TILE + 4 * s + g);
+        gv[s][1] = *mf_chk(T, bp + (row + 1) * MF_TILE + 4 * s + g);
         if constexpr (SPIN == 2) {
             const double* up = (j & 7) ? bp + (row - 1) * MF_TILE : (w.prv ? bp - MF_BLK + 15 * MF_TILE : T.tab);
-            gv[s][2] = up[4 * s + g];
+            gv[s][2] = *mf_chk(T, up + 4 * s + g);
             const PairGeom* ge = D.geom + min(MF_TILE * t + 4 * s + g, npair - 1);
             gv[s][3] = ge->x;
             gv[s][4] = ge->is2;
@@ -3164,7 +3355,8 @@ struct gs_sht {
     int* mf_b0 = nullptr;
     int mf_ntile = 0;
     long long mf_bytes = 0;
-    MfTab mftab() const { return MfTab{mf_tab, mf_off, mf_b0, mf_ntile}; }
+    long long mf_nblk = 0;
+    MfTab mftab() const { return MfTab{mf_tab, mf_off, mf_b0, mf_ntile, mf_nblk}; }
     // ring classes by FFT length
     std::vector<int> cls_M;      // M of each class
     std::vector<int> cls_n;      // pairs in the class
@@ -3893,7 +4085,7 @@ static int sht_set_mfma(gs_sht* p, int on) {
         if (offd) (void)hipFree(offd);
         return fail("offset upload failed");
     }
-    p->mf_tab = tab; p->mf_off = offd; p->mf_b0 = b0d; p->mf_ntile = ntile;
+    p->mf_tab = tab; p->mf_off = offd; p->mf_b0 = b0d; p->mf_ntile = ntile; p->mf_nblk = std::max(1LL, nblk);
     b0d = nullptr;
     hipLaunchKernelGGL(k_mf_fill, dim3(nblocks(npair, 256), L + 1), dim3(256), 0, 0, p->dev(), lmm, lmk, p->mftab());
     const hipError_t e = hipDeviceSynchronize();
@@ -4030,11 +4222,20 @@ int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real,
         return 0;
     }
     if (nmap > 1 && sht_reserve(p, nmap, S(stream))) return -1;
+    double2* ph = reinterpret_cast<double2*>(phib);
+    const char* bme = getenv("GS_SHT_BLOCKS_MFMA");
+    if (p->mf && nfield == 2 && !(bme && atoi(bme) == 0)) {
+        // the tables: every chain of the batch in one matrix-core launch (both
+        // fields' passes; grid tile x phase block x (chain group, field))
+        const dim3 g((unsigned)p->mf_ntile, (unsigned)((p->L + 4) / 4), (unsigned)(2 * ((nmap + 7) / 8)));
+        hipLaunchKernelGGL(k_sht_blocks_mfma<2>, g, dim3(256), (size_t)(p->L + 1) * sizeof(int), S(stream), p->dev(),
+                           p->mftab(), alm_real, nmap, blk, K, ph);
+        GS_LAUNCH_CHECK("k_sht_blocks_mfma");
+    } else {
     const long long nin = (long long)nmap * nfield * p->nlm;
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * nfield,
                        alm_real, GS_ALM_REAL, p->ain, nullptr);
     GS_LAUNCH_CHECK("k_sht_alm_in");
-    double2* ph = reinterpret_cast<double2*>(phib);
     const long long cst = (long long)K * nco * 2 * plane;
     // one launch per chain: the planes are written 16 B per lane at a 64-B stride,
     // each 64-B run completed by the workgroups of its four m, which one chain's
@@ -4058,6 +4259,7 @@ int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real,
     }
 #undef GS_SB
     GS_LAUNCH_CHECK("k_sht_synth_blocks");
+    }
     // ring stage: the plan's FFT scratch (global / split rings) holds three comps,
     // so rings that need it run three comps per launch
     const int ncomp = nmap * K * nco;
@@ -4179,8 +4381,9 @@ int gs_sht_set_mfma(gs_sht* p, int on) {
     if (on && !sht_batch_native(p))
         return set_error("gs_sht_set_mfma: the Legendre tables are for small maps (no split-ring FFT plan)");
     if (on && !p->mf_tab) {
-        // 3 planes x 8 B per (l, m, ring pair), before the onset skip; budget
-        // GS_SHT_MFMA_MAX_GB (16 GB: N_side 512 / l_max 1024 takes 12.9 GB)
+        // one lambda plane, 8 B per (l, m, ring pair) before the onset skip
+        // (0.54 GB at N_side 256 / l_max 512, 4.3 GB at N_side 512 / l_max
+        // 1024); budget GS_SHT_MFMA_MAX_GB (default 16 GB)
         double gb = 16.0;
         if (const char* e = std::getenv("GS_SHT_MFMA_MAX_GB")) gb = std::atof(e);
         const double need = 8.0 * (double)p->npair * (double)p->nlm / 1e9;

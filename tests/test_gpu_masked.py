@@ -443,7 +443,7 @@ def test_f2_masked_asis_driver_vs_oracle(g, gibbs_cr, sht_mode):
 
 @pytest.mark.parametrize("n_iter,group_bytes,stage", [(1, None, "1"), (2, None, "1"), (2, "1", "1"),
                                                      (1, "50000000", "1"), (1, None, "0"), (2, "1", "0")])
-def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes, stage):
+def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes, stage, sht_mode):
     """gs_masked_pixel_mh decides every block on the device from one block
     synthesis + one Gram pass; with a small workspace budget the blocks run in
     groups (one block per group at "1") and the residual is carried between
@@ -456,7 +456,7 @@ def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes, s
         monkeypatch.setenv("GS_F2_GROUP_BYTES", group_bytes)
     bins, blocks, pv = _f2_parts(g)
     seed, chain, it = 313, 1, 9
-    cr = _cr(g, gibbs_cr=False, ula=False, rng="native", seed=seed, chain=chain)
+    cr = _cr(g, sht_mode, gibbs_cr=False, ula=False, rng="native", seed=seed, chain=chain)
     mh = PixelMH(cr, bins, blocks, pv, n_iter_metropolis=n_iter)
     assert mh.K >= 3
     snc = np.stack([g["f2_snc_E"], g["f2_snc_B"]])
@@ -492,7 +492,7 @@ def f2_large():
 
 
 @pytest.mark.parametrize("n_iter", [1, 20, 90])
-def test_f2_large_group_decisions_equal_one_block_groups(f2_large, monkeypatch, n_iter):
+def test_f2_large_group_decisions_equal_one_block_groups(f2_large, monkeypatch, n_iter, sht_mode):
     """the large-R decision path (138 blocks in one group, G's
     triangle beyond 64 KB of LDS) and n_iter_metropolis up to 90 (the log
     uniforms then no longer fit in LDS beside the triangle and are read from
@@ -507,7 +507,7 @@ def test_f2_large_group_decisions_equal_one_block_groups(f2_large, monkeypatch, 
         else:
             monkeypatch.setenv("GS_F2_GROUP_BYTES", group_bytes)
         cr = MaskedCR(q["pix"], 40.0 ** 2, np.full(12 * q["N"] ** 2, 0.2 ** 2), q["bl"], q["L"], q["N"],
-                      mask=q["mask"], gibbs_cr=False, ula=False, rng="native", seed=515, chain=2)
+                      mask=q["mask"], gibbs_cr=False, ula=False, rng="native", seed=515, chain=2, sht_mode=sht_mode)
         mh = PixelMH(cr, q["bins"], q["blocks"], q["pv"], n_iter_metropolis=n_iter)
         assert mh.K == 138
         new, acc = mh.sample(q["snc"], {k: v.copy() for k, v in q["dl"].items()}, iteration=3)
@@ -728,3 +728,31 @@ def test_batch4_replay_tables_centered_driver(g):
     for b in range(NB):
         for sp in ("EE", "BB"):
             _close(h[sp][:, b], np.array(want[b][sp]))
+
+
+@pytest.mark.parametrize("blocks_mfma", ["0", "1"])
+def test_f2_large_vs_oracle_tables(f2_large, monkeypatch, blocks_mfma):
+    """the 138-block large-R sweep on the table path: the matrix-core block
+    synthesis (GS_SHT_BLOCKS_MFMA 1, single-l blocks: every quad straddles
+    block edges) and the recurrence block synthesis (0) against the oracle's
+    full-map likelihood per block."""
+    from gibbssampler_amd.masked import MaskedCR, PixelMH
+    from oracle import harmonic as H
+    monkeypatch.setenv("GS_SHT_BLOCKS_MFMA", blocks_mfma)
+    q = f2_large
+    N, L = q["N"], q["L"]
+    npol = np.full(12 * N * N, 0.2 ** 2)
+    cr = MaskedCR(q["pix"], 40.0 ** 2, npol, q["bl"], L, N, mask=q["mask"], gibbs_cr=False, ula=False, rng="native",
+                  seed=515, chain=2, sht_mode="mfma")
+    mh = PixelMH(cr, q["bins"], q["blocks"], q["pv"])
+    new, acc = mh.sample(q["snc"], {k: v.copy() for k, v in q["dl"].items()}, iteration=3)
+    zero = np.zeros(12 * N * N)
+    mm = MK.MaskedModel(L, N, 2, q["bl"], np.stack([zero, q["pix"]["Q"], q["pix"]["U"]]),
+                        np.stack([zero, q["mask"] / npol, q["mask"] / npol]))
+    model = H.Model(L, N, 2, q["bl"], [1.0, 1.0], q["bins"], blocks=q["blocks"], proposal_variances=q["pv"],
+                    d_alm=np.zeros((2, (L + 1) ** 2)))
+    want, wacc = MK.pixel_mh(mm, model, {k: v.copy() for k, v in q["dl"].items()}, q["snc"], seed=515, chain=2,
+                             iteration=3)
+    assert acc == wacc
+    _close(new["EE"], want["EE"])
+    _close(new["BB"], want["BB"])

@@ -38,3 +38,18 @@ def test_unfold_bins_matches_reference_semantics():
     from gibbssampler_amd.utils import unfold_bins
     b = np.array([0, 1, 2, 5, 9])
     np.testing.assert_array_equal(unfold_bins([1.0, 2.0, 3.0, 4.0], b), [1, 2, 3, 3, 3, 4, 4, 4, 4])
+
+
+def test_graveyard_drains_outside_any_capture():
+    """entries parked during a capture this package did not open
+    (end_capture never runs for it) are released by the next release / park
+    made outside any capture."""
+    from gibbssampler_amd import _capi
+    freed = []
+    _capi._GRAVEYARD.append((freed.append, "handle-a"))       # as if parked inside a foreign capture
+    _capi._GRAVEYARD.append((None, object()))
+    _capi.release(freed.append, "handle-b")
+    assert freed == ["handle-a", "handle-b"] and _capi.graveyard_size() == 0
+    _capi._GRAVEYARD.append((freed.append, "handle-c"))
+    assert _capi.park(object()) is False
+    assert freed[-1] == "handle-c" and _capi.graveyard_size() == 0
