@@ -987,12 +987,15 @@ constexpr int F2_TMAX = (F2_RMAX + 15) / 16;
 template <int T>
 __global__ __launch_bounds__(256) void k_f2_gram_mfma(int R, long long n, const double* __restrict__ Y,
                                                       const double* __restrict__ r, const double* __restrict__ w,
-                                                      double* __restrict__ partial) {
+                                                      double* __restrict__ partial, const int* __restrict__ live) {
     // chain blockIdx.y: rows Y + y (R - 1) n, residual r + y n, partials after the
-    // gridDim.x chunks of each earlier chain (w shared)
+    // gridDim.x chunks of each earlier chain (w shared).  Workgroup x sums chunk
+    // live[x]: the chunks with a nonzero weight (a chunk without adds exact
+    // zeros, so the list leaves every bit of G)
     Y += (long long)blockIdx.y * (R - 1) * n;
     r += (long long)blockIdx.y * n;
     partial += (long long)blockIdx.y * gridDim.x * (((R + 3) / 4) * ((R + 3) / 4 + 1) / 2) * 16;
+    const int chunk = live[blockIdx.x];
     constexpr int SROW = F2_RMAX + 6;
     static_assert(16 * F2_TMAX <= SROW, "tile rows exceed the staged column");
     constexpr int NPAIR = T * (T + 1) / 2;
@@ -1018,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_f2_gram_mfma(int R, long long n, const 
     f64x4 acc[PPW];
 #pragma unroll
     for (int q = 0; q < PPW; ++q) acc[q] = f64x4{0.0, 0.0, 0.0, 0.0};
-    const long long e0 = blockIdx.x * F2_CHUNK, e1 = min(n, e0 + F2_CHUNK);
+    const long long e0 = (long long)chunk * F2_CHUNK, e1 = min(n, e0 + F2_CHUNK);
     const int c = tid & (F2_GSUB - 1), r0 = tid / F2_GSUB;
     double v[LPT], sw;
     auto issue = [&](long long es) {
@@ -1073,13 +1076,13 @@ __global__ __launch_bounds__(256) void k_f2_gram_mfma(int R, long long n, const 
 
 template <int T>
 void launch_gram_mfma_t(int Tr, unsigned nchunk, unsigned nch, hipStream_t st, int R, long long n, const double* Y,
-                        const double* r, const double* w, double* part) {
+                        const double* r, const double* w, double* part, const int* live) {
     if constexpr (T <= F2_TMAX) {
         if (Tr == T) {
-            hipLaunchKernelGGL(k_f2_gram_mfma<T>, dim3(nchunk, nch), dim3(256), 0, st, R, n, Y, r, w, part);
+            hipLaunchKernelGGL(k_f2_gram_mfma<T>, dim3(nchunk, nch), dim3(256), 0, st, R, n, Y, r, w, part, live);
             return;
         }
-        launch_gram_mfma_t<T + 1>(Tr, nchunk, nch, st, R, n, Y, r, w, part);
+        launch_gram_mfma_t<T + 1>(Tr, nchunk, nch, st, R, n, Y, r, w, part, live);
     }
 }
 
@@ -1254,6 +1257,8 @@ struct gs_masked {
     double *f2_da = nullptr, *f2_r = nullptr, *f2_Y = nullptr, *f2_phib = nullptr, *f2_part = nullptr,
            *f2_G = nullptr, *f2_taken = nullptr;
     int *f2_blk = nullptr, *f2_lmaxb = nullptr;
+    int* f2_live = nullptr;          // Gram chunks with a nonzero N^-1 (set at create)
+    int f2_nlive = 0;
     int f2_cap = 0;                  // blocks per chain the Y / phib buffers hold
     int f2_nb = 0;                   // chains the buffers hold
 };
@@ -1272,6 +1277,7 @@ void mc_free(gs_masked* c) {
     if (c->accd) (void)hipFree(c->accd);
     if (c->f2_blk) (void)hipFree(c->f2_blk);
     if (c->f2_lmaxb) (void)hipFree(c->f2_lmaxb);
+    if (c->f2_live) (void)hipFree(c->f2_live);
     delete c;
 }
 
@@ -1445,6 +1451,23 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
         }
     }
     if (!ok) { mc_free(c); return set_error("gs_masked_create: copy failed"); }
+    {
+        // the f2 Gram pass's chunks (F2_CHUNK elements of [field][pixel]) holding a
+        // nonzero weight: the others add exact zeros and are not launched
+        std::vector<double> w((size_t)c->F * c->npix);
+        ok = hipMemcpy(w.data(), c->ninv, w.size() * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+        std::vector<int> live;
+        for (size_t e0 = 0; ok && e0 < w.size(); e0 += F2_CHUNK) {
+            bool any = false;
+            for (size_t e = e0; e < std::min(w.size(), e0 + (size_t)F2_CHUNK) && !any; ++e) any = w[e] != 0.0;
+            if (any) live.push_back((int)(e0 / F2_CHUNK));
+        }
+        if (live.empty()) live.push_back(0);
+        ok = ok && mc_alloc(&c->f2_live, live.size()) == 0 &&
+             hipMemcpy(c->f2_live, live.data(), live.size() * sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+        c->f2_nlive = (int)live.size();
+        if (!ok) { mc_free(c); return set_error("gs_masked_create: chunk list failed"); }
+    }
     // N^-1 never changes for the context: its ring classes are computed once
     // (support skip, constant-ring operator and f2 Parseval forms)
     if (gs_sht_register_weights(c->sht, c->ninv, c->F, nullptr)) { mc_free(c); return -1; }
@@ -1798,11 +1821,11 @@ static int pixel_mh_pass(gs_masked* c, int nb, int K, int n_iter, int maxbins, c
         GS_LAUNCH_CHECK("k_f2_rep_lmax");
         if (gs_sht_synth_blocks(c->sht, nb, F, c->f2_da, c->f2_blk, kn, c->f2_lmaxb, c->f2_phib, c->f2_Y, st, pv))
             return -1;
-        launch_gram_mfma_t<1>((R + 15) / 16, (unsigned)nchunk, (unsigned)nb, st, R, n, c->f2_Y, c->f2_r, c->ninv,
-                              c->f2_part);
+        launch_gram_mfma_t<1>((R + 15) / 16, (unsigned)c->f2_nlive, (unsigned)nb, st, R, n, c->f2_Y, c->f2_r,
+                              c->ninv, c->f2_part, c->f2_live);
         GS_LAUNCH_CHECK("k_f2_gram_mfma");
         hipLaunchKernelGGL(k_f2_gram_finish, dim3(nblocks((long long)R * R, 256), nb), dim3(256), 0, st, R,
-                           (int)nchunk, c->f2_part, c->f2_G);
+                           c->f2_nlive, c->f2_part, c->f2_G);
         GS_LAUNCH_CHECK("k_f2_gram_finish");
         // dynamic LDS: G's lower triangle (<= 124.6 KB at F2_RMAX rows), plus the
         // log uniforms when they fit in what the static arrays leave of 160 KB

@@ -1613,8 +1613,9 @@ __device__ __forceinline__ void parseval_store(const double2* buf, int SB, int n
 
 // synthesis: 1-D grid over (ring pair, component group of NCB) (ring_mc_slot);
 // LDS NCB x SB + twiddles.  pconst (f2 block maps only; nullptr otherwise): a
-// pair of class 0 (no weight) writes zeros, of class 3 (constant weights) its
-// Parseval coordinates instead of its pixels (parseval_store)
+// pair of class 0 (no weight) is skipped (its pixels keep the caller's finite
+// values), one of class 3 (constant weights) writes its Parseval coordinates
+// instead of its pixels (parseval_store)
 template <int NV>
 __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, long long npix,
                                                             const int* __restrict__ pairs,
@@ -1633,16 +1634,10 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring_mc(int L, int npair, lo
     const int nc = min(NCB, ncomp - c0);
     const PairGeom g = geom[p];
     const int cls = pconst ? pconst[p] : 1;
-    if (cls == 0) {                                // no weight: the Gram pass multiplies by 0
-        const bool eqz = g.startS < 0;
-        for (int jj = threadIdx.x; jj < nc * g.nphi; jj += blockDim.x) {
-            const int c = jj / g.nphi, j = jj - c * g.nphi;
-            double* mc = maps + (long long)(c0 + c) * npix;
-            mc[g.startN + j] = 0.0;
-            if (!eqz) mc[g.startS + j] = 0.0;
-        }
-        return;
-    }
+    // no weight: the Gram pass multiplies these pixels by 0 (the caller's maps
+    // hold finite values there -- gs_masked's block maps stay at their
+    // allocation's zeros), so nothing is computed or written
+    if (cls == 0) return;
     const int TC = blockDim.x / NCB;               // fold threads per component
     const int cl = threadIdx.x / TC, tl = threadIdx.x - cl * TC;
     const bool live = cl < nc;
