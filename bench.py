@@ -68,6 +68,8 @@ def parse():
                     help="bracket the CR sweep of every N-th timed step with hipEvents (graph mode); each "
                          "event pair is an extra pair of graph nodes in its step, so sampling every 10th "
                          "sweep keeps the timed steps close to the un-instrumented graph")
+    ap.add_argument("--mask", default="band", choices=["band", "galactic"],
+                    help="masked workloads: SURVEY 8d's |cos theta| > 0.2 band, or data.galactic_mask (wavy edge)")
     ap.add_argument("--skymap", default="none", choices=["store", "none"],
                     help="harmonic workloads: 'none' (default) runs the CR sweep without writing the sky map s -- "
                          "a full-sky run never reads it: the next CR, the MH and the C_l draw use the per-l "
@@ -427,11 +429,12 @@ def run_surface(args, ctx):
     }
 
 
-def _masked_data(N, L, nfields, seed=0):
+def _masked_data(N, L, nfields, seed=0, mask_kind="band"):
     """synfast of the fiducial spectra on the device + white noise + the 80%
-    band mask, as host arrays."""
+    band mask (mask_kind "galactic": data.galactic_mask, a wavy
+    galactic-plane cut whose edge crosses rings), as host arrays."""
     import torch
-    from gibbssampler_amd.data import band_mask, synfast
+    from gibbssampler_amd.data import band_mask, galactic_mask, synfast
     from gibbssampler_amd.problem import fiducial_dl
     dl = fiducial_dl(L, 3)
     ell = np.arange(L + 1, dtype=np.float64)
@@ -445,7 +448,7 @@ def _masked_data(N, L, nfields, seed=0):
     g = torch.Generator(device="cuda").manual_seed(seed + 1)
     sig = torch.tensor([40.0, 0.2, 0.2], dtype=torch.float64, device="cuda")[:, None]
     d = maps + sig * torch.randn(maps.shape, dtype=torch.float64, device="cuda", generator=g)
-    mask = band_mask(N)
+    mask = band_mask(N) if mask_kind == "band" else galactic_mask(N)
     d = (d * torch.from_numpy(mask).cuda()).cpu().numpy()
     return d, mask, dl
 
@@ -557,7 +560,7 @@ def run_masked_head(args, ctx, cpu=None):
     L, N = args.lmax, args.nside
     Npix = 12 * N * N
     B = args.nchains
-    d, mask, dl = _masked_data(N, L, 2)
+    d, mask, dl = _masked_data(N, L, 2, mask_kind=args.mask)
     pix = {"Q": d[1], "U": d[2]}
     bins = default_bins(L, 2)
     blocks = default_blocks(L, bins)
@@ -599,7 +602,12 @@ def run_masked_head(args, ctx, cpu=None):
         smp = G.ASIS(pix, noise_t, noise_p, 0.5, N, L, Npix, pv, metropolis_blocks=blocks, n_iter=args.warmup,
                      all_sph=False, gibbs_cr=True, n_gibbs=20, overrelaxation=True, **kw)
         runner = smp.masked_runner
-        n_sht, what = 61 + 2, ("over-relaxed aux CR n_gibbs 20 (CenteredGibbs.py:733-825), pixel-domain MH "
+        # the over-relaxed CR's transforms: v | s (1 synthesis) then per iteration
+        # s | v, v | s, s | v -- 1 + 20 x 3 = 61 in the reference, whose s | v opening
+        # iteration k > 0 re-transforms the map the previous one transformed (its v
+        # has not changed): 42 distinct ones, the count charged here; + the f2
+        # residual synthesis and the non-centring's (2)
+        n_sht, what = 42 + 2, ("over-relaxed aux CR n_gibbs 20 (CenteredGibbs.py:733-825), pixel-domain MH "
                                f"over {runner.mh.K} blocks decided on the device (f2), EB")
         h = runner.run(init, max(args.warmup, 1))[0]
         last = last_of(h)
@@ -618,18 +626,22 @@ def run_masked_head(args, ctx, cpu=None):
     if pcg is not None:
         its = pcg.pcg_iterations[n_solves0:]
         launched = pcg.pcg_launched[n_solves0:]
+        work = pcg.pcg_work[n_solves0:]
         syncs = pcg.pcg_syncs[n_solves0:]
         # per CG iteration one alm2map + one map2alm; the rhs adds map2alm iter 3 (7 transforms);
         # the algorithmic work counts each chain's own (converged) iterations
         n_sht = 2 * float(np.mean(its)) + 7
         pcg_info = {"solves": len(its), "cg_iterations_per_solve": round(float(np.mean(its)), 1),
                     "cg_iterations_launched_per_solve": round(float(np.mean(launched)), 1),
+                    "cg_iterations_transformed_per_chain_and_solve": round(float(np.mean(work)) / B, 1),
                     "host_syncs_per_solve": round(float(np.mean(syncs)), 2),
                     "ms_per_cg_iteration_launched": round(elapsed / args.steps * 1e3 / max(float(np.mean(launched)),
                                                                                            1.0), 4),
                     "tolerance": pcg.pcg_accuracy, "residual_last": pcg.pcg_residual,
                     "note": "a batch's CG runs until its slowest chain converges (launched >= per-chain count); "
-                            "converged chains' update kernels return at once"}
+                            "from each host state read on only the unconverged chains are transformed "
+                            "(transformed per chain ~ the per-chain count) and converged chains' update kernels "
+                            "return at once"}
     fl = n_sht * sht_flops(N, L, 16) * B
     achieved = fl / (elapsed / args.steps) / 1e12
     # HBM bytes of the step's transforms from the PMC pass of the same batched
@@ -644,8 +656,11 @@ def run_masked_head(args, ctx, cpu=None):
         "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (analytic fiducial EB spectra, synfast on the device + white noise, 80% band mask)",
+        "data": "synthetic (analytic fiducial EB spectra, synfast on the device + white noise, 80% "
+                + ("band mask" if args.mask == "band" else "galactic-like mask with a wavy edge") + ")",
         "config": {"workload": f"{args.workload}: {what}", "surface": "gibbssampler_amd.gibbs (drop-in classes)",
+                   "mask": args.mask, "ring_pair_classes": dict(zip(("no_weight", "varying", "constant"),
+                                                                   runner.cr.ring_classes)),
                    "nside": N, "lmax": L, "nfields": 2, "chains_per_gpu": B, "global_chains": B * ctx.world,
                    "batching": "the GPU's chains as one batch: every transform one batched SHT over the B maps",
                    "bins": "config.py:45 Planck BB", "blocks": "config.py:51-55",

@@ -137,6 +137,7 @@ _SIGS = [
                                            c_double_p, _VP]),
     ("gs_masked_pcg_info", ctypes.c_int, [_VP, c_int_p]),
     ("gs_masked_pcg_info2", ctypes.c_int, [_VP, c_int_p, c_int_p]),
+    ("gs_masked_pcg_work", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_longlong)]),
     ("gs_masked_pcg_apply", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     ("gs_masked_rj_accept", ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_int, _VP, _VP, _VP]),

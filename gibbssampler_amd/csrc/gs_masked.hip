@@ -37,6 +37,7 @@
 #include "gs_rng.h"
 #include "gs_common.h"
 #include "gs_block.h"
+#include "gs_aux.h"
 
 // library-internal SHT entry points (gs_sht.hip)
 extern "C" long long gs_sht_phi_plane(const gs_sht* p);
@@ -46,6 +47,8 @@ extern "C" int gs_sht_register_weights(gs_sht* p, const double* weights, int wnc
 extern "C" int gs_sht_blocks_parseval(const gs_sht* p, int nfield, int ncomp_total);
 extern "C" int gs_sht_parseval_maps(gs_sht* p, int ncomp, double* maps, void* stream);
 extern "C" int gs_sht_ring_class_counts(const gs_sht* p, int counts[3]);
+extern "C" int gs_sht_aux_pass_batch(gs_sht* p, int nmap, int ncomp, const double* alm_in, const double* bl,
+                                     const void* aux, double* alm_out, void* stream);
 
 using namespace gs;
 using gs_detail::set_error;
@@ -53,7 +56,6 @@ using gs_detail::set_error;
 namespace {
 
 constexpr double PI = 3.14159265358979323846;
-constexpr uint32_t TAG_AUX_V = 8;
 constexpr uint32_t TAG_MALA_U = 9;
 constexpr uint32_t TAG_RJ_U = 10;   // RJPO accept uniform: Philox(0, 0, TAG_RJ_U, iteration)
 constexpr int SUB_S = 16;
@@ -99,32 +101,17 @@ __global__ void k_mc_beam(int L, int F, const double* __restrict__ bl, const dou
 
 // v | s (CenteredGibbs.py:693-700; over-relaxed 797-802) and the s | v input
 // y = v + N^-1 d (711-713), per pixel and field row
-__global__ void k_mc_v(long long npix, int F, Rows rows, int over, double alpha, const double* __restrict__ Abs,
-                       const double* __restrict__ ninv, const double* __restrict__ dpix, double mu0, double mu1,
-                       double mu2, const double* __restrict__ zv, long long zvs, uint32_t seed_lo, uint32_t seed_hi,
-                       uint32_t chain, uint32_t sub, uint32_t iter, double* __restrict__ v, double* __restrict__ y) {
+// (mc_aux_pixel, gs_aux.h: the fused ring stage of gs_sht_aux_pass_batch runs the
+// same expressions, so both give the same bits)
+__global__ void k_mc_v(GsAuxPix a, const double* __restrict__ Abs, double* __restrict__ y) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (g >= F * npix) return;
-    // chain b of the batch: its maps (zvs: the chain stride of the replay normals)
-    const long long cb = (long long)blockIdx.y * F * npix;
-    Abs += cb; v += cb; y += cb;
-    if (zv) zv += (long long)blockIdx.y * zvs;
-    chain += blockIdx.y;
-    const int k = (int)(g / npix);
-    const long long p = g % npix;
-    const int row = rows.r[k];
-    const double mu = row == 0 ? mu0 : (row == 1 ? mu1 : mu2);
-    const double ni = ninv[g];
-    const double gam = mu - ni;
-    const double mean = gam * Abs[g];
-    double z;
-    if (zv) z = zv[g];
-    else z = normal1(chain_key(seed_lo, seed_hi, chain), (uint32_t)p, (uint32_t)row, TAG_AUX_V | (sub << 8), iter);
-    double vn;
-    if (!over) vn = z * sqrt(gam) + mean;
-    else vn = mean + alpha * (v[g] - mean) + sqrt(1.0 - alpha * alpha) * z * sqrt(gam);
-    v[g] = vn;
-    y[g] = vn + ni * dpix[g];
+    if (g >= a.F * a.npix) return;
+    // chain b of the batch (blockIdx.y): its maps
+    const int b = blockIdx.y;
+    const long long cb = (long long)b * a.F * a.npix;
+    const int k = (int)(g / a.npix);
+    const long long p = g % a.npix;
+    y[cb + g] = mc_aux_pixel(a, b, k, p, Abs[cb + g]);
 }
 
 __device__ __forceinline__ void slot_normals(const double* __restrict__ zs, long long NR, int F, long long r, int nv,
@@ -1253,6 +1240,8 @@ struct gs_masked {
     double* pcgs = nullptr;          // PcgState [B] of the device CG
     int pcg_syncs = 0;               // host synchronisations of the last solve
     int pcg_launched = 0;            // CG iterations launched by the last solve (>= every chain's count)
+    long long pcg_work = 0;          // chain-iterations transformed by the last solve (compaction: sum of active)
+    int* pcg_act = nullptr;          // [B] the unconverged chains of the running solve
     // f2 block MH workspace (f2_nb chains at a time; allocated on first use, grown as needed)
     double *f2_da = nullptr, *f2_r = nullptr, *f2_Y = nullptr, *f2_phib = nullptr, *f2_part = nullptr,
            *f2_G = nullptr, *f2_taken = nullptr;
@@ -1278,6 +1267,7 @@ void mc_free(gs_masked* c) {
     if (c->f2_blk) (void)hipFree(c->f2_blk);
     if (c->f2_lmaxb) (void)hipFree(c->f2_lmaxb);
     if (c->f2_live) (void)hipFree(c->f2_live);
+    if (c->pcg_act) (void)hipFree(c->pcg_act);
     delete c;
 }
 
@@ -1316,21 +1306,48 @@ int mc_synth(gs_masked* c, int nch, const double* s, double* out, hipStream_t st
 
 // one v | s pass (plain or over-relaxed) for the whole batch; zv: chain 0's
 // replay normals of this pass, zvs their chain stride
+GsAuxPix aux_args(const gs_masked* c, int over, double* v, const double* zv, long long zvs, uint32_t slo,
+                  uint32_t shi, uint32_t chain, uint32_t sub, uint32_t it) {
+    GsAuxPix a;
+    a.ninv = c->ninv; a.dpix = c->dpix; a.v = v; a.zv = zv; a.zvs = zvs; a.npix = c->npix;
+    for (int k = 0; k < 3; ++k) { a.mu[k] = c->mu[k]; a.rows[k] = c->rows.r[k]; }
+    a.F = c->F; a.over = over; a.alpha = c->alpha;
+    a.slo = slo; a.shi = shi; a.chain = chain; a.sub = sub; a.iter = it;
+    return a;
+}
+
 int mc_v(gs_masked* c, int over, const double* s, double* v, const double* zv, long long zvs, uint32_t slo,
          uint32_t shi, uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
     if (mc_synth(c, c->B, s, c->Abs, st)) return -1;
-    hipLaunchKernelGGL(k_mc_v, dim3(nblocks(c->FP, 256), c->B), dim3(256), 0, st, c->npix, c->F, c->rows, over,
-                       c->alpha, c->Abs, c->ninv, c->dpix, c->mu[0], c->mu[1], c->mu[2], zv, zvs, slo, shi, chain, sub,
-                       it, v, c->y);
+    hipLaunchKernelGGL(k_mc_v, dim3(nblocks(c->FP, 256), c->B), dim3(256), 0, st,
+                       aux_args(c, over, v, zv, zvs, slo, shi, chain, sub, it), c->Abs, c->y);
     GS_LAUNCH_CHECK("k_mc_v");
     return 0;
 }
 
-int mc_s(gs_masked* c, int over, double* s, const double* zs, long long zss, uint32_t slo, uint32_t shi,
-         uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
-    // s | v analysis: iter 0 explicit for EB/TEB (CenteredGibbs.py:717,773,812),
-    // healpy's default iter = 3 for TT (CenteredGibbs.py:208)
-    if (gs_sht_map2alm_batch(c->sht, c->B, c->F, GS_ALM_REAL, c->y, nullptr, c->r, c->adj_iter, st)) return -1;
+// the s | v analysis r = map2alm(y): iter 0 explicit for EB/TEB
+// (CenteredGibbs.py:717,773,812), healpy's default iter = 3 for TT (:208)
+int mc_anal(gs_masked* c, hipStream_t st) {
+    return gs_sht_map2alm_batch(c->sht, c->B, c->F, GS_ALM_REAL, c->y, nullptr, c->r, c->adj_iter, st);
+}
+
+// v | s and the s | v analysis it feeds: one fused pass where the plan has one
+// (tables, merged ring stage, iter 0: gs_sht_aux_pass_batch, the maps A b s and
+// y never leave LDS), else mc_v + mc_anal -- the same bits either way
+int mc_vs(gs_masked* c, int over, const double* s, double* v, const double* zv, long long zvs, uint32_t slo,
+          uint32_t shi, uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
+    if (c->adj_iter == 0) {
+        const GsAuxPix a = aux_args(c, over, v, zv, zvs, slo, shi, chain, sub, it);
+        const int rc = gs_sht_aux_pass_batch(c->sht, c->B, c->F, s, c->bl, &a, c->r, st);
+        if (rc <= 0) return rc;
+    }
+    if (mc_v(c, over, s, v, zv, zvs, slo, shi, chain, sub, it, st)) return -1;
+    return mc_anal(c, st);
+}
+
+// s | v from the analysis in c->r (k_mc_s)
+int mc_s_update(gs_masked* c, int over, double* s, const double* zs, long long zss, uint32_t slo, uint32_t shi,
+                uint32_t chain, uint32_t sub, uint32_t it, hipStream_t st) {
     double imu[3] = {0, 0, 0};
     for (int k = 0; k < c->F; ++k) imu[k] = 1.0 / c->mu[c->rows.r[k]];
     const dim3 g(nblocks(c->nlm, 256), c->B), b(256);
@@ -1426,6 +1443,7 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     rc |= mc_alloc(&c->params_pcg, B * (c->L + 1) * GS_NPARAM);
     rc |= mc_alloc(&c->dots, 2 * B);
     rc |= mc_alloc(&c->pcgs, B * (sizeof(PcgState) / sizeof(double)));
+    rc |= mc_alloc(&c->pcg_act, B);
     if (rc) { mc_free(c); return -1; }
     std::vector<int> e2b((size_t)4 * (c->L + 1));
     for (int sp = 0; sp < 4; ++sp)
@@ -1529,11 +1547,36 @@ int gs_masked_gradient(gs_masked* c, const double* dl, const double* s, double* 
 // ---- f1 PCG ----------------------------------------------------------------
 // A Q p for the batch, without its dot product (partial == nullptr) or with the
 // per-block p . Q p of every chain
+// chains act[0 .. na) of a [B][n] array <-> a compact [na][n] one
+__global__ void k_gather_chains(long long n, const int* __restrict__ act, const double* __restrict__ src,
+                                double* __restrict__ dst) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g < n) dst[blockIdx.y * n + g] = src[(long long)act[blockIdx.y] * n + g];
+}
+__global__ void k_scatter_chains(long long n, const int* __restrict__ act, const double* __restrict__ src,
+                                 double* __restrict__ dst) {
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (g < n) dst[(long long)act[blockIdx.y] * n + g] = src[blockIdx.y * n + g];
+}
+
+// na < B (the batched CG's unconverged chains act[0 .. na)): only their maps are
+// transformed -- gathered into a compact batch (map b of a batch is bit-identical
+// to the same map transformed alone, so a chain's result does not depend on
+// which others still run), the results scattered back; converged chains' r is
+// not updated (their update kernels no longer read it)
 static int pcg_apply(gs_masked* c, const double* dl, const double* x, double* out, double* partial, int nb,
-                     const PcgState* state, hipStream_t st) {
+                     const PcgState* state, hipStream_t st, int na = -1, const int* act = nullptr) {
     // r = map2alm(N^-1 A b x): one fused operator pass (the maps stay in LDS on
     // the table path; bit-identical to alm2map_beamed + map2alm_weighted)
-    if (gs_sht_apply_weighted_batch(c->sht, c->B, c->F, x, c->bl, c->ninv, c->pix0, c->r, st)) return -1;
+    if (na >= 0 && na < c->B) {
+        const long long n = c->FR;
+        hipLaunchKernelGGL(k_gather_chains, dim3(nblocks(n, 256), na), dim3(256), 0, st, n, act, x, c->snew);
+        if (gs_sht_apply_weighted_batch(c->sht, na, c->F, c->snew, c->bl, c->ninv, c->pix0, c->grad1, st)) return -1;
+        hipLaunchKernelGGL(k_scatter_chains, dim3(nblocks(n, 256), na), dim3(256), 0, st, n, act, c->grad1, c->r);
+        GS_LAUNCH_CHECK("pcg compact apply");
+    } else if (gs_sht_apply_weighted_batch(c->sht, c->B, c->F, x, c->bl, c->ninv, c->pix0, c->r, st)) {
+        return -1;
+    }
     const dim3 g(partial ? nb : nblocks(c->nlm, RED_BLOCK), c->B), b(RED_BLOCK);
     const double iw = 1.0 / c->w;
     if (c->F == 1) hipLaunchKernelGGL(k_pcg_qdot<1>, g, b, 0, st, c->L, dl, c->bl, x, c->r, iw, out, partial, state);
@@ -1611,8 +1654,12 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
 #undef GS_PI
     hipLaunchKernelGGL(k_pcg_scal<0>, g1, bb, 0, st, nb, c->partial, dst, tol, maxiter);
     GS_LAUNCH_CHECK("k_pcg_init");
+    // the unconverged chains as of the last state read (GS_PCG_COMPACT=0: always all)
+    int na = B;
+    const char* ce = getenv("GS_PCG_COMPACT");
+    const bool compact = B > 1 && !(ce && atoi(ce) == 0);
     auto iteration = [&]() -> int {
-        if (pcg_apply(c, dl, c->pp, c->pq, c->partial, nb, dst, st)) return -1;
+        if (pcg_apply(c, dl, c->pp, c->pq, c->partial, nb, dst, st, na, c->pcg_act)) return -1;
 #define GS_PU(FF) hipLaunchKernelGGL((k_pcg_upd<FF>), gb, bb, 0, st, c->L, nb, c->params_pcg, c->pp, c->pq, x, c->pr, \
                                      c->pz, c->partial, dst)
         if (c->F == 1) GS_PU(1); else if (c->F == 2) GS_PU(2); else GS_PU(3);
@@ -1635,6 +1682,7 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
     };
     if (read_state()) return -1;
     int launched = 0, batch = 8;
+    c->pcg_work = 0;
     std::vector<double> rn_prev((size_t)B);
     for (int b = 0; b < B; ++b) rn_prev[b] = h[b].rn;
     c->pcg_syncs = 1;
@@ -1643,9 +1691,20 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
         for (int j = 0; j < k; ++j)
             if (iteration()) return -1;
         launched += k;
+        c->pcg_work += (long long)k * na;
         if (read_state()) return -1;
         ++c->pcg_syncs;
         if (all_done()) break;
+        if (compact) {
+            std::vector<int> act;
+            for (int b = 0; b < B; ++b)
+                if (!h[b].done) act.push_back(b);
+            if ((int)act.size() < na) {
+                GS_CHECK(hipMemcpyAsync(c->pcg_act, act.data(), act.size() * sizeof(int), hipMemcpyHostToDevice, st));
+                GS_CHECK(hipStreamSynchronize(st));      // (act is host-pageable and goes out of scope)
+                na = (int)act.size();
+            }
+        }
         // predicted remaining iterations of the slowest chain from its residual's
         // decay over this batch
         double rem_max = 1.0;
@@ -1704,6 +1763,12 @@ int gs_masked_pcg_info2(const gs_masked* c, int* host_syncs, int* launched) {
     if (!c) return set_error("null masked context");
     if (host_syncs) *host_syncs = c->pcg_syncs;
     if (launched) *launched = c->pcg_launched;
+    return 0;
+}
+
+int gs_masked_pcg_work(const gs_masked* c, long long* chain_iterations) {
+    if (!c || !chain_iterations) return set_error("gs_masked_pcg_work: null argument");
+    *chain_iterations = c->pcg_work;
     return 0;
 }
 
@@ -1955,21 +2020,27 @@ int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v,
             // v | s plain, then n_gibbs x (s | v, v | s, s | v) over-relaxed; replay
             // normals per chain: zv [B][1 + n_gibbs][F][Npix], zs [B][2 n_gibbs][F][NR]
             const long long zvs = (1LL + c->n_gibbs) * FP, zss = 2LL * c->n_gibbs * FR;
-            if (mc_v(c, 0, s, vv, zv, zvs, slo, shi, ch, SUB_V_INIT, iteration, st)) return -1;
+            // CenteredGibbs.py:733-825: v | s, then per iteration s | v, v | s, s | v.  The
+            // s | v that opens iteration k > 0 follows the one that closed k - 1 with
+            // v unchanged: the reference transforms the same map again
+            // (map2alm(v + N^-1 d), :763-765 = :810-812); here that analysis is the
+            // one already in c->r (deterministic: the same bits), so each iteration
+            // costs one v | s pass and one analysis instead of one and two
+            if (mc_vs(c, 0, s, vv, zv, zvs, slo, shi, ch, SUB_V_INIT, iteration, st)) return -1;
             for (int k = 0; k < c->n_gibbs; ++k) {
                 const double* zs1 = zs ? zs + (2LL * k) * FR : nullptr;
                 const double* zs2 = zs ? zs + (2LL * k + 1) * FR : nullptr;
                 const double* zvk = zv ? zv + (1LL + k) * FP : nullptr;
-                if (mc_s(c, 1, s, zs1, zss, slo, shi, ch, SUB_S + 2 * k, iteration, st)) return -1;
-                if (mc_v(c, 1, s, vv, zvk, zvs, slo, shi, ch, k, iteration, st)) return -1;
-                if (mc_s(c, 1, s, zs2, zss, slo, shi, ch, SUB_S + 2 * k + 1, iteration, st)) return -1;
+                if (mc_s_update(c, 1, s, zs1, zss, slo, shi, ch, SUB_S + 2 * k, iteration, st)) return -1;
+                if (mc_vs(c, 1, s, vv, zvk, zvs, slo, shi, ch, k, iteration, st)) return -1;
+                if (mc_s_update(c, 1, s, zs2, zss, slo, shi, ch, SUB_S + 2 * k + 1, iteration, st)) return -1;
             }
         } else {
             // replay normals per chain: zv [B][n_gibbs][F][Npix], zs [B][n_gibbs][F][NR]
             const long long zvs = (long long)c->n_gibbs * FP, zss = (long long)c->n_gibbs * FR;
             for (int k = 0; k < c->n_gibbs; ++k) {
-                if (mc_v(c, 0, s, vv, zv ? zv + k * FP : nullptr, zvs, slo, shi, ch, k, iteration, st)) return -1;
-                if (mc_s(c, 0, s, zs ? zs + k * FR : nullptr, zss, slo, shi, ch, SUB_S + 2 * k, iteration, st))
+                if (mc_vs(c, 0, s, vv, zv ? zv + k * FP : nullptr, zvs, slo, shi, ch, k, iteration, st)) return -1;
+                if (mc_s_update(c, 0, s, zs ? zs + k * FR : nullptr, zss, slo, shi, ch, SUB_S + 2 * k, iteration, st))
                     return -1;
             }
         }

@@ -42,6 +42,7 @@
 
 #include "gibbs_capi.h"
 #include "gs_common.h"
+#include "gs_aux.h"
 
 using gs_detail::set_error;
 
@@ -1816,21 +1817,44 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring_mc(int L, int npair, lon
     }
 }
 
-// weighted operator ring stage (the masked PCG's A^T N^-1 A): per ring pair the
-// synthesis ring work (fold, inverse DFT), the pixel weights, and the analysis
-// ring work (forward DFT, unfold) in one workgroup, the pixels never leaving
-// LDS: the same arithmetic as k_sht_synth_ring_mc, a map stored and reloaded,
-// and k_sht_anal_ring_mc on weights x map (bit-identical), phases updated in
-// place (each pair's phases are read and written by its own workgroup only)
-template <int NV>
+// the pixel operations of the fused ring stage (k_sht_apply_ring_mc): y -> the
+// analysis input of comp c at the ring pair's pixels iN (north) / iS (south)
+struct PixWeights {                 // the masked PCG's N^-1 (weights [wnc][Npix] shared by the batch)
+    const double* wts;
+    int wnc;
+    long long npix;
+    const double2* wconst;          // registered constant-ring values (nullptr: none)
+    static constexpr bool kConst = true;
+    __device__ __forceinline__ double2 operator()(int c, long long iN, long long iS, bool eq, double2 y) const {
+        const double* wc = wts + (long long)(c % wnc) * npix;
+        return make_double2(wc[iN] * y.x, eq ? 0.0 : wc[iS] * y.y);
+    }
+};
+struct PixAux {                     // the aux-variable v | s update (gs_aux.h), comps (chain, field)
+    gs::GsAuxPix a;
+    static constexpr bool kConst = false;
+    __device__ __forceinline__ double2 operator()(int c, long long iN, long long iS, bool eq, double2 y) const {
+        const int b = c / a.F, k = c - b * a.F;
+        const double yn = gs::mc_aux_pixel(a, b, k, iN, y.x);
+        return make_double2(yn, eq ? 0.0 : gs::mc_aux_pixel(a, b, k, iS, y.y));
+    }
+};
+
+// fused ring stage: per ring pair the synthesis ring work (fold, inverse DFT),
+// a pixel operation (the masked PCG's N^-1 weights: the operator A^T N^-1 A; or
+// the aux-variable v | s update that turns A b s into y = v + N^-1 d), and the
+// analysis ring work (forward DFT, unfold) in one workgroup, the pixels never
+// leaving LDS: the same arithmetic as k_sht_synth_ring_mc, a map stored, the
+// pixel kernel and k_sht_anal_ring_mc (bit-identical), phases updated in place
+// (each pair's phases are read and written by its own workgroup only)
+template <int NV, class Op>
 __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, long long npix,
                                                             const int* __restrict__ pairs,
                                                             const PairGeom* __restrict__ geom, double2* phi,
                                                             const double2* __restrict__ tw, int Mmax,
                                                             const double2* __restrict__ bsk, int ncomp, int NCB, int SB,
-                                                            int twoff, const double* __restrict__ wts, int wnc,
-                                                            int nring, const int* __restrict__ pflag,
-                                                            const double2* __restrict__ wconst) {
+                                                            int twoff, Op op, int nring,
+                                                            const int* __restrict__ pflag) {
     extern __shared__ double2 lbuf[];
     int idx, cg;
     if (!ring_mc_slot(nring, (ncomp + NCB - 1) / NCB, idx, cg)) return;
@@ -1839,7 +1863,8 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
     const int nc = min(NCB, ncomp - c0);
     if (pflag && !pflag[p]) { ring_zero_phases(L, npair, p, phi, c0, nc); return; }
     // registered constant-weight pair (k_ring_classes): no DFTs, see below
-    const bool cring = wconst && (pflag[p] & 2);
+    bool cring = false;
+    if constexpr (Op::kConst) cring = op.wconst && (pflag[p] & 2);
     const PairGeom g = geom[p];
     const int TC = blockDim.x / NCB;
     const int cl = threadIdx.x / TC, tl = threadIdx.x - cl * TC;
@@ -1921,7 +1946,8 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
         const int nh = n / 2 + 1;
         for (int jj = threadIdx.x; jj < nc * nh; jj += blockDim.x) {
             const int c = jj / nh, k = jj - c * nh, nk = (n - k) % n;
-            const double2 wcv = wconst[(long long)p * wnc + (c0 + c) % wnc];
+            double2 wcv = make_double2(0.0, 0.0);
+            if constexpr (Op::kConst) wcv = op.wconst[(long long)p * op.wnc + (c0 + c) % op.wnc];
             const double hp = 0.5 * (wcv.x + wcv.y) * n, hm = 0.5 * (wcv.x - wcv.y) * n;
             double2* bb = lbuf + c * SB;
             const double2 a = bb[k], b = bb[nk];
@@ -1931,12 +1957,10 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
         __syncthreads();
     } else {
         dft_mc<NV>(lbuf, SB, nc, g, +1, twx, twM, bsk);
-        // the ring's pixels (north .x, south .y) times the weights: the analysis input
+        // the pixel operation on the ring's pixels (north .x, south .y): the analysis input
         for (int jj = threadIdx.x; jj < nc * n; jj += blockDim.x) {
             const int c = jj / n, j = jj - c * n;
-            const double* wc = wts + (long long)((c0 + c) % wnc) * npix;
-            const double2 y = lbuf[c * SB + j];
-            lbuf[c * SB + j] = make_double2(wc[g.startN + j] * y.x, eq ? 0.0 : wc[g.startS + j] * y.y);
+            lbuf[c * SB + j] = op(c0 + c, g.startN + j, g.startS + j, eq, lbuf[c * SB + j]);
         }
         __syncthreads();
         dft_mc<NV>(lbuf, SB, nc, g, -1, twx, twM, bsk);
@@ -2553,6 +2577,9 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
     const bool tlive = t < T.ntile && (!pflag || tile_support(pflag, t, D.npair));
     const int cg0 = (wave % H) * CPW;             // this wave's first column group
     const int c0 = blockIdx.z * MPW;
+    // the wave's column groups holding maps (wave-uniform; a batch of fewer maps
+    // than the workgroup's columns -- the batched CG's unconverged chains)
+    const int ncl = min(CPW, (nmap - c0 - cg0 * CPG + CPG - 1) / CPG);
     const int nb = (L - m + MF_TILE) / MF_TILE;
     const long long ti = (long long)m * T.ntile + min(t, T.ntile - 1);
     const int b0 = tlive ? T.b0[ti] : nb;
@@ -2744,8 +2771,10 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
                 }
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
-                    Cp[c] = mfma64(ap, bq[q & 1][2 * c + 0], Cp[c]);
-                    Cm[c] = mfma64(am, bq[q & 1][2 * c + 1], Cm[c]);
+                    if (c < ncl) {                  // (a column group without maps: no MFMAs)
+                        Cp[c] = mfma64(ap, bq[q & 1][2 * c + 0], Cp[c]);
+                        Cm[c] = mfma64(am, bq[q & 1][2 * c + 1], Cm[c]);
+                    }
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -3055,6 +3084,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int win = wgy * WPG + wave / H;
     const int cg0 = (wave % H) * CPW;             // this wave's first column group
+    const int ncl = min(CPW, (nmap - (int)blockIdx.z * MPW - cg0 * CPG + CPG - 1) / CPG);   // groups with maps
     const int lw = m + 32 * win;
     const bool live = lw <= L;
     const int c0 = blockIdx.z * MPW;
@@ -3249,6 +3279,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
                     }
 #pragma unroll
                     for (int c = 0; c < CPW; ++c) {
+                        if (c >= ncl) continue;     // (a column group without maps: no MFMAs)
                         // F1 takes the parity-p combination (p = 0: +, 1: -), F2 the other
                         if constexpr (SPIN == 2) {
                             C[c][p] = mfma64(aq[s & 1][p][c][0], gz[0], C[c][p]);
@@ -3661,7 +3692,8 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       LDS_FFT_MAX * (int)sizeof(double2) + 64 * 4 * (int)sizeof(double2));
         const void* mc[] = {(const void*)k_sht_synth_ring_mc<8>, (const void*)k_sht_anal_ring_mc<8>,
-                            (const void*)k_sht_apply_ring_mc<8>, (const void*)k_sht_parseval_ring_mc<8>};
+                            (const void*)k_sht_apply_ring_mc<8, PixWeights>, (const void*)k_sht_apply_ring_mc<8, PixAux>,
+                            (const void*)k_sht_parseval_ring_mc<8>};
         for (const void* f : mc)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RING_MC_LDS_MAX);
         (void)hipGetLastError();
@@ -4430,13 +4462,45 @@ int gs_sht_apply_weighted_batch(gs_sht* p, int nmap, int ncomp, const double* al
         const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
         const int nc = nmap * ncomp, ncg = (nc + ncb - 1) / ncb;
         const dim3 gm((unsigned)(8 * ((p->merged_n + 15) / 16) * 2 * ncg));
-        const double2* wc = sup && sup == p->wsup ? sht_wconst(p, weights, ncomp) : nullptr;
-        hipLaunchKernelGGL(k_sht_apply_ring_mc<8>, gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
-                           p->merged_pairs, p->geom, p->phi, p->tw, p->Mmax, p->bsk, nc, ncb, SB, toff, weights, ncomp,
-                           p->merged_n, sup, wc);
+        const PixWeights op{weights, ncomp, p->npix, sup && sup == p->wsup ? sht_wconst(p, weights, ncomp) : nullptr};
+        hipLaunchKernelGGL((k_sht_apply_ring_mc<8, PixWeights>), gm, dim3(bdm), ldsm, S(stream), p->L, p->npair,
+                           p->npix, p->merged_pairs, p->geom, p->phi, p->tw, p->Mmax, p->bsk, nc, ncb, SB, toff, op,
+                           p->merged_n, sup);
         GS_LAUNCH_CHECK("k_sht_apply_ring_mc");
     }
     return sht_anal_mfma(p, nmap, ncomp, GS_ALM_REAL, 0, alm_out, S(stream), sup);
+}
+
+// the aux-variable step's v | s and s | v analysis in one pass (gs_masked's
+// masked CR, CenteredGibbs.py:693-717): alm_out = map2alm(y) (real layout, iter
+// 0) with y = the v | s update (GsAuxPix, which also writes v) of alm2map(bl x
+// alm_in), nmap chains of ncomp fields, the maps never leaving LDS.  Returns 1
+// when the plan has no fused path (the caller then runs the two transforms and
+// its pixel kernel); bit-identical to those.
+int gs_sht_aux_pass_batch(gs_sht* p, int nmap, int ncomp, const double* alm_in, const double* bl, const void* aux,
+                          double* alm_out, void* stream) {
+    if (check_sht(p)) return -1;
+    if (ncomp < 1 || ncomp > 3 || nmap < 1 || !alm_in || !aux || !alm_out)
+        return set_error("gs_sht_aux_pass_batch: bad argument");
+    const char* fe = std::getenv("GS_SHT_FUSED_AUX");
+    const int M = p->merged_M;
+    const int ncb = (p->mf && p->merged_n > 0) ? ring_mc_ncb(M, nmap * ncomp) : 1;
+    if (ncb < 2 || (fe && std::atoi(fe) == 0)) return 1;
+    if (sht_reserve(p, nmap, S(stream))) return -1;
+    if (sht_synth_mfma(p, nmap, ncomp, S(stream), nullptr, alm_in, bl)) return -1;
+    {
+        const int bd = ring_block(M), bdm = ncb * bd, SB = std::max(M, 4 * bd), toff = ncb * SB;
+        const size_t ldsm = (size_t)(ncb * SB + M / 2) * sizeof(double2);
+        const int nc = nmap * ncomp, ncg = (nc + ncb - 1) / ncb;
+        const dim3 gm((unsigned)(8 * ((p->merged_n + 15) / 16) * 2 * ncg));
+        const PixAux op{*reinterpret_cast<const gs::GsAuxPix*>(aux)};
+        hipLaunchKernelGGL((k_sht_apply_ring_mc<8, PixAux>), gm, dim3(bdm), ldsm, S(stream), p->L, p->npair, p->npix,
+                           p->merged_pairs, p->geom, p->phi, p->tw, p->Mmax, p->bsk, nc, ncb, SB, toff, op, p->merged_n,
+                           nullptr);
+        GS_LAUNCH_CHECK("k_sht_apply_ring_mc (aux)");
+    }
+    if (sht_anal_mfma(p, nmap, ncomp, GS_ALM_REAL, 0, alm_out, S(stream), nullptr)) return -1;
+    return 0;
 }
 
 int gs_sht_map2alm_batch(gs_sht* p, int nmap, int ncomp, int layout, const double* maps, const double* weights,

@@ -72,6 +72,7 @@ class MaskedCR:
         self.pcg_iterations = []          # per solve: the CG iterations (mean over the batch's chains)
         self.pcg_iterations_chains = []   # per solve: every chain's count
         self.pcg_launched = []            # per solve: CG iterations launched (the slowest chain's)
+        self.pcg_work = []                # per solve: chain-iterations transformed (converged chains dropped)
         self.pcg_syncs = []
         if rng not in ("replay", "native"):
             raise ValueError(rng)
@@ -293,6 +294,9 @@ class MaskedCR:
                     "gs_masked_pcg_info2")
         self.pcg_syncs.append(syncs.value)          # host synchronisations of this solve (one per batch)
         self.pcg_launched.append(launched.value)    # iterations launched (the batch's slowest chain)
+        work = ctypes.c_longlong()
+        _capi.check(self.lib.gs_masked_pcg_work(self.handle, ctypes.byref(work)), "gs_masked_pcg_work")
+        self.pcg_work.append(work.value)
         return x
 
     def pcg_apply(self, dl, x, out=None):

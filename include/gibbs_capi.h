@@ -362,6 +362,10 @@ int gs_masked_pcg_solve(gs_masked* ctx, const double* dl, const double* rhs, dou
                         int maxiter, int* iters, double* rel_residual, void* stream);
 int gs_masked_pcg_info(const gs_masked* ctx, int* host_syncs);
 int gs_masked_pcg_info2(const gs_masked* ctx, int* host_syncs, int* launched);
+/* The last solve's transformed chain-iterations: the sum over its launched CG
+ * iterations of the chains still unconverged at the last state read (the batch
+ * transforms only those; launched x B without that compaction). */
+int gs_masked_pcg_work(const gs_masked* ctx, long long* chain_iterations /* HOST */);
 /* out = Q x, the PCG system operator (C^+ + b A^T N^-1 A b) applied to x
  * (qcinv opfilt_pp fwd_op, CenteredGibbs.py:631,655). */
 int gs_masked_pcg_apply(gs_masked* ctx, const double* dl, const double* x, double* out, void* stream);

@@ -756,3 +756,32 @@ def test_f2_large_vs_oracle_tables(f2_large, monkeypatch, blocks_mfma):
     assert acc == wacc
     _close(new["EE"], want["EE"])
     _close(new["BB"], want["BB"])
+
+
+@pytest.mark.parametrize("F", [2, 3])
+@pytest.mark.parametrize("over", [False, True])
+def test_aux_fused_pass_bit_identical(monkeypatch, F, over):
+    """the table path's fused v | s + s | v-analysis pass (gs_sht_aux_pass_batch:
+    synthesis, the k_mc_v update in the ring workgroup, analysis) and the reuse of
+    the over-relaxation's repeated s | v analysis give the bits of the unfused
+    transforms (GS_SHT_FUSED_AUX=0), 4 chains, native streams."""
+    import torch
+    from gibbssampler_amd import _capi
+    from gibbssampler_amd.masked import MaskedCR
+    N, L, mask, maps, ntemp, npol, bl, dl, s0 = _teb_problem()
+    pix = {"T": maps[0], "Q": maps[1], "U": maps[2]}
+    rows = (1, 2) if F == 2 else (0, 1, 2)
+    spec = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("GS_SHT_FUSED_AUX", fused)
+        cr = MaskedCR(pix, ntemp, npol, bl, L, N, mask=mask, nfields=F, n_gibbs=3, overrelaxation=over, rng="native",
+                      seed=8, chain=2, nchains=4, sht_mode="mfma")
+        s = torch.from_numpy(np.ascontiguousarray(np.stack([np.stack([s0[r] for r in rows]) * (1 + 0.1 * b)
+                                                            for b in range(4)]))).cuda()
+        d = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(np.stack([dl[k] for k in spec]),
+                                                                  (4, len(spec), L + 1)))).cuda()
+        cr.step(_capi.GS_MCR_OVERRELAX if over else _capi.GS_MCR_AUX, d, s, iteration=5)
+        out.append((s.cpu().numpy(), cr.v.cpu().numpy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
