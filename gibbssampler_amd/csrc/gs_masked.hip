@@ -1705,9 +1705,11 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
                 na = (int)act.size();
             }
         }
-        // predicted remaining iterations of the slowest chain from its residual's
-        // decay over this batch
-        double rem_max = 1.0;
+        // predicted remaining iterations of each unconverged chain from its
+        // residual's decay over this batch: the next batch runs until the slowest
+        // is due (one chain), or -- compacting -- until the first is due, so a
+        // chain that converges drops out of the transforms within a few iterations
+        double rem_max = 1.0, rem_min = 64.0;
         for (int b = 0; b < B; ++b) {
             if (h[b].done) continue;
             const double rate = rn_prev[b] > 0.0 && h[b].rn > 0.0 ? std::pow(h[b].rn / rn_prev[b], 1.0 / k) : 0.5;
@@ -1715,8 +1717,10 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
             double rem = 64.0;
             if (rate < 1.0 && rate > 0.0 && h[b].rn > want) rem = std::log(want / h[b].rn) / std::log(rate);
             rem_max = std::max(rem_max, rem);
+            rem_min = std::min(rem_min, rem);
         }
-        batch = (int)std::max(1.0, std::min(64.0, std::floor(rem_max)));
+        const double due = compact ? std::max(1.0, rem_min) : rem_max;
+        batch = (int)std::max(1.0, std::min(64.0, std::floor(due)));
         for (int b = 0; b < B; ++b) rn_prev[b] = h[b].rn;
     }
     c->pcg_launched = launched;
