@@ -12,7 +12,8 @@
 #   masked / configs[1] / SHT kernel stats (two gpurun calls stay within one call's time limit);
 #   c (r04): the chain-batched SHT (N_side 256, 16 spin-2 maps, matrix-core Legendre tables) --
 #   kernel stats and FETCH_SIZE / WRITE_SIZE / SQ passes -- and the N_side 2048 recurrence kernels'
-#   PMC passes; d (r04): HEAD's masked modes at 16 chains per GPU (bench lines + kernel stats)
+#   PMC passes; d (r04): HEAD's masked modes at 16 chains per GPU (bench lines + kernel stats);
+#   e (r05): the same on the galactic-like mask (--mask galactic) + the ASIS kernel stats
 #   (python tools/summarize_sht_pmc.py <tag> folds c's passes into profiles/pmc_traffic.json)
 set -e
 TAG=${1:-r03}
@@ -89,6 +90,20 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "${OUT}_pcg_b16" -o run --
     python3 bench.py --workload masked_centered_pcg --nchains 16 --steps 2 --warmup 1 --no-cpu-baseline \
     > "${OUT}_pcg_b16.log" 2>&1
 echo "profile $TAG d done"
+exit 0
+fi
+if [ "$PART" = e ]; then
+# r05: HEAD's masked modes at 16 chains per GPU on the galactic-like mask (the
+# band mask's lines are part d), and the ASIS kernel stats
+for m in masked_asis masked_centered_ula masked_centered_pcg masked_noncentered; do
+    timeout -k 10 300 python3 bench.py --workload $m --nchains 16 --mask galactic --no-cpu-baseline \
+        > gpurun_out/bench_${TAG}_${m}_b16_galactic.json 2> gpurun_out/bench_${TAG}_${m}_b16_galactic.err
+done
+rm -rf "${OUT}_asis_b16"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "${OUT}_asis_b16" -o run --output-format csv -- \
+    python3 bench.py --workload masked_asis --nchains 16 --steps 2 --warmup 1 --no-cpu-baseline \
+    > "${OUT}_asis_b16.log" 2>&1
+echo "profile $TAG e done"
 exit 0
 fi
 if [ "$PART" = b ] || [ "$PART" = all ]; then
