@@ -252,20 +252,28 @@ __global__ void k_mc_propose(int L, int F, const double* __restrict__ params, co
 //  0: sum C^+ s0^2   1: sum C^+ s1^2   2: s0 . g2   3: s1 . g2
 //  4: sum (s0 - s1 - tau sig g1)^2 / (2 tau sig)   5: sum (s1 - s0 - tau sig g0)^2 / (2 tau sig)
 //  6: sum N^-1 pix0^2   7: sum N^-1 pix1^2
+// The last two from the maps pix = A b s (p0, p1), or -- p0 = nullptr, harmonic
+// inputs r0, r1 = map2alm(N^-1 A b s) of the fused operator -- as (1/w) (b s) . r:
+// A^T = map2alm / w exactly (real layout), so sum N^-1 pix^2 = (b s)^T A^T N^-1 A
+// (b s); the same sum in other rounding, without the maps
 __global__ __launch_bounds__(RED_BLOCK) void k_mc_sums(int L, int F, long long npix, const double* __restrict__ dl,
                                                        const double* __restrict__ params, double tau,
                                                        const double* __restrict__ s0, const double* __restrict__ s1,
                                                        const double* __restrict__ g0, const double* __restrict__ g1,
                                                        const double* __restrict__ g2, const double* __restrict__ ninv,
                                                        const double* __restrict__ p0, const double* __restrict__ p1,
-                                                       double* __restrict__ partial) {
+                                                       double* __restrict__ partial, const double* __restrict__ r0,
+                                                       const double* __restrict__ r1, const double* __restrict__ bl,
+                                                       double inv_w) {
     const long long NR = (long long)(L + 1) * (L + 1);
     const long long nslot = F * NR, npx = F * npix;
+    const bool harm = p0 == nullptr;
     {
         const long long cb = (long long)blockIdx.y * nslot, pb = (long long)blockIdx.y * npx;
         dl += (long long)blockIdx.y * (F == 3 ? 4 : F) * (L + 1);
         params += (long long)blockIdx.y * (L + 1) * GS_NPARAM;
-        s0 += cb; s1 += cb; g0 += cb; g1 += cb; p0 += pb; p1 += pb;
+        s0 += cb; s1 += cb; g0 += cb; g1 += cb;
+        if (harm) { r0 += cb; r1 += cb; } else { p0 += pb; p1 += pb; }
         partial += (long long)blockIdx.y * gridDim.x * NSUM;
     }
     double a[NSUM] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -288,8 +296,12 @@ __global__ __launch_bounds__(RED_BLOCK) void k_mc_sums(int L, int F, long long n
         const double e10 = x1 - x0 - ts * g0[g];
         a[4] += e01 * e01 / (2.0 * ts);
         a[5] += e10 * e10 / (2.0 * ts);
+        if (harm) {
+            a[6] += ((bl[l] * x0) * r0[g]) * inv_w;
+            a[7] += ((bl[l] * x1) * r1[g]) * inv_w;
+        }
     }
-    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < npx; g += stride) {
+    for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; !harm && g < npx; g += stride) {
         const double q0 = p0[g], q1 = p1[g];
         a[6] += q0 * q0 * ninv[g];
         a[7] += q1 * q1 * ninv[g];
@@ -1232,7 +1244,7 @@ struct gs_masked {
     // per chain ([B][...])
     double *params = nullptr, *params_mala = nullptr;
     int* ell2bin = nullptr;
-    double *x = nullptr, *Abs = nullptr, *y = nullptr, *r = nullptr;
+    double *x = nullptr, *Abs = nullptr, *y = nullptr, *r = nullptr, *r1 = nullptr;
     double *grad0 = nullptr, *grad1 = nullptr, *snew = nullptr, *pix0 = nullptr, *pix1 = nullptr, *vtmp = nullptr;
     double *partial = nullptr, *lr = nullptr;
     int32_t* accd = nullptr;         // the last MALA / RJPO accept decisions (device, [B])
@@ -1256,7 +1268,7 @@ namespace {
 
 void mc_free(gs_masked* c) {
     if (c->sht) gs_sht_destroy(c->sht);
-    double* bufs[] = {c->bl, c->dpix, c->ninv, c->g2, c->params, c->params_mala, c->x, c->Abs, c->y, c->r,
+    double* bufs[] = {c->bl, c->dpix, c->ninv, c->g2, c->params, c->params_mala, c->x, c->Abs, c->y, c->r, c->r1,
                       c->grad0, c->grad1, c->snew, c->pix0, c->pix1, c->vtmp, c->partial, c->lr,
                       c->pr, c->pz, c->pp, c->pq, c->params_pcg, c->dots, c->pcgs, c->f2_da, c->f2_r, c->f2_Y,
                       c->f2_phib, c->f2_part, c->f2_G, c->f2_taken};
@@ -1364,6 +1376,17 @@ int mc_s_update(gs_masked* c, int over, double* s, const double* zs, long long z
     return 0;
 }
 
+// the MALA gradient without its map: r = map2alm(N^-1 A b s) from the fused
+// operator pass (gs_sht_apply_weighted_batch; the map stays in LDS on the table
+// path), kept in rbuf for the data term of the log density (k_mc_sums harmonic)
+int mc_gradient_r(gs_masked* c, const double* dl, const double* s, double* grad, double* rbuf, hipStream_t st) {
+    if (gs_sht_apply_weighted_batch(c->sht, c->B, c->F, s, c->bl, c->ninv, c->pix0, rbuf, st)) return -1;
+    hipLaunchKernelGGL(k_mc_grad, dim3(nblocks(c->F * c->nlm, 256), c->B), dim3(256), 0, st, c->L, c->F, dl, c->bl, s,
+                       rbuf, c->g2, 1.0 / c->w, grad);
+    GS_LAUNCH_CHECK("k_mc_grad");
+    return 0;
+}
+
 int mc_gradient(gs_masked* c, const double* dl, const double* s, double* grad, double* pix, hipStream_t st) {
     if (mc_synth(c, c->B, s, pix, st)) return -1;
     // map2alm(N^-1 A b s), N^-1 applied on the ring stage's pixel load
@@ -1427,6 +1450,7 @@ int gs_masked_create(const gs_masked_desc* desc, const double* maps, const doubl
     rc |= mc_alloc(&c->Abs, B * FP);
     rc |= mc_alloc(&c->y, B * FP);
     rc |= mc_alloc(&c->r, B * FR);
+    rc |= mc_alloc(&c->r1, B * FR);
     rc |= mc_alloc(&c->grad0, B * FR);
     rc |= mc_alloc(&c->grad1, B * FR);
     rc |= mc_alloc(&c->snew, B * FR);
@@ -2062,14 +2086,17 @@ int gs_masked_cr(gs_masked* c, int kind, const double* dl, double* s, double* v,
     const double km = (double)c->npix / (4.0 * PI * c->noise_pol0);
     const double kapm[3] = {km, km, km};
     if (mc_params(c, B, dl, kapm, c->params_mala, st)) return -1;
-    if (mc_gradient(c, dl, s, c->grad0, c->pix0, st)) return -1;
+    // the two gradients through the fused operator (no maps); the log densities'
+    // data terms sum_pix N^-1 pix^2 from the operator's output (k_mc_sums)
+    if (mc_gradient_r(c, dl, s, c->grad0, c->r, st)) return -1;
     const uint32_t call = 0;
     hipLaunchKernelGGL(k_mc_propose, dim3(nblocks(c->nlm, 256), B), dim3(256), 0, st, c->L, c->F, c->params_mala, s,
                        c->grad0, c->tau, zm, slo, shi, ch, (uint32_t)(SUB_MALA + call), iteration, c->snew);
     GS_LAUNCH_CHECK("k_mc_propose");
-    if (mc_gradient(c, dl, c->snew, c->grad1, c->pix1, st)) return -1;
+    if (mc_gradient_r(c, dl, c->snew, c->grad1, c->r1, st)) return -1;
     hipLaunchKernelGGL(k_mc_sums, dim3(c->nblk, B), dim3(RED_BLOCK), 0, st, c->L, c->F, c->npix, dl, c->params_mala,
-                       c->tau, s, c->snew, c->grad0, c->grad1, c->g2, c->ninv, c->pix0, c->pix1, c->partial);
+                       c->tau, s, c->snew, c->grad0, c->grad1, c->g2, c->ninv, nullptr, nullptr, c->partial, c->r,
+                       c->r1, c->bl, 1.0 / c->w);
     GS_LAUNCH_CHECK("k_mc_sums");
     hipLaunchKernelGGL(k_mc_accept, dim3(1, B), dim3(256), 0, st, c->nblk, c->partial, FR, um, slo, shi, ch, call,
                        iteration, c->accd, accept, log_ratio ? log_ratio : c->lr);

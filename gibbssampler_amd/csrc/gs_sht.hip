@@ -2516,6 +2516,11 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #ifndef GS_MF_TPF
 #define GS_MF_TPF 2
 #endif
+// synthesis: a quad's A operands computed during the previous quad's MFMAs (1)
+// or at its own start (0, r04)
+#ifndef GS_MF_SPIPE
+#define GS_MF_SPIPE 1
+#endif
 constexpr int MF_CH = 32;                          // l staged per chunk (two blocks)
 constexpr int MF_TL_MAX = 256;                     // tiles of a support-skipping analysis (N_side <= 2048)
 // RIN: the input is the caller's real-layout a_lm (areal, comp stride
@@ -2744,43 +2749,56 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
                 for (int k = 0; k < 5; ++k) c[k] = cq[k];
             }
         };
+        // the A operands of quad q: spin 2 F1 / F2 at l = m + 16 b + 4 q + g (the
+        // VALU kernels' expressions; G+ = the one with lambda's parity: F1 at
+        // even l - m), spin 0 lambda
+        auto opnd = [&](int q, double& ap, double& am) __attribute__((always_inline)) {
+            if constexpr (SPIN == 2) {
+                const double w0 = gv[2 * q];
+                const double w1 = (q > 0 || g > 0 || prev) ? gv[2 * q + 1] : 0.0;
+                const int u = q & 1;
+                const double f1 = fma(cv[u][2] * xis2, w1, -fma(cv[u][0], is2, cv[u][1]) * w0);
+                const double f2 = fma(cv[u][4] * is2, w1, -(cv[u][3] * xis2) * w0);
+                const bool ev = (g & 1) == 0;
+                ap = ev ? f1 : f2;
+                am = ev ? f2 : f1;
+            } else {
+                ap = gv[2 * q];
+                am = gv[2 * q + 1];
+            }
+        };
         lds(lr0, 0, bq[0]);
         ldc(0, cv[0]);
+        double apc = 0.0, amc = 0.0;
+        if (GS_MF_SPIPE) opnd(0, apc, amc);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             if (q + 1 < NQ) { lds(lr0, q + 1, bq[(q + 1) & 1]); ldc(q + 1, cv[(q + 1) & 1]); }
             // keep the order as written: the scheduler would sink the next
             // quad's reads and the table refills behind the MFMAs
             __builtin_amdgcn_sched_barrier(0);
+            if (!GS_MF_SPIPE) opnd(q, apc, amc);
             if (on) {
-                double ap, am;
-                if constexpr (SPIN == 2) {
-                    // F1 / F2 at l = m + 16 b + 4 q + g (the VALU kernels' expressions;
-                    // G+ = the one with lambda's parity: F1 at even l - m)
-                    const double w0 = gv[2 * q];
-                    const double w1 = (q > 0 || g > 0 || prev) ? gv[2 * q + 1] : 0.0;
-                    const int u = q & 1;
-                    const double f1 = fma(cv[u][2] * xis2, w1, -fma(cv[u][0], is2, cv[u][1]) * w0);
-                    const double f2 = fma(cv[u][4] * is2, w1, -(cv[u][3] * xis2) * w0);
-                    const bool ev = (g & 1) == 0;
-                    ap = ev ? f1 : f2;
-                    am = ev ? f2 : f1;
-                } else {
-                    ap = gv[2 * q];
-                    am = gv[2 * q + 1];
-                }
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
                     if (c < ncl) {                  // (a column group without maps: no MFMAs)
-                        Cp[c] = mfma64(ap, bq[q & 1][2 * c + 0], Cp[c]);
-                        Cm[c] = mfma64(am, bq[q & 1][2 * c + 1], Cm[c]);
+                        Cp[c] = mfma64(apc, bq[q & 1][2 * c + 0], Cp[c]);
+                        Cm[c] = mfma64(amc, bq[q & 1][2 * c + 1], Cm[c]);
                     }
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
+            // the next quad's operands while these MFMAs run (their fp64 chain
+            // no longer sits between a quad's loads and its MFMAs; GS_MF_SPIPE 0:
+            // computed at the quad's start, the r04 order, A/B only)
+            double apn = 0.0, amn = 0.0;
+            if (GS_MF_SPIPE && q + 1 < NQ) opnd(q + 1, apn, amn);
+            __builtin_amdgcn_sched_barrier(0);
             if constexpr (SPIN == 2) tload(nblk, nprev, q, gv);
             else { tload(nblk, false, 2 * q, gv); tload(nblk, false, 2 * q + 1, gv); }
             __builtin_amdgcn_sched_barrier(0);
+            apc = apn;
+            amc = amn;
         }
     };
     double2 pf[PER][SPIN == 2 ? 2 : 1];
