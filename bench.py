@@ -75,6 +75,11 @@ def parse():
                          "a full-sky run never reads it: the next CR, the MH and the C_l draw use the per-l "
                          "statistics only, and the reference's run() returns D_l and accept flags only "
                          "(NonCenteredGibbs.py:529-571); 'store' writes s every iteration (HBM roofline)")
+    ap.add_argument("--ramp-ms", type=float, default=None,
+                    help="harmonic modes: milliseconds of the same workload on a scratch runner (other chains, "
+                         "untimed) before the warmup steps, so a short timed region (e.g. --steps 20) is not "
+                         "measured while the GPU's clocks still ramp up (clock_ramp); reported in the line "
+                         "(default 200; 0 turns it off)")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     one = a.workload == "masked" or a.workload in MASKED_HEAD
@@ -90,7 +95,33 @@ def parse():
         harmonic = a.workload != "masked"
         a.steps = a.steps or (500 if harmonic else 50)
         a.warmup = a.warmup if a.warmup is not None else (20 if harmonic else 5)
+    a.ramp_ms = a.ramp_ms if a.ramp_ms is not None else 200.0
     return a
+
+
+def clock_ramp(args, make_runner, ms):
+    """Bring the GPU to its steady clocks before the warmup: a scratch runner of
+    the same workload (its own chains -- seed + 1 -- and buffers; the measured
+    runner is not touched) replays a captured 20-step graph for `ms`
+    milliseconds, untimed.  Measured (r05, 20 timed steps after 5 warmup steps,
+    as the driver runs bench.py): no ramp 0.277-0.285 ms/step, 300 ms of fp64
+    GEMM 0.248-0.252, 300 ms of fp64 elementwise work 0.246, 100 / 300 ms of this
+    ramp 0.237 / 0.2345 -- the 500-step steady state (0.2345-0.241): the clocks
+    ramp on this workload's own instruction mix (VALU-bound), not on any load.
+    Returns the milliseconds spent and the scratch runner, which the caller
+    drops after the timed region (its teardown frees device memory: host time
+    with the GPU idle, which must not fall between the ramp and the warmup)."""
+    import torch
+    if ms <= 0:
+        return 0.0, None
+    scratch = make_runner(args.seed + 1)
+    g = scratch.capture_steps(20)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        g.replay()
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3, scratch
 
 
 def sweep_algorithmic_bytes(L, F, nchains, store=True):
@@ -289,16 +320,21 @@ def run_harmonic(args, ctx, cpu):
     from gibbssampler_amd.samplers import BatchedRunner
 
     P = synthetic_problem(args.lmax, args.nside, args.fields, seed=0)
-    runner = BatchedRunner(kind=args.workload, lmax=P["lmax"], nside=P["nside"], nfields=P["nfields"],
-                           nchains=args.nchains, bl=P["bl"], noise_var=P["noise_var"], bins=P["bins"],
-                           d_alm=P["d_alm"], blocks=P["blocks"], proposal_variances=P["proposal_variances"],
-                           rng="native", seed=args.seed, chain0=ctx.chain0,
-                           store_skymap=args.skymap == "store")
+
+    def make_runner(seed):
+        r = BatchedRunner(kind=args.workload, lmax=P["lmax"], nside=P["nside"], nfields=P["nfields"],
+                          nchains=args.nchains, bl=P["bl"], noise_var=P["noise_var"], bins=P["bins"],
+                          d_alm=P["d_alm"], blocks=P["blocks"], proposal_variances=P["proposal_variances"],
+                          rng="native", seed=seed, chain0=ctx.chain0, store_skymap=args.skymap == "store")
+        r.init(P["dls_init"])
+        return r
+
+    runner = make_runner(args.seed)
     p = runner.plan
-    runner.init(P["dls_init"])
     trace = p.zeros(args.steps, p.nchains, p.nspec, p.maxbins)
     one_graph = not args.no_graph
     warm_graph = None
+    ramp, scratch = 0.0, None
     if one_graph and args.warmup > 0:
         # the W warmup steps as one hipGraph, replayed right before the timed
         # replay (below): besides warming the kernels this pays the process's
@@ -309,6 +345,8 @@ def run_harmonic(args, ctx, cpu):
         # (tools/replay_probe.py)
         warm_graph = runner.capture_steps(args.warmup)
     else:
+        if not one_graph:
+            ramp, scratch = clock_ramp(args, make_runner, args.ramp_ms)
         for _ in range(args.warmup):
             runner.step()
     if one_graph:
@@ -317,6 +355,9 @@ def run_harmonic(args, ctx, cpu):
         # so its duration is measured on its stream over the timed region itself
         runner.capture_steps(args.steps, trace=trace, trace_capacity=args.steps, time_sweeps=True,
                              time_every=args.time_every)
+        # the GEMM ramp between the captures (host time, GPU idle) and the warmup
+        # replay: the GPU enters the warmup and the timed steps at speed
+        ramp, scratch = clock_ramp(args, make_runner, args.ramp_ms)
         if warm_graph is not None:
             warm_graph.replay()
             runner.iteration += args.warmup
@@ -336,6 +377,7 @@ def run_harmonic(args, ctx, cpu):
     t1 = time.perf_counter()
     ctx.barrier()
     elapsed = ctx.max(t1 - t0)
+    del scratch
     sweep_ms, sweep_n = p.sweep_timing(False)
     # the run's only collective: every rank's D_l traces, gathered over RCCL / xGMI
     gathered = ctx.gather(trace)
@@ -375,6 +417,9 @@ def run_harmonic(args, ctx, cpu):
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
         "roofline": sweep_roofline(args, prof, alg_bytes, achieved, sweep_avg_ms, sweep_n, one_graph),
         "cpu_baseline": cpu,
+        "clock_ramp": {"ms": round(ramp, 1),
+                       "work": "a scratch runner of this workload (seed + 1, its own buffers) replaying a 20-step "
+                               "graph, untimed, before the warmup steps (bench.clock_ramp)"},
     }
 
 

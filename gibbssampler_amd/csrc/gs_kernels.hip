@@ -109,6 +109,20 @@ struct gs_plan {
     // us per configs[1] step -- the branch's cross-queue synchronisation.)
     bool cls_pre = false;
     double* cls_var = nullptr;       // [nchains][nspec][maxbins][3]
+    // many-chain NC steps: the MH proposals and native accept uniforms depend
+    // only on the current D_l and the counters, so they are drawn by extra
+    // workgroups at the front of the statistics-finish launch (beside its
+    // bandwidth-bound partial sums) instead of in the prologue, which keeps the
+    // block parameters alone (GS_NC_PRO_DEFER=0|1 at plan creation).
+    bool pro_defer = false;
+    bool pro_pending = false;        // a prologue deferred its draws to the next finish
+    // captured multi-step graphs: the MH launch of step i writes step i + 1's
+    // block parameters (k_mh_reg epilogue), so step i + 1's prologue is no
+    // launch at all (GS_NC_MH_PARAMS=0|1, default with pro_defer)
+    bool mh_params = false;
+    bool params_chained = false;     // the last MH launch wrote them
+    const double* pro_dl = nullptr;
+    uint32_t pro_slo = 0, pro_shi = 0, pro_it = 0;
     bool iter_dev_on = false;
     const uint32_t* itp() const { return iter_dev_on ? iter_dev : nullptr; }
     // graph-captured steps (gs_graph_step): this step's offset from the device
@@ -1122,6 +1136,50 @@ __device__ __forceinline__ void mh_uniform_at(long long g, int nchains, int nspe
     out[g] = uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
 }
 
+// k_stats_finish with nbp + nbu extra workgroups first (pro_defer plans): the
+// MH proposals and native accept uniforms of this step, the same items and
+// code as k_nc_prologue's (bit-identical either way)
+template <int F, int G>
+__global__ __launch_bounds__(256) void k_stats_finish_pro(int L, int nchains, int ntile, int nchunkg, int tm,
+                                                          int nstat, const double* __restrict__ partials,
+                                                          double* __restrict__ stats, int nblk_prop, int nblk_u,
+                                                          double* __restrict__ u_out, int nspec, int nacc,
+                                                          int n_iter_mh, int maxbins,
+                                                          const int* __restrict__ nbins_arr,
+                                                          const double* __restrict__ prop_sd,
+                                                          const double* __restrict__ dl, double* __restrict__ prop,
+                                                          double* __restrict__ logr, uint32_t seed_lo,
+                                                          uint32_t seed_hi, IterArg itarg, int chain0) {
+    const int bx = (int)blockIdx.x;
+    if (bx < nblk_prop) {
+        mh_propose_at<F>(bx * (long long)blockDim.x + threadIdx.x, nchains, maxbins, nbins_arr, prop_sd, dl, prop,
+                         logr, nullptr, seed_lo, seed_hi, itarg, chain0);
+        return;
+    }
+    if (bx < nblk_prop + nblk_u) {
+        mh_uniform_at((bx - nblk_prop) * (long long)blockDim.x + threadIdx.x, nchains, nspec, nbins_arr, nacc,
+                      n_iter_mh, seed_lo, seed_hi, itarg.get(), chain0, u_out);
+        return;
+    }
+    const int b = bx - nblk_prop - nblk_u;
+    const int t = b % ntile;
+    const int q = (b / ntile) % nstat;
+    const int chain = b / (ntile * nstat);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int Lp1 = L + 1;
+    GS_ASSERT(chain < nchains);
+    const double acc = stats_finish_sum<G>(L, ntile, nchunkg, tm, nstat, partials, chain, q, t, w, lane);
+    __shared__ double red[4][WAVE];
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w == 0) {
+        const int ell = L - WAVE * t - 63 + lane;
+        if (ell >= 0)
+            stats[((long long)chain * nstat + q) * Lp1 + ell] = ((red[0][lane] + red[1][lane]) + red[2][lane]) +
+                                                                 red[3][lane];
+    }
+}
+
 // non-centered prologue: the MH proposals depend only on the current D_l, not
 // on the CR draw, so they are made in the same launch as the CR block
 // parameters (proposal workgroups first; both halves are latency-bound).
@@ -1277,6 +1335,7 @@ struct MhEpi {
     uint32_t* counter;      // nullable: [0] iteration base (advanced by adv), [1] finished-workgroup ticket
     int nchains;
     uint32_t adv;
+    double* params;         // nullable: the next step's CR block parameters from the new D_l (k_mh_reg)
 };
 
 // SC: this chain's per-l statistics cached in LDS for the whole kernel (every
@@ -1827,6 +1886,27 @@ __global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, M
     mh_reg_body<F>(chain, chain == 0, L, maxbins, ph, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
                    ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
                    smem);
+    if (epi.params) {
+        // the next step's block parameters (block_params_at's values: the same
+        // D_l words, here from the LDS copy the last phase barrier published)
+        constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
+        constexpr int NW = F == 3 ? gs_block::NP : 2 * F;
+        const int Lp1 = L + 1;
+        const double* Ds = smem + 2 * Lp1 + nacc;
+        for (int l = threadIdx.x; l < Lp1; l += blockDim.x) {
+            int bq[NSP];
+            double dq[NSP];
+#pragma unroll
+            for (int q = 0; q < NSP; ++q) bq[q] = ell2bin[q * Lp1 + l];
+#pragma unroll
+            for (int q = 0; q < NSP; ++q) dq[q] = bq[q] < 0 ? 0.0 : Ds[q * maxbins + max(bq[q], 0)];
+            double pp[gs_block::NP];
+            block_params_from<F, 1>(l, bl[l], dq, k0, k1, k2, pp);
+            double* o = epi.params + ((long long)chain * Lp1 + l) * gs_block::NP;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) o[q] = pp[q];
+        }
+    }
     mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x);
 }
 
@@ -2173,6 +2253,14 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     build_tasks(p);
     p->inkernel_params = p->nchains <= 4;
     p->sweep_latency = getenv("GS_SWEEP_THROUGHPUT") == nullptr;
+    {
+        const char* e = getenv("GS_NC_PRO_DEFER");
+        // measured (tools/step_ab.py, configs[2]): 234.6 -> 233.7 us per step with
+        // the draws deferred, 232.9 with the MH-written parameters as well
+        p->pro_defer = e ? std::atoi(e) != 0 : true;
+        const char* m = getenv("GS_NC_MH_PARAMS");
+        p->mh_params = p->pro_defer && (m ? std::atoi(m) != 0 : true);
+    }
     p->mh_reg = getenv("GS_MH_FUSED") == nullptr;
     const size_t nc = (size_t)p->nchains;
     rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunkg * p->nstat * WAVE);
@@ -2346,6 +2434,24 @@ static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e
 
 static int stats_finish(gs_plan* p, double* stats, void* stream) {
     const long long n = (long long)p->nchains * p->nstat * p->ntile;
+    if (p->pro_pending) {
+        // the prologue's deferred draws in front of the partial sums
+        p->pro_pending = false;
+        const int nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
+        const int nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
+        const int tmf = p->rows_per_task * (4 / p->sweep_tw);
+#define GS_FP(FF, GG) hipLaunchKernelGGL((k_stats_finish_pro<FF, GG>), dim3((unsigned)(n + nbp + nbu)), dim3(256), 0,   \
+                                         S(stream), p->L, p->nchains, p->ntile, p->nchunkg, tmf, p->nstat, p->partials, \
+                                         stats, nbp, nbu, p->u_nat, p->nspec, p->nacc, p->n_iter_mh, p->maxbins,        \
+                                         p->meta, p->prop_sd, p->pro_dl, p->prop, p->logr, p->pro_slo, p->pro_shi,      \
+                                         p->ita(p->pro_it), p->chain0)
+#define GS_FPG(FF) do { if (p->nchains <= 4) GS_FP(FF, 16); else GS_FP(FF, 4); } while (0)
+        if (p->F == 1) GS_FPG(1); else if (p->F == 2) GS_FPG(2); else GS_FPG(3);
+#undef GS_FPG
+#undef GS_FP
+        GS_LAUNCH_CHECK("k_stats_finish_pro");
+        return 0;
+    }
     if (p->nchains <= 4)
         hipLaunchKernelGGL(k_stats_finish<16>, dim3((unsigned)n), dim3(256), 0, S(stream), p->L, p->nchains, p->ntile,
                            p->nchunkg, p->rows_per_task * (4 / p->sweep_tw), p->nstat, p->partials, stats);
@@ -2489,8 +2595,9 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
                      uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi) {
     int maxnb = 0;
-    const MhEpi none{nullptr, 1, nullptr, p->nchains, 0};
-    const MhEpi E = epi ? *epi : none;
+    const MhEpi none{nullptr, 1, nullptr, p->nchains, 0, nullptr};
+    MhEpi E = epi ? *epi : none;
+    p->params_chained = false;
     MhPhases ph{};
     ph.nphase = p->nphase;
     ph.lmin = p->mh_lmin;
@@ -2509,7 +2616,9 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
     const size_t lds_reg = (2 * (size_t)(p->L + 1) + (size_t)p->nacc + 3 * (size_t)p->nspec * p->maxbins) *
                            sizeof(double) + 16 + (size_t)ntab * (sizeof(int4) + sizeof(int2));
     const bool reg = p->mh_reg && p->L + 1 - p->mh_lmin <= MH_REG_THREADS && lds_reg <= 150 * 1024;
+    if (!reg) E.params = nullptr;
     if (reg) {
+        p->params_chained = E.params != nullptr;
         static bool attr_set[4] = {false, false, false, false};
 #define GS_MR(FF) do {                                                                                                 \
         if (!attr_set[FF])                                                                                             \
@@ -2678,6 +2787,28 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
     // native mode: the MH accept uniforms are drawn here too (replay draws them on the host)
     p->u_nat_ready = u_prop == nullptr && p->nacc > 0 && !getenv("GS_MH_INKERNEL_UNIFORMS");
     const int nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
+    const bool chained = p->params_chained && p->graph_off > 0;
+    p->params_chained = false;
+    if (chained && p->pro_defer && u_prop == nullptr && nbq > 0) {
+        // block parameters written by the previous step's MH launch; draws deferred
+        p->pro_pending = true;
+        p->pro_dl = dl; p->pro_slo = slo; p->pro_shi = shi; p->pro_it = it;
+        return 0;
+    }
+    if (p->pro_defer && u_prop == nullptr && nbq > 0) {
+        // native draws: to the front of this step's statistics finish (stats_finish)
+        p->pro_pending = true;
+        p->pro_dl = dl; p->pro_slo = slo; p->pro_shi = shi; p->pro_it = it;
+#define GS_PRQ(FF) hipLaunchKernelGGL((k_nc_prologue<FF>), dim3(nbq), dim3(256), 0, S(stream), 0, nbq, p->u_nat,     \
+                                      p->nspec, p->nacc, p->n_iter_mh, p->L, p->nchains, p->maxbins, p->ell2bin, p->bl, \
+                                      p->kappa[0], p->kappa[1], p->kappa[2], p->params, p->meta, p->prop_sd, dl,        \
+                                      p->prop, p->logr, u_prop, slo, shi, p->ita(it), p->chain0)
+        if (p->F == 1) GS_PRQ(1); else if (p->F == 2) GS_PRQ(2); else GS_PRQ(3);
+#undef GS_PRQ
+        GS_LAUNCH_CHECK("k_nc_prologue");
+        return 0;
+    }
+    p->pro_pending = false;
 #define GS_PRO(FF) hipLaunchKernelGGL((k_nc_prologue<FF>), dim3(nbp + nbq + nbu), dim3(256), 0, S(stream), nbp, nbq,   \
                                       p->u_nat, p->nspec, p->nacc, p->n_iter_mh, p->L,                                  \
                                       p->nchains, p->maxbins, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], \
@@ -2709,6 +2840,7 @@ int gs_nc_decide(gs_plan* p, double* dl, const double* u_acc, uint64_t seed, uin
     if (check_plan(p)) return -1;
     if (!p->has_mh) return set_error("gs_nc_decide: plan has no MH blocks / proposal variances");
     if (!dl) return set_error("gs_nc_decide: null argument");
+    if (p->pro_pending) return set_error("gs_nc_decide: the prologue's draws wait for gs_nc_finish");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     return mh_decide(p, p->stats, dl, u_acc, slo, shi, it, accept_out, stream);
 }
@@ -2719,8 +2851,12 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
     if (!p->has_mh) return set_error("gs_nc_decide_fused: plan has no MH blocks / proposal variances");
     if (!dl) return set_error("gs_nc_decide_fused: null argument");
     if (trace && capacity < 1) return set_error("gs_nc_decide_fused: capacity < 1");
+    if (p->pro_pending) return set_error("gs_nc_decide_fused: the prologue's draws wait for gs_nc_finish");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv};
+    // inside a captured multi-step graph (not its last step) the MH also writes
+    // the next step's block parameters, and that step's prologue launches none
+    double* nextp = p->mh_params && p->iter_dev_on && p->graph_adv == 0 && !p->inkernel_params ? p->params : nullptr;
+    const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv, nextp};
     return mh_decide(p, p->stats, dl, p->u_nat_ready ? p->u_nat : nullptr, slo, shi, it, accept_out, stream, &epi);
 }
 

@@ -251,6 +251,47 @@ def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
             np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("F", [1, 2, 3])
+def test_nc_deferred_draws_and_chained_params_bit_identical(monkeypatch, F):
+    """Many-chain NC steps: the MH proposals and accept uniforms drawn by extra
+    workgroups of the statistics finish instead of the prologue, and inside a
+    captured multi-step graph the next step's block parameters written by the
+    MH launch (no prologue launch after step 0) -- GS_NC_PRO_DEFER=1 against 0 at
+    plan creation: D_l, accept flags and the trace over 5 native steps, eager
+    and as one captured 5-step graph replayed twice."""
+    import torch
+    from gibbssampler_amd.problem import synthetic_problem
+    from gibbssampler_amd.samplers import BatchedRunner
+    P = synthetic_problem(64, 32, F, seed=13)
+
+    def run(defer, graph):
+        monkeypatch.setenv("GS_NC_PRO_DEFER", "1" if defer else "0")
+        r = BatchedRunner("noncentered", P["lmax"], P["nside"], F, 8, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
+                          blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=23,
+                          chain0=1)
+        r.init(P["dls_init"])
+        out = []
+        if graph:
+            trace = r.plan.zeros(5, 8, r.plan.nspec, r.plan.maxbins)
+            acc = r.plan.zeros(5, 8, max(r.plan.nacc, 1), dtype=torch.int32)
+            r.capture_steps(5, trace=trace, trace_capacity=5, accept_trace=acc)
+            for _ in range(2):
+                r.step()
+                out += [trace.cpu().numpy(), acc.cpu().numpy()]
+        else:
+            for _ in range(10):
+                r.step()
+                out += [r.dl.cpu().numpy(), r.accept.cpu().numpy()]
+        out.append(r.dl.cpu().numpy())
+        return out
+
+    for graph in (False, True):
+        a, b = run(True, graph), run(False, graph)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    monkeypatch.delenv("GS_NC_PRO_DEFER", raising=False)
+
+
 @pytest.mark.parametrize("F,nch", [(3, 1), (2, 2), (1, 4)])
 def test_centered_predrawn_variates_bit_identical(monkeypatch, F, nch):
     """Few-chain centered steps draw the C_l variates in extra workgroups of the
