@@ -121,6 +121,9 @@ struct gs_plan {
     // launch at all (GS_NC_MH_PARAMS=0|1, default with pro_defer)
     bool mh_params = false;
     bool params_chained = false;     // the last MH launch wrote them
+    // the deferred draws ride in the sweep launch's front workgroups instead
+    // of the finish (GS_NC_PRO_SWEEP=0|1, default 1)
+    bool pro_in_sweep = true;
     const double* pro_dl = nullptr;
     uint32_t pro_slo = 0, pro_shi = 0, pro_it = 0;
     bool iter_dev_on = false;
@@ -537,13 +540,39 @@ template <int F>
 __device__ void cls_variates_item(const ClsPre& cp, int item, uint32_t seed_lo, uint32_t seed_hi, uint32_t iter,
                                   int chain0);
 
+// many-chain NC steps (pro_defer): the MH proposals and native accept
+// uniforms drawn by n extra workgroups at the FRONT of the throughput-form
+// sweep's grid (they start first and their latency chains -- inverse normal
+// CDFs, log-CDFs -- end long before the sweep does); n is a multiple of 8, so
+// the sweep workgroups' XCD-aware remap keeps its placement
+struct ProPre {
+    int n = 0;                       // extra workgroups (0: none)
+    int nbp = 0, nbu = 0;            // of which proposal / uniform workgroups
+    int nspec = 0, nacc = 0, n_iter_mh = 0, maxbins = 0;
+    const int* nbins = nullptr;      // plan meta (nbins per spectrum, blocks, accept offsets)
+    const double* prop_sd = nullptr;
+    const double* dl = nullptr;
+    double* prop = nullptr;
+    double* logr = nullptr;
+    double* u_out = nullptr;
+};
+template <int F>
+__device__ void pro_pre_item(const ProPre& pp, int bx, int nchains, uint32_t seed_lo, uint32_t seed_hi, IterArg itarg,
+                             int chain0);
+
 template <int F, int ZM, bool STORE, int PRE = 0>
 __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
                                                   const int2* __restrict__ tasks, const double* __restrict__ d,
                                                   const double* __restrict__ params, const double* __restrict__ z,
                                                   double* __restrict__ s, double* __restrict__ partials,
                                                   uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, uint32_t substep,
-                                                  int chain0, SweepOp op, ClsPre cp) {
+                                                  int chain0, SweepOp op, ClsPre cp, ProPre pp) {
+    if constexpr (PRE == 0 && ZM == 0) {
+        if ((int)blockIdx.x < pp.n) {
+            pro_pre_item<F>(pp, (int)blockIdx.x, nchains, seed_lo, seed_hi, itarg, chain0);
+            return;
+        }
+    }
     const uint32_t iter = itarg.get();
     constexpr int NS = SweepAcc<F>::NS;
     __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
@@ -571,8 +600,9 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     // XCDs, so physical id b runs on XCD b % 8; give each XCD a contiguous range
     // of logical ids so that all chains of one (tiles, rows) block share one
     // XCD's L2 for the data reads (speed only -- any placement is correct)
-    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int bid = (int)blockIdx.x - pp.n;     // (pp.n % 8 == 0: the same XCD as blockIdx.x)
+    const int nwg = (int)gridDim.x - pp.n, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int pair = wg / nchains;
     const int chain = wg % nchains;
     const int lane = threadIdx.x & 63;
@@ -1178,6 +1208,17 @@ __global__ __launch_bounds__(256) void k_stats_finish_pro(int L, int nchains, in
             stats[((long long)chain * nstat + q) * Lp1 + ell] = ((red[0][lane] + red[1][lane]) + red[2][lane]) +
                                                                  red[3][lane];
     }
+}
+
+template <int F>
+__device__ void pro_pre_item(const ProPre& pp, int bx, int nchains, uint32_t seed_lo, uint32_t seed_hi, IterArg itarg,
+                             int chain0) {
+    if (bx < pp.nbp)
+        mh_propose_at<F>(bx * (long long)blockDim.x + threadIdx.x, nchains, pp.maxbins, pp.nbins, pp.prop_sd, pp.dl,
+                         pp.prop, pp.logr, nullptr, seed_lo, seed_hi, itarg, chain0);
+    else if (bx < pp.nbp + pp.nbu)
+        mh_uniform_at((bx - pp.nbp) * (long long)blockDim.x + threadIdx.x, nchains, pp.nspec, pp.nbins, pp.nacc,
+                      pp.n_iter_mh, seed_lo, seed_hi, itarg.get(), chain0, pp.u_out);
 }
 
 // non-centered prologue: the MH proposals depend only on the current D_l, not
@@ -2258,6 +2299,8 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
         // measured (tools/step_ab.py, configs[2]): 234.6 -> 233.7 us per step with
         // the draws deferred, 232.9 with the MH-written parameters as well
         p->pro_defer = e ? std::atoi(e) != 0 : true;
+        const char* ps = getenv("GS_NC_PRO_SWEEP");
+        p->pro_in_sweep = ps ? std::atoi(ps) != 0 : true;
         const char* m = getenv("GS_NC_MH_PARAMS");
         p->mh_params = p->pro_defer && (m ? std::atoi(m) != 0 : true);
     }
@@ -2491,7 +2534,8 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
         }
 #define GS_SWL(FF, SS) hipLaunchKernelGGL((k_cr_sweep<FF, 0, SS, 4>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                           p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,    \
-                                          s_out, p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op, cp)
+                                          s_out, p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op, cp, \
+                                          ProPre{})
 #define GS_SWL2(FF) do { if (st) GS_SWL(FF, true); else GS_SWL(FF, false); } while (0)
         if (p->F == 1) GS_SWL2(1); else if (p->F == 2) GS_SWL2(2); else GS_SWL2(3);
 #undef GS_SWL2
@@ -2500,11 +2544,23 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
         if (p->timing && record_ev(e1, S(stream))) return -1;
         return finish ? stats_finish(p, stats, stream) : 0;
     }
+    // the prologue's deferred MH draws in front of this sweep (native, same step)
+    ProPre pp{};
+    if (p->pro_pending && !rep && !given && iteration == p->pro_it && p->pro_in_sweep) {
+        p->pro_pending = false;
+        pp.nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
+        pp.nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
+        pp.n = (pp.nbp + pp.nbu + 7) / 8 * 8;
+        pp.nspec = p->nspec; pp.nacc = p->nacc; pp.n_iter_mh = p->n_iter_mh; pp.maxbins = p->maxbins;
+        pp.nbins = p->meta; pp.prop_sd = p->prop_sd; pp.dl = p->pro_dl;
+        pp.prop = p->prop; pp.logr = p->logr; pp.u_out = p->u_nat;
+        g.x += pp.n;
+    }
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,   \
                                              s_out,                                                                   \
                                              p->partials, slo, shi, p->ita(iteration), substep, p->chain0, \
-                                             op, none)
+                                             op, none, pp)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
                         else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
                         else GS_SW(FF, 0, false); } while (0)
