@@ -118,7 +118,7 @@ struct gs_plan {
     bool pro_pending = false;        // a prologue deferred its draws to the next finish
     // captured multi-step graphs: the MH launch of step i writes step i + 1's
     // block parameters (k_mh_reg epilogue), so step i + 1's prologue is no
-    // launch at all (GS_NC_MH_PARAMS=0|1, default with pro_defer)
+    // launch at all (GS_NC_MH_PARAMS=1 with pro_defer; off by default)
     bool mh_params = false;
     bool params_chained = false;     // the last MH launch wrote them
     // the deferred draws ride in the sweep launch's front workgroups instead
@@ -1701,7 +1701,7 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
                                             const double* __restrict__ prop, const double* __restrict__ logr,
                                             const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
                                             uint32_t iter, int chain0, int32_t* __restrict__ accept_out,
-                                            double* smem) {
+                                            double* smem, double* __restrict__ next_params = nullptr) {
     (void)tl_on;
     GS_TL(0);
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
@@ -1904,6 +1904,41 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
         }
     }
     for (int k = tid; k < nrow; k += blockDim.x) D[k] = Ds[k];
+    if (next_params) {
+        // the next step's block parameters from the final D_l (block_params_at's
+        // values): thread tid's l from the bins it holds in registers and the LDS
+        // D_l the last phase barrier published; the l below the MH range by the
+        // threads past its end (bins loaded here)
+        constexpr int NW = F == 3 ? gs_block::NP : 2 * F;
+        auto put = [&](int l, const double (&dq)[NSP], double bb) __attribute__((always_inline)) {
+            double pp[gs_block::NP];
+            block_params_from<F, 1>(l, bb, dq, k0, k1, k2, pp);
+            double* o = next_params + ((long long)chain * Lp1 + l) * gs_block::NP;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) o[q] = pp[q];
+        };
+        if (lok) {
+            double dq[NSP];
+#pragma unroll
+            for (int q = 0; q < NSP; ++q) {
+                const int bq = unpack16(ebp, q);
+                dq[q] = bq < 0 ? 0.0 : Ds[q * maxbins + max(bq, 0)];
+            }
+            put(l, dq, b);
+        } else {
+            // (the host chains parameters only when such threads exist: spare > 0)
+            const int spare = (int)blockDim.x - (Lp1 - ph.lmin);
+            for (int lx = tid - (Lp1 - ph.lmin); spare > 0 && lx < ph.lmin; lx += spare) {
+                double dq[NSP];
+#pragma unroll
+                for (int q = 0; q < NSP; ++q) {
+                    const int bq = ell2bin[q * Lp1 + lx];
+                    dq[q] = bq < 0 ? 0.0 : Ds[q * maxbins + max(bq, 0)];
+                }
+                put(lx, dq, bl[lx]);
+            }
+        }
+    }
     GS_TL(20);
 }
 
@@ -1926,28 +1961,7 @@ __global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, M
     const int chain = blockIdx.x;
     mh_reg_body<F>(chain, chain == 0, L, maxbins, ph, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
                    ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
-                   smem);
-    if (epi.params) {
-        // the next step's block parameters (block_params_at's values: the same
-        // D_l words, here from the LDS copy the last phase barrier published)
-        constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
-        constexpr int NW = F == 3 ? gs_block::NP : 2 * F;
-        const int Lp1 = L + 1;
-        const double* Ds = smem + 2 * Lp1 + nacc;
-        for (int l = threadIdx.x; l < Lp1; l += blockDim.x) {
-            int bq[NSP];
-            double dq[NSP];
-#pragma unroll
-            for (int q = 0; q < NSP; ++q) bq[q] = ell2bin[q * Lp1 + l];
-#pragma unroll
-            for (int q = 0; q < NSP; ++q) dq[q] = bq[q] < 0 ? 0.0 : Ds[q * maxbins + max(bq[q], 0)];
-            double pp[gs_block::NP];
-            block_params_from<F, 1>(l, bl[l], dq, k0, k1, k2, pp);
-            double* o = epi.params + ((long long)chain * Lp1 + l) * gs_block::NP;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) o[q] = pp[q];
-        }
-    }
+                   smem, epi.params);
     mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x);
 }
 
@@ -2302,7 +2316,11 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
         const char* ps = getenv("GS_NC_PRO_SWEEP");
         p->pro_in_sweep = ps ? std::atoi(ps) != 0 : true;
         const char* m = getenv("GS_NC_MH_PARAMS");
-        p->mh_params = p->pro_defer && (m ? std::atoi(m) != 0 : true);
+        // opt-in: with the draws in the sweep's front workgroups the parameter
+        // launch costs less than the MH epilogue adds (229.3 against 230.0 /
+        // 230.7 us per step; with the draws in the finish it had measured 232.9
+        // against 233.7)
+        p->mh_params = p->pro_defer && (m ? std::atoi(m) != 0 : false);
     }
     p->mh_reg = getenv("GS_MH_FUSED") == nullptr;
     const size_t nc = (size_t)p->nchains;
@@ -2911,7 +2929,10 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
     // inside a captured multi-step graph (not its last step) the MH also writes
     // the next step's block parameters, and that step's prologue launches none
-    double* nextp = p->mh_params && p->iter_dev_on && p->graph_adv == 0 && !p->inkernel_params ? p->params : nullptr;
+    // (the MH workgroup needs a thread past its l range for the l below it)
+    const bool spare = p->mh_lmin == 0 || p->L + 1 - p->mh_lmin < MH_REG_THREADS;
+    double* nextp = p->mh_params && p->iter_dev_on && p->graph_adv == 0 && !p->inkernel_params && spare ? p->params
+                                                                                                        : nullptr;
     const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv, nextp};
     return mh_decide(p, p->stats, dl, p->u_nat_ready ? p->u_nat : nullptr, slo, shi, it, accept_out, stream, &epi);
 }

@@ -161,11 +161,11 @@ int gs_step_noncentered(gs_plan* plan, const double* d_alm, double* dl_binned, d
  * Native RNG, plans of more than 4 chains: the prologue launches the block
  * parameters only and the proposals / accept uniforms are drawn by the launch
  * that reduces the statistics (gs_nc_sweep with finish = 1, or gs_nc_finish);
- * the decide calls fail if that launch has not run since the prologue.  Inside
- * a captured multi-step graph (gs_graph_step offset > 0) the previous step's
- * gs_nc_decide_fused wrote this step's parameters and the prologue launches
- * nothing.  GS_NC_PRO_DEFER=0 at plan creation: all in the prologue (the same
- * values either way). */
+ * the decide calls fail if that launch has not run since the prologue.  With
+ * GS_NC_MH_PARAMS=1 at plan creation, inside a captured multi-step graph
+ * (gs_graph_step offset > 0) the previous step's gs_nc_decide_fused wrote this
+ * step's parameters and the prologue launches nothing.  GS_NC_PRO_DEFER=0: all
+ * in the prologue (the same values either way). */
 int gs_nc_prologue(gs_plan* plan, const double* dl_binned, const double* u_prop_replay, uint64_t seed,
                    uint32_t iteration, void* stream);
 int gs_nc_sweep(gs_plan* plan, const double* d_alm, const double* dl_binned, double* s_out, const double* z_replay,

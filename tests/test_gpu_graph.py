@@ -254,18 +254,24 @@ def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
 @pytest.mark.parametrize("F", [1, 2, 3])
 def test_nc_deferred_draws_and_chained_params_bit_identical(monkeypatch, F):
     """Many-chain NC steps: the MH proposals and accept uniforms drawn by extra
-    workgroups of the statistics finish instead of the prologue, and inside a
-    captured multi-step graph the next step's block parameters written by the
-    MH launch (no prologue launch after step 0) -- GS_NC_PRO_DEFER=1 against 0 at
-    plan creation: D_l, accept flags and the trace over 5 native steps, eager
-    and as one captured 5-step graph replayed twice."""
+    workgroups at the front of the CR sweep (default) or of the statistics
+    finish (GS_NC_PRO_SWEEP=0) instead of the prologue, and optionally
+    (GS_NC_MH_PARAMS=1) the next step's block parameters written by the MH
+    launch inside a captured multi-step graph (no prologue launch after step 0)
+    -- against GS_NC_PRO_DEFER=0 at plan creation: D_l, accept flags and the
+    trace over 5 native steps, eager and as one captured 5-step graph replayed
+    twice."""
     import torch
     from gibbssampler_amd.problem import synthetic_problem
     from gibbssampler_amd.samplers import BatchedRunner
     P = synthetic_problem(64, 32, F, seed=13)
+    keys = ("GS_NC_PRO_DEFER", "GS_NC_PRO_SWEEP", "GS_NC_MH_PARAMS")
 
-    def run(defer, graph):
-        monkeypatch.setenv("GS_NC_PRO_DEFER", "1" if defer else "0")
+    def run(env, graph):
+        for k in keys:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         r = BatchedRunner("noncentered", P["lmax"], P["nside"], F, 8, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
                           blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=23,
                           chain0=1)
@@ -285,11 +291,17 @@ def test_nc_deferred_draws_and_chained_params_bit_identical(monkeypatch, F):
         out.append(r.dl.cpu().numpy())
         return out
 
+    variants = [{"GS_NC_PRO_DEFER": "1"}, {"GS_NC_PRO_DEFER": "1", "GS_NC_PRO_SWEEP": "0"},
+                {"GS_NC_PRO_DEFER": "1", "GS_NC_MH_PARAMS": "1"},
+                {"GS_NC_PRO_DEFER": "1", "GS_NC_PRO_SWEEP": "0", "GS_NC_MH_PARAMS": "1"}]
     for graph in (False, True):
-        a, b = run(True, graph), run(False, graph)
-        for x, y in zip(a, b):
-            np.testing.assert_array_equal(x, y)
-    monkeypatch.delenv("GS_NC_PRO_DEFER", raising=False)
+        want = run({"GS_NC_PRO_DEFER": "0"}, graph)
+        for env in variants:
+            got = run(env, graph)
+            for x, y in zip(got, want):
+                np.testing.assert_array_equal(x, y, err_msg=f"{env} graph={graph}")
+    for k in keys:
+        monkeypatch.delenv(k, raising=False)
 
 
 @pytest.mark.parametrize("F,nch", [(3, 1), (2, 2), (1, 4)])
