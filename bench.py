@@ -522,7 +522,7 @@ def run_masked(args, ctx, cpu=None):
     plan = GibbsPlan(L, N, 3, B, bl, [1.0, 1.0, 1.0], bins, chain0=ctx.chain0)
     d0 = plan.zeros(1, 3, NR)
     dl1 = np.stack([dl[k] for k in ("TT", "EE", "BB", "TE")])
-    dl_t = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(dl1, (B,) + dl1.shape))).cuda().contiguous()
+    dl_t = torch.from_numpy(np.array(np.broadcast_to(dl1, (B,) + dl1.shape))).cuda().contiguous()
     s = torch.zeros((B, 3, NR), dtype=torch.float64, device="cuda")
     it = [0]
 
@@ -563,6 +563,10 @@ def run_masked(args, ctx, cpu=None):
         return None
     fl = sht_flops(N, L, 20)
     achieved = 2 * fl / ((t_syn + t_ana) * 1e-3) / 1e12
+    # HBM bytes of the pair's Legendre kernels from their PMC passes (per launch;
+    # the ring stages are not in them): profiles/pmc_traffic.json
+    tp = load_profile(args.profile_json, f"masked_sht_N{N}_L{L}_TEB")
+    traffic = (tp["alm2map_legendre_bytes"] + tp["map2alm_legendre_bytes"]) if tp else None
     return {
         "metric": METRIC % (N, L),
         "value": round(args.steps * B * ctx.world / elapsed, 4),
@@ -576,7 +580,8 @@ def run_masked(args, ctx, cpu=None):
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
         "roofline": {"bound": "fp64", "kernel": "gs_sht alm2map + map2alm (TEB)", "achieved": round(achieved, 2),
                      "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFS, 4),
-                     "traffic": None, "algorithmic_flops_per_launch": fl,
+                     "traffic": traffic, "traffic_note": (tp or {}).get("source"),
+                     "algorithmic_flops_per_launch": fl,
                      "avg_launch_ms": {"alm2map": round(t_syn, 3), "map2alm": round(t_ana, 3)}},
         "cpu_baseline": _finalize_cpu(cpu),
         "notes": "healpy is absent: the CPU leg's transforms are oracle/sht_cpu.cpp (C++/OpenMP); see DESIGN.md",
