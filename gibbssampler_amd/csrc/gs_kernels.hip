@@ -108,6 +108,7 @@ struct gs_plan {
     // kernel as a parallel graph branch was measured first: 35.5 against 18.3
     // us per configs[1] step -- the branch's cross-queue synchronisation.)
     bool cls_pre = false;
+    bool cls_pre_many = false;       // the same for many chains: front workgroups of the throughput sweep
     double* cls_var = nullptr;       // [nchains][nspec][maxbins][3]
     // many-chain NC steps: the MH proposals and native accept uniforms depend
     // only on the current D_l and the counters, so they are drawn by extra
@@ -555,6 +556,11 @@ struct ProPre {
     double* prop = nullptr;
     double* logr = nullptr;
     double* u_out = nullptr;
+    // many-chain centered / ASIS steps: the C_l draw's random variates (they need
+    // only the bins' degrees of freedom and the counters) by nbv workgroups after
+    // the proposal / uniform ones, as the latency form's ClsPre does for few chains
+    int nbv = 0;
+    ClsPre cp{};
 };
 template <int F>
 __device__ void pro_pre_item(const ProPre& pp, int bx, int nchains, uint32_t seed_lo, uint32_t seed_hi, IterArg itarg,
@@ -1219,6 +1225,9 @@ __device__ void pro_pre_item(const ProPre& pp, int bx, int nchains, uint32_t see
     else if (bx < pp.nbp + pp.nbu)
         mh_uniform_at((bx - pp.nbp) * (long long)blockDim.x + threadIdx.x, nchains, pp.nspec, pp.nbins, pp.nacc,
                       pp.n_iter_mh, seed_lo, seed_hi, itarg.get(), chain0, pp.u_out);
+    else if (bx < pp.nbp + pp.nbu + pp.nbv)
+        cls_variates_item<F>(pp.cp, (bx - pp.nbp - pp.nbu) * blockDim.x + threadIdx.x, seed_lo, seed_hi, itarg.get(),
+                             chain0);
 }
 
 // non-centered prologue: the MH proposals depend only on the current D_l, not
@@ -1377,6 +1386,7 @@ struct MhEpi {
     int nchains;
     uint32_t adv;
     double* params;         // nullable: the next step's CR block parameters from the new D_l (k_mh_reg)
+    const double* dl_in;    // nullable (k_mh_reg): read the chains' D_l from here, write the decisions to dl
 };
 
 // SC: this chain's per-l statistics cached in LDS for the whole kernel (every
@@ -1701,7 +1711,8 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
                                             const double* __restrict__ prop, const double* __restrict__ logr,
                                             const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
                                             uint32_t iter, int chain0, int32_t* __restrict__ accept_out,
-                                            double* smem, double* __restrict__ next_params = nullptr) {
+                                            double* smem, double* __restrict__ next_params = nullptr,
+                                            const double* __restrict__ dl_in = nullptr) {
     (void)tl_on;
     GS_TL(0);
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
@@ -1721,6 +1732,8 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
     const Key key = chain_key(seed_lo, seed_hi, (uint32_t)(chain0 + chain));
     __shared__ int s_ao[4];
     double* D = dl + (long long)chain * nrow;
+    // dl_in (ASIS): the draw's D_l are read from there and the decisions land in dl
+    const double* Din = dl_in ? dl_in + (long long)chain * nrow : D;
     const double* P = prop + (long long)chain * nrow;
     const double* R = logr + (long long)chain * nrow;
     const double* stg = stats + (long long)chain * NS * Lp1;
@@ -1746,7 +1759,7 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
 #pragma unroll
         for (int j = 0; j < MH_FILL; ++j) {
             const int k = min(tid + j * MH_REG_THREADS, nrow - 1);
-            dv[j] = D[k]; pv[j] = P[k]; rv[j] = R[k];
+            dv[j] = Din[k]; pv[j] = P[k]; rv[j] = R[k];
         }
         int4 rr[2];
         int2 tt[2];
@@ -1770,7 +1783,7 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
             tabs[k] = phase_tab[k];
         }
     } else {
-        for (int k = tid; k < nrow; k += MH_REG_THREADS) { Ds[k] = D[k]; Ps[k] = P[k]; Rs[k] = R[k]; }
+        for (int k = tid; k < nrow; k += MH_REG_THREADS) { Ds[k] = Din[k]; Ps[k] = P[k]; Rs[k] = R[k]; }
         for (int k = tid; k < ntab; k += MH_REG_THREADS) { rngs[k] = phase_rng[k]; tabs[k] = phase_tab[k]; }
     }
     if (u_acc) {
@@ -1961,18 +1974,24 @@ __global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, M
     const int chain = blockIdx.x;
     mh_reg_body<F>(chain, chain == 0, L, maxbins, ph, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
                    ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
-                   smem, epi.params);
+                   smem, epi.params, epi.dl_in);
     mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x);
 }
 
 // stats of s_nc = A^+ s, A = chol(C(dl)) (ASIS.py:185-189)
+// (pp.n front workgroups: the ASIS MH proposals from the same dl, ProPre)
 template <int F>
 __global__ void k_stats_to_nc(int L, int nchains, int maxbins, const double* __restrict__ dl,
-                              const int* __restrict__ ell2bin, double* __restrict__ stats) {
+                              const int* __restrict__ ell2bin, double* __restrict__ stats, ProPre pp,
+                              uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, int chain0) {
+    if ((int)blockIdx.x < pp.n) {
+        pro_pre_item<F>(pp, (int)blockIdx.x, nchains, seed_lo, seed_hi, itarg, chain0);
+        return;
+    }
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     constexpr int NS = SweepAcc<F>::NS;
     const int Lp1 = L + 1;
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = ((int)blockIdx.x - pp.n) * blockDim.x + threadIdx.x;
     if (g >= nchains * Lp1) return;
     const int chain = g / Lp1, l = g % Lp1;
     const double* D = dl + (long long)chain * NSP * maxbins;
@@ -2339,7 +2358,11 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
         const char* e = getenv("GS_CLS_PRE");
         p->cls_pre = e ? std::atoi(e) != 0 : p->nchains <= 4;
     }
-    if (p->cls_pre) rc |= dev_alloc(&p->cls_var, nc * p->nspec * maxbins * 3);
+    {
+        const char* e = getenv("GS_CLS_PRE_MANY");
+        p->cls_pre_many = !p->cls_pre && (e ? std::atoi(e) != 0 : true);
+    }
+    if (p->cls_pre || p->cls_pre_many) rc |= dev_alloc(&p->cls_var, nc * p->nspec * maxbins * 3);
     if (rc) { gs_plan_destroy(p); return -1; }
     *out = p;
     return 0;
@@ -2564,16 +2587,24 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
     }
     // the prologue's deferred MH draws in front of this sweep (native, same step)
     ProPre pp{};
+    if (cls_pre_done && p->cls_pre_many && !rep && !given && p->cls_var) {
+        // the C_l draw's variates in front workgroups (many chains, centered CR)
+        pp.cp.nspec = p->nspec; pp.cp.maxbins = p->maxbins; pp.cp.bins = p->bins; pp.cp.nbins = p->meta;
+        pp.cp.out = p->cls_var;
+        pp.cp.nitem = p->nchains * p->nspec * p->maxbins;
+        pp.nbv = (pp.cp.nitem + 255) / 256;
+        *cls_pre_done = true;
+    }
     if (p->pro_pending && !rep && !given && iteration == p->pro_it && p->pro_in_sweep) {
         p->pro_pending = false;
         pp.nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
         pp.nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
-        pp.n = (pp.nbp + pp.nbu + 7) / 8 * 8;
         pp.nspec = p->nspec; pp.nacc = p->nacc; pp.n_iter_mh = p->n_iter_mh; pp.maxbins = p->maxbins;
         pp.nbins = p->meta; pp.prop_sd = p->prop_sd; pp.dl = p->pro_dl;
         pp.prop = p->prop; pp.logr = p->logr; pp.u_out = p->u_nat;
-        g.x += pp.n;
     }
+    pp.n = (pp.nbp + pp.nbu + pp.nbv + 7) / 8 * 8;
+    g.x += pp.n;
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,   \
                                              s_out,                                                                   \
@@ -2669,7 +2700,7 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
                      uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi) {
     int maxnb = 0;
-    const MhEpi none{nullptr, 1, nullptr, p->nchains, 0, nullptr};
+    const MhEpi none{nullptr, 1, nullptr, p->nchains, 0, nullptr, nullptr};
     MhEpi E = epi ? *epi : none;
     p->params_chained = false;
     MhPhases ph{};
@@ -2691,6 +2722,12 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
                            sizeof(double) + 16 + (size_t)ntab * (sizeof(int4) + sizeof(int2));
     const bool reg = p->mh_reg && p->L + 1 - p->mh_lmin <= MH_REG_THREADS && lds_reg <= 150 * 1024;
     if (!reg) E.params = nullptr;
+    if (!reg && E.dl_in) {
+        // the older MH forms read and write dl in place: copy the input first
+        const size_t bytes = (size_t)p->nchains * p->nspec * p->maxbins * sizeof(double);
+        GS_CHECK(hipMemcpyAsync(dl, E.dl_in, bytes, hipMemcpyDeviceToDevice, S(stream)));
+        E.dl_in = nullptr;
+    }
     if (reg) {
         p->params_chained = E.params != nullptr;
         static bool attr_set[4] = {false, false, false, false};
@@ -2749,16 +2786,31 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
     return 0;
 }
 
-int gs_stats_to_noncentered(gs_plan* p, const double* dl, double* stats, void* stream) {
-    if (check_plan(p)) return -1;
-    if (!dl || !stats) return set_error("gs_stats_to_noncentered: null argument");
+// pro: also the MH proposals from dl (native draws) in front workgroups
+static int stats_to_nc_launch(gs_plan* p, const double* dl, double* stats, void* stream, bool pro = false,
+                              uint64_t seed = 0, uint32_t it = 0) {
     const long long n = (long long)p->nchains * (p->L + 1);
-#define GS_TN(FF) hipLaunchKernelGGL((k_stats_to_nc<FF>), dim3(nblk(n, 256)), dim3(256), 0, S(stream), p->L, p->nchains, \
-                                     p->maxbins, dl, p->ell2bin, stats)
+    ProPre pp{};
+    if (pro) {
+        pp.nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
+        pp.n = pp.nbp;
+        pp.nspec = p->nspec; pp.nacc = p->nacc; pp.n_iter_mh = p->n_iter_mh; pp.maxbins = p->maxbins;
+        pp.nbins = p->meta; pp.prop_sd = p->prop_sd; pp.dl = dl; pp.prop = p->prop; pp.logr = p->logr;
+    }
+    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
+#define GS_TN(FF) hipLaunchKernelGGL((k_stats_to_nc<FF>), dim3(nblk(n, 256) + (unsigned)pp.n), dim3(256), 0, S(stream), \
+                                     p->L, p->nchains, p->maxbins, dl, p->ell2bin, stats, pp, slo, shi, p->ita(it),     \
+                                     p->chain0)
     if (p->F == 1) GS_TN(1); else if (p->F == 2) GS_TN(2); else GS_TN(3);
 #undef GS_TN
     GS_LAUNCH_CHECK("k_stats_to_nc");
     return 0;
+}
+
+int gs_stats_to_noncentered(gs_plan* p, const double* dl, double* stats, void* stream) {
+    if (check_plan(p)) return -1;
+    if (!dl || !stats) return set_error("gs_stats_to_noncentered: null argument");
+    return stats_to_nc_launch(p, dl, stats, stream);
 }
 
 int gs_recentre(gs_plan* p, const double* dl_new, const double* dl_old, double* s, void* stream) {
@@ -2782,7 +2834,8 @@ static int step_sweep(gs_plan* p, int mode, const double* d_alm, const double* d
         return sweep_launch(p, d_alm, nullptr, z, seed, it, 0, s_out, p->stats, false, stream, finish, mode, dl,
                             cls_pre_done);
     if (gs_block_params(p, mode, dl, p->params, stream)) return -1;
-    return sweep_launch(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, false, stream, finish);
+    return sweep_launch(p, d_alm, p->params, z, seed, it, 0, s_out, p->stats, false, stream, finish, -1, nullptr,
+                        mode == GS_MODE_CENTERED ? cls_pre_done : nullptr);
 }
 
 // ---- fused iterations ------------------------------------------------------
@@ -2981,21 +3034,17 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
     if (!d_alm || !dl) return set_error("gs_step_asis_fused: null argument");
     double* tmp = dl_tmp_out ? dl_tmp_out : p->dl_tmp;
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream)) return -1;
-    if (gs_cls_draw(p, p->stats, nullptr, seed, it, tmp, stream)) return -1;
-    if (gs_stats_to_noncentered(p, tmp, p->stats, stream)) return -1;
-    const size_t bytes = (size_t)p->nchains * p->nspec * p->maxbins * sizeof(double);
-    GS_CHECK(hipMemcpyAsync(dl, tmp, bytes, hipMemcpyDeviceToDevice, S(stream)));
-    const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
-#define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
-                                     p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, nullptr, slo, shi,        \
-                                     p->ita(it), p->chain0)
-    if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
-#undef GS_MP
-    GS_LAUNCH_CHECK("k_mh_propose");
+    bool pre = false;
+    if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream, true, &pre)) return -1;
+    if (cls_draw_launch(p, p->stats, nullptr, seed, it, tmp, nullptr, 1, nullptr, stream, pre ? p->cls_var : nullptr))
+        return -1;
+    // the non-centred statistics and, in front workgroups of the same launch,
+    // the MH proposals from the drawn D_l (tmp); the MH reads tmp and writes dl
+    // (no copy: the same values as copying tmp to dl first)
+    if (stats_to_nc_launch(p, tmp, p->stats, stream, true, seed, it)) return -1;
     // the trace record and the counter advance ride in the MH launch (no kernel
     // after it reads the counter: the re-centring uses D_l only)
-    const MhEpi epi{trace, trace ? capacity : 1, p->adv_counter(), p->nchains, p->graph_adv};
+    const MhEpi epi{trace, trace ? capacity : 1, p->adv_counter(), p->nchains, p->graph_adv, nullptr, tmp};
     if (mh_decide(p, p->stats, dl, nullptr, slo, shi, it, accept_out, stream, &epi)) return -1;
     if (recentre && s_out) {
         const bool quirk = (p->quirks & GS_QUIRK_ASIS_RECENTRE_CENTERED) != 0;

@@ -340,6 +340,48 @@ def test_centered_predrawn_variates_bit_identical(monkeypatch, F, nch):
     monkeypatch.delenv("GS_CLS_PRE", raising=False)
 
 
+@pytest.mark.parametrize("kind,F", [("centered", 3), ("centered", 2), ("asis", 3), ("asis", 1)])
+def test_many_chain_predrawn_variates_bit_identical(monkeypatch, kind, F):
+    """Many-chain centered / ASIS steps draw the C_l variates in front workgroups
+    of the CR sweep and the draw reads them (GS_CLS_PRE_MANY=0 at plan creation:
+    the draw computes them itself); the ASIS step also runs its MH proposals in
+    front workgroups of the non-centring launch and its MH reads the drawn D_l
+    where they were drawn.  Same bits: D_l, maps, accept flags and the trace over
+    4 native steps at L 512 (Planck BB bins), eager and as one captured 4-step
+    graph replayed twice."""
+    import torch
+    from gibbssampler_amd.problem import synthetic_problem
+    from gibbssampler_amd.samplers import BatchedRunner
+    P = synthetic_problem(512, 128, F, seed=17)
+    nch = 8
+
+    def run(pre, graph):
+        monkeypatch.setenv("GS_CLS_PRE_MANY", "1" if pre else "0")
+        r = BatchedRunner(kind, P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
+                          blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=41,
+                          chain0=5)
+        r.init(P["dls_init"])
+        out = []
+        if graph:
+            trace = r.plan.zeros(4, nch, r.plan.nspec, r.plan.maxbins)
+            acc = r.plan.zeros(4, nch, max(r.plan.nacc, 1), dtype=torch.int32)
+            r.capture_steps(4, trace=trace, trace_capacity=4, accept_trace=acc)
+            for _ in range(2):
+                r.step()
+                out += [trace.cpu().numpy(), acc.cpu().numpy()]
+        else:
+            for _ in range(4):
+                r.step()
+                out += [r.dl.cpu().numpy(), r.accept.cpu().numpy()]
+        return out + [r.dl.cpu().numpy(), r.s.cpu().numpy()]
+
+    for graph in (False, True):
+        a, b = run(True, graph), run(False, graph)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    monkeypatch.delenv("GS_CLS_PRE_MANY", raising=False)
+
+
 @pytest.mark.parametrize("F,nch", [(3, 1), (1, 2), (2, 2)])
 def test_centered_one_launch_bit_identical(monkeypatch, F, nch):
     """The one-launch centered step (k_centered_fused: sweep, statistics finish
