@@ -2325,7 +2325,9 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_upload(&p->ell2blk, e2k);
     rc |= dev_alloc(&p->gbuf, (size_t)p->nchains * 2 * (L + 1));
     build_tasks(p);
-    p->inkernel_params = p->nchains <= 4;
+    // many chains: the parameter table by the prologue (GS_INKERNEL_PARAMS=1: every
+    // sweep lane computes its operator, as the few-chain plans do)
+    p->inkernel_params = p->nchains <= 4 || getenv("GS_INKERNEL_PARAMS") != nullptr;
     p->sweep_latency = getenv("GS_SWEEP_THROUGHPUT") == nullptr;
     {
         const char* e = getenv("GS_NC_PRO_DEFER");
@@ -2922,10 +2924,11 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
         p->pro_dl = dl; p->pro_slo = slo; p->pro_shi = shi; p->pro_it = it;
         return 0;
     }
-    if (p->pro_defer && u_prop == nullptr && nbq > 0) {
-        // native draws: to the front of this step's statistics finish (stats_finish)
+    if (p->pro_defer && u_prop == nullptr && (nbq > 0 || p->nchains > 4)) {
+        // native draws: to the front of this step's sweep (or statistics finish)
         p->pro_pending = true;
         p->pro_dl = dl; p->pro_slo = slo; p->pro_shi = shi; p->pro_it = it;
+        if (nbq == 0) return 0;                   // the sweep computes the operator: no launch
 #define GS_PRQ(FF) hipLaunchKernelGGL((k_nc_prologue<FF>), dim3(nbq), dim3(256), 0, S(stream), 0, nbq, p->u_nat,     \
                                       p->nspec, p->nacc, p->n_iter_mh, p->L, p->nchains, p->maxbins, p->ell2bin, p->bl, \
                                       p->kappa[0], p->kappa[1], p->kappa[2], p->params, p->meta, p->prop_sd, dl,        \
