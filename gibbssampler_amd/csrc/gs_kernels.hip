@@ -71,6 +71,15 @@ struct gs_plan {
     int2* phase_tab = nullptr;       // (spectrum, block) pairs, phase-major
     int4* phase_rng = nullptr;       // per phase entry: (lo bin, hi bin, l0, l1); wide blocks first
     int phase_nwide[4] = {0, 0, 0, 0};
+    // the MH split over two workgroups per chain (F >= 2; GS_MH_SPLIT=0|1, default 1):
+    // BB shares no likelihood term with T / E, so its blocks are decided by a
+    // workgroup of their own beside the T / E phases' one; tables of the split form
+    bool mh_split = false;
+    int sph_n[2] = {0, 0};                   // phases per workgroup kind
+    int sph_sp[2][4][2], sph_off[2][4], sph_cnt[2][4], sph_nwide[2][4], sph_own[2] = {0, 0};
+    int2* phase_tab_s = nullptr;
+    int4* phase_rng_s = nullptr;
+    int ntab_s = 0;
     int mh_lmin = 0;
     int phase_sp[4][2] = {{-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}};
     int* ell2blk = nullptr;          // [nspec][L+1] MH block of each l (-1: none)
@@ -1371,6 +1380,7 @@ struct MhPhases {
     int n[4];
     int nwide[4];
     int lmin;     // smallest multipole any MH block covers (terms below it are never read)
+    int own;      // spectra (bit per spectrum) whose D_l this workgroup decides and writes back
 };
 
 // optional tail of the fused MH kernel (graph-captured NC steps): record this
@@ -1592,13 +1602,16 @@ constexpr int MH_REG_THREADS = 1024;
 // the graph-step tail of an MH launch: this chain's D_l into the trace (each
 // thread re-reads the D_l words it just wrote) and the device counter advance
 // by the last of the nblk MH workgroups
+// (own, maxbins: the spectra rows this workgroup wrote back -- the split MH)
 __device__ __forceinline__ void mh_epilogue(const MhEpi& epi, uint32_t iter, int chain, int nrow,
-                                            const double* __restrict__ dl, unsigned nblk) {
+                                            const double* __restrict__ dl, unsigned nblk, int maxbins = 1,
+                                            int own = -1) {
     if (epi.trace) {
         const long long slot = (long long)((iter + (uint32_t)epi.cap - 1u) % (uint32_t)epi.cap);
         double* tr = epi.trace + (slot * epi.nchains + chain) * nrow;
         const double* D = dl + (long long)chain * nrow;
-        for (int k = threadIdx.x; k < nrow; k += blockDim.x) tr[k] = D[k];
+        for (int k = threadIdx.x; k < nrow; k += blockDim.x)
+            if ((own >> (k / maxbins)) & 1) tr[k] = D[k];
     }
     if (epi.counter) ticket_advance(epi.counter, nblk, epi.adv);
 }
@@ -1916,7 +1929,8 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
             }
         }
     }
-    for (int k = tid; k < nrow; k += blockDim.x) D[k] = Ds[k];
+    for (int k = tid; k < nrow; k += blockDim.x)
+        if ((ph.own >> (k / maxbins)) & 1) D[k] = Ds[k];
     if (next_params) {
         // the next step's block parameters from the final D_l (block_params_at's
         // values): thread tid's l from the bins it holds in registers and the LDS
@@ -1968,14 +1982,17 @@ __global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, M
                                                            const double* __restrict__ logr,
                                                            const double* __restrict__ u_acc, uint32_t seed_lo,
                                                            uint32_t seed_hi, IterArg itarg, int chain0,
-                                                           int32_t* __restrict__ accept_out, MhEpi epi) {
+                                                           int32_t* __restrict__ accept_out, MhEpi epi,
+                                                           MhPhases ph1, int nsplit) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const uint32_t iter = itarg.get();
-    const int chain = blockIdx.x;
-    mh_reg_body<F>(chain, chain == 0, L, maxbins, ph, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
+    // nsplit 2: workgroup 2c decides chain c's T / E phases, 2c + 1 its BB blocks
+    const int chain = (int)blockIdx.x / nsplit, kind = (int)blockIdx.x % nsplit;
+    const MhPhases& phk = kind ? ph1 : ph;
+    mh_reg_body<F>(chain, blockIdx.x == 0, L, maxbins, phk, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
                    ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
                    smem, epi.params, epi.dl_in);
-    mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x);
+    mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x, maxbins, phk.own);
 }
 
 // stats of s_nc = A^+ s, A = chol(C(dl)) (ASIS.py:185-189)
@@ -2302,7 +2319,43 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
         p->phase_n[ph] = (int)ptab.size() - p->phase_off[ph];
     }
     p->mh_lmin = std::min(lmin, L);
+    // the split form's tables: kind 0 the T / E phases ([EE] [TT] [TE] or [EE]),
+    // kind 1 [BB]; the same entries in the same order per spectrum
+    std::vector<int2> stab;
+    std::vector<int4> srng;
+    if (F >= 2) {
+        const std::vector<std::vector<std::vector<int>>> kinds =
+            F == 2 ? std::vector<std::vector<std::vector<int>>>{{{0}}, {{1}}}
+                   : std::vector<std::vector<std::vector<int>>>{{{1}, {0}, {3}}, {{2}}};
+        for (int k = 0; k < 2; ++k) {
+            p->sph_n[k] = (int)kinds[k].size();
+            for (int ph = 0; ph < p->sph_n[k]; ++ph) {
+                p->sph_off[k][ph] = (int)stab.size();
+                p->sph_nwide[k][ph] = 0;
+                p->sph_sp[k][ph][0] = kinds[k][ph][0];
+                p->sph_sp[k][ph][1] = -1;
+                const int sp = kinds[k][ph][0];
+                p->sph_own[k] |= 1 << sp;
+                for (int pass = 0; pass < 2; ++pass)
+                    for (int b = 0; b < p->nblocks[sp]; ++b) {
+                        const int lo = blocks[sp * (maxbins + 1) + b], hi = blocks[sp * (maxbins + 1) + b + 1];
+                        const int l0 = hi > lo ? bins[sp * (maxbins + 1) + lo] : 0;
+                        const int l1 = hi > lo ? bins[sp * (maxbins + 1) + hi] : 0;
+                        if ((l1 - l0 > MH_SMALL) != (pass == 0)) continue;
+                        stab.push_back(make_int2(sp, b));
+                        srng.push_back(make_int4(lo, hi, l0, l1));
+                        if (pass == 0) p->sph_nwide[k][ph]++;
+                    }
+                p->sph_cnt[k][ph] = (int)stab.size() - p->sph_off[k][ph];
+            }
+        }
+        // the T / E workgroup also owns the rows of no MH spectrum (none for F >= 2)
+        p->ntab_s = (int)stab.size();
+        const char* e = getenv("GS_MH_SPLIT");
+        p->mh_split = e ? std::atoi(e) != 0 : true;
+    }
     int rc = 0;
+    if (!stab.empty()) { rc |= dev_upload(&p->phase_tab_s, stab); rc |= dev_upload(&p->phase_rng_s, srng); }
     rc |= dev_upload(&p->bl, bl);
     rc |= dev_upload(&p->ell2bin, ell2bin);
     rc |= dev_upload(&p->bins, bins);
@@ -2373,7 +2426,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
     void* bufs[] = {p->iter_dev, p->fsync, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
-                    p->params, p->stats, p->prop, p->logr, p->dl_tmp, p->cls_var};
+                    p->params, p->stats, p->prop, p->logr, p->dl_tmp, p->cls_var, p->phase_tab_s, p->phase_rng_s};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -2708,6 +2761,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
     MhPhases ph{};
     ph.nphase = p->nphase;
     ph.lmin = p->mh_lmin;
+    ph.own = -1;
     for (int q = 0; q < 4; ++q) {
         ph.sp[q][0] = p->phase_sp[q][0]; ph.sp[q][1] = p->phase_sp[q][1];
         ph.off[q] = p->phase_off[q]; ph.n[q] = p->phase_n[q]; ph.nwide[q] = p->phase_nwide[q];
@@ -2730,6 +2784,26 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
         GS_CHECK(hipMemcpyAsync(dl, E.dl_in, bytes, hipMemcpyDeviceToDevice, S(stream)));
         E.dl_in = nullptr;
     }
+    // the split form (two workgroups per chain): not with the MH-written next
+    // parameters (they need every spectrum's final D_l in one workgroup)
+    const bool split = reg && p->mh_split && p->ntab_s > 0 && E.params == nullptr;
+    MhPhases ph1{};
+    if (split) {
+        MhPhases* k2[2] = {&ph, &ph1};
+        for (int k = 0; k < 2; ++k) {
+            MhPhases& h = *k2[k];
+            h = MhPhases{};
+            h.nphase = p->sph_n[k];
+            h.lmin = p->mh_lmin;
+            h.own = k == 0 ? ~p->sph_own[1] : p->sph_own[1];
+            for (int q = 0; q < 4; ++q) {
+                const bool on = q < h.nphase;
+                h.sp[q][0] = on ? p->sph_sp[k][q][0] : -1; h.sp[q][1] = -1;
+                h.off[q] = on ? p->sph_off[k][q] : 0; h.n[q] = on ? p->sph_cnt[k][q] : 0;
+                h.nwide[q] = on ? p->sph_nwide[k][q] : 0;
+            }
+        }
+    }
     if (reg) {
         p->params_chained = E.params != nullptr;
         static bool attr_set[4] = {false, false, false, false};
@@ -2738,10 +2812,11 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
             GS_CHECK(hipFuncSetAttribute((const void*)k_mh_reg<FF>, hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                          150 * 1024));                                                                 \
         attr_set[FF] = true;                                                                                           \
-        hipLaunchKernelGGL((k_mh_reg<FF>), dim3(p->nchains), dim3(MH_REG_THREADS), lds_reg, S(stream), p->L,           \
-                           p->maxbins, ph, ntab, p->phase_tab, p->phase_rng, p->meta, p->nacc, p->n_iter_mh, p->ell2blk,     \
+        hipLaunchKernelGGL((k_mh_reg<FF>), dim3(p->nchains * (split ? 2 : 1)), dim3(MH_REG_THREADS), lds_reg, S(stream), \
+                           p->L, p->maxbins, ph, split ? p->ntab_s : ntab, split ? p->phase_tab_s : p->phase_tab,          \
+                           split ? p->phase_rng_s : p->phase_rng, p->meta, p->nacc, p->n_iter_mh, p->ell2blk,           \
                            p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop, p->logr,      \
-                           u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out, E); } while (0)
+                           u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out, E, ph1, split ? 2 : 1); } while (0)
         if (p->F == 1) GS_MR(1); else if (p->F == 2) GS_MR(2); else GS_MR(3);
 #undef GS_MR
         GS_LAUNCH_CHECK("k_mh_reg");

@@ -382,6 +382,47 @@ def test_many_chain_predrawn_variates_bit_identical(monkeypatch, kind, F):
     monkeypatch.delenv("GS_CLS_PRE_MANY", raising=False)
 
 
+@pytest.mark.parametrize("kind,F,L", [("noncentered", 3, 1024), ("noncentered", 2, 512), ("asis", 3, 512),
+                                      ("noncentered", 3, 64)])
+def test_mh_split_bit_identical(monkeypatch, kind, F, L):
+    """The MH decided by two workgroups per chain (T / E phases and the BB
+    blocks, which share no likelihood term) against one workgroup per chain
+    (GS_MH_SPLIT=0 at plan creation): D_l, accept flags and the trace over 4
+    native steps, eager and as one captured 4-step graph replayed twice."""
+    import torch
+    from gibbssampler_amd.problem import synthetic_problem
+    from gibbssampler_amd.samplers import BatchedRunner
+    P = synthetic_problem(L, min(L // 2, 256), F, seed=29)
+    nch = 6
+
+    def run(split, graph):
+        monkeypatch.setenv("GS_MH_SPLIT", "1" if split else "0")
+        r = BatchedRunner(kind, P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
+                          blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=43,
+                          chain0=3, store_skymap=False)
+        r.init(P["dls_init"])
+        out = []
+        if graph:
+            trace = r.plan.zeros(4, nch, r.plan.nspec, r.plan.maxbins)
+            acc = r.plan.zeros(4, nch, max(r.plan.nacc, 1), dtype=torch.int32)
+            r.capture_steps(4, trace=trace, trace_capacity=4, accept_trace=acc)
+            for _ in range(2):
+                r.step()
+                out += [trace.cpu().numpy(), acc.cpu().numpy()]
+        else:
+            for _ in range(4):
+                r.step()
+                out += [r.dl.cpu().numpy(), r.accept.cpu().numpy()]
+        return out + [r.dl.cpu().numpy()]
+
+    for graph in (False, True):
+        a, b = run(True, graph), run(False, graph)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+        assert a[-2].any()                                # some blocks accepted
+    monkeypatch.delenv("GS_MH_SPLIT", raising=False)
+
+
 @pytest.mark.parametrize("F,nch", [(3, 1), (1, 2), (2, 2)])
 def test_centered_one_launch_bit_identical(monkeypatch, F, nch):
     """The one-launch centered step (k_centered_fused: sweep, statistics finish
