@@ -249,9 +249,17 @@ __device__ __forceinline__ double bm_log_tab(double x, const double* __restrict_
 __device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const double* __restrict__ tab,
                                               double& sn, double& cs) {
     const uint32_t k = wz >> 24;
-    const double y = ((double)((wz >> 5) & 0x7FFFFu) * 67108864.0 + (double)(ww >> 6) + 0.5) *
-                     (1.0 / 9007199254740992.0);
-    const double ph = y * 6.283185307179586;
+    // ph = ((K + 0.5) 2^-53) 2 pi with the power-of-two scaling folded into the
+    // constant: the scaling is exact, so this is the same product (same bits)
+    // in one multiply instead of two
+    // y = K + 0.5 (K < 2^45, exact either way) built from the bits: 2^52 + K as
+    // a double (hi word 0x433 | K >> 32, lo word the low 32 bits of K), less
+    // 2^52 - 0.5 -- integer ops and one add instead of two conversions and two ops
+    const uint32_t kh = (wz >> 5) & 0x7FFFFu;                      // K = kh 2^26 + (ww >> 6)
+    const uint32_t lo = __builtin_amdgcn_alignbit(kh, ww, 6);      // (kh << 26) | (ww >> 6)
+    const uint32_t hi = ((wz >> 11) & 0x1FFFu) | 0x43300000u;      // 0x433 | kh >> 6
+    const double y = __hiloint2double((int)hi, (int)lo) - 4503599627370495.5;
+    const double ph = y * (6.283185307179586 / 9007199254740992.0);
     const double p2 = ph * ph;
     double ps = fma(p2, -1.984126984126984e-4, 8.333333333333333e-3);
     ps = fma(ps, p2, -0.16666666666666666);
@@ -265,10 +273,33 @@ __device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const do
     cs = fma(ck, cph, -(sk * sph));
 }
 
+// sqrt(x) for the Box-Muller radius x = -2 ln u1, u1 in (0, 1]: x is +-0 or
+// lies in [2^-53, 75], never below the 2^-767 where the compiler's fp64 sqrt
+// expansion rescales its argument (by 2^256 in, 2^-128 out).  This is that
+// expansion (rsq seed, one Goldschmidt step, two Newton corrections) without
+// the rescaling, whose scale factors are 2^0 on this range: the same
+// instructions on the same values, the same bits.  Its +-0 / +inf class select
+// becomes a clamp of the seed: for x > 0 here rsq(x) <= 2^26.5 < 2^30 (no
+// change), and for x = +-0 the clamped seed carries the signed zero through
+// every step (g0 = x 2^30 = +-0, ..., g3 = +-0 = x, what the select returned).
+// Seven instructions fewer per draw.
+__device__ __forceinline__ double bm_sqrt_radius(double x) {
+    const double y0 = fmin(fabs(__builtin_amdgcn_rsq(x)), 1073741824.0);
+    const double g0 = x * y0;
+    const double h0 = y0 * 0.5;
+    const double r0 = fma(-h0, g0, 0.5);
+    const double g1 = fma(g0, r0, g0);
+    const double h1 = fma(h0, r0, h0);
+    const double d0 = fma(-g1, g1, x);
+    const double g2 = fma(d0, h1, g1);
+    const double d1 = fma(-g2, g2, x);
+    return fma(d1, h1, g2);
+}
+
 __device__ __forceinline__ void box_muller_tab(uint4 w, const double* __restrict__ tab, double& z0, double& z1) {
     const double u1 = u53(w.x, w.y);
     const double lg = bm_log_tab(u1, tab);
-    const double r = sqrt(-2.0 * lg);
+    const double r = bm_sqrt_radius(-2.0 * lg);
     double sn, cs;
     bm_sincos_tab(w.z, w.w, tab, sn, cs);
     z0 = r * cs;
