@@ -115,10 +115,33 @@ __device__ __forceinline__ void bm_sincos2pi(double u, double& sn, double& cs) {
     cs = ((k + 1) & 2) ? -b : b;
 }
 
+// sqrt(x) for the Box-Muller radius x = -2 ln u1, u1 in (0, 1]: x is +-0 or
+// lies in [2^-53, 75], never below the 2^-767 where the compiler's fp64 sqrt
+// expansion rescales its argument (by 2^256 in, 2^-128 out).  This is that
+// expansion (rsq seed, one Goldschmidt step, two Newton corrections) without
+// the rescaling, whose scale factors are 2^0 on this range: the same
+// instructions on the same values, the same bits.  Its +-0 / +inf class select
+// becomes a clamp of the seed: for x > 0 here rsq(x) <= 2^26.5 < 2^30 (no
+// change), and for x = +-0 the clamped seed carries the signed zero through
+// every step (g0 = x 2^30 = +-0, ..., g3 = +-0 = x, what the select returned).
+// Seven instructions fewer per draw.
+__device__ __forceinline__ double bm_sqrt_radius(double x) {
+    const double y0 = fmin(fabs(__builtin_amdgcn_rsq(x)), 1073741824.0);
+    const double g0 = x * y0;
+    const double h0 = y0 * 0.5;
+    const double r0 = fma(-h0, g0, 0.5);
+    const double g1 = fma(g0, r0, g0);
+    const double h1 = fma(h0, r0, h0);
+    const double d0 = fma(-g1, g1, x);
+    const double g2 = fma(d0, h1, g1);
+    const double d1 = fma(-g2, g2, x);
+    return fma(d1, h1, g2);
+}
+
 __device__ __forceinline__ void box_muller(uint4 w, double& z0, double& z1) {
     const double u1 = u53(w.x, w.y);
     const double u2 = u53(w.z, w.w);
-    const double r = sqrt(-2.0 * bm_log(u1));
+    const double r = bm_sqrt_radius(-2.0 * bm_log(u1));
     double sn, cs;
     bm_sincos2pi(u2, sn, cs);
     z0 = r * cs;
@@ -229,7 +252,11 @@ __device__ __forceinline__ void bm_stage_tables(double* tab) {
 __device__ __forceinline__ double bm_log_tab(double x, const double* __restrict__ tab) {
     int e;
     double m = frexp(x, &e);
-    if (m < 0.70710678118654752440) { m *= 2.0; e -= 1; }
+    // m < sqrt(1/2): m *= 2, e -= 1 -- the doubling as an exponent add (exact,
+    // the same bits; one ldexp instead of an add and two selects)
+    const int lo = m < 0.70710678118654752440 ? 1 : 0;
+    m = ldexp(m, lo);
+    e -= lo;
     int k = (int)((m - BM_LOG_LO) * BM_LOG_INVW);
     k = min(max(k, 0), 127);
     const double c = tab[2 * k], nlc = tab[2 * k + 1];
@@ -271,29 +298,6 @@ __device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const do
     const double sk = tab[256 + 2 * k], ck = tab[256 + 2 * k + 1];
     sn = fma(sk, cph, ck * sph);
     cs = fma(ck, cph, -(sk * sph));
-}
-
-// sqrt(x) for the Box-Muller radius x = -2 ln u1, u1 in (0, 1]: x is +-0 or
-// lies in [2^-53, 75], never below the 2^-767 where the compiler's fp64 sqrt
-// expansion rescales its argument (by 2^256 in, 2^-128 out).  This is that
-// expansion (rsq seed, one Goldschmidt step, two Newton corrections) without
-// the rescaling, whose scale factors are 2^0 on this range: the same
-// instructions on the same values, the same bits.  Its +-0 / +inf class select
-// becomes a clamp of the seed: for x > 0 here rsq(x) <= 2^26.5 < 2^30 (no
-// change), and for x = +-0 the clamped seed carries the signed zero through
-// every step (g0 = x 2^30 = +-0, ..., g3 = +-0 = x, what the select returned).
-// Seven instructions fewer per draw.
-__device__ __forceinline__ double bm_sqrt_radius(double x) {
-    const double y0 = fmin(fabs(__builtin_amdgcn_rsq(x)), 1073741824.0);
-    const double g0 = x * y0;
-    const double h0 = y0 * 0.5;
-    const double r0 = fma(-h0, g0, 0.5);
-    const double g1 = fma(g0, r0, g0);
-    const double h1 = fma(h0, r0, h0);
-    const double d0 = fma(-g1, g1, x);
-    const double g2 = fma(d0, h1, g1);
-    const double d1 = fma(-g2, g2, x);
-    return fma(d1, h1, g2);
 }
 
 __device__ __forceinline__ void box_muller_tab(uint4 w, const double* __restrict__ tab, double& z0, double& z1) {
