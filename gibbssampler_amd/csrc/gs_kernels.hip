@@ -1375,13 +1375,36 @@ constexpr int MH_SMALL = 16;   // blocks of <= MH_SMALL multipoles are decided b
 
 struct MhPhases {
     int nphase;
-    int sp[4][2];
+    int sp0[4], sp1[4];     // the phase's two spectra
     int off[4];
     int n[4];
     int nwide[4];
     int lmin;     // smallest multipole any MH block covers (terms below it are never read)
     int own;      // spectra (bit per spectrum) whose D_l this workgroup decides and writes back
 };
+
+// a[q] for a wave-uniform q < 4 by constant indices (scalar selects)
+__device__ __forceinline__ int mh_pick(const int (&a)[4], int q) {
+    return q == 0 ? a[0] : (q == 1 ? a[1] : (q == 2 ? a[2] : a[3]));
+}
+
+// the kind-th workgroup's phases (k_mh_reg's split): a field-by-field select
+// with constant indices, so neither by-value argument needs an address
+__device__ __forceinline__ MhPhases mh_select(bool k1, const MhPhases& a, const MhPhases& b) {
+    MhPhases r;
+    r.nphase = k1 ? b.nphase : a.nphase;
+    r.lmin = k1 ? b.lmin : a.lmin;
+    r.own = k1 ? b.own : a.own;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        r.sp0[q] = k1 ? b.sp0[q] : a.sp0[q];
+        r.sp1[q] = k1 ? b.sp1[q] : a.sp1[q];
+        r.off[q] = k1 ? b.off[q] : a.off[q];
+        r.n[q] = k1 ? b.n[q] : a.n[q];
+        r.nwide[q] = k1 ? b.nwide[q] : a.nwide[q];
+    }
+    return r;
+}
 
 // optional tail of the fused MH kernel (graph-captured NC steps): record this
 // chain's D_l in the trace and advance the device iteration counter once the
@@ -1461,12 +1484,13 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     lds_fill4(e2b, ell2bin, NSP * Lp1);
     __syncthreads();
     for (int q = 0; q < ph.nphase; ++q) {
-        const int nb = ph.n[q];
+        const int nb = mh_pick(ph.n, q);
         if (nb == 0) continue;
-        const int sp0 = ph.sp[q][0], sp1 = ph.sp[q][1];
-        const int2* tab = phase_tab + ph.off[q];
-        const int4* rng = phase_rng + ph.off[q];
-        const int nwide = ph.nwide[q];
+        const int sp0 = mh_pick(ph.sp0, q), sp1 = mh_pick(ph.sp1, q);
+        const int off = mh_pick(ph.off, q);
+        const int2* tab = phase_tab + off;
+        const int4* rng = phase_rng + off;
+        const int nwide = mh_pick(ph.nwide, q);
         // per-l likelihood differences of the phase's spectra
         for (int l = ph.lmin + tid; l < Lp1; l += blockDim.x) {
             double vo[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1834,12 +1858,15 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
     bool okcur = true;
     if constexpr (F == 3) okcur = psd_ok(vcur[0], vcur[1], vcur[3]);
     for (int q = 0; q < ph.nphase; ++q) {
-        const int nb = ph.n[q];
+        // the phase's scalars picked with constant indices (a runtime index into
+        // the by-value kernel argument would copy it to scratch in every thread)
+        const int nb = mh_pick(ph.n, q);
         if (nb == 0) continue;
-        const int sp0 = ph.sp[q][0], sp1 = ph.sp[q][1];
-        const int2* tab = tabs + ph.off[q];
-        const int4* rng = rngs + ph.off[q];
-        const int nwide = ph.nwide[q];
+        const int sp0 = mh_pick(ph.sp0, q), sp1 = mh_pick(ph.sp1, q);
+        const int off = mh_pick(ph.off, q);
+        const int2* tab = tabs + off;
+        const int4* rng = rngs + off;
+        const int nwide = mh_pick(ph.nwide, q);
         // per-l likelihood differences of the phase's proposals on their own parts
         double pvk[2] = {0.0, 0.0}, fnk[2] = {0.0, 0.0};
         bool okk[2] = {false, false};
@@ -1988,7 +2015,7 @@ __global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, M
     const uint32_t iter = itarg.get();
     // nsplit 2: workgroup 2c decides chain c's T / E phases, 2c + 1 its BB blocks
     const int chain = (int)blockIdx.x / nsplit, kind = (int)blockIdx.x % nsplit;
-    const MhPhases& phk = kind ? ph1 : ph;
+    const MhPhases phk = mh_select(kind != 0, ph, ph1);
     mh_reg_body<F>(chain, blockIdx.x == 0, L, maxbins, phk, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
                    ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
                    smem, epi.params, epi.dl_in);
@@ -2763,7 +2790,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
     ph.lmin = p->mh_lmin;
     ph.own = -1;
     for (int q = 0; q < 4; ++q) {
-        ph.sp[q][0] = p->phase_sp[q][0]; ph.sp[q][1] = p->phase_sp[q][1];
+        ph.sp0[q] = p->phase_sp[q][0]; ph.sp1[q] = p->phase_sp[q][1];
         ph.off[q] = p->phase_off[q]; ph.n[q] = p->phase_n[q]; ph.nwide[q] = p->phase_nwide[q];
         maxnb = std::max(maxnb, p->phase_n[q]);
     }
@@ -2798,7 +2825,7 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
             h.own = k == 0 ? ~p->sph_own[1] : p->sph_own[1];
             for (int q = 0; q < 4; ++q) {
                 const bool on = q < h.nphase;
-                h.sp[q][0] = on ? p->sph_sp[k][q][0] : -1; h.sp[q][1] = -1;
+                h.sp0[q] = on ? p->sph_sp[k][q][0] : -1; h.sp1[q] = -1;
                 h.off[q] = on ? p->sph_off[k][q] : 0; h.n[q] = on ? p->sph_cnt[k][q] : 0;
                 h.nwide[q] = on ? p->sph_nwide[k][q] : 0;
             }

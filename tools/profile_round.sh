@@ -8,7 +8,7 @@
 #                             asis C4 (per GPU), the drop-in surface, masked C5, HEAD's masked modes
 #   prof_<tag>_<mode>         kernel stats of configs[1], the masked workloads, SHT at N_side 2048
 # usage (GPU box): bash tools/profile_round.sh <tag> [a|b|c|d|all]   (then python tools/summarize_profile.py <tag>)
-#   a: the harmonic trace, PMC passes and harmonic bench lines; b: the masked bench lines and the
+#   a: the harmonic trace, PMC passes and harmonic bench lines (= p then h); b: the masked bench lines and the
 #   masked / configs[1] / SHT kernel stats (two gpurun calls stay within one call's time limit);
 #   c (r04): the chain-batched SHT (N_side 256, 16 spin-2 maps, matrix-core Legendre tables) --
 #   kernel stats and FETCH_SIZE / WRITE_SIZE / SQ passes -- and the N_side 2048 recurrence kernels'
@@ -20,7 +20,7 @@ TAG=${1:-r03}
 PART=${2:-all}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
-if [ "$PART" = a ] || [ "$PART" = all ]; then
+if [ "$PART" = a ] || [ "$PART" = p ] || [ "$PART" = all ]; then
 rm -rf "$OUT"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
@@ -40,6 +40,10 @@ pmc store --steps 5 --warmup 2 --skymap store
 pmc c2 --workload centered --nside 256 --lmax 512 --nchains 1 --steps 20 --warmup 2 --time-every 100
 pmc c4 --workload asis --steps 5 --warmup 2
 echo "profiles done"
+fi
+# h: the harmonic bench lines alone (after summarize_profile.py has folded part p's passes into
+# profiles/pmc_traffic.json, so the lines' roofline reads this build's counters)
+if [ "$PART" = a ] || [ "$PART" = h ] || [ "$PART" = all ]; then
 timeout -k 10 400 python3 bench.py > gpurun_out/bench_${TAG}_default.json 2> gpurun_out/bench_${TAG}_default.err
 timeout -k 10 400 python3 bench.py --no-cpu-baseline --skymap store > gpurun_out/bench_${TAG}_default_store.json \
     2> gpurun_out/bench_${TAG}_default_store.err
