@@ -2194,8 +2194,13 @@ void build_tasks(gs_plan* p) {
     // measured slower there in r02 (sweep 282-294 vs 261-281 us), but short
     // tasks (the latency form, few chains) take it: their finish is a chain of
     // memory latencies, one per group of chunk partials it reads.
+    // r05, after the sweep's per-row instruction count fell (406 -> 379) and the
+    // MH lost its scratch copies, 1 x 4 is the faster shape for many chains too:
+    // NC TEB 32 chains at L 1024 212.2-212.7 against 215.2-215.8 us per step,
+    // ASIS 225.5 against 231.4 (tools/step_ab.py; 16 rows per task stays best
+    // with either shape: 12 / 20 / 24 / 32 rows 220.1 / 220.3 / 221.9 / 221.1).
     // GS_SWEEP_TW=1|2|4 overrides (A/B timing).
-    int tw = tm <= 4 ? 1 : 2;
+    int tw = 1;
     if (const char* env = getenv("GS_SWEEP_TW")) {
         const int v = atoi(env);
         if (v == 1 || v == 2 || v == 4) tw = v;
