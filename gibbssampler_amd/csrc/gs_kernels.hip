@@ -272,6 +272,19 @@ __device__ __forceinline__ void load_d(const double* __restrict__ d, long long N
         for (int c = 0; c < NV; ++c) dv[f][c] = d[f * NR + r + c];
 }
 
+// the same entry's loads with the field bases wave-uniform (SGPRs) and the
+// row offset a 32-bit byte count (F (L+1)^2 doubles per chain < 4 GiB): the
+// scalar-base + 32-bit vector-offset load form, no 64-bit address arithmetic
+template <int F>
+__device__ __forceinline__ void load_d2_off(const char* const (&db)[F], uint32_t rb, double (&dv)[F][2]) {
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+        const double2 v = *reinterpret_cast<const double2*>(db[f] + rb);
+        dv[f][0] = v.x;
+        dv[f][1] = v.y;
+    }
+}
+
 // ZM: 0 native RNG draw, 1 replay (z from memory), 2 statistics of a given s
 template <int F, int ZM, bool STORE, int NV>
 __device__ __forceinline__ void sweep_entry(const double (&dv)[F][2], const double* __restrict__ zc,
@@ -661,11 +674,28 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     if (m1 - 1 <= ell_lo && ell_lo >= 0) {
         // off-diagonal block: every lane active on every row; the next row's
         // data is loaded before this row's draw (register double buffer)
+        if constexpr (ZM == 0 && !STORE) {
+            // the headline form (native draws, no map written): 32-bit row offsets
+            uint32_t i32 = (uint32_t)i;
+            const char* db[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f)
+                db[f] = reinterpret_cast<const char*>(d + (size_t)f * (size_t)NR);   // wave-uniform bases
+            GS_ASSERT(NR * 8 < (1ll << 32));
+            for (; m < m1; ++m) {
+                const uint32_t r = 2u * i32 - (uint32_t)(L + 1);
+                load_d2_off<F>(db, r * 8u, dv);
+                sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, (long long)r, i32, tag, iter, key, pm, acc, tab);
+                GS_ASSERT((long long)r + 1 < NR && (long long)r > L);
+                i32 += (uint32_t)(L - m);
+            }
+        } else {
         for (; m < m1; ++m) {
             load_d<F, 2>(d, NR, 2 * i - (L + 1), dv);
             sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, 2 * i - (L + 1), (uint32_t)i, tag, iter, key, pm, acc, tab);
             GS_ASSERT(2 * i - (L + 1) + 1 < NR && 2 * i - (L + 1) > L);
             i += L - m;
+        }
         }
     } else {
         for (; m < m1; ++m) {
