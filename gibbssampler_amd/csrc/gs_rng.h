@@ -38,8 +38,10 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         uint32_t n0, n2;
         if constexpr (UKEY) {
-            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c1), "s"(k0));
-            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c3), "s"(k1));
+            // the builtin rather than inline asm: the hazard recognizer treats an
+            // asm block conservatively (an s_nop after each pair in the sweep)
+            n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, k0, 0x96);
+            n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, k1, 0x96);
         } else {
             n0 = hi1 ^ c1 ^ k0;
             n2 = hi0 ^ c3 ^ k1;
