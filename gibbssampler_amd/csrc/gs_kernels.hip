@@ -697,6 +697,21 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
             i += L - m;
         }
         }
+    } else if constexpr (ZM == 0 && !STORE) {
+        // diagonal block of the headline form (lanes l < m idle): the same
+        // 32-bit row offsets
+        const char* db[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) db[f] = reinterpret_cast<const char*>(d + (size_t)f * (size_t)NR);
+        uint32_t i32 = (uint32_t)i;
+        for (; m < m1; ++m) {
+            if (lane_ok && ell >= m) {
+                const uint32_t r = 2u * i32 - (uint32_t)(L + 1);
+                load_d2_off<F>(db, r * 8u, dv);
+                sweep_entry<F, ZM, STORE, 2>(dv, zc, sc, NR, (long long)r, i32, tag, iter, key, pm, acc, tab);
+            }
+            i32 += (uint32_t)(L - m);
+        }
     } else {
         for (; m < m1; ++m) {
             if (lane_ok && ell >= m) {
