@@ -180,8 +180,8 @@ def load_profile(path, key):
 
 
 def cpu_baseline_child(args):
-    """The CPU baselines on the host's cores (one chain per core, at most 16:
-    the GPU box's CPU share per GPU), run as a child process before this process
+    """The CPU baselines on the host's cores (one chain per core, at most 32:
+    one GPU's share of the 8-GPU node's 256 cores), run as a child process before this process
     touches the GPU: the reference-structured port and the algorithm-matched
     port (oracle/cpu_baseline.py)."""
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
@@ -208,7 +208,7 @@ def cpu_baseline_child(args):
 def cpu_baseline_masked_child(args):
     """The masked workloads' CPU leg (oracle/cpu_baseline_masked.py: the reference's
     masked samplers with the C++/OpenMP HEALPix SHT of oracle/sht_cpu.cpp on
-    min(affinity, 16) threads), run as a child process before this process
+    min(affinity, 32) threads), run as a child process before this process
     touches the GPU; a PCG workload's rate is completed with the device solve's
     CG iteration count after the timed region (cpu_baseline_masked.finalize)."""
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")

@@ -6,6 +6,7 @@ device pointers from torch tensors, the HIP stream from
 ``torch.cuda.current_stream().cuda_stream``.  There is no CPU fallback: if the
 library is missing or fails to load, every entry point raises.
 """
+import contextlib
 import ctypes
 import os
 
@@ -72,6 +73,8 @@ _VP = ctypes.c_void_p
 _SIGS = [
     ("gs_abi_version", ctypes.c_int, []),
     ("gs_last_error", ctypes.c_char_p, []),
+    ("gs_option_set", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
+    ("gs_option_get", ctypes.c_char_p, [ctypes.c_char_p]),
     ("gs_plan_create", ctypes.c_int, [ctypes.POINTER(GsModelDesc), ctypes.POINTER(_VP)]),
     ("gs_plan_destroy", ctypes.c_int, [_VP]),
     ("gs_plan_info", ctypes.c_int, [_VP, c_int_p, c_int_p, c_int_p, c_int_p]),
@@ -181,6 +184,33 @@ def check(rc, what="gibbs_hip"):
         raise GibbsHipError(f"{what} failed: {msg}")
 
 
+def set_option(name, value):
+    """Library option (include/gibbs_capi.h gs_option_set): read when a plan,
+    SHT or masked context is created; value None unsets it."""
+    lib = load()
+    v = None if value is None else str(value).encode()
+    check(lib.gs_option_set(name.encode(), v), f"gs_option_set({name})")
+
+
+def get_option(name):
+    r = load().gs_option_get(name.encode())
+    return None if r is None else r.decode()
+
+
+@contextlib.contextmanager
+def options(**kw):
+    """Set library options for the body (restored afterwards), e.g.
+    ``with options(GS_SWEEP_TW=2): BatchedRunner(...)``."""
+    old = {k: get_option(k) for k in kw}
+    try:
+        for k, v in kw.items():
+            set_option(k, v)
+        yield
+    finally:
+        for k, v in old.items():
+            set_option(k, v)
+
+
 def ptr(t):
     """Device pointer of a torch tensor (None -> NULL)."""
     if t is None:
@@ -223,10 +253,7 @@ def capturing():
 
 
 def _drain():
-    """Run the deferred releases (no capture open).  Also reached from release /
-    park outside any capture, so entries parked during a capture that this
-    package did not open (torch.cuda.graph used directly: end_capture never
-    runs) are freed at the next teardown instead of living forever."""
+    """Run the deferred releases (no capture open)."""
     while _GRAVEYARD:
         fn, h = _GRAVEYARD.pop()
         if fn is not None:
@@ -241,7 +268,6 @@ def release(fn, handle):
     if capturing():
         _GRAVEYARD.append((fn, handle))
     else:
-        _drain()
         fn(handle)
 
 
@@ -251,8 +277,18 @@ def park(obj):
     if capturing():
         _GRAVEYARD.append((None, obj))
         return True
-    _drain()
     return False
+
+
+def flush():
+    """Free what was parked during captures this package did not open
+    (torch.cuda.graph used directly: end_capture never runs for them).  Only at
+    this explicit point -- never from an unrelated teardown -- because a graph
+    captured outside the package may still replay kernels that use those
+    buffers: call it once such graphs are gone.  No-op while any
+    capture is open on the current stream."""
+    if not capturing():
+        _drain()
 
 
 def begin_capture():

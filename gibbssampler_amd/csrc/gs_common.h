@@ -13,6 +13,11 @@ inline int set_error(const std::string& msg) {
     return -1;
 }
 
+// library options (include/gibbs_capi.h gs_option_set): the value of a
+// registered option, or nullptr when it is unset.  Read when a plan, SHT or
+// masked context is created; the library reads no environment variables.
+const char* option(const char* name);
+
 }  // namespace gs_detail
 
 #define GS_CHECK(expr)                                                                        \

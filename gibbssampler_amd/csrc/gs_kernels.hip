@@ -21,6 +21,8 @@
 #include <cstring>
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "gibbs_capi.h"
 #include "gs_rng.h"
@@ -61,9 +63,6 @@ struct gs_plan {
     // the latency form of the sweep (all loads first) may be used for short tasks;
     // GS_SWEEP_THROUGHPUT at plan creation forces the throughput form (A/B timing)
     bool sweep_latency = true;
-    // the register / LDS-resident MH kernel where it fits (GS_MH_FUSED at plan
-    // creation: the older k_mh_fused, for A/B timing)
-    bool mh_reg = true;
     // MH phases: spectra whose blocks are mutually independent run in one launch
     int nphase = 0;
     int phase_n[4] = {0, 0, 0, 0};
@@ -106,10 +105,6 @@ struct gs_plan {
     bool u_nat_ready = false;
     // device iteration counter (hipGraph replay of whole steps)
     uint32_t* iter_dev = nullptr;
-    // arrival counters of the one-launch centered step (k_centered_fused)
-    uint32_t* fsync = nullptr;
-    int ncu = 0;                     // compute units of the device
-    bool centered_fused = false;     // GS_CENTERED_FUSED at plan creation: the one-launch step (measured slower)
     // few-chain centered steps: the C_l draw's random variates (Gamma / normal)
     // depend on the bins' degrees of freedom and the counters only, so extra
     // workgroups of the latency-form sweep draw them while the sweep runs, and
@@ -121,19 +116,14 @@ struct gs_plan {
     double* cls_var = nullptr;       // [nchains][nspec][maxbins][3]
     // many-chain NC steps: the MH proposals and native accept uniforms depend
     // only on the current D_l and the counters, so they are drawn by extra
-    // workgroups at the front of the statistics-finish launch (beside its
-    // bandwidth-bound partial sums) instead of in the prologue, which keeps the
-    // block parameters alone (GS_NC_PRO_DEFER=0|1 at plan creation).
-    bool pro_defer = false;
-    bool pro_pending = false;        // a prologue deferred its draws to the next finish
-    // captured multi-step graphs: the MH launch of step i writes step i + 1's
-    // block parameters (k_mh_reg epilogue), so step i + 1's prologue is no
-    // launch at all (GS_NC_MH_PARAMS=1 with pro_defer; off by default)
-    bool mh_params = false;
-    bool params_chained = false;     // the last MH launch wrote them
-    // the deferred draws ride in the sweep launch's front workgroups instead
-    // of the finish (GS_NC_PRO_SWEEP=0|1, default 1)
-    bool pro_in_sweep = true;
+    // workgroups at the front of the CR sweep's launch (or, when the sweep
+    // cannot take them -- replayed normals -- of the statistics finish) instead
+    // of in the prologue, which keeps the block parameters alone
+    bool pro_pending = false;        // a prologue deferred its draws to the sweep / finish
+    // the proposal launch of this step also wrote a snapshot of the chains'
+    // D_l into dl_tmp: the split MH reads its start state from there (both
+    // workgroups of a chain see the pre-MH D_l whatever their order)
+    bool snap_ok = false;
     const double* pro_dl = nullptr;
     uint32_t pro_slo = 0, pro_shi = 0, pro_it = 0;
     bool iter_dev_on = false;
@@ -394,34 +384,13 @@ __device__ __forceinline__ void sweep_operator(bool ok, int chain, int ell, int 
 // chunk-waves of a tile add their sums in LDS in chunk order ((c0 + c1) + c2) +
 // c3, and the tile's first chunk-wave stores one partial per chunk group (every
 // wave of the workgroup reaches the barrier; an inactive wave adds zeros).
-// a statistic word: a plain load, or (SC1: statistics handed over inside one
-// launch by write-through stores) an sc1 load, served past the CU's L1
-template <bool SC1>
-__device__ __forceinline__ double ld_stat(const double* p) {
-    if constexpr (SC1)
-        return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    else
-        return *p;
-}
-
-// SC1: write-through (sc1) stores, for a hand-off inside the launch (k_centered_fused)
-template <bool SC1>
-__device__ __forceinline__ void st_word(double* p, double v) {
-    if constexpr (SC1)
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = v;
-}
-
-template <int NS, bool SC1 = false>
+template <int NS>
 __device__ __forceinline__ void sweep_partials_store(const double (&acc)[NS], int tw, int w, int lane, bool store_ok,
                                                      double* __restrict__ po, double* red) {
     if (tw == 4) {
         if (store_ok)
 #pragma unroll
-            for (int q = 0; q < NS; ++q) st_word<SC1>(po + q * WAVE + lane, acc[q]);
+            for (int q = 0; q < NS; ++q) po[q * WAVE + lane] = acc[q];
         return;
     }
     const int cw = 4 / tw, ci = w / tw, ti = w % tw;
@@ -434,7 +403,7 @@ __device__ __forceinline__ void sweep_partials_store(const double (&acc)[NS], in
         for (int q = 0; q < NS; ++q) {
             double v = acc[q];
             for (int k = 1; k < cw; ++k) v += red[(((k - 1) * tw + ti) * NS + q) * WAVE + lane];
-            st_word<SC1>(po + q * WAVE + lane, v);
+            po[q * WAVE + lane] = v;
         }
     }
 }
@@ -445,7 +414,7 @@ __device__ __forceinline__ void sweep_partials_store(const double (&acc)[NS], in
 // Box-Muller tables, the operator's D_l -- is issued before any of them is
 // used (one memory round trip instead of one per row plus two for the
 // prologue).  Same arithmetic in the same order as the throughput form below.
-template <int F, bool STORE, int PRE, bool SC1 = false>
+template <int F, bool STORE, int PRE>
 __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
                                                  const int2* __restrict__ tasks, const double* __restrict__ d,
                                                  double* __restrict__ s,
@@ -545,7 +514,7 @@ __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, 
         }
     }
     double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
-    sweep_partials_store<NS, SC1>(acc, tw, w, lane, t < ntile && (cw * gc.y) * tm <= lhi, po, red);
+    sweep_partials_store<NS>(acc, tw, w, lane, t < ntile && (cw * gc.y) * tm <= lhi, po, red);
 }
 
 // the C_l draw's variates computed by extra workgroups of the latency-form
@@ -563,7 +532,7 @@ template <int F>
 __device__ void cls_variates_item(const ClsPre& cp, int item, uint32_t seed_lo, uint32_t seed_hi, uint32_t iter,
                                   int chain0);
 
-// many-chain NC steps (pro_defer): the MH proposals and native accept
+// many-chain NC steps: the MH proposals and native accept
 // uniforms drawn by n extra workgroups at the FRONT of the throughput-form
 // sweep's grid (they start first and their latency chains -- inverse normal
 // CDFs, log-CDFs -- end long before the sweep does); n is a multiple of 8, so
@@ -578,6 +547,7 @@ struct ProPre {
     double* prop = nullptr;
     double* logr = nullptr;
     double* u_out = nullptr;
+    double* snap = nullptr;          // nullable: the proposals' start D_l copied here (split MH)
     // many-chain centered / ASIS steps: the C_l draw's random variates (they need
     // only the bins' degrees of freedom and the counters) by nbv workgroups after
     // the proposal / uniform ones, as the latency form's ClsPre does for few chains
@@ -728,7 +698,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
 
 // one wave's share of a (chain, statistic, tile) finish: the sum of chunks w,
 // w + 4, ... of the tile's 64 l (lanes; coalesced rows of the partials)
-template <int G, bool SC1 = false>
+template <int G>
 __device__ __forceinline__ double stats_finish_sum(int L, int ntile, int nchunkg, int tm, int nstat,
                                                    const double* partials, int chain, int q, int t,
                                                    int w, int lane) {
@@ -751,16 +721,16 @@ __device__ __forceinline__ double stats_finish_sum(int L, int ntile, int nchunkg
         for (; c + 12 <= cmax; c += 16) {
             double v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = ld_stat<SC1>(pp + (c + 4 * j) * cs);
+            for (int j = 0; j < 4; ++j) v[j] = *(pp + (c + 4 * j) * cs);
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc += v[j];
         }
-        for (; c <= cmax; c += 4) acc += ld_stat<SC1>(pp + c * cs);
+        for (; c <= cmax; c += 4) acc += *(pp + c * cs);
     } else {
         for (int c = w; c <= cmax; c += 4 * G) {
             double v[G];
 #pragma unroll
-            for (int j = 0; j < G; ++j) v[j] = ld_stat<SC1>(pp + min(c + 4 * j, cmax) * cs);
+            for (int j = 0; j < G; ++j) v[j] = *(pp + min(c + 4 * j, cmax) * cs);
 #pragma unroll
             for (int j = 0; j < G; ++j)
                 if (c + 4 * j <= cmax) acc += v[j];
@@ -841,7 +811,7 @@ __device__ __forceinline__ void cls_variates(int sp, int b, int l0, int l1, Key 
     }
 }
 
-template <int F, bool SC1 = false>
+template <int F>
 __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, int maxbins, const int* __restrict__ bins,
                                               const int* __restrict__ nbins_arr, const double* stats,
                                               const double* __restrict__ variates, uint32_t seed_lo, uint32_t seed_hi,
@@ -883,8 +853,8 @@ __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, i
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int l = max(min(l0 + j, l1 - 1), 0);
-                va[j] = ld_stat<SC1>(st + 0 * Lp1 + l); vd[j] = ld_stat<SC1>(st + 1 * Lp1 + l);
-                vc[j] = ld_stat<SC1>(st + 3 * Lp1 + l);
+                va[j] = *(st + 0 * Lp1 + l); vd[j] = *(st + 1 * Lp1 + l);
+                vc[j] = *(st + 3 * Lp1 + l);
             }
             double vr[3];
             if (pre) {
@@ -900,8 +870,8 @@ __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, i
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int l = min(lg + j, l1 - 1);
-                        va[j] = ld_stat<SC1>(st + 0 * Lp1 + l); vd[j] = ld_stat<SC1>(st + 1 * Lp1 + l);
-                        vc[j] = ld_stat<SC1>(st + 3 * Lp1 + l);
+                        va[j] = *(st + 0 * Lp1 + l); vd[j] = *(st + 1 * Lp1 + l);
+                        vc[j] = *(st + 3 * Lp1 + l);
                     }
                 }
 #pragma unroll
@@ -950,7 +920,7 @@ __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, i
         constexpr int G = 24;
         double v[G];
 #pragma unroll
-        for (int j = 0; j < G; ++j) v[j] = ld_stat<SC1>(st + ssrow * Lp1 + max(min(l0 + j, l1 - 1), 0));
+        for (int j = 0; j < G; ++j) v[j] = *(st + ssrow * Lp1 + max(min(l0 + j, l1 - 1), 0));
         double X;
         if (variates) X = variates[((long long)chain * NSP + sp) * maxbins + b];
         else if (pre) X = pre[(((long long)chain * NSP + sp) * maxbins + b) * 3];
@@ -959,7 +929,7 @@ __device__ __forceinline__ void cls_draw_body(int chain, int sp, int b, int L, i
         for (int lg = l0; lg < l1; lg += G) {
             if (lg > l0) {
 #pragma unroll
-                for (int j = 0; j < G; ++j) v[j] = ld_stat<SC1>(st + ssrow * Lp1 + min(lg + j, l1 - 1));
+                for (int j = 0; j < G; ++j) v[j] = *(st + ssrow * Lp1 + min(lg + j, l1 - 1));
             }
 #pragma unroll
             for (int j = 0; j < G; ++j) {
@@ -1005,98 +975,6 @@ __device__ void cls_variates_item(const ClsPre& cp, int item, uint32_t seed_lo, 
     q[0] = v[0]; q[1] = v[1]; q[2] = v[2];
 }
 
-
-// One launch per centered step for few chains (configs[1], r03): the CR sweep
-// (latency form), the statistics finish and the C_l draw with in-launch
-// hand-offs instead of two kernel boundaries (CenteredGibbs.py:54-93,317-353).
-// Every workgroup runs its sweep task and stores its partials write-through
-// (sc1); after every wave's vmcnt(0) and a barrier one lane takes an arrival
-// ticket.  The last nhelp arrivers become helpers: they wait for all tickets
-// (sc1 polls), finish the statistics (one (chain, statistic, tile) per wave,
-// the same sums as k_stats_finish; sc1 loads and stores), meet at a second
-// counter, and draw the C_l (the k_cls_draw items, sc1 loads of the
-// statistics).  The last helper resets the counters and advances the device
-// iteration counter.  Deadlock freedom: a workgroup waits only once it is one
-// of the last nhelp arrivers, i.e. when at most nhelp - 1 workgroups have not
-// arrived, and the host launches this form only when nhelp is below the
-// device's CU count (each waiting helper holds at most one CU's slot).
-template <int F>
-__global__ __launch_bounds__(256, 1) void k_centered_fused(int L, int nchains, int ntile, int nchunkg, int tm, int tmf,
-                                                           int tw,
-                                                           const int2* __restrict__ tasks, const double* __restrict__ d,
-                                                           double* __restrict__ s, double* partials,
-                                                           uint32_t seed_lo, uint32_t seed_hi, IterArg itarg,
-                                                           int chain0, SweepOp op, int nhelp, uint32_t* sync,
-                                                           double* stats, int maxbins, const int* __restrict__ bins,
-                                                           const int* __restrict__ nbins_arr, double* __restrict__ dl_out,
-                                                           double* __restrict__ trace, int cap,
-                                                           uint32_t* __restrict__ counter, uint32_t adv) {
-    constexpr int NS = SweepAcc<F>::NS;
-    constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
-    const uint32_t iter = itarg.get();
-    __shared__ double tab[BM_TAB_DOUBLES];
-    __shared__ double red[3 * NS * WAVE];
-    __shared__ uint32_t s_ticket;
-    cr_sweep_latency<F, true, 4, true>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo, seed_hi,
-                                       iter, 0, chain0, op, tab, red);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this wave's sc1 partial stores have completed
-    __syncthreads();
-    const uint32_t nwg = gridDim.x;
-    if (threadIdx.x == 0)
-        s_ticket = __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t tk = s_ticket;
-    if (tk < nwg - (uint32_t)nhelp) return;
-    const int h = (int)(tk - (nwg - (uint32_t)nhelp));
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (threadIdx.x == 0)
-        while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg) __builtin_amdgcn_s_sleep(1);
-    __syncthreads();
-    // ---- the statistics finish: one (chain, statistic, tile) per helper, its
-    // four waves as k_stats_finish's (chunk groups w, w + 4, ...; the same sums)
-    const int Lp1 = L + 1;
-    const int nunit = nchains * NS * ntile;
-    for (int u = h; u < nunit; u += nhelp) {
-        const int t = u % ntile, q = (u / ntile) % NS, chain = u / (ntile * NS);
-        // tmf: the rows of one chunk group (tm x 4 / tw), the finish's chunk unit
-        const double a = stats_finish_sum<16, true>(L, ntile, nchunkg, tmf, NS, partials, chain, q, t, w, lane);
-        red[w * WAVE + lane] = a;
-        __syncthreads();
-        if (w == 0) {
-            const int ell = L - WAVE * t - 63 + lane;
-            const double v = ((red[lane] + red[WAVE + lane]) + red[2 * WAVE + lane]) + red[3 * WAVE + lane];
-            if (ell >= 0) st_word<true>(stats + ((long long)chain * NS + q) * Lp1 + ell, v);
-        }
-        __syncthreads();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)nhelp)
-            __builtin_amdgcn_s_sleep(1);
-    }
-    __syncthreads();
-    // ---- the C_l draw: k_cls_draw's (chain, spectrum, bin) items ----
-    const int nitem = nchains * NSP * maxbins;
-    for (int i = h * blockDim.x + threadIdx.x; i < nitem; i += nhelp * blockDim.x) {
-        const int b = i % maxbins, sp = (i / maxbins) % NSP, chain = i / (maxbins * NSP);
-        cls_draw_body<F, true>(chain, sp, b, L, maxbins, bins, nbins_arr, stats, nullptr, seed_lo, seed_hi, iter,
-                               chain0, dl_out, trace, cap, nchains);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t e = __hip_atomic_fetch_add(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (e == (uint32_t)nhelp - 1) {
-            // every workgroup has read the iteration counter (all arrived) and
-            // every helper has passed both waits: reset for the next launch
-            __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&sync[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (counter) __hip_atomic_fetch_add(&counter[0], adv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
 
 // ============================================================================
 // non-centered Metropolis-within-Gibbs (NonCenteredGibbs.py:292-445)
@@ -1171,10 +1049,13 @@ __device__ __forceinline__ void mh_propose_at(long long g, int nchains, int maxb
                                               const double* __restrict__ prop_sd, const double* __restrict__ dl,
                                               double* __restrict__ prop, double* __restrict__ logr,
                                               const double* __restrict__ u_prop, uint32_t seed_lo,
-                                              uint32_t seed_hi, IterArg itarg, int chain0) {
+                                              uint32_t seed_hi, IterArg itarg, int chain0,
+                                              double* __restrict__ snap = nullptr) {
     const uint32_t iter = itarg.get();
     constexpr int NSP = F == 1 ? 1 : (F == 2 ? 2 : 4);
     if (g >= (long long)nchains * NSP * maxbins) return;
+    // (snap: a copy of the D_l the proposals start from, every item, for the split MH)
+    if (snap) snap[g] = dl[g];
     const int b = (int)(g % maxbins);
     const int sp = (int)((g / maxbins) % NSP);
     const int chain = (int)(g / ((long long)maxbins * NSP));
@@ -1203,9 +1084,10 @@ __global__ __launch_bounds__(256) void k_mh_propose(int nchains, int maxbins, co
                                                     const double* __restrict__ prop_sd, const double* __restrict__ dl,
                                                     double* __restrict__ prop, double* __restrict__ logr,
                                                     const double* __restrict__ u_prop, uint32_t seed_lo,
-                                                    uint32_t seed_hi, IterArg itarg, int chain0) {
+                                                    uint32_t seed_hi, IterArg itarg, int chain0,
+                                                    double* __restrict__ snap) {
     mh_propose_at<F>(blockIdx.x * (long long)blockDim.x + threadIdx.x, nchains, maxbins, nbins_arr, prop_sd, dl, prop,
-                     logr, u_prop, seed_lo, seed_hi, itarg, chain0);
+                     logr, u_prop, seed_lo, seed_hi, itarg, chain0, snap);
 }
 
 // flat accept order of the plan (same counters as k_mh_fused / k_mh_accept)
@@ -1226,7 +1108,7 @@ __device__ __forceinline__ void mh_uniform_at(long long g, int nchains, int nspe
     out[g] = uniform1(key, blk, (uint32_t)sp | ((uint32_t)att << 8), TAG_MH_U, iter);
 }
 
-// k_stats_finish with nbp + nbu extra workgroups first (pro_defer plans): the
+// k_stats_finish with nbp + nbu extra workgroups first (deferred draws the sweep could not take: replayed normals): the
 // MH proposals and native accept uniforms of this step, the same items and
 // code as k_nc_prologue's (bit-identical either way)
 template <int F, int G>
@@ -1239,11 +1121,12 @@ __global__ __launch_bounds__(256) void k_stats_finish_pro(int L, int nchains, in
                                                           const double* __restrict__ prop_sd,
                                                           const double* __restrict__ dl, double* __restrict__ prop,
                                                           double* __restrict__ logr, uint32_t seed_lo,
-                                                          uint32_t seed_hi, IterArg itarg, int chain0) {
+                                                          uint32_t seed_hi, IterArg itarg, int chain0,
+                                                          double* __restrict__ snap) {
     const int bx = (int)blockIdx.x;
     if (bx < nblk_prop) {
         mh_propose_at<F>(bx * (long long)blockDim.x + threadIdx.x, nchains, maxbins, nbins_arr, prop_sd, dl, prop,
-                         logr, nullptr, seed_lo, seed_hi, itarg, chain0);
+                         logr, nullptr, seed_lo, seed_hi, itarg, chain0, snap);
         return;
     }
     if (bx < nblk_prop + nblk_u) {
@@ -1275,7 +1158,7 @@ __device__ void pro_pre_item(const ProPre& pp, int bx, int nchains, uint32_t see
                              int chain0) {
     if (bx < pp.nbp)
         mh_propose_at<F>(bx * (long long)blockDim.x + threadIdx.x, nchains, pp.maxbins, pp.nbins, pp.prop_sd, pp.dl,
-                         pp.prop, pp.logr, nullptr, seed_lo, seed_hi, itarg, chain0);
+                         pp.prop, pp.logr, nullptr, seed_lo, seed_hi, itarg, chain0, pp.snap);
     else if (bx < pp.nbp + pp.nbu)
         mh_uniform_at((bx - pp.nbp) * (long long)blockDim.x + threadIdx.x, nchains, pp.nspec, pp.nbins, pp.nacc,
                       pp.n_iter_mh, seed_lo, seed_hi, itarg.get(), chain0, pp.u_out);
@@ -1295,7 +1178,8 @@ __global__ __launch_bounds__(256) void k_nc_prologue(int nblk_prop, int nblk_par
                                                      const int* __restrict__ nbins_arr, const double* __restrict__ prop_sd,
                                                      const double* __restrict__ dl, double* __restrict__ prop,
                                                      double* __restrict__ logr, const double* __restrict__ u_prop,
-                                                     uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, int chain0) {
+                                                     uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, int chain0,
+                                                     double* __restrict__ snap) {
     if ((int)blockIdx.x >= nblk_prop + nblk_par) {
         // native accept uniforms of this step's MH (k_mh_fused reads them from LDS)
         mh_uniform_at(((int)blockIdx.x - nblk_prop - nblk_par) * (long long)blockDim.x + threadIdx.x, nchains, nspec,
@@ -1304,7 +1188,7 @@ __global__ __launch_bounds__(256) void k_nc_prologue(int nblk_prop, int nblk_par
     }
     if ((int)blockIdx.x < nblk_prop)
         mh_propose_at<F>(blockIdx.x * (long long)blockDim.x + threadIdx.x, nchains, maxbins, nbins_arr, prop_sd, dl,
-                         prop, logr, u_prop, seed_lo, seed_hi, itarg, chain0);
+                         prop, logr, u_prop, seed_lo, seed_hi, itarg, chain0, snap);
     else
         block_params_at<F, 1>(((int)blockIdx.x - nblk_prop) * blockDim.x + threadIdx.x, L, nchains, maxbins, dl,
                               ell2bin, bl, k0, k1, k2, params);
@@ -1463,7 +1347,6 @@ struct MhEpi {
     uint32_t* counter;      // nullable: [0] iteration base (advanced by adv), [1] finished-workgroup ticket
     int nchains;
     uint32_t adv;
-    double* params;         // nullable: the next step's CR block parameters from the new D_l (k_mh_reg)
     const double* dl_in;    // nullable (k_mh_reg): read the chains' D_l from here, write the decisions to dl
 };
 
@@ -1484,7 +1367,7 @@ __device__ __forceinline__ void lds_fill4(T* __restrict__ dst, const T* __restri
     }
 }
 
-template <int F, bool SC>
+template <int F>
 __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases ph, const int2* __restrict__ phase_tab,
                                                   const int4* __restrict__ phase_rng,
                                                   const int* __restrict__ bins, const int* __restrict__ blocks,
@@ -1506,8 +1389,7 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     double* g = smem;                               // [2][L+1]
     double* ub = g + 2 * Lp1;                       // [phase blocks x n_iter]
     double* Ds = ub + maxnb * n_iter_mh;            // [NSP][maxbins] LDS copy of this chain's D_l
-    double* stl = Ds + NSP * maxbins;               // [NS][L+1] statistics (SC only)
-    double* ul = stl + (SC ? NS * Lp1 : 0);         // [nacc] this chain's accept uniforms (u_acc given)
+    double* ul = Ds + NSP * maxbins;                // [nacc] this chain's accept uniforms (u_acc given)
     int* e2b = reinterpret_cast<int*>(ul + (u_acc ? nacc : 0));   // [NSP][L+1]
     const int chain = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
@@ -1519,12 +1401,11 @@ __global__ __launch_bounds__(1024) void k_mh_fused(int L, int maxbins, MhPhases 
     const double* P = prop + (long long)chain * NSP * maxbins;
     const double* R = logr + (long long)chain * NSP * maxbins;
     const double* stg = stats + (long long)chain * NS * Lp1;
-    const double* st = SC ? stl : stg;
+    const double* st = stg;
     // LDS fill: the chain's D_l (kept in LDS for the whole sweep, written back at
-    // the end), statistics (SC), accept uniforms (u_acc) and the l -> bin map;
+    // the end), accept uniforms (u_acc) and the l -> bin map;
     // four loads in flight per thread and array
     lds_fill4(Ds, D, NSP * maxbins);
-    if constexpr (SC) lds_fill4(stl, stg, NS * Lp1);
     if (u_acc) lds_fill4(ul, u_acc + (long long)chain * nacc, nacc);
     lds_fill4(e2b, ell2bin, NSP * Lp1);
     __syncthreads();
@@ -1793,7 +1674,7 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
                                             const double* __restrict__ prop, const double* __restrict__ logr,
                                             const double* __restrict__ u_acc, uint32_t seed_lo, uint32_t seed_hi,
                                             uint32_t iter, int chain0, int32_t* __restrict__ accept_out,
-                                            double* smem, double* __restrict__ next_params = nullptr,
+                                            double* smem,
                                             const double* __restrict__ dl_in = nullptr) {
     (void)tl_on;
     GS_TL(0);
@@ -2003,41 +1884,6 @@ __device__ __forceinline__ void mh_reg_body(int chain, bool tl_on, int L, int ma
     }
     for (int k = tid; k < nrow; k += blockDim.x)
         if ((ph.own >> (k / maxbins)) & 1) D[k] = Ds[k];
-    if (next_params) {
-        // the next step's block parameters from the final D_l (block_params_at's
-        // values): thread tid's l from the bins it holds in registers and the LDS
-        // D_l the last phase barrier published; the l below the MH range by the
-        // threads past its end (bins loaded here)
-        constexpr int NW = F == 3 ? gs_block::NP : 2 * F;
-        auto put = [&](int l, const double (&dq)[NSP], double bb) __attribute__((always_inline)) {
-            double pp[gs_block::NP];
-            block_params_from<F, 1>(l, bb, dq, k0, k1, k2, pp);
-            double* o = next_params + ((long long)chain * Lp1 + l) * gs_block::NP;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) o[q] = pp[q];
-        };
-        if (lok) {
-            double dq[NSP];
-#pragma unroll
-            for (int q = 0; q < NSP; ++q) {
-                const int bq = unpack16(ebp, q);
-                dq[q] = bq < 0 ? 0.0 : Ds[q * maxbins + max(bq, 0)];
-            }
-            put(l, dq, b);
-        } else {
-            // (the host chains parameters only when such threads exist: spare > 0)
-            const int spare = (int)blockDim.x - (Lp1 - ph.lmin);
-            for (int lx = tid - (Lp1 - ph.lmin); spare > 0 && lx < ph.lmin; lx += spare) {
-                double dq[NSP];
-#pragma unroll
-                for (int q = 0; q < NSP; ++q) {
-                    const int bq = ell2bin[q * Lp1 + lx];
-                    dq[q] = bq < 0 ? 0.0 : Ds[q * maxbins + max(bq, 0)];
-                }
-                put(lx, dq, bl[lx]);
-            }
-        }
-    }
     GS_TL(20);
 }
 
@@ -2063,7 +1909,7 @@ __global__ __launch_bounds__(MH_REG_THREADS) void k_mh_reg(int L, int maxbins, M
     const MhPhases phk = mh_select(kind != 0, ph, ph1);
     mh_reg_body<F>(chain, blockIdx.x == 0, L, maxbins, phk, ntab, phase_tab, phase_rng, meta, nacc, n_iter_mh, ell2blk,
                    ell2bin, bl, k0, k1, k2, stats, dl, prop, logr, u_acc, seed_lo, seed_hi, iter, chain0, accept_out,
-                   smem, epi.params, epi.dl_in);
+                   smem, epi.dl_in);
     mh_epilogue(epi, iter, chain, (F == 1 ? 1 : (F == 2 ? 2 : 4)) * maxbins, dl, gridDim.x, maxbins, phk.own);
 }
 
@@ -2188,6 +2034,26 @@ __global__ void k_record_trace(long long n, const double* __restrict__ dl, doubl
 // ============================================================================
 // host side
 // ============================================================================
+// the library options (gs_option_set): a fixed set of names
+static const char* const k_options[] = {
+    "GS_SWEEP_TW", "GS_SWEEP_THROUGHPUT", "GS_MH_SPLIT", "GS_CLS_PRE", "GS_CLS_PRE_MANY", "GS_F2_GROUP_BYTES",
+    "GS_F2_BATCH_BYTES", "GS_SHT_LDS_FFT_MAX", "GS_SHT_SEG", "GS_SHT_SYN", "GS_SHT_ANA", "GS_SHT_MERGE_RINGS",
+    "GS_SHT_CONST_RINGS", "GS_SHT_BLOCKS_MFMA", "GS_SHT_BLK_STAGE", "GS_SHT_FUSED_AUX", "GS_SHT_MFMA_MAX_GB"};
+static bool opt_known(const char* name) {
+    for (const char* k : k_options)
+        if (std::strcmp(k, name) == 0) return true;
+    return false;
+}
+static std::mutex& opt_mu() { static std::mutex m; return m; }
+static std::map<std::string, std::string>& opt_tab() { static std::map<std::string, std::string> t; return t; }
+
+const char* gs_detail::option(const char* name) {
+    std::lock_guard<std::mutex> g(opt_mu());
+    const auto it = opt_tab().find(name);
+    // the map's nodes are stable: the pointer stays valid until the option is reset
+    return it == opt_tab().end() ? nullptr : it->second.c_str();
+}
+
 namespace {
 
 template <typename T>
@@ -2223,11 +2089,7 @@ void build_tasks(gs_plan* p) {
     // r02 with the workgroup-per-tile statistics finish: NC TEB 32 chains at
     // L 1024: 12 / 16 / 20 / 24 rows 308.5 / 308.5 / 312.0 / 319.3 us per step;
     // centered 1 chain at L 512: 2 / 4 / 8 rows 25.7 / 22.4 / 26.0 us
-    int tm = L > 512 ? 16 : (L > 256 ? 4 : 8);
-    if (const char* env = getenv("GS_SWEEP_ROWS")) {
-        const int v = atoi(env);
-        if (v >= 1 && v <= 1024) tm = v;
-    }
+    const int tm = L > 512 ? 16 : (L > 256 ? 4 : 8);
     p->rows_per_task = tm;
     p->nchunk = L / tm + 1;
     p->ntask = (int)waves(tm);
@@ -2244,9 +2106,9 @@ void build_tasks(gs_plan* p) {
     // NC TEB 32 chains at L 1024 212.2-212.7 against 215.2-215.8 us per step,
     // ASIS 225.5 against 231.4 (tools/step_ab.py; 16 rows per task stays best
     // with either shape: 12 / 20 / 24 / 32 rows 220.1 / 220.3 / 221.9 / 221.1).
-    // GS_SWEEP_TW=1|2|4 overrides (A/B timing).
+    // option GS_SWEEP_TW = 1 | 2 | 4 overrides (the stored-map line: 2).
     int tw = 1;
-    if (const char* env = getenv("GS_SWEEP_TW")) {
+    if (const char* env = gs_detail::option("GS_SWEEP_TW")) {
         const int v = atoi(env);
         if (v == 1 || v == 2 || v == 4) tw = v;
     }
@@ -2299,6 +2161,15 @@ extern "C" {
 
 int gs_abi_version(void) { return GS_ABI_VERSION; }
 const char* gs_last_error(void) { return gs_detail::g_last_error.c_str(); }
+
+int gs_option_set(const char* name, const char* value) {
+    if (!name || !opt_known(name)) return set_error(std::string("gs_option_set: unknown option ") + (name ? name : "(null)"));
+    std::lock_guard<std::mutex> g(opt_mu());
+    if (value) opt_tab()[name] = value; else opt_tab().erase(name);
+    return 0;
+}
+
+const char* gs_option_get(const char* name) { return name ? gs_detail::option(name) : nullptr; }
 
 int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     if (!desc || !out) return set_error("gs_plan_create: null argument");
@@ -2428,7 +2299,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
         }
         // the T / E workgroup also owns the rows of no MH spectrum (none for F >= 2)
         p->ntab_s = (int)stab.size();
-        const char* e = getenv("GS_MH_SPLIT");
+        const char* e = gs_detail::option("GS_MH_SPLIT");
         p->mh_split = e ? std::atoi(e) != 0 : true;
     }
     int rc = 0;
@@ -2455,25 +2326,11 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_upload(&p->ell2blk, e2k);
     rc |= dev_alloc(&p->gbuf, (size_t)p->nchains * 2 * (L + 1));
     build_tasks(p);
-    // many chains: the parameter table by the prologue (GS_INKERNEL_PARAMS=1: every
-    // sweep lane computes its operator, as the few-chain plans do)
-    p->inkernel_params = p->nchains <= 4 || getenv("GS_INKERNEL_PARAMS") != nullptr;
-    p->sweep_latency = getenv("GS_SWEEP_THROUGHPUT") == nullptr;
-    {
-        const char* e = getenv("GS_NC_PRO_DEFER");
-        // measured (tools/step_ab.py, configs[2]): 234.6 -> 233.7 us per step with
-        // the draws deferred, 232.9 with the MH-written parameters as well
-        p->pro_defer = e ? std::atoi(e) != 0 : true;
-        const char* ps = getenv("GS_NC_PRO_SWEEP");
-        p->pro_in_sweep = ps ? std::atoi(ps) != 0 : true;
-        const char* m = getenv("GS_NC_MH_PARAMS");
-        // opt-in: with the draws in the sweep's front workgroups the parameter
-        // launch costs less than the MH epilogue adds (229.3 against 230.0 /
-        // 230.7 us per step; with the draws in the finish it had measured 232.9
-        // against 233.7)
-        p->mh_params = p->pro_defer && (m ? std::atoi(m) != 0 : false);
-    }
-    p->mh_reg = getenv("GS_MH_FUSED") == nullptr;
+    // many chains: the parameter table by the prologue (r05: every sweep lane
+    // computing its operator measured 231.8 against 223.8 us per NC step at
+    // configs[2]); few chains: in the sweep, no parameter launch
+    p->inkernel_params = p->nchains <= 4;
+    p->sweep_latency = gs_detail::option("GS_SWEEP_THROUGHPUT") == nullptr;
     const size_t nc = (size_t)p->nchains;
     rc |= dev_alloc(&p->partials, nc * p->ntile * p->nchunkg * p->nstat * WAVE);
     rc |= dev_alloc(&p->params, nc * (L + 1) * NP);
@@ -2483,15 +2340,12 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->dl_tmp, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->u_nat, nc * std::max(p->nacc, 1));
     rc |= dev_alloc(&p->iter_dev, 4);
-    rc |= dev_alloc(&p->fsync, 4);
-    if (hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) p->ncu = 0;
-    p->centered_fused = getenv("GS_CENTERED_FUSED") != nullptr;
     {
-        const char* e = getenv("GS_CLS_PRE");
+        const char* e = gs_detail::option("GS_CLS_PRE");
         p->cls_pre = e ? std::atoi(e) != 0 : p->nchains <= 4;
     }
     {
-        const char* e = getenv("GS_CLS_PRE_MANY");
+        const char* e = gs_detail::option("GS_CLS_PRE_MANY");
         p->cls_pre_many = !p->cls_pre && (e ? std::atoi(e) != 0 : true);
     }
     if (p->cls_pre || p->cls_pre_many) rc |= dev_alloc(&p->cls_var, nc * p->nspec * maxbins * 3);
@@ -2502,7 +2356,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
-    void* bufs[] = {p->iter_dev, p->fsync, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
+    void* bufs[] = {p->iter_dev, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
                     p->params, p->stats, p->prop, p->logr, p->dl_tmp, p->cls_var, p->phase_tab_s, p->phase_rng_s};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2635,10 +2489,9 @@ static int timing_begin(gs_plan* p, hipStream_t s, hipEvent_t* e0, hipEvent_t* e
         // timing-only events: no system-scope fence at record (a fence per
         // record writes back and invalidates the caches -- ~6 us between the
         // graph's kernels and a slower next kernel); read after a device sync
-        static const bool fence = getenv("GS_TIMING_EVENT_FENCE") != nullptr;
         for (int k = 0; k < 64; ++k) {
             hipEvent_t e;
-            GS_CHECK(fence ? hipEventCreate(&e) : hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+            GS_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
             p->ev.push_back(e);
         }
     }
@@ -2660,12 +2513,13 @@ static int stats_finish(gs_plan* p, double* stats, void* stream) {
                                          S(stream), p->L, p->nchains, p->ntile, p->nchunkg, tmf, p->nstat, p->partials, \
                                          stats, nbp, nbu, p->u_nat, p->nspec, p->nacc, p->n_iter_mh, p->maxbins,        \
                                          p->meta, p->prop_sd, p->pro_dl, p->prop, p->logr, p->pro_slo, p->pro_shi,      \
-                                         p->ita(p->pro_it), p->chain0)
+                                         p->ita(p->pro_it), p->chain0, p->dl_tmp)
 #define GS_FPG(FF) do { if (p->nchains <= 4) GS_FP(FF, 16); else GS_FP(FF, 4); } while (0)
         if (p->F == 1) GS_FPG(1); else if (p->F == 2) GS_FPG(2); else GS_FPG(3);
 #undef GS_FPG
 #undef GS_FP
         GS_LAUNCH_CHECK("k_stats_finish_pro");
+        p->snap_ok = true;
         return 0;
     }
     if (p->nchains <= 4)
@@ -2727,13 +2581,14 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
         pp.nbv = (pp.cp.nitem + 255) / 256;
         *cls_pre_done = true;
     }
-    if (p->pro_pending && !rep && !given && iteration == p->pro_it && p->pro_in_sweep) {
+    if (p->pro_pending && !rep && !given && iteration == p->pro_it) {
         p->pro_pending = false;
+        p->snap_ok = true;
         pp.nbp = nblk((long long)p->nchains * p->nspec * p->maxbins, 256);
         pp.nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
         pp.nspec = p->nspec; pp.nacc = p->nacc; pp.n_iter_mh = p->n_iter_mh; pp.maxbins = p->maxbins;
         pp.nbins = p->meta; pp.prop_sd = p->prop_sd; pp.dl = p->pro_dl;
-        pp.prop = p->prop; pp.logr = p->logr; pp.u_out = p->u_nat;
+        pp.prop = p->prop; pp.logr = p->logr; pp.u_out = p->u_nat; pp.snap = p->dl_tmp;
     }
     pp.n = (pp.nbp + pp.nbu + pp.nbv + 7) / 8 * 8;
     g.x += pp.n;
@@ -2798,7 +2653,7 @@ int gs_mh_propose(gs_plan* p, const double* dl, const double* u_prop, uint64_t s
     GS_CHECK(hipMemsetAsync(logr_out, 0, nprop * sizeof(double), S(stream)));
 #define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
                                      p->maxbins, p->meta, p->prop_sd, dl, prop_out, logr_out, u_prop, slo, shi,     \
-                                     p->ita(iteration), p->chain0)
+                                     p->ita(iteration), p->chain0, nullptr)
     if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
 #undef GS_MP
     GS_LAUNCH_CHECK("k_mh_propose");
@@ -2821,10 +2676,11 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
     const long long nprop = (long long)p->nchains * p->nspec * p->maxbins;
 #define GS_MP(FF) hipLaunchKernelGGL((k_mh_propose<FF>), dim3(nblk(nprop, 256)), dim3(256), 0, S(stream), p->nchains, \
                                      p->maxbins, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi, p->ita(iteration), \
-                                     p->chain0)
+                                     p->chain0, p->dl_tmp)
     if (p->F == 1) GS_MP(1); else if (p->F == 2) GS_MP(2); else GS_MP(3);
 #undef GS_MP
     GS_LAUNCH_CHECK("k_mh_propose");
+    p->snap_ok = true;
     return mh_decide(p, stats, dl, u_acc, slo, shi, iteration, accept_out, stream);
 }
 
@@ -2832,9 +2688,11 @@ int gs_nc_mh(gs_plan* p, const double* stats, double* dl, const double* u_prop, 
 static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* u_acc, uint32_t slo, uint32_t shi,
                      uint32_t iteration, int32_t* accept_out, void* stream, const MhEpi* epi) {
     int maxnb = 0;
-    const MhEpi none{nullptr, 1, nullptr, p->nchains, 0, nullptr, nullptr};
+    const MhEpi none{nullptr, 1, nullptr, p->nchains, 0, nullptr};
     MhEpi E = epi ? *epi : none;
-    p->params_chained = false;
+    // the proposal launch's D_l snapshot belongs to this decision only
+    const bool snap = p->snap_ok;
+    p->snap_ok = false;
     MhPhases ph{};
     ph.nphase = p->nphase;
     ph.lmin = p->mh_lmin;
@@ -2848,22 +2706,29 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
                            sizeof(double) + (size_t)p->nspec * (p->L + 1) * sizeof(int);
     const size_t lds_u = u_acc ? (size_t)p->nacc * sizeof(double) : 0;
     // r03: the register / LDS-resident form when the phase l range is at most
-    // one l per thread and its arrays fit the LDS (GS_MH_FUSED=1: the older form)
+    // one l per thread and its arrays fit the LDS (k_mh_fused otherwise)
     int ntab = 0;
     for (int q = 0; q < p->nphase; ++q) ntab += p->phase_n[q];
     const size_t lds_reg = (2 * (size_t)(p->L + 1) + (size_t)p->nacc + 3 * (size_t)p->nspec * p->maxbins) *
                            sizeof(double) + 16 + (size_t)ntab * (sizeof(int4) + sizeof(int2));
-    const bool reg = p->mh_reg && p->L + 1 - p->mh_lmin <= MH_REG_THREADS && lds_reg <= 150 * 1024;
-    if (!reg) E.params = nullptr;
+    const bool reg = p->L + 1 - p->mh_lmin <= MH_REG_THREADS && lds_reg <= 150 * 1024;
     if (!reg && E.dl_in) {
         // the older MH forms read and write dl in place: copy the input first
         const size_t bytes = (size_t)p->nchains * p->nspec * p->maxbins * sizeof(double);
         GS_CHECK(hipMemcpyAsync(dl, E.dl_in, bytes, hipMemcpyDeviceToDevice, S(stream)));
         E.dl_in = nullptr;
     }
-    // the split form (two workgroups per chain): not with the MH-written next
-    // parameters (they need every spectrum's final D_l in one workgroup)
-    const bool split = reg && p->mh_split && p->ntab_s > 0 && E.params == nullptr;
+    // the split form (two workgroups per chain): both workgroups of a chain read
+    // its start D_l, the T / E one writes its rows of dl at its end, so neither
+    // may read dl itself -- the BB workgroup's PSD test of the T / E state would
+    // depend on the order the two run in.  They read a stable copy:
+    // the caller's dl_in (ASIS: the drawn D_l) or the snapshot the proposal
+    // launch wrote (dl_tmp); without either the chain runs in one workgroup.
+    bool split = reg && p->mh_split && p->ntab_s > 0;
+    if (split && !E.dl_in) {
+        if (snap) E.dl_in = p->dl_tmp;
+        else split = false;
+    }
     MhPhases ph1{};
     if (split) {
         MhPhases* k2[2] = {&ph, &ph1};
@@ -2882,7 +2747,6 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
         }
     }
     if (reg) {
-        p->params_chained = E.params != nullptr;
         static bool attr_set[4] = {false, false, false, false};
 #define GS_MR(FF) do {                                                                                                 \
         if (!attr_set[FF])                                                                                             \
@@ -2899,18 +2763,12 @@ static int mh_decide(gs_plan* p, const double* stats, double* dl, const double* 
         GS_LAUNCH_CHECK("k_mh_reg");
         return 0;
     }
-    const size_t lds_sc = lds + lds_u + (size_t)p->nstat * (p->L + 1) * sizeof(double);
-    // the LDS statistics cache is off by default: measured 37.6 us with it
-    // against 35.8 us reading the statistics from L2 (GS_MH_STATS_CACHE=1 on)
-    const bool sc = lds_sc <= 156 * 1024 && getenv("GS_MH_STATS_CACHE") != nullptr;
     if (lds <= 128 * 1024) {
-#define GS_MF(FF) if (sc) GS_MF2(FF, true, lds_sc); else GS_MF2(FF, false, lds + lds_u)
-#define GS_MF2(FF, SCV, LDSV) hipLaunchKernelGGL((k_mh_fused<FF, SCV>), dim3(p->nchains), dim3(1024), LDSV, S(stream), p->L, p->maxbins, ph, \
+#define GS_MF(FF) hipLaunchKernelGGL((k_mh_fused<FF>), dim3(p->nchains), dim3(1024), lds + lds_u, S(stream), p->L, p->maxbins, ph, \
                                      p->phase_tab, p->phase_rng, p->bins, p->blocks, p->meta + 8, p->nacc, p->n_iter_mh, p->ell2blk,    \
                                      p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], stats, dl, p->prop,       \
                                      p->logr, u_acc, slo, shi, p->ita(iteration), p->chain0, accept_out, E)
         if (p->F == 1) { GS_MF(1); } else if (p->F == 2) { GS_MF(2); } else { GS_MF(3); }
-#undef GS_MF2
 #undef GS_MF
         GS_LAUNCH_CHECK("k_mh_fused");
         return 0;
@@ -2993,51 +2851,15 @@ static int step_sweep(gs_plan* p, int mode, const double* d_alm, const double* d
 }
 
 // ---- fused iterations ------------------------------------------------------
-static int centered_fused_launch(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed,
-                                 uint32_t it, double* trace, int cap, uint32_t* counter, void* stream);
 
 int gs_step_centered(gs_plan* p, const double* d_alm, double* dl, double* s_out, const double* z,
                      const double* igvar, uint64_t seed, uint32_t it, void* stream) {
     if (check_plan(p)) return -1;
     if (!d_alm || !dl) return set_error("gs_step_centered: null argument");
-    if (!z && !igvar) {
-        // native draws: the one-launch step where the plan allows it
-        const int rc = centered_fused_launch(p, d_alm, dl, s_out, seed, it, nullptr, 1, nullptr, stream);
-        if (rc <= 0) return rc;
-    }
     bool pre = false;
     if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, z, seed, it, s_out, stream, true, igvar ? nullptr : &pre))
         return -1;
     return cls_draw_launch(p, p->stats, igvar, seed, it, dl, nullptr, 1, nullptr, stream, pre ? p->cls_var : nullptr);
-}
-
-// the one-launch centered step (k_centered_fused) where the plan allows it:
-// the latency form of the sweep (few chains, short tasks, s stored) and fewer
-// helpers than the device's CUs (at most nhelp - 1 workgroups wait while the
-// rest are still to arrive).  Opt-in (GS_CENTERED_FUSED): measured slower than
-// the three launches.  Returns 1 when not taken (the caller launches three).
-static int centered_fused_launch(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed,
-                                 uint32_t it, double* trace, int cap, uint32_t* counter, void* stream) {
-    if (!p->centered_fused || !p->inkernel_params || p->rows_per_task > 4 || !p->sweep_latency || !s_out) return 1;
-    const int nunit = p->nchains * p->nstat * p->ntile;
-    const int nitem = p->nchains * p->nspec * p->maxbins;
-    const int nwg = p->nchains * p->npair;
-    const int nhelp = std::min(nwg, std::max(nunit, (nitem + 255) / 256));
-    if (p->ncu <= 0 || nhelp >= p->ncu) return 1;
-    const SweepOp op{GS_MODE_CENTERED, p->maxbins, dl, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2]};
-    const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (timing_begin(p, S(stream), &e0, &e1)) return -1;
-#define GS_CF(FF) hipLaunchKernelGGL((k_centered_fused<FF>), dim3((unsigned)nwg), dim3(256), 0, S(stream), p->L,          \
-                                     p->nchains, p->ntile, p->nchunkg, p->rows_per_task,                             \
-                                     p->rows_per_task * (4 / p->sweep_tw), p->sweep_tw, p->tasks, d_alm, s_out, p->partials, slo, shi, p->ita(it), p->chain0, \
-                                     op, nhelp, p->fsync, p->stats, p->maxbins, p->bins, p->meta, dl, trace, cap,      \
-                                     counter, p->graph_adv)
-    if (p->F == 1) GS_CF(1); else if (p->F == 2) GS_CF(2); else GS_CF(3);
-#undef GS_CF
-    GS_LAUNCH_CHECK("k_centered_fused");
-    if (p->timing && record_ev(e1, S(stream))) return -1;
-    return 0;
 }
 
 int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* s_out, uint64_t seed, uint32_t it,
@@ -3046,11 +2868,6 @@ int gs_step_centered_fused(gs_plan* p, const double* d_alm, double* dl, double* 
     if (!p->iter_dev_on) return set_error("gs_step_centered_fused: device iteration counter not enabled");
     if (trace && capacity < 1) return set_error("gs_step_centered_fused: capacity < 1");
     if (!d_alm || !dl) return set_error("gs_step_centered_fused: null argument");
-    {
-        const int rc = centered_fused_launch(p, d_alm, dl, s_out, seed, it, trace, trace ? capacity : 1,
-                                             p->adv_counter(), stream);
-        if (rc <= 0) return rc;
-    }
     bool pre = false;
     if (step_sweep(p, GS_MODE_CENTERED, d_alm, dl, nullptr, seed, it, s_out, stream, true, &pre)) return -1;
     return cls_draw_launch(p, p->stats, nullptr, seed, it, dl, trace, trace ? capacity : 1, p->adv_counter(), stream,
@@ -3066,17 +2883,10 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
     // block parameters here (table) unless the sweep computes them per lane
     const int nbq = p->inkernel_params ? 0 : nblk((long long)p->nchains * (p->L + 1), 256);
     // native mode: the MH accept uniforms are drawn here too (replay draws them on the host)
-    p->u_nat_ready = u_prop == nullptr && p->nacc > 0 && !getenv("GS_MH_INKERNEL_UNIFORMS");
+    p->u_nat_ready = u_prop == nullptr && p->nacc > 0;
     const int nbu = p->u_nat_ready ? nblk((long long)p->nchains * p->nacc, 256) : 0;
-    const bool chained = p->params_chained && p->graph_off > 0;
-    p->params_chained = false;
-    if (chained && p->pro_defer && u_prop == nullptr && nbq > 0) {
-        // block parameters written by the previous step's MH launch; draws deferred
-        p->pro_pending = true;
-        p->pro_dl = dl; p->pro_slo = slo; p->pro_shi = shi; p->pro_it = it;
-        return 0;
-    }
-    if (p->pro_defer && u_prop == nullptr && (nbq > 0 || p->nchains > 4)) {
+    p->snap_ok = false;
+    if (u_prop == nullptr && (nbq > 0 || p->nchains > 4)) {
         // native draws: to the front of this step's sweep (or statistics finish)
         p->pro_pending = true;
         p->pro_dl = dl; p->pro_slo = slo; p->pro_shi = shi; p->pro_it = it;
@@ -3084,7 +2894,7 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
 #define GS_PRQ(FF) hipLaunchKernelGGL((k_nc_prologue<FF>), dim3(nbq), dim3(256), 0, S(stream), 0, nbq, p->u_nat,     \
                                       p->nspec, p->nacc, p->n_iter_mh, p->L, p->nchains, p->maxbins, p->ell2bin, p->bl, \
                                       p->kappa[0], p->kappa[1], p->kappa[2], p->params, p->meta, p->prop_sd, dl,        \
-                                      p->prop, p->logr, u_prop, slo, shi, p->ita(it), p->chain0)
+                                      p->prop, p->logr, u_prop, slo, shi, p->ita(it), p->chain0, nullptr)
         if (p->F == 1) GS_PRQ(1); else if (p->F == 2) GS_PRQ(2); else GS_PRQ(3);
 #undef GS_PRQ
         GS_LAUNCH_CHECK("k_nc_prologue");
@@ -3095,10 +2905,11 @@ int gs_nc_prologue(gs_plan* p, const double* dl, const double* u_prop, uint64_t 
                                       p->u_nat, p->nspec, p->nacc, p->n_iter_mh, p->L,                                  \
                                       p->nchains, p->maxbins, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2], \
                                       p->params, p->meta, p->prop_sd, dl, p->prop, p->logr, u_prop, slo, shi,            \
-                                      p->ita(it), p->chain0)
+                                      p->ita(it), p->chain0, p->dl_tmp)
     if (p->F == 1) GS_PRO(1); else if (p->F == 2) GS_PRO(2); else GS_PRO(3);
 #undef GS_PRO
     GS_LAUNCH_CHECK("k_nc_prologue");
+    p->snap_ok = true;
     return 0;
 }
 
@@ -3135,13 +2946,7 @@ int gs_nc_decide_fused(gs_plan* p, double* dl, uint64_t seed, uint32_t it, int32
     if (trace && capacity < 1) return set_error("gs_nc_decide_fused: capacity < 1");
     if (p->pro_pending) return set_error("gs_nc_decide_fused: the prologue's draws wait for gs_nc_finish");
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    // inside a captured multi-step graph (not its last step) the MH also writes
-    // the next step's block parameters, and that step's prologue launches none
-    // (the MH workgroup needs a thread past its l range for the l below it)
-    const bool spare = p->mh_lmin == 0 || p->L + 1 - p->mh_lmin < MH_REG_THREADS;
-    double* nextp = p->mh_params && p->iter_dev_on && p->graph_adv == 0 && !p->inkernel_params && spare ? p->params
-                                                                                                        : nullptr;
-    const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv, nextp};
+    const MhEpi epi{trace, std::max(capacity, 1), p->adv_counter(), p->nchains, p->graph_adv, nullptr};
     return mh_decide(p, p->stats, dl, p->u_nat_ready ? p->u_nat : nullptr, slo, shi, it, accept_out, stream, &epi);
 }
 
@@ -3199,7 +3004,7 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
     if (stats_to_nc_launch(p, tmp, p->stats, stream, true, seed, it)) return -1;
     // the trace record and the counter advance ride in the MH launch (no kernel
     // after it reads the counter: the re-centring uses D_l only)
-    const MhEpi epi{trace, trace ? capacity : 1, p->adv_counter(), p->nchains, p->graph_adv, nullptr, tmp};
+    const MhEpi epi{trace, trace ? capacity : 1, p->adv_counter(), p->nchains, p->graph_adv, tmp};
     if (mh_decide(p, p->stats, dl, nullptr, slo, shi, it, accept_out, stream, &epi)) return -1;
     if (recentre && s_out) {
         const bool quirk = (p->quirks & GS_QUIRK_ASIS_RECENTRE_CENTERED) != 0;

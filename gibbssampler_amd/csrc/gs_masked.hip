@@ -1678,10 +1678,9 @@ int gs_masked_pcg_solve(gs_masked* c, const double* dl, const double* rhs, doubl
 #undef GS_PI
     hipLaunchKernelGGL(k_pcg_scal<0>, g1, bb, 0, st, nb, c->partial, dst, tol, maxiter);
     GS_LAUNCH_CHECK("k_pcg_init");
-    // the unconverged chains as of the last state read (GS_PCG_COMPACT=0: always all)
+    // the unconverged chains as of the last state read
     int na = B;
-    const char* ce = getenv("GS_PCG_COMPACT");
-    const bool compact = B > 1 && !(ce && atoi(ce) == 0);
+    const bool compact = B > 1;
     auto iteration = [&]() -> int {
         if (pcg_apply(c, dl, c->pp, c->pq, c->partial, nb, dst, st, na, c->pcg_act)) return -1;
 #define GS_PU(FF) hipLaunchKernelGGL((k_pcg_upd<FF>), gb, bb, 0, st, c->L, nb, c->params_pcg, c->pp, c->pq, x, c->pr, \
@@ -1852,7 +1851,7 @@ static int f2_group(const gs_masked* c) {
     const long long nco = c->F == 1 ? 1 : 2;
     const long long per = nco * (2 * gs_sht_phi_plane(c->sht) * 16 + c->npix * 8);
     long long budget = 6LL << 30;
-    if (const char* e = getenv("GS_F2_GROUP_BYTES")) budget = std::max(1LL, atoll(e));
+    if (const char* e = gs_detail::option("GS_F2_GROUP_BYTES")) budget = std::max(1LL, atoll(e));
     return (int)std::max(1LL, std::min<long long>(F2_RMAX - 1, budget / std::max(per, 1LL)));
 }
 
@@ -1868,10 +1867,65 @@ static long long f2_chain_bytes(const gs_masked* c, int kcap) {
            (long long)(kcap + 1) * (kcap + 1) * 8 + n * 8 + (long long)c->F * c->NR * 8;
 }
 
+// the budget is also capped at 3/4 of what the device can give the workspace
+// (its free memory plus the f2 buffers this context holds, which are freed
+// before the new ones are allocated), so a batch on a smaller or shared GPU
+// runs in more passes instead of failing its allocation
 static int f2_chains_per_pass(const gs_masked* c, int kcap) {
     long long budget = 64LL << 30;
-    if (const char* e = getenv("GS_F2_BATCH_BYTES")) budget = std::max(1LL, atoll(e));
+    if (const char* e = gs_detail::option("GS_F2_BATCH_BYTES")) budget = std::max(1LL, atoll(e));
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+        const long long held = c->f2_cap > 0 ? (long long)c->f2_nb * f2_chain_bytes(c, c->f2_cap) : 0;
+        budget = std::min(budget, ((long long)fr + held) / 4 * 3);
+    } else {
+        (void)hipGetLastError();
+    }
     return (int)std::max(1LL, std::min<long long>(c->B, budget / std::max(1LL, f2_chain_bytes(c, kcap))));
+}
+
+static void f2_release(gs_masked* c) {
+    double* bufs[] = {c->f2_Y, c->f2_phib, c->f2_part, c->f2_G, c->f2_taken, c->f2_da, c->f2_r};
+    for (double* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->f2_lmaxb) (void)hipFree(c->f2_lmaxb);
+    c->f2_Y = c->f2_phib = c->f2_part = c->f2_G = c->f2_taken = c->f2_da = c->f2_r = nullptr;
+    c->f2_lmaxb = nullptr;
+    c->f2_cap = 0;
+    c->f2_nb = 0;
+}
+
+// the f2 workspace for NB chains of kcap blocks; on an allocation failure the
+// chains per pass are halved (down to 1) instead of failing the sweep.
+// Returns the chains per pass, or -1 when even one chain does not fit.
+static int f2_reserve(gs_masked* c, int kcap, int NB) {
+    if (c->f2_cap >= kcap && c->f2_nb >= NB) return c->f2_nb;
+    const int F = c->F, nco = F == 1 ? 1 : 2;
+    const long long n = (long long)F * c->npix;
+    const long long nchunk = (n + F2_CHUNK - 1) / F2_CHUNK;
+    const int nb4max = (kcap + 1 + 3) / 4;
+    for (;;) {
+        f2_release(c);
+        const size_t nb = (size_t)NB;
+        int rc = 0;
+        rc |= mc_alloc(&c->f2_Y, nb * kcap * n);
+        rc |= mc_alloc(&c->f2_phib, nb * kcap * nco * 2 * gs_sht_phi_plane(c->sht) * 2);
+        rc |= mc_alloc(&c->f2_part, nb * nchunk * (nb4max * (nb4max + 1) / 2) * 16);
+        rc |= mc_alloc(&c->f2_G, nb * (kcap + 1) * (kcap + 1));
+        rc |= mc_alloc(&c->f2_taken, nb * kcap);
+        rc |= mc_alloc(&c->f2_da, nb * F * c->NR);
+        rc |= mc_alloc(&c->f2_r, nb * n);
+        rc |= mc_alloc(&c->f2_lmaxb, nb * kcap);
+        if (!rc) {
+            c->f2_cap = kcap;
+            c->f2_nb = NB;
+            return NB;
+        }
+        (void)hipGetLastError();
+        f2_release(c);
+        if (NB == 1) return -1;
+        NB = (NB + 1) / 2;
+    }
 }
 
 // one pass over nb chains (pointers at the pass's first chain; chain-0-relative
@@ -1961,36 +2015,11 @@ int gs_masked_pixel_mh(gs_masked* c, int K, int n_iter, int maxbins, const int* 
         !prop_binned || !binned || !accept_out)
         return set_error("gs_masked_pixel_mh: null argument");
     const hipStream_t st = S(stream);
-    const int F = c->F, nco = F == 1 ? 1 : 2;
+    const int F = c->F;
     const int KG = f2_group(c);
     const int kcap = std::min(K, KG);
-    const long long n = (long long)F * c->npix;
-    const long long nchunk = (n + F2_CHUNK - 1) / F2_CHUNK;
-    const int nb4max = (kcap + 1 + 3) / 4;
-    const int NB = f2_chains_per_pass(c, kcap);
-    if (c->f2_cap < kcap || c->f2_nb < NB) {
-        double* bufs[] = {c->f2_Y, c->f2_phib, c->f2_part, c->f2_G, c->f2_taken, c->f2_da, c->f2_r};
-        for (double* b : bufs)
-            if (b) (void)hipFree(b);
-        if (c->f2_lmaxb) (void)hipFree(c->f2_lmaxb);
-        c->f2_Y = c->f2_phib = c->f2_part = c->f2_G = c->f2_taken = c->f2_da = c->f2_r = nullptr;
-        c->f2_lmaxb = nullptr;
-        c->f2_cap = 0;
-        c->f2_nb = 0;
-        const size_t nb = (size_t)NB;
-        int rc = 0;
-        rc |= mc_alloc(&c->f2_Y, nb * kcap * n);
-        rc |= mc_alloc(&c->f2_phib, nb * kcap * nco * 2 * gs_sht_phi_plane(c->sht) * 2);
-        rc |= mc_alloc(&c->f2_part, nb * nchunk * (nb4max * (nb4max + 1) / 2) * 16);
-        rc |= mc_alloc(&c->f2_G, nb * (kcap + 1) * (kcap + 1));
-        rc |= mc_alloc(&c->f2_taken, nb * kcap);
-        rc |= mc_alloc(&c->f2_da, nb * F * c->NR);
-        rc |= mc_alloc(&c->f2_r, nb * n);
-        rc |= mc_alloc(&c->f2_lmaxb, nb * kcap);
-        if (rc) return -1;
-        c->f2_cap = kcap;
-        c->f2_nb = NB;
-    }
+    const int NB = f2_reserve(c, kcap, f2_chains_per_pass(c, kcap));
+    if (NB < 1) return set_error("gs_masked_pixel_mh: the f2 workspace of one chain does not fit in device memory");
     if (!c->f2_blk && mc_alloc(&c->f2_blk, (size_t)F * (c->L + 1))) return -1;
     const long long dls = (long long)F * (c->L + 1), bins = (long long)F * maxbins, acc = (long long)K * n_iter;
     for (int b = 0; b < c->B; b += NB) {

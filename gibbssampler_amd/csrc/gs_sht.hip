@@ -3477,7 +3477,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     if (nside < 1 || nside > 8192 || (nside & (nside - 1))) return set_error("gs_sht_create: nside must be a power of two <= 8192");
     if (lmax < 0 || lmax > 4 * nside) return set_error("gs_sht_create: lmax out of range (0..4 nside)");
     gs_sht* p = new gs_sht();
-    if (const char* e = std::getenv("GS_SHT_LDS_FFT_MAX")) {
+    if (const char* e = gs_detail::option("GS_SHT_LDS_FFT_MAX")) {
         const int v = std::atoi(e);
         if (v >= 16 && v <= LDS_FFT_MAX && (v & (v - 1)) == 0) p->lds_fft_max = v;
     }
@@ -3496,7 +3496,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
             sr = 1; paired = 0;
             for (auto o : opts)
                 if (waves(o.first, o.second) >= 4096) { sr = o.first; paired = o.second; break; }
-            if (const char* e = std::getenv(env)) {
+            if (const char* e = gs_detail::option(env)) {
                 int a = 0, b = 0;
                 if (std::sscanf(e, "%d,%d", &a, &b) == 2) { sr = a; paired = b ? 1 : 0; }
             }
@@ -3519,7 +3519,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     // 32-l granularity.  GS_SHT_SEG (0 = off) / GS_SHT_ANA set one segment length
     // and one analysis shape for every launch (tests)
     {
-        const char* e = std::getenv("GS_SHT_SEG");
+        const char* e = gs_detail::option("GS_SHT_SEG");
         const bool small = p->ana_sr == 1 && !p->ana_paired;
         int sg = small ? 64 : 0;
         if (e) sg = std::atoi(e);
@@ -3530,7 +3530,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         p->seg = sg >= L + 1 ? 0 : sg;
         p->syn_seg = p->seg;
         for (int nc = 1; nc <= 3; ++nc) { p->ana_sr_nc[nc] = p->ana_sr; p->ana_seg_nc[nc] = p->seg; }
-        if (small && !e && !std::getenv("GS_SHT_ANA") && p->seg == 64) {
+        if (small && !e && !gs_detail::option("GS_SHT_ANA") && p->seg == 64) {
             p->seg = 32;
             for (int nc = 1; nc <= 2; ++nc) { p->ana_sr_nc[nc] = 2; p->ana_seg_nc[nc] = 32; }
         }
@@ -3667,7 +3667,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         // (GS_SHT_MERGE_RINGS=0/1 forces it off/on where legal)
         const int mmax = Ms.empty() ? 0 : Ms.back();
         bool merge = mmax <= 2048 && mmax <= p->lds_fft_max && p->nsplit == 0;
-        if (const char* e = std::getenv("GS_SHT_MERGE_RINGS")) merge = std::atoi(e) != 0 && mmax <= p->lds_fft_max && p->nsplit == 0;
+        if (const char* e = gs_detail::option("GS_SHT_MERGE_RINGS")) merge = std::atoi(e) != 0 && mmax <= p->lds_fft_max && p->nsplit == 0;
         if (merge && Ms.size() > 1) {
             std::vector<int> all(p->npair);
             for (int r = 0; r < p->npair; ++r) all[r] = r;
@@ -3739,10 +3739,9 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         sht_free(p);
         return set_error(std::string("gs_sht_create: setup kernels failed: ") + hipGetErrorString(e));
     }
-    if (!getenv("GS_SHT_NO_SIDE_STREAM") &&
-        (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
-         hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess)) {
+    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess) {
         sht_free(p);
         return set_error("gs_sht_create: side stream / events");
     }
@@ -3829,11 +3828,8 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
 // the LDS (NCB buffers of the longest FFT + its twiddles) and by 1024 threads
 // at ring_block(M) threads (<= 8 values each) per component
 static int ring_mc_ncb(int M, int ncomp) {
-    static const int want = [] {
-        const char* e = getenv("GS_SHT_RING_NC");
-        return e ? std::max(1, atoi(e)) : 2;
-    }();
-    int ncb = std::min(want, ncomp);
+    // (2, 3, 4 measured: 2 is the fastest for the operator, synthesis and analysis)
+    int ncb = std::min(2, ncomp);
     ncb = std::min(ncb, 1024 / ring_block(M));
     const int SB = std::max(M, 4 * ring_block(M));
     while (ncb > 1 && (size_t)(ncb * SB + M / 2) * sizeof(double2) > (size_t)RING_MC_LDS_MAX) --ncb;
@@ -3963,21 +3959,11 @@ static int sht_reserve(gs_sht* p, int nmap, hipStream_t st) {
 // ---- the matrix-core Legendre stage (plans with mf set) --------------------------
 constexpr int MF_CGW = 4;         // 16-column groups per workgroup (16 maps spin 2, 32 spin 0)
 
-// launch shapes (speed only; every shape gives the same bits): column groups
-// per wave in the synthesis (GS_SHT_MFS_CPW 4 / 2) and the analysis
-// (GS_SHT_MFA_CPW 4 / 2), analysis workgroup size (GS_SHT_MFA_NT 256 / 512).
-// Measured (N_side 256, 16 spin-2 maps, rocprofv3 averages, XCD-aware
-// orders): synthesis CPW 4 / 2 = 550 / 598 us; analysis (CPW, NT) (4, 256) /
-// (4, 512) / (2, 512) = 737 / 825 / 1040 us
-static int mf_env(const char* name, int a, int b, int dflt) {
-    const char* e = getenv(name);
-    if (!e) return dflt;
-    const int v = atoi(e);
-    return v == a || v == b ? v : dflt;
-}
-static int mfs_cpw() { static const int v = mf_env("GS_SHT_MFS_CPW", 2, 4, 4); return v; }
-static int mfa_cpw() { static const int v = mf_env("GS_SHT_MFA_CPW", 2, 4, 4); return v; }
-static int mfa_nt() { static const int v = mf_env("GS_SHT_MFA_NT", 256, 512, 256); return v; }
+// launch shapes: 4 column groups per wave in both table kernels and 256-thread
+// analysis workgroups.  Measured (N_side 256, 16 spin-2 maps, rocprofv3
+// averages, XCD-aware orders): synthesis CPW 4 / 2 = 550 / 598 us; analysis
+// (CPW, NT) (4, 256) / (4, 512) / (2, 512) = 737 / 825 / 1040 us
+constexpr int MFS_CPW = 4, MFA_CPW = 4, MFA_NT = 256;
 
 extern "C++" {
 template <int CPW, bool RIN>
@@ -4031,41 +4017,29 @@ static void sht_anal_mfma_v(gs_sht* p, int nmap, int ncomp, int layout, int acc,
 // instead of the plan's ain (filled by k_sht_alm_in)
 static int sht_synth_mfma(gs_sht* p, int nmap, int ncomp, hipStream_t st, const int* pflag = nullptr,
                           const double* areal = nullptr, const double* bl = nullptr) {
-    const bool two = mfs_cpw() == 2;
-    if (areal) {
-        if (two) sht_synth_mfma_r<2, true>(p, nmap, ncomp, st, pflag, areal, bl);
-        else sht_synth_mfma_r<4, true>(p, nmap, ncomp, st, pflag, areal, bl);
-    } else {
-        if (two) sht_synth_mfma_r<2, false>(p, nmap, ncomp, st, pflag, nullptr, nullptr);
-        else sht_synth_mfma_r<4, false>(p, nmap, ncomp, st, pflag, nullptr, nullptr);
-    }
+    if (areal) sht_synth_mfma_r<MFS_CPW, true>(p, nmap, ncomp, st, pflag, areal, bl);
+    else sht_synth_mfma_r<MFS_CPW, false>(p, nmap, ncomp, st, pflag, nullptr, nullptr);
     GS_LAUNCH_CHECK("k_sht_synth_mfma");
     return 0;
 }
 
 static int sht_anal_mfma(gs_sht* p, int nmap, int ncomp, int layout, int acc, double* alm, hipStream_t st,
                          const int* pflag = nullptr) {
-    const int cpw = mfa_cpw(), nt = mfa_nt();
-    if (cpw == 2 && nt == 512) sht_anal_mfma_v<2, 512>(p, nmap, ncomp, layout, acc, alm, st, pflag);
-    else if (cpw == 2) sht_anal_mfma_v<2, 256>(p, nmap, ncomp, layout, acc, alm, st, pflag);
-    else if (nt == 512) sht_anal_mfma_v<4, 512>(p, nmap, ncomp, layout, acc, alm, st, pflag);
-    else sht_anal_mfma_v<4, 256>(p, nmap, ncomp, layout, acc, alm, st, pflag);
+    sht_anal_mfma_v<MFA_CPW, MFA_NT>(p, nmap, ncomp, layout, acc, alm, st, pflag);
     GS_LAUNCH_CHECK("k_sht_anal_mfma");
     return 0;
 }
 
 // the ring-pair support flags of a weighted analysis on the table path, or
-// nullptr: no skipping (GS_SHT_SUPPORT_SKIP=0, or more tiles than the
-// analysis' list holds)
+// nullptr: no skipping (more tiles than the analysis' list holds)
 // (the registered weights' classes when wts is the registered array: computed
 // once; otherwise k_pair_support for this call)
 // *out = nullptr: no skipping.  A failed launch is an error (the sticky error
 // is reported, not cleared).
 static int sht_support(gs_sht* p, const double* wts, int wnc, hipStream_t st, const int** out) {
-    static const bool on = [] { const char* e = getenv("GS_SHT_SUPPORT_SKIP"); return !e || atoi(e) != 0; }();
     *out = nullptr;
     const int nt = (p->npair + 15) / 16;
-    if (!on || !p->mf || !wts || nt > MF_TL_MAX || nt != p->mf_ntile) return 0;
+    if (!p->mf || !wts || nt > MF_TL_MAX || nt != p->mf_ntile) return 0;
     if (wts == p->wreg && wnc == p->wreg_nc && p->wsup) { *out = p->wsup; return 0; }
     hipLaunchKernelGGL(k_pair_support, dim3(p->npair), dim3(256), 0, st, p->npix, p->geom, wts, wnc, p->support);
     GS_LAUNCH_CHECK("k_pair_support");
@@ -4076,7 +4050,7 @@ static int sht_support(gs_sht* p, const double* wts, int wnc, hipStream_t st, co
 // the registered ring constants for these weights (nullptr: not registered, or
 // the constant-ring forms turned off by GS_SHT_CONST_RINGS=0)
 static bool const_rings_on() {                     // read per call: tests A/B it in one process
-    const char* e = getenv("GS_SHT_CONST_RINGS");
+    const char* e = gs_detail::option("GS_SHT_CONST_RINGS");
     return !e || atoi(e) != 0;
 }
 static const double2* sht_wconst(const gs_sht* p, const double* wts, int wnc) {
@@ -4268,7 +4242,7 @@ int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real,
     }
     if (nmap > 1 && sht_reserve(p, nmap, S(stream))) return -1;
     double2* ph = reinterpret_cast<double2*>(phib);
-    const char* bme = getenv("GS_SHT_BLOCKS_MFMA");
+    const char* bme = gs_detail::option("GS_SHT_BLOCKS_MFMA");
     if (p->mf && nfield == 2 && !(bme && atoi(bme) == 0)) {
         // the tables: every chain of the batch in one matrix-core launch (both
         // fields' passes; grid tile x phase block x (chain group, field))
@@ -4290,7 +4264,7 @@ int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real,
     // staged variant when m = 0's coefficients, a_lm and block indices fit 64 KB
     // of LDS (GS_SHT_BLK_STAGE=0 turns it off: tests)
     const size_t stg = (size_t)(p->L + 1) * (4 * sizeof(double2) + nfield * (sizeof(double2) + sizeof(int)));
-    const char* stg_env = getenv("GS_SHT_BLK_STAGE");
+    const char* stg_env = gs_detail::option("GS_SHT_BLK_STAGE");
     const bool stage_off = stg_env && atoi(stg_env) == 0;
     const bool use_stg = stg <= 64 * 1024 && !stage_off;
 #define GS_SB(NF, SR) do { if (use_stg) hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR, true>), grid, dim3(LEG_BLOCK), \
@@ -4430,7 +4404,7 @@ int gs_sht_set_mfma(gs_sht* p, int on) {
         // (0.54 GB at N_side 256 / l_max 512, 4.3 GB at N_side 512 / l_max
         // 1024); budget GS_SHT_MFMA_MAX_GB (default 16 GB)
         double gb = 16.0;
-        if (const char* e = std::getenv("GS_SHT_MFMA_MAX_GB")) gb = std::atof(e);
+        if (const char* e = gs_detail::option("GS_SHT_MFMA_MAX_GB")) gb = std::atof(e);
         const double need = 8.0 * (double)p->npair * (double)p->nlm / 1e9;
         if (need > gb) return set_error("gs_sht_set_mfma: the Legendre table exceeds GS_SHT_MFMA_MAX_GB");
     }
@@ -4465,7 +4439,7 @@ int gs_sht_apply_weighted_batch(gs_sht* p, int nmap, int ncomp, const double* al
         return set_error("gs_sht_apply_weighted_batch: bad argument");
     const int M = p->merged_M;
     const int ncb = (p->mf && p->merged_n > 0) ? ring_mc_ncb(M, nmap * ncomp) : 1;
-    if (ncb < 2 || std::getenv("GS_SHT_NO_FUSED_APPLY")) {
+    if (ncb < 2) {
         if (!maps_scratch) return set_error("gs_sht_apply_weighted_batch: this plan needs maps_scratch");
         if (sht_alm2map(p, nmap, ncomp, GS_ALM_REAL, alm_in, bl, maps_scratch, stream)) return -1;
         return gs_sht_map2alm_batch(p, nmap, ncomp, GS_ALM_REAL, maps_scratch, weights, alm_out, 0, stream);
@@ -4500,7 +4474,7 @@ int gs_sht_aux_pass_batch(gs_sht* p, int nmap, int ncomp, const double* alm_in, 
     if (check_sht(p)) return -1;
     if (ncomp < 1 || ncomp > 3 || nmap < 1 || !alm_in || !aux || !alm_out)
         return set_error("gs_sht_aux_pass_batch: bad argument");
-    const char* fe = std::getenv("GS_SHT_FUSED_AUX");
+    const char* fe = gs_detail::option("GS_SHT_FUSED_AUX");
     const int M = p->merged_M;
     const int ncb = (p->mf && p->merged_n > 0) ? ring_mc_ncb(M, nmap * ncomp) : 1;
     if (ncb < 2 || (fe && std::atoi(fe) == 0)) return 1;

@@ -92,6 +92,23 @@ typedef struct gs_model_desc {
 int gs_abi_version(void);
 const char* gs_last_error(void);
 
+/* Library options: named settings read when a plan, SHT or masked context is
+ * created (the library reads no environment variables).  Speed-only shape
+ * selectors (every value gives the same bits) and the variant switches the
+ * bit-identity tests compare, plus the f2 / table workspace budgets:
+ *   GS_SWEEP_TW          1 | 2 | 4  CR-sweep workgroup shape (tiles x chunks;
+ *                                   2 suits --skymap store, 1 the default)
+ *   GS_SWEEP_THROUGHPUT  1          few-chain plans use the throughput form
+ *   GS_MH_SPLIT          0 | 1      NC MH in one / two workgroups per chain
+ *   GS_CLS_PRE, GS_CLS_PRE_MANY  0 | 1  C_l-draw variates inside the sweep
+ *   GS_F2_GROUP_BYTES, GS_F2_BATCH_BYTES  f2 workspace budgets (bytes)
+ *   GS_SHT_LDS_FFT_MAX, GS_SHT_SEG, GS_SHT_SYN, GS_SHT_ANA, GS_SHT_MERGE_RINGS,
+ *   GS_SHT_CONST_RINGS, GS_SHT_BLOCKS_MFMA, GS_SHT_BLK_STAGE, GS_SHT_FUSED_AUX,
+ *   GS_SHT_MFMA_MAX_GB   SHT launch shapes / paths (gs_sht.hip documents each)
+ * gs_option_set(name, NULL) unsets; an unknown name is an error. */
+int gs_option_set(const char* name, const char* value);
+const char* gs_option_get(const char* name);   /* NULL when unset or unknown */
+
 int gs_plan_create(const gs_model_desc* desc, gs_plan** out);
 int gs_plan_destroy(gs_plan* plan);
 /* query sizes of the plan's layouts */

@@ -184,9 +184,9 @@ def main():
     ap.add_argument("--nside", type=int, default=512)
     ap.add_argument("--fields", type=int, default=3)
     ap.add_argument("--budget", type=float, default=10.0)
-    ap.add_argument("--cores", type=int, default=0, help="0: the process's CPU affinity, at most 16")
+    ap.add_argument("--cores", type=int, default=0, help="0: the process's CPU affinity, at most 32 (one GPU's share of a 256-core 8-GPU node)")
     a = ap.parse_args()
-    cores = a.cores or min(len(os.sched_getaffinity(0)), 16)
+    cores = a.cores or min(len(os.sched_getaffinity(0)), 32)
     out = {"cores": cores, "affinity": len(os.sched_getaffinity(0))}
     for key, matched in (("reference", False), ("matched", True)):
         rate, n, dt = run_parallel(a.lmax, a.nside, a.fields, a.budget, cores, matched)

@@ -3,8 +3,8 @@ INFRASTRUCTURE: only bench.py's cpu_baseline leg runs it, as a child process).
 
 The reference's masked samplers restated by oracle/masked.py, with the
 transforms by oracle/sht_cpu.cpp (C++/OpenMP HEALPix SHT, the stand-in for
-healpy's libsharp, which is absent offline), on min(CPU affinity, 16) threads
-(16 = the GPU box's CPU share per GPU).  One chain, numpy's RNG (the draws'
+healpy's libsharp, which is absent offline), on min(CPU affinity, 32) threads
+(32 = one GPU's share of the 8-GPU node's 256 cores).  One chain, numpy's RNG (the draws'
 source does not change the work).  The reference's per-call work structure is
 kept: the pixel-domain MH scores every Metropolis block with a full synthesis
 (NonCenteredGibbs.py:333-355, 401-445), the over-relaxation runs its 1 + 3 n_gibbs

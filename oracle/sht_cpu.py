@@ -42,8 +42,9 @@ def _load():
 
 
 def threads():
-    """the worker count: min(CPU affinity, 16) -- 16 = the GPU box's CPU share per GPU"""
-    return max(1, min(len(os.sched_getaffinity(0)), 16))
+    """the worker count: min(CPU affinity, 32) -- 32 = one GPU's fair share of the
+    8-GPU node's 256 cores"""
+    return max(1, min(len(os.sched_getaffinity(0)), 32))
 
 
 def nlm(lmax):

@@ -111,3 +111,20 @@ def test_create_rejects_bad_sizes(lib):
     assert b"lmax" in lib2.gs_last_error()
     assert lib2.gs_masked_create(None, None, None, ctypes.byref(out)) == -1
     assert not out.value
+
+
+def test_library_options_registry():
+    """gs_option_set / gs_option_get (the library reads no environment
+    variables): a registered name round-trips and unsets; an unknown name is an
+    error with a message, not a silent no-op."""
+    _capi.load()
+    assert _capi.get_option("GS_SWEEP_TW") is None
+    with _capi.options(GS_SWEEP_TW=2):
+        assert _capi.get_option("GS_SWEEP_TW") == "2"
+    assert _capi.get_option("GS_SWEEP_TW") is None
+    with pytest.raises(_capi.GibbsHipError, match="unknown option"):
+        _capi.set_option("GS_NO_SUCH_KNOB", 1)
+    assert _capi.get_option("GS_NO_SUCH_KNOB") is None
+    src = "".join(open(os.path.join(ROOT, "gibbssampler_amd", "csrc", f)).read()
+                  for f in os.listdir(os.path.join(ROOT, "gibbssampler_amd", "csrc")))
+    assert "getenv" not in src

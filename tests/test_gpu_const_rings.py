@@ -56,7 +56,7 @@ def _spec(F):
 
 @pytest.mark.parametrize("maskkind", ["band", "galactic"])
 @pytest.mark.parametrize("F", [2, 3])
-def test_operator_vs_oracle_and_pixel_route(monkeypatch, maskkind, F):
+def test_operator_vs_oracle_and_pixel_route(gsopt, maskkind, F):
     """Q x (the fused operator on tables, constant-ring shortcut) against the
     oracle's pcg_operator and against the pixel route of the same context."""
     import torch
@@ -70,7 +70,7 @@ def test_operator_vs_oracle_and_pixel_route(monkeypatch, maskkind, F):
     want = MK.pcg_operator(mm, dlu, x)
     for k in range(F):
         _close(got[k], want[k], rtol=1e-10)
-    monkeypatch.setenv("GS_SHT_CONST_RINGS", "0")
+    gsopt.setenv("GS_SHT_CONST_RINGS", "0")
     pix = cr.pcg_apply(dl_t, x_t).cpu().numpy()
     np.testing.assert_allclose(got, pix, rtol=1e-12, atol=1e-14 * np.abs(pix).max())
     assert not np.array_equal(got, pix)            # the shortcut did run (rounding differs)
@@ -107,14 +107,14 @@ def _mh_model(mm, L, N, bl, bins, blocks, pv):
 
 @pytest.mark.parametrize("sht_mode", ["recurrence", "mfma"])
 @pytest.mark.parametrize("maskkind,group", [("band", None), ("galactic", None), ("galactic", "1")])
-def test_pixel_mh_parseval_vs_oracle(monkeypatch, maskkind, group, sht_mode):
+def test_pixel_mh_parseval_vs_oracle(gsopt, maskkind, group, sht_mode):
     """one f2 sweep (native streams) with the Parseval rows against the oracle's
     full-map likelihood per block, and equal to the pixel route's decisions;
     group "1": one block per Gram group (the residual carried between groups
     in the mixed coordinates)."""
     from gibbssampler_amd.masked import PixelMH
     if group is not None:
-        monkeypatch.setenv("GS_F2_GROUP_BYTES", group)
+        gsopt.setenv("GS_F2_GROUP_BYTES", group)
     N, L = 16, 32
     cr, mm, dl, s0 = _cr(N, L, maskkind, gibbs_cr=False, ula=False, rng="native", seed=77, chain=3,
                          sht_mode=sht_mode)
@@ -131,7 +131,7 @@ def test_pixel_mh_parseval_vs_oracle(monkeypatch, maskkind, group, sht_mode):
     assert acc == wacc
     n_acc = sum(int(np.sum(v)) for v in acc.values())
     assert 0 < n_acc < mh.K                          # both decision branches
-    monkeypatch.setenv("GS_SHT_CONST_RINGS", "0")
+    gsopt.setenv("GS_SHT_CONST_RINGS", "0")
     new0, acc0 = mh.sample(snc, init, iteration=5)
     assert acc0 == acc
     for sp in ("EE", "BB"):

@@ -218,7 +218,7 @@ def test_asis_skymap_without_quirk(F):
 
 @pytest.mark.parametrize("kind,F", [("centered", 1), ("centered", 2), ("centered", 3), ("noncentered", 2),
                                     ("noncentered", 3), ("asis", 3)])
-def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
+def test_sweep_latency_form_bit_identical(gsopt, kind, F):
     """Plans of <= 4 chains with <= 4 rows per task (257 <= L <= 512) run the
     latency form of the sweep (every load issued first); it must give the same
     bits as the throughput form (GS_SWEEP_THROUGHPUT=1 at plan creation): same
@@ -230,9 +230,9 @@ def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
 
     def run(env, graph):
         if env:
-            monkeypatch.setenv("GS_SWEEP_THROUGHPUT", "1")
+            gsopt.setenv("GS_SWEEP_THROUGHPUT", "1")
         else:
-            monkeypatch.delenv("GS_SWEEP_THROUGHPUT", raising=False)
+            gsopt.delenv("GS_SWEEP_THROUGHPUT", raising=False)
         r = BatchedRunner(kind, P["lmax"], P["nside"], F, 2, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
                           blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=17)
         assert r.plan.rows_per_task == 4
@@ -251,61 +251,50 @@ def test_sweep_latency_form_bit_identical(monkeypatch, kind, F):
             np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("F", [1, 2, 3])
-def test_nc_deferred_draws_and_chained_params_bit_identical(monkeypatch, F):
-    """Many-chain NC steps: the MH proposals and accept uniforms drawn by extra
-    workgroups at the front of the CR sweep (default) or of the statistics
-    finish (GS_NC_PRO_SWEEP=0) instead of the prologue, and optionally
-    (GS_NC_MH_PARAMS=1) the next step's block parameters written by the MH
-    launch inside a captured multi-step graph (no prologue launch after step 0)
-    -- against GS_NC_PRO_DEFER=0 at plan creation: D_l, accept flags and the
-    trace over 5 native steps, eager and as one captured 5-step graph replayed
-    twice."""
+@pytest.mark.parametrize("graph", [False, True])
+def test_mh_split_non_psd_start_bit_identical(gsopt, graph):
+    """the split NC MH (T / E workgroup and BB workgroup per chain)
+    from a start whose TE block is NOT positive definite in some bins.  The BB
+    blocks' acceptance depends on the PSD test of the T / E state, and the T / E
+    workgroup writes its decisions into dl; both workgroups therefore read the
+    snapshot the proposal launch wrote, and the result must equal the one-
+    workgroup MH (GS_MH_SPLIT=0) whatever order the two workgroups run in: D_l
+    and accept flags over 4 native steps at configs[2]-like 32 chains, L 256."""
     import torch
     from gibbssampler_amd.problem import synthetic_problem
     from gibbssampler_amd.samplers import BatchedRunner
-    P = synthetic_problem(64, 32, F, seed=13)
-    keys = ("GS_NC_PRO_DEFER", "GS_NC_PRO_SWEEP", "GS_NC_MH_PARAMS")
+    P = synthetic_problem(256, 128, 3, seed=31)
+    nch = 32
+    start = {k: np.array(v, dtype=np.float64) for k, v in P["dls_init"].items()}
+    bad = np.arange(2, len(start["TE"]), 3)
+    start["TE"][bad] = 2.0 * np.sqrt(start["TT"][bad] * start["EE"][bad]) + 1.0     # TE^2 > TT EE
 
-    def run(env, graph):
-        for k in keys:
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        r = BatchedRunner("noncentered", P["lmax"], P["nside"], F, 8, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
-                          blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=23,
-                          chain0=1)
-        r.init(P["dls_init"])
+    def run(split):
+        gsopt.setenv("GS_MH_SPLIT", "1" if split else "0")
+        r = BatchedRunner("noncentered", P["lmax"], P["nside"], 3, nch, P["bl"], P["noise_var"], P["bins"],
+                          P["d_alm"], blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native",
+                          seed=47, chain0=0, store_skymap=False)
+        r.init(start)
         out = []
         if graph:
-            trace = r.plan.zeros(5, 8, r.plan.nspec, r.plan.maxbins)
-            acc = r.plan.zeros(5, 8, max(r.plan.nacc, 1), dtype=torch.int32)
-            r.capture_steps(5, trace=trace, trace_capacity=5, accept_trace=acc)
-            for _ in range(2):
-                r.step()
-                out += [trace.cpu().numpy(), acc.cpu().numpy()]
+            trace = r.plan.zeros(4, nch, r.plan.nspec, r.plan.maxbins)
+            acc = r.plan.zeros(4, nch, max(r.plan.nacc, 1), dtype=torch.int32)
+            r.capture_steps(4, trace=trace, trace_capacity=4, accept_trace=acc)
+            r.step()
+            out += [trace.cpu().numpy(), acc.cpu().numpy()]
         else:
-            for _ in range(10):
+            for _ in range(4):
                 r.step()
                 out += [r.dl.cpu().numpy(), r.accept.cpu().numpy()]
-        out.append(r.dl.cpu().numpy())
         return out
 
-    variants = [{"GS_NC_PRO_DEFER": "1"}, {"GS_NC_PRO_DEFER": "1", "GS_NC_PRO_SWEEP": "0"},
-                {"GS_NC_PRO_DEFER": "1", "GS_NC_MH_PARAMS": "1"},
-                {"GS_NC_PRO_DEFER": "1", "GS_NC_PRO_SWEEP": "0", "GS_NC_MH_PARAMS": "1"}]
-    for graph in (False, True):
-        want = run({"GS_NC_PRO_DEFER": "0"}, graph)
-        for env in variants:
-            got = run(env, graph)
-            for x, y in zip(got, want):
-                np.testing.assert_array_equal(x, y, err_msg=f"{env} graph={graph}")
-    for k in keys:
-        monkeypatch.delenv(k, raising=False)
+    a, b = run(True), run(False)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
 
 
 @pytest.mark.parametrize("F,nch", [(3, 1), (2, 2), (1, 4)])
-def test_centered_predrawn_variates_bit_identical(monkeypatch, F, nch):
+def test_centered_predrawn_variates_bit_identical(gsopt, F, nch):
     """Few-chain centered steps draw the C_l variates in extra workgroups of the
     sweep, and the draw after the statistics reads them (GS_CLS_PRE=0 at plan
     creation: the draw computes them itself).  Same bits: maps, D_l and the
@@ -316,7 +305,7 @@ def test_centered_predrawn_variates_bit_identical(monkeypatch, F, nch):
     P = synthetic_problem(512, 128, F, seed=9)
 
     def run(pre, graph):
-        monkeypatch.setenv("GS_CLS_PRE", "1" if pre else "0")
+        gsopt.setenv("GS_CLS_PRE", "1" if pre else "0")
         r = BatchedRunner("centered", P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
                           rng="native", seed=29, chain0=3)
         r.init(P["dls_init"])
@@ -337,11 +326,11 @@ def test_centered_predrawn_variates_bit_identical(monkeypatch, F, nch):
         a, b = run(True, graph), run(False, graph)
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
-    monkeypatch.delenv("GS_CLS_PRE", raising=False)
+    gsopt.delenv("GS_CLS_PRE", raising=False)
 
 
 @pytest.mark.parametrize("kind,F", [("centered", 3), ("centered", 2), ("asis", 3), ("asis", 1)])
-def test_many_chain_predrawn_variates_bit_identical(monkeypatch, kind, F):
+def test_many_chain_predrawn_variates_bit_identical(gsopt, kind, F):
     """Many-chain centered / ASIS steps draw the C_l variates in front workgroups
     of the CR sweep and the draw reads them (GS_CLS_PRE_MANY=0 at plan creation:
     the draw computes them itself); the ASIS step also runs its MH proposals in
@@ -356,7 +345,7 @@ def test_many_chain_predrawn_variates_bit_identical(monkeypatch, kind, F):
     nch = 8
 
     def run(pre, graph):
-        monkeypatch.setenv("GS_CLS_PRE_MANY", "1" if pre else "0")
+        gsopt.setenv("GS_CLS_PRE_MANY", "1" if pre else "0")
         r = BatchedRunner(kind, P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
                           blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=41,
                           chain0=5)
@@ -379,12 +368,12 @@ def test_many_chain_predrawn_variates_bit_identical(monkeypatch, kind, F):
         a, b = run(True, graph), run(False, graph)
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
-    monkeypatch.delenv("GS_CLS_PRE_MANY", raising=False)
+    gsopt.delenv("GS_CLS_PRE_MANY", raising=False)
 
 
 @pytest.mark.parametrize("kind,F,L", [("noncentered", 3, 1024), ("noncentered", 2, 512), ("asis", 3, 512),
                                       ("noncentered", 3, 64)])
-def test_mh_split_bit_identical(monkeypatch, kind, F, L):
+def test_mh_split_bit_identical(gsopt, kind, F, L):
     """The MH decided by two workgroups per chain (T / E phases and the BB
     blocks, which share no likelihood term) against one workgroup per chain
     (GS_MH_SPLIT=0 at plan creation): D_l, accept flags and the trace over 4
@@ -396,7 +385,7 @@ def test_mh_split_bit_identical(monkeypatch, kind, F, L):
     nch = 6
 
     def run(split, graph):
-        monkeypatch.setenv("GS_MH_SPLIT", "1" if split else "0")
+        gsopt.setenv("GS_MH_SPLIT", "1" if split else "0")
         r = BatchedRunner(kind, P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
                           blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=43,
                           chain0=3, store_skymap=False)
@@ -420,46 +409,7 @@ def test_mh_split_bit_identical(monkeypatch, kind, F, L):
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
         assert a[-2].any()                                # some blocks accepted
-    monkeypatch.delenv("GS_MH_SPLIT", raising=False)
-
-
-@pytest.mark.parametrize("F,nch", [(3, 1), (1, 2), (2, 2)])
-def test_centered_one_launch_bit_identical(monkeypatch, F, nch):
-    """The one-launch centered step (k_centered_fused: sweep, statistics finish
-    and C_l draw with in-launch hand-offs; GS_CENTERED_FUSED=1 at plan creation)
-    gives the same bits as the three launches: maps and D_l over 3 native steps,
-    eager and as one captured 3-step graph (the counter advance and the trace
-    ride in the fused launch)."""
-    from gibbssampler_amd.problem import synthetic_problem
-    from gibbssampler_amd.samplers import BatchedRunner
-    P = synthetic_problem(300, 128, F, seed=7)
-
-    def run(fused, graph):
-        if fused:
-            monkeypatch.setenv("GS_CENTERED_FUSED", "1")
-        else:
-            monkeypatch.delenv("GS_CENTERED_FUSED", raising=False)
-        r = BatchedRunner("centered", P["lmax"], P["nside"], F, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
-                          rng="native", seed=23)
-        assert r.plan.rows_per_task == 4
-        r.init(P["dls_init"])
-        trace = None
-        if graph:
-            trace = r.plan.zeros(3, nch, r.plan.nspec, r.plan.maxbins)
-            r.capture_steps(3, trace=trace, trace_capacity=3)
-            r.step()
-        else:
-            for _ in range(3):
-                r.step()
-        out = [r.dl.cpu().numpy(), r.s.cpu().numpy()]
-        if trace is not None:
-            out.append(trace.cpu().numpy())
-        return out
-
-    for graph in (False, True):
-        a, b = run(True, graph), run(False, graph)
-        for x, y in zip(a, b):
-            np.testing.assert_array_equal(x, y)
+    gsopt.delenv("GS_MH_SPLIT", raising=False)
 
 
 def _noncentered_runner(seed, chain0=2):

@@ -443,7 +443,7 @@ def test_f2_masked_asis_driver_vs_oracle(g, gibbs_cr, sht_mode):
 
 @pytest.mark.parametrize("n_iter,group_bytes,stage", [(1, None, "1"), (2, None, "1"), (2, "1", "1"),
                                                      (1, "50000000", "1"), (1, None, "0"), (2, "1", "0")])
-def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes, stage, sht_mode):
+def test_f2_device_sweep_groups_vs_oracle(g, gsopt, n_iter, group_bytes, stage, sht_mode):
     """gs_masked_pixel_mh decides every block on the device from one block
     synthesis + one Gram pass; with a small workspace budget the blocks run in
     groups (one block per group at "1") and the residual is carried between
@@ -451,9 +451,9 @@ def test_f2_device_sweep_groups_vs_oracle(g, monkeypatch, n_iter, group_bytes, s
     full-map likelihood per block (oracle/masked.pixel_mh).  stage "0": the
     block synthesis without the LDS-staged inputs (the large-l_max form)."""
     from gibbssampler_amd.masked import PixelMH
-    monkeypatch.setenv("GS_SHT_BLK_STAGE", stage)
+    gsopt.setenv("GS_SHT_BLK_STAGE", stage)
     if group_bytes is not None:
-        monkeypatch.setenv("GS_F2_GROUP_BYTES", group_bytes)
+        gsopt.setenv("GS_F2_GROUP_BYTES", group_bytes)
     bins, blocks, pv = _f2_parts(g)
     seed, chain, it = 313, 1, 9
     cr = _cr(g, sht_mode, gibbs_cr=False, ula=False, rng="native", seed=seed, chain=chain)
@@ -492,7 +492,7 @@ def f2_large():
 
 
 @pytest.mark.parametrize("n_iter", [1, 20, 90])
-def test_f2_large_group_decisions_equal_one_block_groups(f2_large, monkeypatch, n_iter, sht_mode):
+def test_f2_large_group_decisions_equal_one_block_groups(f2_large, gsopt, n_iter, sht_mode):
     """the large-R decision path (138 blocks in one group, G's
     triangle beyond 64 KB of LDS) and n_iter_metropolis up to 90 (the log
     uniforms then no longer fit in LDS beside the triangle and are read from
@@ -503,9 +503,9 @@ def test_f2_large_group_decisions_equal_one_block_groups(f2_large, monkeypatch, 
     out = []
     for group_bytes in (None, "1"):
         if group_bytes is None:
-            monkeypatch.delenv("GS_F2_GROUP_BYTES", raising=False)
+            gsopt.delenv("GS_F2_GROUP_BYTES", raising=False)
         else:
-            monkeypatch.setenv("GS_F2_GROUP_BYTES", group_bytes)
+            gsopt.setenv("GS_F2_GROUP_BYTES", group_bytes)
         cr = MaskedCR(q["pix"], 40.0 ** 2, np.full(12 * q["N"] ** 2, 0.2 ** 2), q["bl"], q["L"], q["N"],
                       mask=q["mask"], gibbs_cr=False, ula=False, rng="native", seed=515, chain=2, sht_mode=sht_mode)
         mh = PixelMH(cr, q["bins"], q["blocks"], q["pv"], n_iter_metropolis=n_iter)
@@ -731,14 +731,14 @@ def test_batch4_replay_tables_centered_driver(g):
 
 
 @pytest.mark.parametrize("blocks_mfma", ["0", "1"])
-def test_f2_large_vs_oracle_tables(f2_large, monkeypatch, blocks_mfma):
+def test_f2_large_vs_oracle_tables(f2_large, gsopt, blocks_mfma):
     """the 138-block large-R sweep on the table path: the matrix-core block
     synthesis (GS_SHT_BLOCKS_MFMA 1, single-l blocks: every quad straddles
     block edges) and the recurrence block synthesis (0) against the oracle's
     full-map likelihood per block."""
     from gibbssampler_amd.masked import MaskedCR, PixelMH
     from oracle import harmonic as H
-    monkeypatch.setenv("GS_SHT_BLOCKS_MFMA", blocks_mfma)
+    gsopt.setenv("GS_SHT_BLOCKS_MFMA", blocks_mfma)
     q = f2_large
     N, L = q["N"], q["L"]
     npol = np.full(12 * N * N, 0.2 ** 2)
@@ -760,7 +760,7 @@ def test_f2_large_vs_oracle_tables(f2_large, monkeypatch, blocks_mfma):
 
 @pytest.mark.parametrize("F", [2, 3])
 @pytest.mark.parametrize("over", [False, True])
-def test_aux_fused_pass_bit_identical(monkeypatch, F, over):
+def test_aux_fused_pass_bit_identical(gsopt, F, over):
     """the table path's fused v | s + s | v-analysis pass (gs_sht_aux_pass_batch:
     synthesis, the k_mc_v update in the ring workgroup, analysis) and the reuse of
     the over-relaxation's repeated s | v analysis give the bits of the unfused
@@ -774,7 +774,7 @@ def test_aux_fused_pass_bit_identical(monkeypatch, F, over):
     spec = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
     out = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("GS_SHT_FUSED_AUX", fused)
+        gsopt.setenv("GS_SHT_FUSED_AUX", fused)
         cr = MaskedCR(pix, ntemp, npol, bl, L, N, mask=mask, nfields=F, n_gibbs=3, overrelaxation=over, rng="native",
                       seed=8, chain=2, nchains=4, sht_mode="mfma")
         s = torch.from_numpy(np.ascontiguousarray(np.stack([np.stack([s0[r] for r in rows]) * (1 + 0.1 * b)

@@ -181,14 +181,14 @@ def test_single_modes_vs_scipy(N, L, modes):
 
 @pytest.mark.parametrize("thr", [32, 64])
 @pytest.mark.parametrize("ncomp", [1, 3])
-def test_large_ring_fft_paths_vs_oracle(thr, ncomp, monkeypatch):
+def test_large_ring_fft_paths_vs_oracle(thr, ncomp, gsopt):
     """The ring-FFT paths N_side >= 2048 takes (rings whose Bluestein length
     exceeds the LDS: split into two half-length Bluesteins in LDS, or the
     global-scratch FFT), exercised at N_side 16 by lowering the LDS threshold
     of the plan (GS_SHT_LDS_FFT_MAX)."""
     torch = _torch()
     from gibbssampler_amd.sht import HealpixSHT
-    monkeypatch.setenv("GS_SHT_LDS_FFT_MAX", str(thr))
+    gsopt.setenv("GS_SHT_LDS_FFT_MAX", str(thr))
     N, L = 16, 40
     sht = HealpixSHT(N, L)
     rng = np.random.default_rng(thr + ncomp)
@@ -212,15 +212,15 @@ SHAPES = [("2,1", "4,1"), ("2,0", "2,1"), ("1,1", "2,0"), ("1,0", "1,1"), ("2,1"
 
 @pytest.mark.parametrize("syn,ana", SHAPES)
 @pytest.mark.parametrize("N,L", [(16, 32), (64, 100)])
-def test_legendre_launch_shapes_vs_oracle(monkeypatch, syn, ana, N, L):
+def test_legendre_launch_shapes_vs_oracle(gsopt, syn, ana, N, L):
     """Every Legendre launch shape the plan may pick (ring groups per lane 1/2
     for synthesis, 1/2/4 for analysis; m paired or not) -- chosen by map size
     for occupancy, forced here with GS_SHT_SYN / GS_SHT_ANA -- against the
     dense oracle (TEB, both directions; 64/100 with several ring groups)."""
     torch = _torch()
     from gibbssampler_amd.sht import HealpixSHT
-    monkeypatch.setenv("GS_SHT_SYN", syn)
-    monkeypatch.setenv("GS_SHT_ANA", ana)
+    gsopt.setenv("GS_SHT_SYN", syn)
+    gsopt.setenv("GS_SHT_ANA", ana)
     sht = HealpixSHT(N, L)
     rng = np.random.default_rng(N + L)
     a = _rand_alm(L, 3, rng)
@@ -236,16 +236,16 @@ def test_legendre_launch_shapes_vs_oracle(monkeypatch, syn, ana, N, L):
 @pytest.mark.parametrize("seg", [4, 8, 20])
 @pytest.mark.parametrize("ana", ["1,0", "2,1", "4,1"])
 @pytest.mark.parametrize("N,L", [(16, 32), (64, 100)])
-def test_segmented_analysis_vs_oracle(monkeypatch, seg, ana, N, L):
+def test_segmented_analysis_vs_oracle(gsopt, seg, ana, N, L):
     """l-segmented analysis and synthesis (GS_SHT_SEG: every m's l range split
     into segments entered with the plan-time recurrence state; the default for
     small maps) against the dense oracle, for every analysis launch shape, with
     segment starts before, inside and after the polar onsets."""
     torch = _torch()
     from gibbssampler_amd.sht import HealpixSHT
-    monkeypatch.setenv("GS_SHT_SEG", str(seg))
-    monkeypatch.setenv("GS_SHT_ANA", ana)
-    monkeypatch.setenv("GS_SHT_SYN", "1,0")        # the segmented synthesis's shape
+    gsopt.setenv("GS_SHT_SEG", str(seg))
+    gsopt.setenv("GS_SHT_ANA", ana)
+    gsopt.setenv("GS_SHT_SYN", "1,0")        # the segmented synthesis's shape
     sht = HealpixSHT(N, L)
     rng = np.random.default_rng(seg + N + L)
     for ncomp in (1, 2, 3):
@@ -261,7 +261,7 @@ def test_segmented_analysis_vs_oracle(monkeypatch, seg, ana, N, L):
 
 
 @pytest.mark.parametrize("N,L,seg", [(256, 512, 64), (256, 512, 16), (512, 1024, 64)])
-def test_segmented_analysis_matches_single_walk(monkeypatch, N, L, seg):
+def test_segmented_analysis_matches_single_walk(gsopt, N, L, seg):
     """At the HEAD masked modes' size (and N_side 512): segmented and
     single-walk analysis and synthesis agree to rounding (the segment states continue the
     same recurrence; only the reduction grouping of a few l differs), iter 0
@@ -273,9 +273,9 @@ def test_segmented_analysis_matches_single_walk(monkeypatch, N, L, seg):
     alm = torch.from_numpy(_rand_alm(L, 3, rng)).cuda()
     out = {}
     for sg in (0, seg):
-        monkeypatch.setenv("GS_SHT_SEG", str(sg))
-        monkeypatch.setenv("GS_SHT_ANA", "1,0")
-        monkeypatch.setenv("GS_SHT_SYN", "1,0")
+        gsopt.setenv("GS_SHT_SEG", str(sg))
+        gsopt.setenv("GS_SHT_ANA", "1,0")
+        gsopt.setenv("GS_SHT_SYN", "1,0")
         sht = HealpixSHT(N, L)
         out[sg] = [sht.map2alm(maps, iter=it, layout="complex", ncomp=3).cpu().numpy() for it in (0, 3)]
         out[sg].append(sht.alm2map(alm, ncomp=3, layout="complex").cpu().numpy())
@@ -286,14 +286,14 @@ def test_segmented_analysis_matches_single_walk(monkeypatch, N, L, seg):
 
 @pytest.mark.parametrize("merge", ["0", "1"])
 @pytest.mark.parametrize("N,L", [(16, 40), (64, 128)])
-def test_ring_stage_merged_and_per_class_vs_oracle(monkeypatch, merge, N, L):
+def test_ring_stage_merged_and_per_class_vs_oracle(gsopt, merge, N, L):
     """Small maps run the whole ring stage as one launch (every FFT length in
     one grid, GS_SHT_MERGE_RINGS default on for lengths <= 2048); larger maps
     one launch per length class.  Both against the dense oracle, TEB, both
     directions."""
     torch = _torch()
     from gibbssampler_amd.sht import HealpixSHT
-    monkeypatch.setenv("GS_SHT_MERGE_RINGS", merge)
+    gsopt.setenv("GS_SHT_MERGE_RINGS", merge)
     sht = HealpixSHT(N, L)
     rng = np.random.default_rng(N + L + int(merge))
     a = _rand_alm(L, 3, rng)
@@ -333,7 +333,7 @@ def test_cpu_baseline_sht_equals_device(N, L, comps):
 
 
 @pytest.mark.parametrize("N,L", [(64, 100), (256, 512)])
-def test_default_small_map_shapes_match_single_walk(monkeypatch, N, L):
+def test_default_small_map_shapes_match_single_walk(gsopt, N, L):
     """The small-map default plan mixes launch shapes over one 32-l segment
     table: synthesis and TEB analysis in 64-l segments with one ring group per
     lane (two table rows per segment), T and spin-2 analysis in 32-l segments
@@ -345,9 +345,9 @@ def test_default_small_map_shapes_match_single_walk(monkeypatch, N, L):
     out = {}
     for mode in ("default", "walk"):
         if mode == "walk":
-            monkeypatch.setenv("GS_SHT_SEG", "0")
-            monkeypatch.setenv("GS_SHT_ANA", "1,0")
-            monkeypatch.setenv("GS_SHT_SYN", "1,0")
+            gsopt.setenv("GS_SHT_SEG", "0")
+            gsopt.setenv("GS_SHT_ANA", "1,0")
+            gsopt.setenv("GS_SHT_SYN", "1,0")
         sht = HealpixSHT(N, L)
         res = []
         for ncomp in (1, 2, 3):
@@ -364,7 +364,7 @@ def test_default_small_map_shapes_match_single_walk(monkeypatch, N, L):
 
 @pytest.mark.parametrize("N,L,ncomp,env", [(16, 32, 2, None), (64, 100, 3, None), (256, 512, 2, None),
                                            (64, 128, 2, "split"), (32, 64, 1, None)])
-def test_fused_beam_and_weight_bit_identical(N, L, ncomp, env, monkeypatch):
+def test_fused_beam_and_weight_bit_identical(N, L, ncomp, env, gsopt):
     """gs_sht_alm2map_beamed / gs_sht_map2alm_weighted (the masked CR's b s
     synthesis and N^-1-weighted analysis, CenteredGibbs.py:298-299,510-513,698-699)
     equal the separate multiply + plain transform bit for bit: merged and
@@ -372,8 +372,8 @@ def test_fused_beam_and_weight_bit_identical(N, L, ncomp, env, monkeypatch):
     scratch ring paths forced by a small LDS FFT cap."""
     torch = _torch()
     if env == "split":
-        monkeypatch.setenv("GS_SHT_LDS_FFT_MAX", "64")
-        monkeypatch.setenv("GS_SHT_MERGE_RINGS", "0")
+        gsopt.setenv("GS_SHT_LDS_FFT_MAX", "64")
+        gsopt.setenv("GS_SHT_MERGE_RINGS", "0")
     from gibbssampler_amd.sht import HealpixSHT
     sht = HealpixSHT(N, L)
     rng = np.random.default_rng(7 * N + L + ncomp)

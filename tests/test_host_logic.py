@@ -40,16 +40,18 @@ def test_unfold_bins_matches_reference_semantics():
     np.testing.assert_array_equal(unfold_bins([1.0, 2.0, 3.0, 4.0], b), [1, 2, 3, 3, 3, 4, 4, 4, 4])
 
 
-def test_graveyard_drains_outside_any_capture():
-    """ADVICE r04: entries parked during a capture this package did not open
-    (end_capture never runs for it) are released by the next release / park
-    made outside any capture."""
+def test_graveyard_drains_only_at_explicit_points():
+    """ADVICE r05: entries parked during a capture this package did not open
+    (end_capture never runs for it) stay parked through unrelated releases and
+    parks -- a graph captured outside the package may still replay kernels that
+    use them -- and are freed by the explicit flush()."""
     from gibbssampler_amd import _capi
     freed = []
     _capi._GRAVEYARD.append((freed.append, "handle-a"))       # as if parked inside a foreign capture
     _capi._GRAVEYARD.append((None, object()))
     _capi.release(freed.append, "handle-b")
-    assert freed == ["handle-a", "handle-b"] and _capi.graveyard_size() == 0
-    _capi._GRAVEYARD.append((freed.append, "handle-c"))
+    assert freed == ["handle-b"] and _capi.graveyard_size() == 2
     assert _capi.park(object()) is False
-    assert freed[-1] == "handle-c" and _capi.graveyard_size() == 0
+    assert _capi.graveyard_size() == 2
+    _capi.flush()
+    assert freed == ["handle-b", "handle-a"] and _capi.graveyard_size() == 0

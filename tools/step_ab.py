@@ -1,11 +1,12 @@
-"""A/B of plan-creation settings (environment variables read when a plan is
-built, e.g. GS_SWEEP_ROWS) on one workload, in ONE process, interleaved
+"""A/B of plan-creation settings (library options read when a plan is built,
+include/gibbs_capi.h gs_option_set, e.g. GS_SWEEP_TW) on one workload, in ONE process, interleaved
 (box-to-box and process-to-process spread is +-5%): each setting gets its own
 BatchedRunner with K steps captured in a hipGraph; replays alternate.
 
 usage (GPU box):
   python tools/step_ab.py KIND L NSIDE NCHAINS STEPS "VAR=a" "VAR=b" ...
-  e.g.  python tools/step_ab.py centered 512 256 1 200 GS_SWEEP_ROWS=4 GS_SWEEP_ROWS=8
+  e.g.  python tools/step_ab.py noncentered 1024 512 32 200 GS_SWEEP_TW=1 GS_SWEEP_TW=2
+(GIBBS_HIP_LIB=<path> switches whole builds instead: tools/build_variants.sh)
 The r02 sweep-shape A/B (1 tile x 4 chunks vs 4 x 1, GS_SWEEP_TW) ran this way.
 GS_AB_NOSTORE=1 in the environment: runners without the sky-map store."""
 import os
@@ -15,6 +16,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gibbssampler_amd import _capi  # noqa: E402
 from gibbssampler_amd.problem import synthetic_problem  # noqa: E402
 from gibbssampler_amd.samplers import BatchedRunner  # noqa: E402
 
@@ -25,8 +27,8 @@ def main(kind, L, nside, nch, steps, *settings, rounds=9):
     runners = {}
     for st in settings:
         k, v = st.split("=", 1)
-        old = os.environ.get(k)
-        os.environ[k] = v
+        old = _capi.get_option(k)
+        _capi.set_option(k, v)
         r = BatchedRunner(kind, P["lmax"], P["nside"], 3, nch, P["bl"], P["noise_var"], P["bins"], P["d_alm"],
                           blocks=P["blocks"], proposal_variances=P["proposal_variances"], rng="native", seed=5,
                           store_skymap=os.environ.get("GS_AB_NOSTORE") is None)
@@ -34,10 +36,7 @@ def main(kind, L, nside, nch, steps, *settings, rounds=9):
         r.step()
         r.capture_steps(steps)
         runners[st] = r
-        if old is None:
-            del os.environ[k]
-        else:
-            os.environ[k] = old
+        _capi.set_option(k, old)
     res = {k: [] for k in runners}
     for rnd in range(rounds):
         for k, r in runners.items():
