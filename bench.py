@@ -498,19 +498,15 @@ def _masked_data(N, L, nfields, seed=0, mask_kind="band"):
     return d, mask, dl
 
 
-def run_masked(args, ctx, cpu=None):
-    """BASELINE configs[4]: CenteredGibbs TEB, masked (f_sky 0.8), aux-variable CR
-    with n_gibbs = 1 (a9, TEB) + inverse-Wishart / inverse-Gamma C_l draw, one
-    chain per GPU.  Per iteration: b s -> alm2map (TEB) -> v | s -> map2alm
-    (TEB) -> s | v, then the sweep statistics and the C_l draw; all on the device."""
+def masked_c5_setup(args, ctx):
+    """configs[4]'s per-iteration step (the closure run_masked times;
+    tools/step_traffic.py counts its HBM bytes)."""
     import torch
     from gibbssampler_amd import _capi
     from gibbssampler_amd.engine import GibbsPlan
     from gibbssampler_amd.masked import MaskedCR
     from gibbssampler_amd.problem import gauss_beam
-    from gibbssampler_amd.sht import HealpixSHT
     L, N = args.lmax, args.nside
-    Npix = 12 * N * N
     NR = (L + 1) ** 2
     B = args.nchains
     d, mask, dl = _masked_data(N, L, 3)
@@ -533,6 +529,21 @@ def run_masked(args, ctx, cpu=None):
         out = plan.cls_draw(st, None, seed=args.seed, iteration=it[0])
         dl_t.copy_(out[:, :, :L + 1])          # unbinned bins: bin b = l
 
+    return step
+
+
+def run_masked(args, ctx, cpu=None):
+    """BASELINE configs[4]: CenteredGibbs TEB, masked (f_sky 0.8), aux-variable CR
+    with n_gibbs = 1 (a9, TEB) + inverse-Wishart / inverse-Gamma C_l draw, one
+    chain per GPU.  Per iteration: b s -> alm2map (TEB) -> v | s -> map2alm
+    (TEB) -> s | v, then the sweep statistics and the C_l draw; all on the device."""
+    import torch
+    from gibbssampler_amd.sht import HealpixSHT
+    L, N = args.lmax, args.nside
+    Npix = 12 * N * N
+    NR = (L + 1) ** 2
+    B = args.nchains
+    step = masked_c5_setup(args, ctx)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -588,21 +599,10 @@ def run_masked(args, ctx, cpu=None):
     }
 
 
-def run_masked_head(args, ctx, cpu=None):
-    """HEAD's real run modes (main_polarization.py:109-126,154) through the
-    drop-in class surface, EB, one chain per GPU, N_side 256 / L 512 with the
-    reference's Planck BB bins and 1 + 134 Metropolis blocks (config.py:45-55):
-
-      masked_centered_ula  CenteredGibbs(mask, gibbs_cr=True, ula=True): per
-                           iteration the aux-variable CR + MALA composition
-                           (CenteredGibbs.py:831-834) and the C_l draw;
-      masked_asis          ASIS(mask, all_sph=False, gibbs_cr=True, n_gibbs=20,
-                           overrelaxation=True): over-relaxed aux CR (61 SHTs),
-                           centred C_l draw, the pixel-domain MH sweep (f2,
-                           decided on the device), re-centring.
-
-    The reference's init CR (the PCG) runs in the warm-up; the timed region
-    continues the chain for --steps iterations."""
+def masked_head_setup(args, ctx):
+    """HEAD's masked run modes (run_masked_head's set-up, warm-up included):
+    returns (runner, go, n_sht, what, pcg); go() runs the timed --steps
+    iterations (tools/step_traffic.py counts their HBM bytes)."""
     import torch
     from gibbssampler_amd import gibbs as G
     from gibbssampler_amd.masked import MaskedRunner
@@ -662,6 +662,28 @@ def run_masked_head(args, ctx, cpu=None):
         h = runner.run(init, max(args.warmup, 1))[0]
         last = last_of(h)
         go = lambda: runner.run(last, args.steps, s_init=runner.s)
+    return runner, go, n_sht, what, pcg
+
+
+def run_masked_head(args, ctx, cpu=None):
+    """HEAD's real run modes (main_polarization.py:109-126,154) through the
+    drop-in class surface, EB, one chain per GPU, N_side 256 / L 512 with the
+    reference's Planck BB bins and 1 + 134 Metropolis blocks (config.py:45-55):
+
+      masked_centered_ula  CenteredGibbs(mask, gibbs_cr=True, ula=True): per
+                           iteration the aux-variable CR + MALA composition
+                           (CenteredGibbs.py:831-834) and the C_l draw;
+      masked_asis          ASIS(mask, all_sph=False, gibbs_cr=True, n_gibbs=20,
+                           overrelaxation=True): over-relaxed aux CR (61 SHTs),
+                           centred C_l draw, the pixel-domain MH sweep (f2,
+                           decided on the device), re-centring.
+
+    The reference's init CR (the PCG) runs in the warm-up; the timed region
+    continues the chain for --steps iterations."""
+    import torch
+    L, N = args.lmax, args.nside
+    B = args.nchains
+    runner, go, n_sht, what, pcg = masked_head_setup(args, ctx)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()

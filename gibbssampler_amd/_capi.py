@@ -158,8 +158,10 @@ _SIGS = [
 EXPORTED = [n for n, _, _ in _SIGS]
 
 
-def load(path=None):
-    """Load the HIP library (raises GibbsHipError when absent)."""
+def load(path=None, allow_missing=False):
+    """Load the HIP library (raises GibbsHipError when absent).  allow_missing:
+    tolerate entry points an older build lacks (the A/B tools load earlier
+    builds side by side; the product path never passes it)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -169,6 +171,8 @@ def load(path=None):
                             "(there is no CPU fallback)")
     lib = ctypes.CDLL(p)
     for name, res, args in _SIGS:
+        if allow_missing and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -124,6 +124,7 @@ struct gs_plan {
     // D_l into dl_tmp: the split MH reads its start state from there (both
     // workgroups of a chain see the pre-MH D_l whatever their order)
     bool snap_ok = false;
+    int* sweep_q = nullptr;          // [9] the sweep's per-XCD work-queue counters (GS_SWEEP_DYN builds)
     const double* pro_dl = nullptr;
     uint32_t pro_slo = 0, pro_shi = 0, pro_it = 0;
     bool iter_dev_on = false;
@@ -469,7 +470,7 @@ __device__ __forceinline__ void cr_sweep_latency(int L, int nchains, int ntile, 
 #pragma unroll
     for (int k = 0; k < (BM_TAB_DOUBLES + 255) / 256; ++k) {
         const int j = threadIdx.x + 256 * k;
-        tv[k] = j < 256 ? BM_LOG_TAB[j] : BM_TRIG_TAB[min(j - 256, 511)];
+        tv[k] = j < BM_LOG_DOUBLES ? BM_LOG_TAB[j] : BM_TRIG_TAB[min(j - BM_LOG_DOUBLES, 511)];
     }
     const double bq = op.bl[lc];
     // 3. this l's D_l (the latency form always computes the operator in-kernel,
@@ -558,49 +559,24 @@ template <int F>
 __device__ void pro_pre_item(const ProPre& pp, int bx, int nchains, uint32_t seed_lo, uint32_t seed_hi, IterArg itarg,
                              int chain0);
 
-template <int F, int ZM, bool STORE, int PRE = 0>
-__global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
-                                                  const int2* __restrict__ tasks, const double* __restrict__ d,
-                                                  const double* __restrict__ params, const double* __restrict__ z,
-                                                  double* __restrict__ s, double* __restrict__ partials,
-                                                  uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, uint32_t substep,
-                                                  int chain0, SweepOp op, ClsPre cp, ProPre pp) {
-    if constexpr (PRE == 0 && ZM == 0) {
-        if ((int)blockIdx.x < pp.n) {
-            pro_pre_item<F>(pp, (int)blockIdx.x, nchains, seed_lo, seed_hi, itarg, chain0);
-            return;
-        }
-    }
-    const uint32_t iter = itarg.get();
+// diagnostic timeline of the sweep's workgroups (-DGS_SWEEP_WGTIME, build
+// variant "wgtime"; tools/sweep_timeline.py): per physical workgroup its first
+// and last s_memrealtime, HW_ID and XCC_ID
+#if defined(GS_SWEEP_WGTIME)
+constexpr int SW_TL_MAX = 16384;
+__device__ unsigned long long g_sw_tl[4 * SW_TL_MAX];
+#endif
+
+// one (tile group, row chunk) task of one chain: logical workgroup wg
+template <int F, int ZM, bool STORE>
+__device__ __forceinline__ void cr_sweep_task(int wg, int L, int nchains, int ntile, int nchunkg, int tm, int tw,
+                                              const int2* __restrict__ tasks, const double* __restrict__ d,
+                                              const double* __restrict__ params, const double* __restrict__ z,
+                                              double* __restrict__ s, double* __restrict__ partials,
+                                              uint32_t seed_lo, uint32_t seed_hi, uint32_t iter, uint32_t substep,
+                                              int chain0, const SweepOp& op, const double* __restrict__ tab,
+                                              double* red) {
     constexpr int NS = SweepAcc<F>::NS;
-    __shared__ double tab[ZM == 0 ? BM_TAB_DOUBLES : 1];
-    __shared__ double red[3 * NS * WAVE];           // chunk-wave sums of tw < 4 shapes
-    if constexpr (PRE > 0) {
-        static_assert(ZM == 0, "latency form: native draws only");
-        // the variate workgroups sit at the END of the grid, so the sweep's
-        // workgroups keep physical ids 0.. and their XCD-aware remap (b % 8 =
-        // the XCD) stays exact for any cp.n
-        const int nsw = (int)gridDim.x - cp.n;
-        if ((int)blockIdx.x >= nsw) {
-            cls_variates_item<F>(cp, ((int)blockIdx.x - nsw) * blockDim.x + threadIdx.x, seed_lo, seed_hi, iter,
-                                 chain0);
-            return;
-        }
-        cr_sweep_latency<F, STORE, PRE>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo,
-                                        seed_hi, iter, substep, chain0, op, tab, red, (int)blockIdx.x, nsw);
-        return;
-    }
-    if constexpr (ZM == 0) {
-        bm_stage_tables(tab);
-        __syncthreads();
-    }
-    // XCD-aware remap (bijective): workgroups are dealt round-robin over the 8
-    // XCDs, so physical id b runs on XCD b % 8; give each XCD a contiguous range
-    // of logical ids so that all chains of one (tiles, rows) block share one
-    // XCD's L2 for the data reads (speed only -- any placement is correct)
-    const int bid = (int)blockIdx.x - pp.n;     // (pp.n % 8 == 0: the same XCD as blockIdx.x)
-    const int nwg = (int)gridDim.x - pp.n, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int pair = wg / nchains;
     const int chain = wg % nchains;
     const int lane = threadIdx.x & 63;
@@ -642,8 +618,7 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     // row m starts at complex index S(m) = m(2L+3-m)/2 (l = m); slot r = 2i-(L+1)
     long long i = (long long)m * (2 * L + 1 - m) / 2 + ell;
     if (m1 - 1 <= ell_lo && ell_lo >= 0) {
-        // off-diagonal block: every lane active on every row; the next row's
-        // data is loaded before this row's draw (register double buffer)
+        // off-diagonal block: every lane active on every row
         if constexpr (ZM == 0 && !STORE) {
             // the headline form (native draws, no map written): 32-bit row offsets
             uint32_t i32 = (uint32_t)i;
@@ -694,6 +669,103 @@ __global__ __launch_bounds__(256, 1) void k_cr_sweep(int L, int nchains, int nti
     }
     double* po = partials + (((long long)chain * ntile + t) * nchunkg + gc.y) * NS * WAVE;
     sweep_partials_store<NS>(acc, tw, w, lane, tile_ok && (cw * gc.y) * tm <= lhi, po, red);
+}
+
+// nlog: logical workgroups (chains x task pairs); the grid holds nlog sweep
+// workgroups, or (experiment GS_SWEEP_DYN) fewer that take logical ones from a
+// work queue (qc[0]: next task, qc[1]: finished workgroups)
+#ifndef GS_SWEEP_MINW
+#define GS_SWEEP_MINW 1
+#endif
+template <int F, int ZM, bool STORE, int PRE = 0>
+__global__ __launch_bounds__(256, GS_SWEEP_MINW) void k_cr_sweep(int L, int nchains, int ntile, int nchunkg, int tm, int tw,
+                                                  const int2* __restrict__ tasks, const double* __restrict__ d,
+                                                  const double* __restrict__ params, const double* __restrict__ z,
+                                                  double* __restrict__ s, double* __restrict__ partials,
+                                                  uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, uint32_t substep,
+                                                  int chain0, SweepOp op, ClsPre cp, ProPre pp, int nlog,
+                                                  int* __restrict__ qc) {
+    if constexpr (PRE == 0 && ZM == 0) {
+        if ((int)blockIdx.x < pp.n) {
+            pro_pre_item<F>(pp, (int)blockIdx.x, nchains, seed_lo, seed_hi, itarg, chain0);
+            return;
+        }
+    }
+    const uint32_t iter = itarg.get();
+    constexpr int NS = SweepAcc<F>::NS;
+    __shared__ __attribute__((aligned(16))) double tab[ZM == 0 ? BM_TAB_DOUBLES : 2];
+    __shared__ double red[3 * NS * WAVE];           // chunk-wave sums of tw < 4 shapes
+    if constexpr (PRE > 0) {
+        static_assert(ZM == 0, "latency form: native draws only");
+        // the variate workgroups sit at the END of the grid, so the sweep's
+        // workgroups keep physical ids 0.. and their XCD-aware remap (b % 8 =
+        // the XCD) stays exact for any cp.n
+        const int nsw = (int)gridDim.x - cp.n;
+        if ((int)blockIdx.x >= nsw) {
+            cls_variates_item<F>(cp, ((int)blockIdx.x - nsw) * blockDim.x + threadIdx.x, seed_lo, seed_hi, iter,
+                                 chain0);
+            return;
+        }
+        cr_sweep_latency<F, STORE, PRE>(L, nchains, ntile, nchunkg, tm, tw, tasks, d, s, partials, seed_lo,
+                                        seed_hi, iter, substep, chain0, op, tab, red, (int)blockIdx.x, nsw);
+        return;
+    }
+    if constexpr (ZM == 0) {
+        bm_stage_tables(tab);
+        __syncthreads();
+    }
+    // XCD-aware remap (bijective): workgroups are dealt round-robin over the 8
+    // XCDs, so physical id b runs on XCD b % 8; give each XCD a contiguous range
+    // of logical ids so that all chains of one (tiles, rows) block share one
+    // XCD's L2 for the data reads (speed only -- any placement is correct)
+    const int bid = (int)blockIdx.x - pp.n;     // (pp.n % 8 == 0: the same XCD as blockIdx.x)
+    const int nwg = (int)gridDim.x - pp.n, xcd = bid & 7, q8 = nlog >> 3, r8 = nlog & 7;
+    const int base = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+#if defined(GS_SWEEP_WGTIME)
+    const unsigned long long tl0 = wall_clock64();
+#endif
+#if !defined(GS_SWEEP_DYN)
+    cr_sweep_task<F, ZM, STORE>(base + (bid >> 3), L, nchains, ntile, nchunkg, tm, tw, tasks, d, params, z, s,
+                                partials, seed_lo, seed_hi, iter, substep, chain0, op, tab, red);
+    (void)nwg; (void)qc;
+#else
+    // per-XCD work queues (qc[x], x = this workgroup's XCD under the b % 8
+    // placement): each workgroup takes the next task of its XCD's logical range
+    // (dealt heaviest first), then steals from the other XCDs' ranges; qc[8]
+    // counts finished workgroups, the last one resets the queues for the next
+    // launch (every workgroup has taken its last task index by then)
+    __shared__ int s_task;
+    for (int v = 0; v < 8; ++v) {
+        const int x = (xcd + v) & 7;
+        const int bx = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+        const int cnt = q8 + (x < r8 ? 1 : 0);
+        for (;;) {
+            if (threadIdx.x == 0) s_task = atomicAdd(&qc[x], 1);
+            __syncthreads();
+            const int k = s_task;
+            __syncthreads();
+            if (k >= cnt) break;
+            cr_sweep_task<F, ZM, STORE>(bx + k, L, nchains, ntile, nchunkg, tm, tw, tasks, d, params, z, s,
+                                        partials, seed_lo, seed_hi, iter, substep, chain0, op, tab, red);
+            __syncthreads();                    // red is reused by the next task
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (atomicAdd(&qc[8], 1) == nwg - 1)
+            for (int x = 0; x < 9; ++x) atomicExch(&qc[x], 0);
+    }
+    (void)base;
+#endif
+#if defined(GS_SWEEP_WGTIME)
+    __syncthreads();
+    if (threadIdx.x == 0 && bid < SW_TL_MAX) {
+        unsigned long long* o = g_sw_tl + 4 * (size_t)bid;
+        o[0] = tl0;
+        o[1] = wall_clock64();
+        o[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+        o[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);    // HW_REG_XCC_ID
+    }
+#endif
 }
 
 // one wave's share of a (chain, statistic, tile) finish: the sum of chunks w,
@@ -2340,6 +2412,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->dl_tmp, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->u_nat, nc * std::max(p->nacc, 1));
     rc |= dev_alloc(&p->iter_dev, 4);
+    rc |= dev_alloc(&p->sweep_q, 9);
     {
         const char* e = gs_detail::option("GS_CLS_PRE");
         p->cls_pre = e ? std::atoi(e) != 0 : p->nchains <= 4;
@@ -2356,7 +2429,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
-    void* bufs[] = {p->iter_dev, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
+    void* bufs[] = {p->iter_dev, p->sweep_q, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
                     p->params, p->stats, p->prop, p->logr, p->dl_tmp, p->cls_var, p->phase_tab_s, p->phase_rng_s};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2541,7 +2614,8 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
         return set_error("gs_cr_sweep: null argument");
     const SweepOp op{pmode, p->maxbins, dl, p->ell2bin, p->bl, p->kappa[0], p->kappa[1], p->kappa[2]};
     const uint32_t slo = (uint32_t)(seed & 0xFFFFFFFFu), shi = (uint32_t)(seed >> 32);
-    dim3 g((unsigned)((long long)p->nchains * p->npair)), b(256);
+    const int nlog = (int)((long long)p->nchains * p->npair);
+    dim3 g((unsigned)nlog), b(256);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing_begin(p, S(stream), &e0, &e1)) return -1;
     const bool rep = z != nullptr, st = s_out != nullptr;
@@ -2562,7 +2636,7 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
 #define GS_SWL(FF, SS) hipLaunchKernelGGL((k_cr_sweep<FF, 0, SS, 4>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                           p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,    \
                                           s_out, p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op, cp, \
-                                          ProPre{})
+                                          ProPre{}, nlog, p->sweep_q)
 #define GS_SWL2(FF) do { if (st) GS_SWL(FF, true); else GS_SWL(FF, false); } while (0)
         if (p->F == 1) GS_SWL2(1); else if (p->F == 2) GS_SWL2(2); else GS_SWL2(3);
 #undef GS_SWL2
@@ -2591,12 +2665,20 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
         pp.prop = p->prop; pp.logr = p->logr; pp.u_out = p->u_nat; pp.snap = p->dl_tmp;
     }
     pp.n = (pp.nbp + pp.nbu + pp.nbv + 7) / 8 * 8;
+#if defined(GS_SWEEP_DYN)
+    // experiment: GS_SWEEP_DYN workgroups per CU taking tasks from the queue
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) ncu = 256;
+        g.x = (unsigned)std::min(nlog, GS_SWEEP_DYN * ncu / 8 * 8);
+    }
+#endif
     g.x += pp.n;
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,   \
                                              s_out,                                                                   \
                                              p->partials, slo, shi, p->ita(iteration), substep, p->chain0, \
-                                             op, none, pp)
+                                             op, none, pp, nlog, p->sweep_q)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
                         else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
                         else GS_SW(FF, 0, false); } while (0)
@@ -3012,6 +3094,14 @@ int gs_step_asis_fused(gs_plan* p, const double* d_alm, double* dl, double* s_ou
     }
     return 0;
 }
+
+#if defined(GS_SWEEP_WGTIME)
+int gs_debug_sweep_timeline(unsigned long long* out, int n) {
+    GS_CHECK(hipDeviceSynchronize());
+    GS_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sw_tl), sizeof(unsigned long long) * 4 * std::min(n, SW_TL_MAX)));
+    return 0;
+}
+#endif
 
 #if defined(GS_MH_TIMELINE)
 int gs_debug_mh_timeline(unsigned long long* out) {

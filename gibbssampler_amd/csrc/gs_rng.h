@@ -120,13 +120,16 @@ __device__ __forceinline__ void bm_sincos2pi(double u, double& sn, double& cs) {
 // sqrt(x) for the Box-Muller radius x = -2 ln u1, u1 in (0, 1]: x is +-0 or
 // lies in [2^-53, 75], never below the 2^-767 where the compiler's fp64 sqrt
 // expansion rescales its argument (by 2^256 in, 2^-128 out).  This is that
-// expansion (rsq seed, one Goldschmidt step, two Newton corrections) without
-// the rescaling, whose scale factors are 2^0 on this range: the same
-// instructions on the same values, the same bits.  Its +-0 / +inf class select
-// becomes a clamp of the seed: for x > 0 here rsq(x) <= 2^26.5 < 2^30 (no
-// change), and for x = +-0 the clamped seed carries the signed zero through
-// every step (g0 = x 2^30 = +-0, ..., g3 = +-0 = x, what the select returned).
-// Seven instructions fewer per draw.
+// expansion (rsq seed, one Goldschmidt step, a Newton correction) without the
+// rescaling, whose scale factors are 2^0 on this range, and without its second
+// Newton correction: the rsq seed is good to ~2^-22, the Goldschmidt step
+// doubles that and the Newton step leaves <= 1 ulp (r06: the correctly-rounded
+// second correction cost two fp64 FMAs per normal pair, 1.7 % of the headline
+// step, tools/lib_ab.py; the native streams are checked against the oracle's
+// libm Box-Muller at 1e-10).  Its +-0 / +inf class select becomes a clamp of
+// the seed: for x > 0 here rsq(x) <= 2^26.5 < 2^30 (no change), and for x = +-0
+// the clamped seed carries the signed zero through every step (g0 = x 2^30 =
+// +-0, ..., g2 = +-0 = x, what the select returned).
 __device__ __forceinline__ double bm_sqrt_radius(double x) {
     const double y0 = fmin(fabs(__builtin_amdgcn_rsq(x)), 1073741824.0);
     const double g0 = x * y0;
@@ -135,9 +138,7 @@ __device__ __forceinline__ double bm_sqrt_radius(double x) {
     const double g1 = fma(g0, r0, g0);
     const double h1 = fma(h0, r0, h0);
     const double d0 = fma(-g1, g1, x);
-    const double g2 = fma(d0, h1, g1);
-    const double d1 = fma(-g2, g2, x);
-    return fma(d1, h1, g2);
+    return fma(d0, h1, g1);
 }
 
 __device__ __forceinline__ void box_muller(uint4 w, double& z0, double& z1) {
@@ -239,34 +240,40 @@ __device__ inline void gamma_mt_pair(double alpha0, double alpha1, Key k, uint32
 }
 
 // ---- table-driven fp64 Box-Muller for the CR sweep ------------------------
-// The tables (gs_bm_tables.h, correctly rounded) are staged in LDS once per
-// workgroup: tab[0..255] = {c_k, -ln c_k} (128 cells of [sqrt(1/2), sqrt(2))),
-// tab[256..767] = {sin, cos}(2 pi k / 256).  Accuracy ~1-2 ulp: every
-// operation is fp64; only the polynomial degree drops (|r| < 0.0055 for the
-// log1p, |phi| < 2 pi / 256 for the trigonometric remainder).
-constexpr int BM_TAB_DOUBLES = 768;
+// The tables (gs_bm_tables.h, correctly rounded) are staged in LDS (a 16-B
+// aligned array: each cell is one 16-B read) once per workgroup: tab[0..1023] = {c_k, -ln c_k} (512 cells of the frexp mantissa
+// [1/2, 1)), tab[1024..1535] = {sin, cos}(2 pi (k + 1/2) / 256).  Every
+// operation is fp64; the table cells bound the polynomial arguments (|r| <
+// 1.09e-3 for the log1p, |phi| <= pi / 256 for the trigonometric remainder), so
+// low degrees reach ~1 ulp: log1p truncated after r^5 / 5 (relative error <
+// r^5 / 6 < 2.6e-16), sin after phi^5, cos after phi^6 (< 1e-17 absolute).
+// r06: the cells follow the frexp mantissa directly (the r05 table covered
+// [sqrt(1/2), sqrt(2)), which needed a compare, a select, an ldexp and an
+// exponent fix-up per draw, and a float->int index) and are twice as many, and
+// the trig cells are centred: 10 instructions fewer per normal pair.
+constexpr int BM_LOG_DOUBLES = 2 * BM_LOG_CELLS;
+constexpr int BM_TAB_DOUBLES = BM_LOG_DOUBLES + 512;
 
 __device__ __forceinline__ void bm_stage_tables(double* tab) {
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) tab[k] = BM_LOG_TAB[k];
-    for (int k = threadIdx.x; k < 512; k += blockDim.x) tab[256 + k] = BM_TRIG_TAB[k];
+    for (int k = threadIdx.x; k < BM_LOG_DOUBLES; k += blockDim.x) tab[k] = BM_LOG_TAB[k];
+    for (int k = threadIdx.x; k < 512; k += blockDim.x) tab[BM_LOG_DOUBLES + k] = BM_TRIG_TAB[k];
 }
 
+// ln(x) for x in [2^-54, 1) (the uniform of u53): x = m 2^e, m in [1/2, 1);
+// the cell of m is the top 9 mantissa bits -- a bit field of x's high word (x
+// and m share the mantissa); ln x = e ln 2 - ln c_k + log1p(m c_k - 1).  e <= 0
+// and ln m < 0 have one sign, and the last cell (m -> 1) has c = 1 exactly, so
+// nothing cancels.
 __device__ __forceinline__ double bm_log_tab(double x, const double* __restrict__ tab) {
     int e;
-    double m = frexp(x, &e);
-    // m < sqrt(1/2): m *= 2, e -= 1 -- the doubling as an exponent add (exact,
-    // the same bits; one ldexp instead of an add and two selects)
-    const int lo = m < 0.70710678118654752440 ? 1 : 0;
-    m = ldexp(m, lo);
-    e -= lo;
-    int k = (int)((m - BM_LOG_LO) * BM_LOG_INVW);
-    k = min(max(k, 0), 127);
-    const double c = tab[2 * k], nlc = tab[2 * k + 1];
+    const double m = frexp(x, &e);
+    // byte offset of cell k's {c_k, -ln c_k} pair: ((hi >> 11) & 511) * 16
+    static_assert(BM_LOG_CELLS == 512, "the bit field below assumes 9 index bits");
+    const uint32_t off = ((uint32_t)__double2hiint(x) >> 7) & 0x1FF0u;
+    const double2 cv = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(tab) + off);
+    const double c = cv.x, nlc = cv.y;
     const double r = fma(m, c, -1.0);
-    double p = 0.14285714285714285;
-    p = fma(p, r, -0.16666666666666666);
-    p = fma(p, r, 0.2);
-    p = fma(p, r, -0.25);
+    double p = fma(r, 0.2, -0.25);
     p = fma(p, r, 0.3333333333333333);
     p = fma(p, r, -0.5);
     const double l1p = fma(p * r, r, r);
@@ -274,30 +281,29 @@ __device__ __forceinline__ double bm_log_tab(double x, const double* __restrict_
     return fma(de, 0.6931471805599453, fma(de, 2.3190468138462996e-17, nlc + l1p));
 }
 
-// sin, cos of 2 pi u for u = (K + 0.5) 2^-53, K = (wz >> 5) 2^26 + (ww >> 6)
+// sin, cos of 2 pi u for u = (K + 0.5) 2^-53, K = (wz >> 5) 2^26 + (ww >> 6):
+// cell k = the top 8 bits (wz >> 24), the remainder angle measured from the
+// cell's centre, phi = (K' + 0.5 - 2^44) 2 pi 2^-53 with K' the low 45 bits
 __device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const double* __restrict__ tab,
                                               double& sn, double& cs) {
     const uint32_t k = wz >> 24;
-    // ph = ((K + 0.5) 2^-53) 2 pi with the power-of-two scaling folded into the
-    // constant: the scaling is exact, so this is the same product (same bits)
-    // in one multiply instead of two
-    // y = K + 0.5 (K < 2^45, exact either way) built from the bits: 2^52 + K as
-    // a double (hi word 0x433 | K >> 32, lo word the low 32 bits of K), less
-    // 2^52 - 0.5 -- integer ops and one add instead of two conversions and two ops
-    const uint32_t kh = (wz >> 5) & 0x7FFFFu;                      // K = kh 2^26 + (ww >> 6)
+    // 2^52 + K' as a double from its bits (hi word 0x433 | K' >> 32, lo word the
+    // low 32 bits of K'), less 2^52 + 2^44: K' - 2^44, exact; then one fma
+    // (y + 1/2) 2 pi 2^-53 (the power-of-two scaling folded into the constant)
+    const uint32_t kh = (wz >> 5) & 0x7FFFFu;                      // K' = kh 2^26 + (ww >> 6)
     const uint32_t lo = __builtin_amdgcn_alignbit(kh, ww, 6);      // (kh << 26) | (ww >> 6)
     const uint32_t hi = ((wz >> 11) & 0x1FFFu) | 0x43300000u;      // 0x433 | kh >> 6
-    const double y = __hiloint2double((int)hi, (int)lo) - 4503599627370495.5;
-    const double ph = y * (6.283185307179586 / 9007199254740992.0);
+    const double y = __hiloint2double((int)hi, (int)lo) - 4521191813414912.0;
+    constexpr double S = 6.283185307179586 / 9007199254740992.0;
+    const double ph = fma(y, S, 0.5 * S);
     const double p2 = ph * ph;
-    double ps = fma(p2, -1.984126984126984e-4, 8.333333333333333e-3);
-    ps = fma(ps, p2, -0.16666666666666666);
+    const double ps = fma(p2, 8.333333333333333e-3, -0.16666666666666666);
     const double sph = fma(ph * p2, ps, ph);
-    double pc = fma(p2, 2.48015873015873e-5, -1.388888888888889e-3);
-    pc = fma(pc, p2, 4.1666666666666664e-2);
+    double pc = fma(p2, -1.388888888888889e-3, 4.1666666666666664e-2);
     pc = fma(pc, p2, -0.5);
     const double cph = fma(pc, p2, 1.0);
-    const double sk = tab[256 + 2 * k], ck = tab[256 + 2 * k + 1];
+    const double2 tv = reinterpret_cast<const double2*>(tab + BM_LOG_DOUBLES)[k];     // 16-B aligned tab
+    const double sk = tv.x, ck = tv.y;
     sn = fma(sk, cph, ck * sph);
     cs = fma(ck, cph, -(sk * sph));
 }
