@@ -153,6 +153,47 @@ def sweep_roofline(args, prof, alg_bytes, achieved, sweep_avg_ms, sweep_n, one_g
                 "note": "the sweep is close to issue-bound as well (Philox + Box-Muller per normal, DESIGN.md 3): "
                         "valu_issue_frac = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) from "
                         "the profile pass (profiles/pmc_traffic.json)"}
+    # the issue ceiling from the MEASURED instruction-class mix (VERDICT r05 item 1;
+    # tools/sweep_issue_model.py): the loop's VALU opcodes from the ISA, each
+    # priced at its measured cycles per wave-instruction (8 waves per SIMD,
+    # tools/microbench/valu_rate.py), x the launch's wave-rows: the rate at which
+    # 1024 SIMDs at the 2.4 GHz peak clock could issue rows of this mix
+    model = {}
+    try:
+        with open(os.path.join(HERE, "profiles", "r06_sweep_issue_model.json")) as f:
+            model = json.load(f)
+    except (OSError, ValueError):
+        pass
+    if model and args.lmax == 1024 and args.nchains == 32 and args.fields == 3:
+        rows = model["wave_rows_per_launch"]
+        cpr = model["issue_cycles_per_row"]
+        ach = rows / (sweep_avg_ms * 1e-3) / 1e9
+        peak = VALU_SIMDS * VALU_CLOCK_GHZ / cpr
+        cyc = prof.get("valu_busy_simd_cycles_per_launch")
+        return {"bound": "valu", "kernel": "k_cr_sweep (sky map not stored)",
+                "achieved": round(ach, 4), "peak": round(peak, 4), "unit": "G wave-rows/s",
+                "frac": round(ach / peak, 4), **common,
+                "issue_model": {"wave_rows_per_launch": rows, "issue_cycles_per_row": cpr,
+                                "valu_instructions_per_row": model["valu_instructions_per_row"],
+                                "class_cycles_per_row": {k: v["cycles"] for k, v in model["classes"].items()},
+                                "class_cycles_per_instr": {k: v["cycles_per_instr"] for k, v in model["classes"].items()},
+                                "microbench_loop_overhead_per_instr": model.get("microbench_loop_overhead_per_instr"),
+                                "source": "profiles/r06_sweep_issue_model.json (tools/sweep_issue_model.py) x "
+                                          "profiles/r06_valu_rate.json (tools/microbench/valu_rate.py)"},
+                "pmc": {"valu_busy_simd_cycles_per_launch": cyc,
+                        "valu_busy_frac_of_peak_clock": round(cyc / (VALU_SIMDS * VALU_CLOCK_GHZ * 1e9 *
+                                                                     sweep_avg_ms * 1e-3), 4) if cyc else None,
+                        "valu_busy_frac_at_run_clock": prof.get("valu_issue_frac"),
+                        "dual_issue_frac": prof.get("dual_issue_frac"),
+                        "source": prof.get("valu_source")},
+                "hbm_frac_unique_bytes": round(achieved / HBM_PEAK_GBS, 4),
+                "note": "issue-bound: Philox4x32-10 + fp64 Box-Muller per normal (DESIGN.md 3).  peak = 1024 SIMDs x "
+                        "2.4 GHz / the mix-weighted cycles per wave-row; achieved = the launch's wave-rows / its "
+                        "duration measured here (hipEvents in the timed graph).  Measured class costs (8 waves per "
+                        "SIMD, the microbench loop's overhead calibrated out on v_fma_f64 = 4): fp64 and most 32-bit "
+                        "VALU ~3.9-4.0, v_mad_u64_u32 4.2, v_bitop3 3.2, v_add/xor_u32 2.1 (they dual-issue only "
+                        "beside each other: mixed with fp64 every op costs a quad-cycle; the launch's PMC "
+                        "dual-issue fraction is pmc.dual_issue_frac), v_rsq_f64 16."}
     cyc = prof.get("valu_busy_simd_cycles_per_launch")
     peak = VALU_SIMDS * VALU_CLOCK_GHZ
     ach = cyc / (sweep_avg_ms * 1e-3) / 1e9 if cyc else None

@@ -124,7 +124,6 @@ struct gs_plan {
     // D_l into dl_tmp: the split MH reads its start state from there (both
     // workgroups of a chain see the pre-MH D_l whatever their order)
     bool snap_ok = false;
-    int* sweep_q = nullptr;          // [9] the sweep's per-XCD work-queue counters (GS_SWEEP_DYN builds)
     const double* pro_dl = nullptr;
     uint32_t pro_slo = 0, pro_shi = 0, pro_it = 0;
     bool iter_dev_on = false;
@@ -671,9 +670,12 @@ __device__ __forceinline__ void cr_sweep_task(int wg, int L, int nchains, int nt
     sweep_partials_store<NS>(acc, tw, w, lane, tile_ok && (cw * gc.y) * tm <= lhi, po, red);
 }
 
-// nlog: logical workgroups (chains x task pairs); the grid holds nlog sweep
-// workgroups, or (experiment GS_SWEEP_DYN) fewer that take logical ones from a
-// work queue (qc[0]: next task, qc[1]: finished workgroups)
+// nlog: logical workgroups (chains x task pairs), one per sweep workgroup.
+// r06 measured and not kept: fewer, persistent workgroups (4 per CU) taking the
+// tasks in strides or from a global / per-XCD work queue -- occupancy 4.0 instead
+// of ~3.1-3.3, but 200-289 against 191-195 us per configs[2] step: the loop-form
+// kernel allocates more registers (and spills) and a global queue loses the
+// XCD-local data reads (tools/sweep_timeline.py, tools/lib_ab.py)
 #ifndef GS_SWEEP_MINW
 #define GS_SWEEP_MINW 1
 #endif
@@ -683,8 +685,7 @@ __global__ __launch_bounds__(256, GS_SWEEP_MINW) void k_cr_sweep(int L, int ncha
                                                   const double* __restrict__ params, const double* __restrict__ z,
                                                   double* __restrict__ s, double* __restrict__ partials,
                                                   uint32_t seed_lo, uint32_t seed_hi, IterArg itarg, uint32_t substep,
-                                                  int chain0, SweepOp op, ClsPre cp, ProPre pp, int nlog,
-                                                  int* __restrict__ qc) {
+                                                  int chain0, SweepOp op, ClsPre cp, ProPre pp, int nlog) {
     if constexpr (PRE == 0 && ZM == 0) {
         if ((int)blockIdx.x < pp.n) {
             pro_pre_item<F>(pp, (int)blockIdx.x, nchains, seed_lo, seed_hi, itarg, chain0);
@@ -719,43 +720,13 @@ __global__ __launch_bounds__(256, GS_SWEEP_MINW) void k_cr_sweep(int L, int ncha
     // of logical ids so that all chains of one (tiles, rows) block share one
     // XCD's L2 for the data reads (speed only -- any placement is correct)
     const int bid = (int)blockIdx.x - pp.n;     // (pp.n % 8 == 0: the same XCD as blockIdx.x)
-    const int nwg = (int)gridDim.x - pp.n, xcd = bid & 7, q8 = nlog >> 3, r8 = nlog & 7;
+    const int xcd = bid & 7, q8 = nlog >> 3, r8 = nlog & 7;
     const int base = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
 #if defined(GS_SWEEP_WGTIME)
     const unsigned long long tl0 = wall_clock64();
 #endif
-#if !defined(GS_SWEEP_DYN)
     cr_sweep_task<F, ZM, STORE>(base + (bid >> 3), L, nchains, ntile, nchunkg, tm, tw, tasks, d, params, z, s,
                                 partials, seed_lo, seed_hi, iter, substep, chain0, op, tab, red);
-    (void)nwg; (void)qc;
-#else
-    // per-XCD work queues (qc[x], x = this workgroup's XCD under the b % 8
-    // placement): each workgroup takes the next task of its XCD's logical range
-    // (dealt heaviest first), then steals from the other XCDs' ranges; qc[8]
-    // counts finished workgroups, the last one resets the queues for the next
-    // launch (every workgroup has taken its last task index by then)
-    __shared__ int s_task;
-    for (int v = 0; v < 8; ++v) {
-        const int x = (xcd + v) & 7;
-        const int bx = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
-        const int cnt = q8 + (x < r8 ? 1 : 0);
-        for (;;) {
-            if (threadIdx.x == 0) s_task = atomicAdd(&qc[x], 1);
-            __syncthreads();
-            const int k = s_task;
-            __syncthreads();
-            if (k >= cnt) break;
-            cr_sweep_task<F, ZM, STORE>(bx + k, L, nchains, ntile, nchunkg, tm, tw, tasks, d, params, z, s,
-                                        partials, seed_lo, seed_hi, iter, substep, chain0, op, tab, red);
-            __syncthreads();                    // red is reused by the next task
-        }
-    }
-    if (threadIdx.x == 0) {
-        if (atomicAdd(&qc[8], 1) == nwg - 1)
-            for (int x = 0; x < 9; ++x) atomicExch(&qc[x], 0);
-    }
-    (void)base;
-#endif
 #if defined(GS_SWEEP_WGTIME)
     __syncthreads();
     if (threadIdx.x == 0 && bid < SW_TL_MAX) {
@@ -2412,7 +2383,6 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
     rc |= dev_alloc(&p->dl_tmp, nc * p->nspec * maxbins);
     rc |= dev_alloc(&p->u_nat, nc * std::max(p->nacc, 1));
     rc |= dev_alloc(&p->iter_dev, 4);
-    rc |= dev_alloc(&p->sweep_q, 9);
     {
         const char* e = gs_detail::option("GS_CLS_PRE");
         p->cls_pre = e ? std::atoi(e) != 0 : p->nchains <= 4;
@@ -2429,7 +2399,7 @@ int gs_plan_create(const gs_model_desc* desc, gs_plan** out) {
 
 int gs_plan_destroy(gs_plan* p) {
     if (!p) return 0;
-    void* bufs[] = {p->iter_dev, p->sweep_q, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
+    void* bufs[] = {p->iter_dev, p->ell2blk, p->gbuf, p->phase_tab, p->phase_rng, p->meta, p->bl, p->ell2bin, p->bins, p->blocks, p->prop_sd, p->tasks, p->partials, p->u_nat,
                     p->params, p->stats, p->prop, p->logr, p->dl_tmp, p->cls_var, p->phase_tab_s, p->phase_rng_s};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2636,7 +2606,7 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
 #define GS_SWL(FF, SS) hipLaunchKernelGGL((k_cr_sweep<FF, 0, SS, 4>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                           p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,    \
                                           s_out, p->partials, slo, shi, p->ita(iteration), substep, p->chain0, op, cp, \
-                                          ProPre{}, nlog, p->sweep_q)
+                                          ProPre{}, nlog)
 #define GS_SWL2(FF) do { if (st) GS_SWL(FF, true); else GS_SWL(FF, false); } while (0)
         if (p->F == 1) GS_SWL2(1); else if (p->F == 2) GS_SWL2(2); else GS_SWL2(3);
 #undef GS_SWL2
@@ -2665,20 +2635,12 @@ static int sweep_launch(gs_plan* p,const double* d_alm, const double* params, co
         pp.prop = p->prop; pp.logr = p->logr; pp.u_out = p->u_nat; pp.snap = p->dl_tmp;
     }
     pp.n = (pp.nbp + pp.nbu + pp.nbv + 7) / 8 * 8;
-#if defined(GS_SWEEP_DYN)
-    // experiment: GS_SWEEP_DYN workgroups per CU taking tasks from the queue
-    {
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess) ncu = 256;
-        g.x = (unsigned)std::min(nlog, GS_SWEEP_DYN * ncu / 8 * 8);
-    }
-#endif
     g.x += pp.n;
 #define GS_SW(FF, RR, SS) hipLaunchKernelGGL((k_cr_sweep<FF, RR, SS>), g, b, 0, S(stream), p->L, p->nchains, p->ntile, \
                                              p->nchunkg, p->rows_per_task, p->sweep_tw, p->tasks, d_alm, params, z,   \
                                              s_out,                                                                   \
                                              p->partials, slo, shi, p->ita(iteration), substep, p->chain0, \
-                                             op, none, pp, nlog, p->sweep_q)
+                                             op, none, pp, nlog)
 #define GS_SWF(FF) do { if (given) GS_SW(FF, 2, false); else if (rep && st) GS_SW(FF, 1, true); \
                         else if (rep) GS_SW(FF, 1, false); else if (st) GS_SW(FF, 0, true);            \
                         else GS_SW(FF, 0, false); } while (0)

@@ -250,7 +250,8 @@ __device__ inline void gamma_mt_pair(double alpha0, double alpha1, Key k, uint32
 // r06: the cells follow the frexp mantissa directly (the r05 table covered
 // [sqrt(1/2), sqrt(2)), which needed a compare, a select, an ldexp and an
 // exponent fix-up per draw, and a float->int index) and are twice as many, and
-// the trig cells are centred: 10 instructions fewer per normal pair.
+// the trig cells are centred, and the log returns -2 ln u (the radius argument,
+// the factor folded into its constants): 11 instructions fewer per normal pair.
 constexpr int BM_LOG_DOUBLES = 2 * BM_LOG_CELLS;
 constexpr int BM_TAB_DOUBLES = BM_LOG_DOUBLES + 512;
 
@@ -259,26 +260,28 @@ __device__ __forceinline__ void bm_stage_tables(double* tab) {
     for (int k = threadIdx.x; k < 512; k += blockDim.x) tab[BM_LOG_DOUBLES + k] = BM_TRIG_TAB[k];
 }
 
-// ln(x) for x in [2^-54, 1) (the uniform of u53): x = m 2^e, m in [1/2, 1);
-// the cell of m is the top 9 mantissa bits -- a bit field of x's high word (x
-// and m share the mantissa); ln x = e ln 2 - ln c_k + log1p(m c_k - 1).  e <= 0
-// and ln m < 0 have one sign, and the last cell (m -> 1) has c = 1 exactly, so
-// nothing cancels.
-__device__ __forceinline__ double bm_log_tab(double x, const double* __restrict__ tab) {
+// -2 ln(x 2^-53) for x = K + 1/2 in [1/2, 2^53) (u53's uniform before its exact
+// 2^-53 scaling, which becomes an integer exponent offset): the Box-Muller radius
+// argument directly.  x = m 2^e, m in [1/2, 1); the cell of m is the top 9
+// mantissa bits -- a bit field of x's high word (x and m share the mantissa);
+// -2 ln x = e (-2 ln 2) + 2 ln c_k - 2 log1p(m c_k - 1), the last term as
+// r (-2 + r (1 + r (-2/3 + r (1/2 - 2/5 r)))).  e <= 0 and ln m < 0 have one
+// sign, and the last cell (m -> 1) has c = 1 exactly, so nothing cancels.
+__device__ __forceinline__ double bm_m2log_tab(double x, const double* __restrict__ tab) {
     int e;
     const double m = frexp(x, &e);
-    // byte offset of cell k's {c_k, -ln c_k} pair: ((hi >> 11) & 511) * 16
+    e -= 53;
+    // byte offset of cell k's {c_k, 2 ln c_k} pair: ((hi >> 11) & 511) * 16
     static_assert(BM_LOG_CELLS == 512, "the bit field below assumes 9 index bits");
     const uint32_t off = ((uint32_t)__double2hiint(x) >> 7) & 0x1FF0u;
     const double2 cv = *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(tab) + off);
-    const double c = cv.x, nlc = cv.y;
-    const double r = fma(m, c, -1.0);
-    double p = fma(r, 0.2, -0.25);
-    p = fma(p, r, 0.3333333333333333);
-    p = fma(p, r, -0.5);
-    const double l1p = fma(p * r, r, r);
+    const double r = fma(m, cv.x, -1.0);
+    double q = fma(r, -0.4, 0.5);
+    q = fma(q, r, -0.6666666666666666);
+    q = fma(q, r, 1.0);
+    q = fma(q, r, -2.0);
     const double de = (double)e;
-    return fma(de, 0.6931471805599453, fma(de, 2.3190468138462996e-17, nlc + l1p));
+    return fma(de, -1.3862943611198906, fma(de, -4.638093627692599e-17, cv.y + q * r));
 }
 
 // sin, cos of 2 pi u for u = (K + 0.5) 2^-53, K = (wz >> 5) 2^26 + (ww >> 6):
@@ -309,9 +312,9 @@ __device__ __forceinline__ void bm_sincos_tab(uint32_t wz, uint32_t ww, const do
 }
 
 __device__ __forceinline__ void box_muller_tab(uint4 w, const double* __restrict__ tab, double& z0, double& z1) {
-    const double u1 = u53(w.x, w.y);
-    const double lg = bm_log_tab(u1, tab);
-    const double r = bm_sqrt_radius(-2.0 * lg);
+    // u1 = x 2^-53 (u53), x = K + 1/2 formed exactly as u53 forms it
+    const double x = (double)(w.x >> 5) * 67108864.0 + (double)(w.y >> 6) + 0.5;
+    const double r = bm_sqrt_radius(bm_m2log_tab(x, tab));
     double sn, cs;
     bm_sincos_tab(w.z, w.w, tab, sn, cs);
     z0 = r * cs;

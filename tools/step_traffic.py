@@ -40,15 +40,23 @@ def main():
             marker()
             step()
             marker()
+            n_sht, ncomp = 2.0, 3
         else:
             runner, go, n_sht, what, pcg = bench.masked_head_setup(args, ctx)
+            n0 = len(pcg.pcg_iterations) if pcg is not None else 0
             torch.cuda.synchronize()
             marker()
             go()
             marker()
+            ncomp = 2
+            if pcg is not None:     # bench.py's count: 2 per CG iteration + 7 for the right-hand side
+                import numpy as np
+                n_sht = 2 * float(np.mean(pcg.pcg_iterations[n0:])) + 7
         torch.cuda.synchronize()
-        print(f"step_traffic {args.workload} N_side {args.nside} l_max {args.lmax} chains {args.nchains} "
-              f"mask {args.mask}: done", flush=True)
+        import json
+        print("STEP_TRAFFIC " + json.dumps({"workload": args.workload, "nside": args.nside, "lmax": args.lmax,
+                                           "nchains": args.nchains, "mask": args.mask, "n_sht": n_sht,
+                                           "ncomp": ncomp}), flush=True)
     finally:
         ctx.close()
 

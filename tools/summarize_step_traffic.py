@@ -7,7 +7,10 @@ kernels and the ratio to the step's algorithmic bytes (every transform reads its
 input and writes its output once: 8 ncomp ((L+1)^2 + Npix) bytes per map and
 transform, bench.py's SHT count per step).
 
-usage: python tools/summarize_step_traffic.py <key> <fetch_dir> <write_dir> <n_sht> <nchains> <ncomp> <nside> <lmax>
+usage: python tools/summarize_step_traffic.py <fetch_dir> <write_dir> <log>
+(<log>: tools/step_traffic.py's output, whose STEP_TRAFFIC line names the
+workload and its SHT count; the record goes to pmc_traffic.json key
+step_<workload>_N<nside>_L<lmax>_B<nchains>_<mask>)
 """
 import collections
 import csv
@@ -33,14 +36,16 @@ def window(path, counter):
 
 
 def main():
-    key, fdir, wdir = sys.argv[1:4]
-    n_sht, B, ncomp, N, L = float(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7]), int(sys.argv[8])
+    fdir, wdir, log = sys.argv[1:4]
+    meta = json.loads(next(l for l in open(log) if l.startswith("STEP_TRAFFIC "))[len("STEP_TRAFFIC "):])
+    n_sht, B, ncomp, N, L = float(meta["n_sht"]), meta["nchains"], meta["ncomp"], meta["nside"], meta["lmax"]
+    key = f"step_{meta['workload']}_N{N}_L{L}_B{B}_{meta['mask']}"
     f = window(os.path.join(fdir, "run_counter_collection.csv"), "FETCH_SIZE")
     w = window(os.path.join(wdir, "run_counter_collection.csv"), "WRITE_SIZE")
     per = {k: 2 * 1024 * f.get(k, 0.0) + 1024 * w.get(k, 0.0) for k in set(f) | set(w)}
     total = sum(per.values())
     alg = n_sht * 8 * ncomp * ((L + 1) ** 2 + 12 * N * N) * B
-    tag = os.path.basename(os.path.dirname(fdir.rstrip("/")))
+    tag = "r06_" + key
     dst = {}
     for d, c in ((fdir, "fetch"), (wdir, "write")):
         out = os.path.join(ROOT, "profiles", f"{tag}_{c}.csv")
