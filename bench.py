@@ -615,10 +615,9 @@ def run_masked(args, ctx, cpu=None):
         return None
     fl = sht_flops(N, L, 20)
     achieved = 2 * fl / ((t_syn + t_ana) * 1e-3) / 1e12
-    # HBM bytes of the pair's Legendre kernels from their PMC passes (per launch;
-    # the ring stages are not in them): profiles/pmc_traffic.json
-    tp = load_profile(args.profile_json, f"masked_sht_N{N}_L{L}_TEB")
-    traffic = (tp["alm2map_legendre_bytes"] + tp["map2alm_legendre_bytes"]) if tp else None
+    # HBM bytes of one whole step (every kernel between two markers,
+    # tools/step_traffic.py + tools/summarize_step_traffic.py): profiles/pmc_traffic.json
+    tp = load_profile(args.profile_json, f"step_masked_N{N}_L{L}_B{B}_{args.mask}")
     return {
         "metric": METRIC % (N, L),
         "value": round(args.steps * B * ctx.world / elapsed, 4),
@@ -632,7 +631,11 @@ def run_masked(args, ctx, cpu=None):
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
         "roofline": {"bound": "fp64", "kernel": "gs_sht alm2map + map2alm (TEB)", "achieved": round(achieved, 2),
                      "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFS, 4),
-                     "traffic": traffic, "traffic_note": (tp or {}).get("source"),
+                     "traffic": tp.get("hbm_bytes_per_step"),
+                     "traffic_unit": "HBM bytes per step (every kernel of one step, PMC)",
+                     "traffic_over_algorithmic": tp.get("traffic_over_algorithmic"),
+                     "algorithmic_bytes_per_step": tp.get("algorithmic_bytes_per_step"),
+                     "traffic_source": tp.get("source"),
                      "algorithmic_flops_per_launch": fl,
                      "avg_launch_ms": {"alm2map": round(t_syn, 3), "map2alm": round(t_ana, 3)}},
         "cpu_baseline": _finalize_cpu(cpu),
@@ -757,11 +760,9 @@ def run_masked_head(args, ctx, cpu=None):
                             "return at once"}
     fl = n_sht * sht_flops(N, L, 16) * B
     achieved = fl / (elapsed / args.steps) / 1e12
-    # HBM bytes of the step's transforms from the PMC pass of the same batched
-    # transform (profiles/pmc_traffic.json; the SHT kernels are ~90 % of the step)
-    tprof = load_profile(args.profile_json, f"masked_sht_N{N}_L{L}_B{B}")
-    traffic = (int(n_sht * tprof["bytes_per_transform_per_map"] * B)
-               if tprof.get("bytes_per_transform_per_map") else None)
+    # HBM bytes of one whole step (every kernel between two markers,
+    # tools/step_traffic.py + tools/summarize_step_traffic.py): profiles/pmc_traffic.json
+    tprof = load_profile(args.profile_json, f"step_{args.workload}_N{N}_L{L}_B{B}_{args.mask}")
     return {
         "metric": METRIC % (N, L),
         "value": round(args.steps * B * ctx.world / elapsed, 4),
@@ -780,8 +781,10 @@ def run_masked_head(args, ctx, cpu=None):
                    "rng": "native philox4x32-10", "parallelism": f"chains sharded over {ctx.world} GPU(s)"},
         "roofline": {"bound": "fp64", "kernel": f"{n_sht:.1f} spin-2 SHT-equivalents per chain-iteration",
                      "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP64_VALU_PEAK_TFS, 4), "traffic": traffic,
-                     "traffic_unit": "HBM bytes per step (the transforms', PMC)",
+                     "frac": round(achieved / FP64_VALU_PEAK_TFS, 4), "traffic": tprof.get("hbm_bytes_per_step"),
+                     "traffic_unit": "HBM bytes per step (every kernel of one step, PMC)",
+                     "traffic_over_algorithmic": tprof.get("traffic_over_algorithmic"),
+                     "algorithmic_bytes_per_step": tprof.get("algorithmic_bytes_per_step"),
                      "traffic_source": tprof.get("source"),
                      "algorithmic_flops_per_step": fl},
         "cpu_baseline": _finalize_cpu(cpu, pcg_info["cg_iterations_per_solve"] if pcg_info else None),

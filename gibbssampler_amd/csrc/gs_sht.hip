@@ -96,6 +96,20 @@ struct LegCoef {
     double Rm, pad;
 };
 
+// The analysis' form of (l, m): the recurrence step l -> l + 1 (a, b of l + 1)
+// and the spin-2 terms of l divided by Q_l, which the ring reduction's output
+// multiplies back (acq[l] = Q_l; 0 for l < 2):
+//   F1 / (is2 Q) = R' (x lambda_{l-1}) - (P' + sin^2) lambda_l
+//   F2 / (is2 Q) = Rm' lambda_{l-1} - T' (x lambda_l)
+// 12 scalar registers per l (LegCoef's walk reads 16: its l and the a, b of
+// l + 1), and every fp64 operation takes at most one of them (the VALU reads
+// one scalar operand per instruction).
+struct AnaCoef {
+    double a1, b1;   // lambda_{l+1} = a1 (x lambda_l - b1 lambda_{l-1})
+    double P, R;     // P / Q, R / Q
+    double T, Rm;    // T / Q, Rm / Q
+};
+
 struct ShtDev {
     int L, npair, ngroup, nlm;
     const PairGeom* geom;
@@ -257,6 +271,13 @@ __global__ __launch_bounds__(256) void k_sht_onset(ShtDev D, const double* __res
 // with exactly the transform's step and rescaling (rec_step below), so a
 // segment entered at lA continues the same sequence a single walk would hold
 __device__ __forceinline__ void rec_step(const LegCoef& c, double x, double& v0, double& v1);
+
+// x lambda as its own rounded product (never contracted into a neighbouring
+// add): the recurrence and the spin-2 terms share it (rec_from below)
+__device__ __forceinline__ double mul_nc(double a, double b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
 __global__ __launch_bounds__(256) void k_sht_segstate(ShtDev D) {
     const int L = D.L, npair = D.npair, S = D.seg;
     const int m = blockIdx.y;
@@ -343,16 +364,31 @@ struct SynAcc {
     double sp[4], sn[4];        // Q re, Q im, U re, U im: parity + / -
 };
 
+// The spin-2 terms of one (l, ring pair), without their common factor 1/sin^2:
+//   F1 / is2 = R (x lambda_{l-1}) - (P + Q sin^2) lambda_l
+//   F2 / is2 = Rm lambda_{l-1} - T (x lambda_l)
+// (LegCoef's F1, F2 divided by is2).  x lambda_l is the recurrence's own
+// product and x lambda_{l-1} the previous step's, so a unit costs 5 fp64 ops
+// here instead of 8; the factor is2 goes onto the ring's phases (analysis) or
+// its output sums (synthesis) once per m.
+__device__ __forceinline__ double spin_f1(const LegCoef& c, double v0, double xv1, double s2) {
+    return fma(c.R, xv1, -(fma(c.Q, s2, c.P) * v0));
+}
+__device__ __forceinline__ double spin_f2(const LegCoef& c, double v1, double xv0) {
+    return fma(c.Rm, v1, -(c.T * xv0));
+}
+
+// v0 = lambda_l, v1 = lambda_{l-1}, xv0 = x v0, xv1 = x v1 (mul_nc products)
 template <int NC, bool EVEN>
-__device__ __forceinline__ void syn_accumulate(SynAcc& A, const LegCoef& c, double v0, double v1, double is2,
-                                               double xis2, double2 aT, double2 aE, double2 aB) {
+__device__ __forceinline__ void syn_accumulate(SynAcc& A, const LegCoef& c, double v0, double v1, double xv0,
+                                               double xv1, double s2, double2 aT, double2 aE, double2 aB) {
     if constexpr (NC != 2) {
         if (EVEN) { A.tp[0] = fma(aT.x, v0, A.tp[0]); A.tp[1] = fma(aT.y, v0, A.tp[1]); }
         else      { A.tn[0] = fma(aT.x, v0, A.tn[0]); A.tn[1] = fma(aT.y, v0, A.tn[1]); }
     }
     if constexpr (NC != 1) {
-        const double F1 = fma(c.R * xis2, v1, -fma(c.P, is2, c.Q) * v0);
-        const double F2 = fma(c.Rm * is2, v1, -(c.T * xis2) * v0);
+        const double F1 = spin_f1(c, v0, xv1, s2);
+        const double F2 = spin_f2(c, v1, xv0);
         double* a1 = EVEN ? A.sp : A.sn;   // F1 carries lambda's parity
         double* a2 = EVEN ? A.sn : A.sp;   // F2 the opposite one
         a1[0] = fma(aE.x, F1, a1[0]); a2[0] = fma(-aB.y, F2, a2[0]);
@@ -362,11 +398,38 @@ __device__ __forceinline__ void syn_accumulate(SynAcc& A, const LegCoef& c, doub
     }
 }
 
-__device__ __forceinline__ void rec_step(const LegCoef& c, double x, double& v0, double& v1) {
-    const double vn = c.a * fma(-c.b, v1, x * v0);
+// a ring pair's phases from its sums: T from the parity sums; Q, U = -(...)
+// times the spin-2 terms' common factor is2
+template <int NC>
+__device__ __forceinline__ void syn_store(const SynAcc& A, double2* __restrict__ phi, long long plane, long long o,
+                                          double is2) {
+    int comp = 0;
+    if constexpr (NC != 2) {
+        phi[(2 * comp + 0) * plane + o] = make_double2(A.tp[0] + A.tn[0], A.tp[1] + A.tn[1]);
+        phi[(2 * comp + 1) * plane + o] = make_double2(A.tp[0] - A.tn[0], A.tp[1] - A.tn[1]);
+        ++comp;
+    }
+    if constexpr (NC != 1) {
+        const double w = -is2;
+        phi[(2 * comp + 0) * plane + o] = make_double2(w * (A.sp[0] + A.sn[0]), w * (A.sp[1] + A.sn[1]));
+        phi[(2 * comp + 1) * plane + o] = make_double2(w * (A.sp[0] - A.sn[0]), w * (A.sp[1] - A.sn[1]));
+        ++comp;
+        phi[(2 * comp + 0) * plane + o] = make_double2(w * (A.sp[2] + A.sn[2]), w * (A.sp[3] + A.sn[3]));
+        phi[(2 * comp + 1) * plane + o] = make_double2(w * (A.sp[2] - A.sn[2]), w * (A.sp[3] - A.sn[3]));
+    }
+}
+
+// one recurrence step from the product xv0 = mul_nc(x, v0)
+__device__ __forceinline__ void rec_from(const LegCoef& c, double xv0, double& v0, double& v1) {
+    const double vn = c.a * fma(-c.b, v1, xv0);
     v1 = v0;
     v0 = vn;
 }
+__device__ __forceinline__ void rec_step(const LegCoef& c, double x, double& v0, double& v1) {
+    rec_from(c, mul_nc(x, v0), v0, v1);
+}
+// ring constants of the spin-2 terms: sin^2 = 1 / is2 (0 on an idle lane)
+__device__ __forceinline__ double ring_s2(bool act, double is2) { return act ? 1.0 / is2 : 0.0; }
 
 template <int NC, int SR>
 __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const LegCoef* __restrict__ coef,
@@ -380,7 +443,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g0 = tile * (LEG_BLOCK / 64) * SR + wave * SR;   // onset group of slot 0
-    double x[SR], is2[SR], xis2[SR];
+    double x[SR], s2[SR];
     int pr[SR];
     bool act[SR];
 #pragma unroll
@@ -388,8 +451,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
         pr[r] = (g0 + r) * 64 + lane;
         act[r] = pr[r] < npair;
         x[r] = act[r] ? D.geom[pr[r]].x : 0.0;
-        is2[r] = act[r] ? D.geom[pr[r]].is2 : 0.0;
-        xis2[r] = x[r] * is2[r];
+        s2[r] = ring_s2(act[r], act[r] ? D.geom[pr[r]].is2 : 0.0);
     }
     const double2 z2 = make_double2(0.0, 0.0);
     for (int h = 0; h < 2; ++h) {
@@ -404,7 +466,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
             lmin = min(lmin, ls[r]);
         }
         SynAcc A[SR];
-        double v0[SR], v1[SR];
+        double v0[SR], v1[SR], xv1[SR];
         int kk[SR];
 #pragma unroll
         for (int r = 0; r < SR; ++r) {
@@ -443,8 +505,9 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
             for (int r = 0; r < SR; ++r) {
                 if (l < ls[r]) continue;
                 const double w0 = kk[r] == 0 ? v0[r] : 0.0, w1 = kk[r] == 0 ? v1[r] : 0.0;
-                if (even) syn_accumulate<NC, true>(A[r], c, w0, w1, is2[r], xis2[r], t, e, b);
-                else syn_accumulate<NC, false>(A[r], c, w0, w1, is2[r], xis2[r], t, e, b);
+                const double xw0 = mul_nc(x[r], w0), xw1 = mul_nc(x[r], w1);
+                if (even) syn_accumulate<NC, true>(A[r], c, w0, w1, xw0, xw1, s2[r], t, e, b);
+                else syn_accumulate<NC, false>(A[r], c, w0, w1, xw0, xw1, s2[r], t, e, b);
                 if (l < L) {
                     rec_step(cn, x[r], v0[r], v1[r]);
                     if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
@@ -452,7 +515,10 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
             }
             ++l;
         }
-        // ---- fast path: every live slot active and representable ----
+        // ---- fast path: every live slot active and representable; x lambda_{l-1}
+        // carried from the previous step (the same rounded product) ----
+#pragma unroll
+        for (int r = 0; r < SR; ++r) xv1[r] = mul_nc(x[r], v1[r]);
         if (l <= L && ((l - m) & 1)) {
             const LegCoef c = cf[l];
             const LegCoef cn = cf[min(l + 1, L)];
@@ -460,8 +526,10 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 if (ls[r] > L) continue;
-                syn_accumulate<NC, false>(A[r], c, v0[r], v1[r], is2[r], xis2[r], t, e, b);
-                if (l < L) rec_step(cn, x[r], v0[r], v1[r]);
+                const double xv0 = mul_nc(x[r], v0[r]);
+                syn_accumulate<NC, false>(A[r], c, v0[r], v1[r], xv0, xv1[r], s2[r], t, e, b);
+                rec_from(cn, xv0, v0[r], v1[r]);     // past L: unused
+                xv1[r] = xv0;
             }
             ++l;
         }
@@ -487,10 +555,13 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 if (ls[r] > L) continue;
-                syn_accumulate<NC, true>(A[r], c0, v0[r], v1[r], is2[r], xis2[r], t0, e0, b0);
-                rec_step(c1, x[r], v0[r], v1[r]);
-                syn_accumulate<NC, false>(A[r], c1, v0[r], v1[r], is2[r], xis2[r], t1, e1, b1);
-                rec_step(c2, x[r], v0[r], v1[r]);
+                const double xa = mul_nc(x[r], v0[r]);
+                syn_accumulate<NC, true>(A[r], c0, v0[r], v1[r], xa, xv1[r], s2[r], t0, e0, b0);
+                rec_from(c1, xa, v0[r], v1[r]);
+                const double xb = mul_nc(x[r], v0[r]);
+                syn_accumulate<NC, false>(A[r], c1, v0[r], v1[r], xb, xa, s2[r], t1, e1, b1);
+                rec_from(c2, xb, v0[r], v1[r]);
+                xv1[r] = xb;
             }
         }
         if (l <= L) {
@@ -499,7 +570,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 if (ls[r] > L) continue;
-                syn_accumulate<NC, true>(A[r], c, v0[r], v1[r], is2[r], xis2[r], t, e, b);
+                syn_accumulate<NC, true>(A[r], c, v0[r], v1[r], mul_nc(x[r], v0[r]), xv1[r], s2[r], t, e, b);
             }
         }
         // ---- outputs ----
@@ -507,21 +578,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 #pragma unroll
         for (int r = 0; r < SR; ++r) {
             if (!act[r]) continue;
-            const long long o = phi_at(m, pr[r], npair);
-            int comp = 0;
-            if constexpr (NC != 2) {
-                phi[(2 * comp + 0) * plane + o] = make_double2(A[r].tp[0] + A[r].tn[0], A[r].tp[1] + A[r].tn[1]);
-                phi[(2 * comp + 1) * plane + o] = make_double2(A[r].tp[0] - A[r].tn[0], A[r].tp[1] - A[r].tn[1]);
-                ++comp;
-            }
-            if constexpr (NC != 1) {
-                // Q = -(...), U = -(...)
-                phi[(2 * comp + 0) * plane + o] = make_double2(-(A[r].sp[0] + A[r].sn[0]), -(A[r].sp[1] + A[r].sn[1]));
-                phi[(2 * comp + 1) * plane + o] = make_double2(-(A[r].sp[0] - A[r].sn[0]), -(A[r].sp[1] - A[r].sn[1]));
-                ++comp;
-                phi[(2 * comp + 0) * plane + o] = make_double2(-(A[r].sp[2] + A[r].sn[2]), -(A[r].sp[3] + A[r].sn[3]));
-                phi[(2 * comp + 1) * plane + o] = make_double2(-(A[r].sp[2] - A[r].sn[2]), -(A[r].sp[3] - A[r].sn[3]));
-            }
+            syn_store<NC>(A[r], phi, plane, phi_at(m, pr[r], npair), D.geom[pr[r]].is2);
         }
     }
 }
@@ -558,7 +615,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
     const bool act = pr < npair;
     const double x = act ? D.geom[pr].x : 0.0;
     const double is2 = act ? D.geom[pr].is2 : 0.0;
-    const double xis2 = x * is2;
+    const double s2 = ring_s2(act, is2);
     int ls = __builtin_amdgcn_readfirstlane(D.lstart[(long long)m * D.ngroup + grp]);
     const bool tab = ls <= L && ls < lA;
     if (tab) ls = lA;
@@ -621,8 +678,9 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
             const double2 b = NC != 1 ? aB(l) : z2;
             const LegCoef cn = cf(min(l + 1, L));
             const double w0 = kk == 0 ? v0 : 0.0, w1 = kk == 0 ? v1 : 0.0;
-            if (((l - m) & 1) == 0) syn_accumulate<NC, true>(A, c, w0, w1, is2, xis2, t, e, b);
-            else syn_accumulate<NC, false>(A, c, w0, w1, is2, xis2, t, e, b);
+            const double xw0 = mul_nc(x, w0), xw1 = mul_nc(x, w1);
+            if (((l - m) & 1) == 0) syn_accumulate<NC, true>(A, c, w0, w1, xw0, xw1, s2, t, e, b);
+            else syn_accumulate<NC, false>(A, c, w0, w1, xw0, xw1, s2, t, e, b);
             if (l < L) {
                 rec_step(cn, x, v0, v1);
                 if (kk < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++kk; }
@@ -630,27 +688,33 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
             ++l;
         }
         // fast path (onset state loaded above when the onset is the first l)
+        double xv1 = mul_nc(x, v1);
         if (l <= lend && ((l - m) & 1)) {
             const LegCoef c = cf(l);
             const LegCoef cn = cf(min(l + 1, L));
             const double2 t = NC != 2 ? aT(l) : z2, e = NC != 1 ? aE(l) : z2, b = NC != 1 ? aB(l) : z2;
-            syn_accumulate<NC, false>(A, c, v0, v1, is2, xis2, t, e, b);
-            if (l < L) rec_step(cn, x, v0, v1);
+            const double xv0 = mul_nc(x, v0);
+            syn_accumulate<NC, false>(A, c, v0, v1, xv0, xv1, s2, t, e, b);
+            rec_from(cn, xv0, v0, v1);               // past L: unused
+            xv1 = xv0;
             ++l;
         }
         for (; l + 1 <= lend; l += 2) {
             const LegCoef c0 = cf(l), c1 = cf(l + 1), c2 = cf(min(l + 2, L));
             const double2 t0 = NC != 2 ? aT(l) : z2, e0 = NC != 1 ? aE(l) : z2, b0 = NC != 1 ? aB(l) : z2;
             const double2 t1 = NC != 2 ? aT(l + 1) : z2, e1 = NC != 1 ? aE(l + 1) : z2, b1 = NC != 1 ? aB(l + 1) : z2;
-            syn_accumulate<NC, true>(A, c0, v0, v1, is2, xis2, t0, e0, b0);
-            rec_step(c1, x, v0, v1);
-            syn_accumulate<NC, false>(A, c1, v0, v1, is2, xis2, t1, e1, b1);
-            rec_step(c2, x, v0, v1);
+            const double xa = mul_nc(x, v0);
+            syn_accumulate<NC, true>(A, c0, v0, v1, xa, xv1, s2, t0, e0, b0);
+            rec_from(c1, xa, v0, v1);
+            const double xb = mul_nc(x, v0);
+            syn_accumulate<NC, false>(A, c1, v0, v1, xb, xa, s2, t1, e1, b1);
+            rec_from(c2, xb, v0, v1);
+            xv1 = xb;
         }
         if (l <= lend) {
             const LegCoef c = cf(l);
             const double2 t = NC != 2 ? aT(l) : z2, e = NC != 1 ? aE(l) : z2, b = NC != 1 ? aB(l) : z2;
-            syn_accumulate<NC, true>(A, c, v0, v1, is2, xis2, t, e, b);
+            syn_accumulate<NC, true>(A, c, v0, v1, mul_nc(x, v0), xv1, s2, t, e, b);
         }
     }
     // segment partial sums -> LDS; wave 0 adds them in segment order
@@ -668,21 +732,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
 #pragma unroll
         for (int i = 0; i < 4; ++i) { A.sp[i] += o[(4 + i) * 64]; A.sn[i] += o[(8 + i) * 64]; }
     }
-    const long long plane = phi_plane(L, npair);
-    const long long o = phi_at(m, pr, npair);
-    int comp = 0;
-    if constexpr (NC != 2) {
-        phi[(2 * comp + 0) * plane + o] = make_double2(A.tp[0] + A.tn[0], A.tp[1] + A.tn[1]);
-        phi[(2 * comp + 1) * plane + o] = make_double2(A.tp[0] - A.tn[0], A.tp[1] - A.tn[1]);
-        ++comp;
-    }
-    if constexpr (NC != 1) {
-        phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[0] + A.sn[0]), -(A.sp[1] + A.sn[1]));
-        phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[0] - A.sn[0]), -(A.sp[1] - A.sn[1]));
-        ++comp;
-        phi[(2 * comp + 0) * plane + o] = make_double2(-(A.sp[2] + A.sn[2]), -(A.sp[3] + A.sn[3]));
-        phi[(2 * comp + 1) * plane + o] = make_double2(-(A.sp[2] - A.sn[2]), -(A.sp[3] - A.sn[3]));
-    }
+    syn_store<NC>(A, phi, phi_plane(L, npair), phi_at(m, pr, npair), is2);
 }
 
 // ---------------------------------------------------------------------------
@@ -1994,11 +2044,16 @@ __global__ __launch_bounds__(1024) void k_sht_apply_ring_mc(int L, int npair, lo
 // pairs in registers; the workgroup then reduces the chunk's NO x ANA_C
 // partial sums over its 256 lanes in LDS in a fixed order.
 // ---------------------------------------------------------------------------
+// v0 = lambda_l, v1 = lambda_{l-1}, xv0 / xv1 = their mul_nc products with x;
+// the spin-2 phases fp / fn [cq..] carry the factor is2 and the outputs the
+// factor Q_l (AnaCoef)
 template <int NC, bool EVEN, bool SLOW>
-__device__ __forceinline__ void ana_term(double* a, const LegCoef& c, double v0, double v1, int k, double is2,
-                                         double xis2, const double2* fp, const double2* fn) {
+__device__ __forceinline__ void ana_term(double* a, const AnaCoef& c, double v0, double v1, double xv0, double xv1,
+                                         int k, double s2, const double2* fp, const double2* fn) {
     const double lam = SLOW ? (k == 0 ? v0 : 0.0) : v0;
     const double lam1 = SLOW ? (k == 0 ? v1 : 0.0) : v1;
+    const double xl = SLOW ? (k == 0 ? xv0 : 0.0) : xv0;
+    const double xl1 = SLOW ? (k == 0 ? xv1 : 0.0) : xv1;
     int o = 0;
     if constexpr (NC != 2) {
         const double2 t = EVEN ? fp[0] : fn[0];
@@ -2008,8 +2063,8 @@ __device__ __forceinline__ void ana_term(double* a, const LegCoef& c, double v0,
     }
     if constexpr (NC != 1) {
         constexpr int cq = NC == 3 ? 1 : 0;
-        const double F1 = fma(c.R * xis2, lam1, -fma(c.P, is2, c.Q) * lam);
-        const double F2 = fma(c.Rm * is2, lam1, -(c.T * xis2) * lam);
+        const double F1 = fma(c.R, xl1, -((c.P + s2) * lam));
+        const double F2 = fma(c.Rm, lam1, -(c.T * xl));
         const double2 Q1 = EVEN ? fp[cq] : fn[cq];          // F1 parity
         const double2 U1 = EVEN ? fp[cq + 1] : fn[cq + 1];
         const double2 Q2 = EVEN ? fn[cq] : fp[cq];          // F2 parity
@@ -2021,14 +2076,21 @@ __device__ __forceinline__ void ana_term(double* a, const LegCoef& c, double v0,
     }
 }
 
+// the analysis' recurrence step (the same arithmetic as rec_from)
+__device__ __forceinline__ void rec_ana(const AnaCoef& c, double xv0, double& v0, double& v1) {
+    const double vn = c.a1 * fma(-c.b1, v1, xv0);
+    v1 = v0;
+    v0 = vn;
+}
+
 template <int NC, int ASR, bool SEGL>
-__global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegCoef* __restrict__ coef,
+__global__ __launch_bounds__(LEG_BLOCK, 2) void k_sht_anal_leg(ShtDev D, const AnaCoef* __restrict__ coef,
                                                             const double2* __restrict__ phi,
                                                             double2* __restrict__ part, int paired) {
     // SEGL (l-segmented launches): the segment's coefficients (<= seg + 2 l) are
     // staged once per workgroup in LDS with coalesced loads instead of one
     // scalar load (a memory latency) per l step and wave
-    __shared__ __attribute__((aligned(16))) LegCoef cstage[SEGL ? 68 : 1];
+    __shared__ __attribute__((aligned(16))) AnaCoef cstage[SEGL ? 68 : 1];
     constexpr int NO = NC == 1 ? 2 : (NC == 2 ? 4 : 6);   // real outputs per l
     constexpr int NV = NO * ANA_C;
     static_assert(NV <= 32, "chunk too large for the wave reduction");
@@ -2047,7 +2109,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = tile * (LEG_BLOCK / 64) * ASR + wave * ASR;
     const long long plane = phi_plane(L, npair);
-    double x[ASR], is2[ASR], xis2[ASR];
+    double x[ASR], s2[ASR];
     int pr[ASR];
     bool act[ASR];
 #pragma unroll
@@ -2055,8 +2117,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
         pr[r] = (g0 + r) * 64 + lane;
         act[r] = pr[r] < npair;
         x[r] = act[r] ? D.geom[pr[r]].x : 0.0;
-        is2[r] = act[r] ? D.geom[pr[r]].is2 : 0.0;
-        xis2[r] = x[r] * is2[r];
+        s2[r] = ring_s2(act[r], act[r] ? D.geom[pr[r]].is2 : 0.0);
     }
     for (int h = 0; h < 2; ++h) {
         const int m = h == 0 ? q : L - q;
@@ -2094,6 +2155,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                 v1[r] = s0.x; v0[r] = s0.y;
                 kk[r] = D.sstk[o];
             }
+            const double is2 = act[r] && ls[r] <= L ? D.geom[pr[r]].is2 : 0.0;
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 double2 a = make_double2(0.0, 0.0), b = a;
@@ -2101,18 +2163,20 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                     a = phi[(2LL * c + 0) * plane + phi_at(m, pr[r], npair)];
                     b = phi[(2LL * c + 1) * plane + phi_at(m, pr[r], npair)];
                 }
-                fp[r][c] = make_double2(a.x + b.x, a.y + b.y);
-                fn[r][c] = make_double2(a.x - b.x, a.y - b.y);
+                // spin-2 components carry the factor is2 of their terms
+                const double w = (NC == 3 && c == 0) || NC == 1 ? 1.0 : is2;
+                fp[r][c] = make_double2(w * (a.x + b.x), w * (a.y + b.y));
+                fn[r][c] = make_double2(w * (a.x - b.x), w * (a.y - b.y));
             }
         }
         const long long obase = cidx(L, m, m) - m;
-        const LegCoef* cf = coef + obase;
+        const AnaCoef* cf = coef + obase;
         if constexpr (SEGL) {
             __syncthreads();                        // the previous m's readers are done
             const double2* src = reinterpret_cast<const double2*>(coef);
             double2* dst = reinterpret_cast<double2*>(cstage);
-            for (int i = tid; i < (D.seg + 2) * 4; i += LEG_BLOCK)
-                dst[i] = src[(obase + min(lA + i / 4, L)) * 4 + (i & 3)];
+            for (int i = tid; i < (D.seg + 2) * 3; i += LEG_BLOCK)
+                dst[i] = src[(obase + min(lA + i / 3, L)) * 3 + i % 3];
             __syncthreads();
             cf = cstage - lA;                       // cf[l], lA <= l <= lA + seg + 1
         }
@@ -2174,7 +2238,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                     const int comp = oo >> 1;
                     double* dst = reinterpret_cast<double*>(
                         part + (((long long)tile * 4 + wave) * ncb + bmap * NC + comp) * D.nlm + obase + l);
-                    dst[oo & 1] = sum;
+                    dst[oo & 1] = sum;          // spin 2: without the factor Q_l (the finish applies it)
                 }
             }
         };
@@ -2191,8 +2255,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
             for (int cc = 0; cc < ANA_C; ++cc) {
                 const int l = l0 + cc;
                 if (l > lend) break;
-                const LegCoef c = cf[l];
-                const LegCoef cn = cf[min(l + 1, L)];
+                const AnaCoef c = cf[l];
 #pragma unroll
                 for (int r = 0; r < ASR; ++r) {
                     if (l < ls[r]) continue;                 // uniform per wave
@@ -2201,10 +2264,11 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                         v1[r] = s0.x; v0[r] = s0.y;
                         kk[r] = D.stk[(long long)m * npair + pr[r]];
                     }
-                    if ((cc & 1) == 0) ana_term<NC, true, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
-                    else ana_term<NC, false, true>(acc + cc * NO, c, v0[r], v1[r], kk[r], is2[r], xis2[r], fp[r], fn[r]);
+                    const double xw0 = mul_nc(x[r], v0[r]), xw1 = mul_nc(x[r], v1[r]);
+                    if ((cc & 1) == 0) ana_term<NC, true, true>(acc + cc * NO, c, v0[r], v1[r], xw0, xw1, kk[r], s2[r], fp[r], fn[r]);
+                    else ana_term<NC, false, true>(acc + cc * NO, c, v0[r], v1[r], xw0, xw1, kk[r], s2[r], fp[r], fn[r]);
                     if (l < L) {
-                        rec_step(cn, x[r], v0[r], v1[r]);
+                        rec_ana(c, xw0, v0[r], v1[r]);
                         if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
                     }
                 }
@@ -2225,8 +2289,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
             if (live) { l0 += ANA_C; break; }
         }
         // phase 2: full chunks, no guards (a dead slot, ls > L, has zero phases
-        // and zero state and adds exact zeros; cf[L + 1] exists: the coefficient
-        // table is padded by one entry)
+        // and zero state and adds exact zeros)
 #if defined(GS_ASM_MARKERS)
         asm volatile("; ANA_FAST_BEGIN");
 #endif
@@ -2244,20 +2307,29 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
                 for (int i = 0; i < NV; ++i) acc[i] = 0.0;
 #if GS_ANA_PF > 0
                 // coefficient lines GS_ANA_PF l ahead pulled into L2 by a vector load
-                // (lane-dependent address: two 128-B lines); consumed one chunk later
+                // (lanes 0-2: the chunk's 192 B from three 64-B steps; the table is
+                // padded by 4 entries); consumed one chunk later
                 acc[0] = pfv == 7.0e300 ? 1.0 : 0.0;
-                pfv = reinterpret_cast<const double*>(cf + min(l0 + GS_ANA_PF + 2 * (lane & 1), L + 1))[0];
+                pfv = reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + min(l0 + GS_ANA_PF, L + 1))
+                                                      + (lane % 3) * 64)[0];
 #endif
+                // x lambda_{l-1}: carried from the previous step inside the chunk
+                // (the same rounded product), recomputed at its start (a carry
+                // across chunks costs the 4-slot TEB kernel its second wave)
+                double xv1[ASR];
+#pragma unroll
+                for (int r = 0; r < ASR; ++r) xv1[r] = mul_nc(x[r], v1[r]);
 #pragma unroll
                 for (int cc = 0; cc < ANA_C; ++cc) {
                     const int l = l0 + cc;
-                    const LegCoef c = cf[l];
-                    const LegCoef cn = cf[l + 1];
+                    const AnaCoef c = cf[l];
 #pragma unroll
                     for (int r = 0; r < ASR; ++r) {
-                        if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
-                        else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], 0, is2[r], xis2[r], fp[r], fn[r]);
-                        rec_step(cn, x[r], v0[r], v1[r]);
+                        const double xv0 = mul_nc(x[r], v0[r]);
+                        if ((cc & 1) == 0) ana_term<NC, true, false>(acc + cc * NO, c, v0[r], v1[r], xv0, xv1[r], 0, s2[r], fp[r], fn[r]);
+                        else ana_term<NC, false, false>(acc + cc * NO, c, v0[r], v1[r], xv0, xv1[r], 0, s2[r], fp[r], fn[r]);
+                        rec_ana(c, xv0, v0[r], v1[r]);
+                        xv1[r] = xv0;
                     }
                 }
                 if (pend) fin_chunk(rv, pl0);
@@ -2290,11 +2362,12 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_anal_leg(ShtDev D, const LegC
     }
 }
 
-// sum tiles in fixed order, weight, sign, write the caller's layout (accumulate
+// sum tiles in fixed order, weight, sign (spin 2: and the factor Q_l the
+// Legendre stage left out, AnaCoef), write the caller's layout (accumulate
 // into it when acc != 0: the Jacobi steps of map2alm(iter > 0))
 template <int NC>
 __global__ void k_sht_anal_finish(int L, int nlm, int ntile, const double2* __restrict__ part, double w, int layout,
-                                  int acc, double* __restrict__ alm, int nmap) {
+                                  int acc, double* __restrict__ alm, int nmap, const double* __restrict__ acq) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     const int ncb = NC * nmap;                     // comps of the batch: comp = b * NC + c
     if (g >= (long long)ncb * nlm) return;
@@ -2305,9 +2378,6 @@ __global__ void k_sht_anal_finish(int L, int nlm, int ntile, const double2* __re
         const double2 v = part[((long long)t * ncb + comp) * nlm + i];
         s.x += v.x; s.y += v.y;
     }
-    const bool spin0 = NC == 1 || (NC == 3 && comp % NC == 0);
-    const double f = spin0 ? w : -w;
-    s.x *= f; s.y *= f;
     // (l, m) of complex index i
     // m = largest with cidx(L, m, m) = m(2L+3-m)/2 <= i
     const double b = 2.0 * L + 3.0;
@@ -2316,6 +2386,10 @@ __global__ void k_sht_anal_finish(int L, int nlm, int ntile, const double2* __re
     while (m > 0 && (long long)m * (2 * L + 3 - m) / 2 > i) --m;
     while (m < L && (long long)(m + 1) * (2 * L + 2 - m) / 2 <= i) ++m;
     const int l = (int)(i - (long long)m * (2 * L + 1 - m) / 2);
+    const bool spin0 = NC == 1 || (NC == 3 && comp % NC == 0);
+    const double f = spin0 ? w : -w;
+    s.x *= f; s.y *= f;
+    if (!spin0) { s.x *= acq[l]; s.y *= acq[l]; }
     double* out = alm + comp * alm_comp_stride(layout, L);
     if (layout == GS_ALM_COMPLEX) {
         if (acc) { out[2 * i] += s.x; out[2 * i + 1] += s.y; }
@@ -3376,6 +3450,8 @@ struct gs_sht {
     long long npix = 0;
     PairGeom* geom = nullptr;
     LegCoef* coef = nullptr;
+    AnaCoef* acoef = nullptr;    // [nlm + 4] the analysis' form (AnaCoef)
+    double* acq = nullptr;       // [L + 1] Q_l
     int* lstart = nullptr;
     double2* st = nullptr;
     int* stk = nullptr;
@@ -3450,7 +3526,7 @@ int sht_alloc(gs_sht* p, T** dst, size_t n) {
 }
 
 void sht_free(gs_sht* p) {
-    void* bufs[] = {p->geom, p->coef, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->sscr,
+    void* bufs[] = {p->geom, p->coef, p->acoef, p->acq, p->lstart, p->st, p->stk, p->tw, p->bsk, p->phi, p->part, p->gscr, p->sscr,
                     p->mapw, p->ain, p->segoff, p->sst, p->sstk, p->merged_pairs, p->mf_tab, p->mf_off, p->mf_b0, p->support,
                     p->wsup, p->wconst};
     for (void* b : bufs)
@@ -3612,9 +3688,23 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
             coef[base + l] = c;
         }
     }
+    std::vector<AnaCoef> acoef(p->nlm + 4, AnaCoef{});
+    std::vector<double> acq(L + 1, 0.0);
+    for (int l = 2; l <= L; ++l) acq[l] = coef[l].Q;          // m = 0 row: Q depends on l only
+    for (int m = 0; m <= L; ++m) {
+        const long long base = (long long)m * (2 * L + 1 - m) / 2;
+        for (int l = m; l <= L; ++l) {
+            const LegCoef& c = coef[base + l];
+            AnaCoef& e = acoef[base + l];
+            if (l < L) { e.a1 = coef[base + l + 1].a; e.b1 = coef[base + l + 1].b; }
+            if (l >= 2) { e.P = c.P / c.Q; e.R = c.R / c.Q; e.T = c.T / c.Q; e.Rm = c.Rm / c.Q; }
+        }
+    }
     int rc = 0;
     rc |= sht_alloc(p, &p->geom, geom.size());
     rc |= sht_alloc(p, &p->coef, coef.size() + 1);   // + one zero entry past (L, L)
+    rc |= sht_alloc(p, &p->acoef, acoef.size());
+    rc |= sht_alloc(p, &p->acq, acq.size());
     rc |= sht_alloc(p, &p->lstart, (size_t)(L + 1) * p->ngroup);
     rc |= sht_alloc(p, &p->st, (size_t)(L + 1) * p->npair);
     rc |= sht_alloc(p, &p->stk, (size_t)(L + 1) * p->npair);
@@ -3690,7 +3780,9 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     }
     if (hipMemcpy(p->geom, geom.data(), geom.size() * sizeof(PairGeom), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->coef, coef.data(), coef.size() * sizeof(LegCoef), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(p->coef + coef.size(), 0, sizeof(LegCoef)) != hipSuccess) {
+        hipMemset(p->coef + coef.size(), 0, sizeof(LegCoef)) != hipSuccess ||
+        hipMemcpy(p->acoef, acoef.data(), acoef.size() * sizeof(AnaCoef), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->acq, acq.data(), acq.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
         sht_free(p);
         return set_error("gs_sht_create: table upload failed");
     }
@@ -4199,9 +4291,9 @@ static int sht_analysis(gs_sht* p, int nmap, int ncomp, int layout, const double
     const dim3 grid(p->ana_paired ? p->L / 2 + 1 : p->L + 1, ntile, nsegz * nmap);
     const ShtDev D = p->devseg(sl);
 #define GS_AL(NC, SR) do { if (sl > 0 && sl <= 64) \
-        hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, true>), grid, dim3(LEG_BLOCK), 0, S(stream), D, p->coef, \
+        hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, true>), grid, dim3(LEG_BLOCK), 0, S(stream), D, p->acoef, \
                            p->phi, p->part, p->ana_paired); \
-    else hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), D, p->coef, \
+    else hipLaunchKernelGGL((k_sht_anal_leg<NC, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), D, p->acoef, \
                             p->phi, p->part, p->ana_paired); } while (0)
 #define GS_AL2(NC) do { if (sr == 4) GS_AL(NC, 4); else if (sr == 2) GS_AL(NC, 2); \
                         else GS_AL(NC, 1); } while (0)
@@ -4212,7 +4304,7 @@ static int sht_analysis(gs_sht* p, int nmap, int ncomp, int layout, const double
     const double w = 4.0 * PI / (double)p->npix;
     const long long n = (long long)nmap * ncomp * p->nlm;
 #define GS_AF(NC) hipLaunchKernelGGL((k_sht_anal_finish<NC>), dim3(nblocks(n, 256)), dim3(256), 0, S(stream), p->L, p->nlm, \
-                                     ntile * 4, p->part, w, layout, acc, alm, nmap)
+                                     ntile * 4, p->part, w, layout, acc, alm, nmap, p->acq)
     if (ncomp == 1) GS_AF(1); else if (ncomp == 2) GS_AF(2); else GS_AF(3);
 #undef GS_AF
     GS_LAUNCH_CHECK("k_sht_anal_finish");

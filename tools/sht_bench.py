@@ -140,7 +140,14 @@ if __name__ == "__main__":
     ap.add_argument("--mfma", action="store_true", help="batched timings on the matrix-core table path")
     ap.add_argument("--apply", action="store_true", help="also the fused weighted operator (masked PCG)")
     ap.add_argument("--band", type=float, default=0.2, help="--apply: zero weight where |cos theta| <= band")
+    ap.add_argument("--opt", action="append", default=[], help="NAME=VALUE library option (gs_option_set) "
+                                                               "before the plan is made, e.g. GS_SHT_ANA=2,1")
     args = ap.parse_args()
+    if args.opt:
+        from gibbssampler_amd import _capi
+        for o in args.opt:
+            k, v = o.split("=", 1)
+            _capi.set_option(k, v)
     if args.batch:
         bench_batch(args.nside, args.lmax or 2 * args.nside, args.reps, [int(b) for b in args.batch.split(",")],
                     tuple(int(c) for c in args.ncomp.split(",")), mfma=args.mfma, apply=args.apply, band=args.band)
