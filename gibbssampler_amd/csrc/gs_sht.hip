@@ -340,23 +340,36 @@ __device__ __forceinline__ int l_of_cidx(int L, long long i) {
 // applies the per-l beam on the way in: (b_l s) rounded, then the 1/sqrt 2 --
 // the same two roundings as a separate beam pass (the masked CR's b s, whose
 // k_mc_beam launch and scratch write this replaces)
+// acq != nullptr (the on-the-fly synthesis: its AnaCoef terms are F / Q_l):
+// the spin-2 comps of each map (nc comps: 2 = E, B; 3 = T, E, B) leave scaled by Q_l
 __global__ void k_sht_alm_in(int L, int nlm, int ncomp, const double* __restrict__ alm, int layout,
-                             double2* __restrict__ ain, const double* __restrict__ bl) {
+                             double2* __restrict__ ain, const double* __restrict__ bl, int nc = 1,
+                             const double* __restrict__ acq = nullptr) {
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (g >= (long long)ncomp * nlm) return;
     const int comp = (int)(g / nlm);
     const long long i = g % nlm;
     const double* a = alm + comp * alm_comp_stride(layout, L);
-    if (layout == GS_ALM_COMPLEX) { ain[g] = make_double2(a[2 * i], a[2 * i + 1]); return; }
-    if (i <= L) { ain[g] = make_double2(bl ? bl[i] * a[i] : a[i], 0.0); return; }
-    constexpr double IS2 = 0.70710678118654752440;
-    const long long r = 2 * i - (L + 1);
-    if (bl) {
-        const double b = bl[l_of_cidx(L, i)];
-        ain[g] = make_double2((b * a[r]) * IS2, (b * a[r + 1]) * IS2);
-        return;
+    double2 v;
+    if (layout == GS_ALM_COMPLEX) {
+        v = make_double2(a[2 * i], a[2 * i + 1]);
+    } else if (i <= L) {
+        v = make_double2(bl ? bl[i] * a[i] : a[i], 0.0);
+    } else {
+        constexpr double IS2 = 0.70710678118654752440;
+        const long long r = 2 * i - (L + 1);
+        if (bl) {
+            const double b = bl[l_of_cidx(L, i)];
+            v = make_double2((b * a[r]) * IS2, (b * a[r + 1]) * IS2);
+        } else {
+            v = make_double2(a[r] * IS2, a[r + 1] * IS2);
+        }
     }
-    ain[g] = make_double2(a[r] * IS2, a[r + 1] * IS2);
+    if (acq && !(nc == 1 || (nc == 3 && comp % 3 == 0))) {
+        const double q = acq[i <= L ? (int)i : l_of_cidx(L, i)];
+        v = make_double2(v.x * q, v.y * q);
+    }
+    ain[g] = v;
 }
 
 struct SynAcc {
@@ -364,31 +377,28 @@ struct SynAcc {
     double sp[4], sn[4];        // Q re, Q im, U re, U im: parity + / -
 };
 
-// The spin-2 terms of one (l, ring pair), without their common factor 1/sin^2:
-//   F1 / is2 = R (x lambda_{l-1}) - (P + Q sin^2) lambda_l
-//   F2 / is2 = Rm lambda_{l-1} - T (x lambda_l)
-// (LegCoef's F1, F2 divided by is2).  x lambda_l is the recurrence's own
-// product and x lambda_{l-1} the previous step's, so a unit costs 5 fp64 ops
-// here instead of 8; the factor is2 goes onto the ring's phases (analysis) or
-// its output sums (synthesis) once per m.
-__device__ __forceinline__ double spin_f1(const LegCoef& c, double v0, double xv1, double s2) {
-    return fma(c.R, xv1, -(fma(c.Q, s2, c.P) * v0));
-}
-__device__ __forceinline__ double spin_f2(const LegCoef& c, double v1, double xv0) {
-    return fma(c.Rm, v1, -(c.T * xv0));
-}
+// The spin-2 terms of one (l, ring pair) in the on-the-fly kernels, without
+// their common factors 1/sin^2 and Q_l:
+//   F1 / (is2 Q) = R' (x lambda_{l-1}) - (P' + sin^2) lambda_l
+//   F2 / (is2 Q) = Rm' lambda_{l-1} - T' (x lambda_l)
+// (AnaCoef).  x lambda_l is the recurrence's own product and x lambda_{l-1}
+// the previous step's, so a unit costs 5 fp64 ops instead of 8; is2 goes onto
+// the ring's phases (analysis) or its output sums (synthesis) once per m, Q_l
+// onto the a_lm (synthesis) or the reduced outputs (analysis).
 
-// v0 = lambda_l, v1 = lambda_{l-1}, xv0 = x v0, xv1 = x v1 (mul_nc products)
+// v0 = lambda_l, v1 = lambda_{l-1}, xv0 = x v0, xv1 = x v1 (mul_nc products);
+// c in the AnaCoef form (spin-2 terms / Q_l: aE, aB arrive scaled by Q_l,
+// k_sht_alm_in), the factor is2 applied at the output (syn_store)
 template <int NC, bool EVEN>
-__device__ __forceinline__ void syn_accumulate(SynAcc& A, const LegCoef& c, double v0, double v1, double xv0,
+__device__ __forceinline__ void syn_accumulate(SynAcc& A, const AnaCoef& c, double v0, double v1, double xv0,
                                                double xv1, double s2, double2 aT, double2 aE, double2 aB) {
     if constexpr (NC != 2) {
         if (EVEN) { A.tp[0] = fma(aT.x, v0, A.tp[0]); A.tp[1] = fma(aT.y, v0, A.tp[1]); }
         else      { A.tn[0] = fma(aT.x, v0, A.tn[0]); A.tn[1] = fma(aT.y, v0, A.tn[1]); }
     }
     if constexpr (NC != 1) {
-        const double F1 = spin_f1(c, v0, xv1, s2);
-        const double F2 = spin_f2(c, v1, xv0);
+        const double F1 = fma(c.R, xv1, -((c.P + s2) * v0));
+        const double F2 = fma(c.Rm, v1, -(c.T * xv0));
         double* a1 = EVEN ? A.sp : A.sn;   // F1 carries lambda's parity
         double* a2 = EVEN ? A.sn : A.sp;   // F2 the opposite one
         a1[0] = fma(aE.x, F1, a1[0]); a2[0] = fma(-aB.y, F2, a2[0]);
@@ -428,11 +438,18 @@ __device__ __forceinline__ void rec_from(const LegCoef& c, double xv0, double& v
 __device__ __forceinline__ void rec_step(const LegCoef& c, double x, double& v0, double& v1) {
     rec_from(c, mul_nc(x, v0), v0, v1);
 }
+// the on-the-fly kernels' step from an AnaCoef (a, b of l + 1 stored at l):
+// the same arithmetic as rec_from
+__device__ __forceinline__ void rec_ana(const AnaCoef& c, double xv0, double& v0, double& v1) {
+    const double vn = c.a1 * fma(-c.b1, v1, xv0);
+    v1 = v0;
+    v0 = vn;
+}
 // ring constants of the spin-2 terms: sin^2 = 1 / is2 (0 on an idle lane)
 __device__ __forceinline__ double ring_s2(bool act, double is2) { return act ? 1.0 / is2 : 0.0; }
 
 template <int NC, int SR>
-__global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const LegCoef* __restrict__ coef,
+__global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const AnaCoef* __restrict__ coef,
                                                              const double2* __restrict__ ain,
                                                              double2* __restrict__ phi, int paired) {
     const int L = D.L, npair = D.npair, nlm = D.nlm;
@@ -477,7 +494,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
             v0[r] = 0.0; v1[r] = 0.0; kk[r] = 0;
         }
         const long long base = cidx(L, m, m) - m;              // + l = complex index of (l, m)
-        const LegCoef* cf = coef + base;
+        const AnaCoef* cf = coef + base;
         const double2* aT = ain + base;
         const double2* aE = ain + (NC == 3 ? nlm : 0) + base;
         const double2* aB = aE + nlm;
@@ -495,12 +512,11 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
                 if (ls[r] <= L && (l < ls[r] || __any(kk[r] < 0))) live = false;
             }
             if (live) break;
-            const LegCoef c = cf[l];
+            const AnaCoef c = cf[l];
             const double2 t = NC != 2 ? aT[l] : z2;
             const double2 e = NC != 1 ? aE[l] : z2;
             const double2 b = NC != 1 ? aB[l] : z2;
             const bool even = ((l - m) & 1) == 0;
-            const LegCoef cn = cf[min(l + 1, L)];
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 if (l < ls[r]) continue;
@@ -509,7 +525,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
                 if (even) syn_accumulate<NC, true>(A[r], c, w0, w1, xw0, xw1, s2[r], t, e, b);
                 else syn_accumulate<NC, false>(A[r], c, w0, w1, xw0, xw1, s2[r], t, e, b);
                 if (l < L) {
-                    rec_step(cn, x[r], v0[r], v1[r]);
+                    rec_ana(c, mul_nc(x[r], v0[r]), v0[r], v1[r]);
                     if (kk[r] < 0 && fabs(v0[r]) > SC_HI) { v0[r] *= SC_DN; v1[r] *= SC_DN; ++kk[r]; }
                 }
             }
@@ -520,15 +536,14 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 #pragma unroll
         for (int r = 0; r < SR; ++r) xv1[r] = mul_nc(x[r], v1[r]);
         if (l <= L && ((l - m) & 1)) {
-            const LegCoef c = cf[l];
-            const LegCoef cn = cf[min(l + 1, L)];
+            const AnaCoef c = cf[l];
             const double2 t = NC != 2 ? aT[l] : z2, e = NC != 1 ? aE[l] : z2, b = NC != 1 ? aB[l] : z2;
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 if (ls[r] > L) continue;
                 const double xv0 = mul_nc(x[r], v0[r]);
                 syn_accumulate<NC, false>(A[r], c, v0[r], v1[r], xv0, xv1[r], s2[r], t, e, b);
-                rec_from(cn, xv0, v0[r], v1[r]);     // past L: unused
+                rec_ana(c, xv0, v0[r], v1[r]);       // past L: unused
                 xv1[r] = xv0;
             }
             ++l;
@@ -542,14 +557,14 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
         double pfv = 0.0;
         const double* pfs = (lane & 3) == 0 ? reinterpret_cast<const double*>(cf)
                           : reinterpret_cast<const double*>(NC == 1 ? aT : ((lane & 3) == 1 ? aT : ((lane & 3) == 2 ? aE : aB)));
-        const int pfw = (lane & 3) == 0 ? 8 : 2;            // doubles per l of the stream
+        const int pfw = (lane & 3) == 0 ? 6 : 2;            // doubles per l of the stream
 #endif
         for (; l + 1 <= L; l += 2) {
 #if GS_SYN_PF > 0
             if (pfv == 7.0e300) { if constexpr (NC == 1) A[0].tp[0] += 1.0; else A[0].sp[0] += 1.0; }
             pfv = pfs[(long long)min(l + GS_SYN_PF, L) * pfw];
 #endif
-            const LegCoef c0 = cf[l], c1 = cf[l + 1], c2 = cf[min(l + 2, L)];
+            const AnaCoef c0 = cf[l], c1 = cf[l + 1];
             const double2 t0 = NC != 2 ? aT[l] : z2, e0 = NC != 1 ? aE[l] : z2, b0 = NC != 1 ? aB[l] : z2;
             const double2 t1 = NC != 2 ? aT[l + 1] : z2, e1 = NC != 1 ? aE[l + 1] : z2, b1 = NC != 1 ? aB[l + 1] : z2;
 #pragma unroll
@@ -557,15 +572,15 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
                 if (ls[r] > L) continue;
                 const double xa = mul_nc(x[r], v0[r]);
                 syn_accumulate<NC, true>(A[r], c0, v0[r], v1[r], xa, xv1[r], s2[r], t0, e0, b0);
-                rec_from(c1, xa, v0[r], v1[r]);
+                rec_ana(c0, xa, v0[r], v1[r]);
                 const double xb = mul_nc(x[r], v0[r]);
                 syn_accumulate<NC, false>(A[r], c1, v0[r], v1[r], xb, xa, s2[r], t1, e1, b1);
-                rec_from(c2, xb, v0[r], v1[r]);
+                rec_ana(c1, xb, v0[r], v1[r]);
                 xv1[r] = xb;
             }
         }
         if (l <= L) {
-            const LegCoef c = cf[l];
+            const AnaCoef c = cf[l];
             const double2 t = NC != 2 ? aT[l] : z2, e = NC != 1 ? aE[l] : z2, b = NC != 1 ? aB[l] : z2;
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
@@ -591,7 +606,7 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_leg(ShtDev D, const Leg
 // L + 1 - m.  Waves whose segment starts past L end at once (before the
 // barrier; an ended wave no longer counts at it).
 template <int NC>
-__global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegCoef* __restrict__ coef,
+__global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const AnaCoef* __restrict__ coef,
                                                            const double2* __restrict__ ain,
                                                            double2* __restrict__ phi) {
     // per wave a slice of SEG_SLICE doubles: the segment's recurrence / spin-2
@@ -637,12 +652,12 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
     const long long base = cidx(L, m, m) - m;
     double* slice = sred + (long long)sg * SEG_SLICE;
     {
-        const LegCoef* cfg = coef + base;
+        const AnaCoef* cfg = coef + base;
         auto put = [&](int slot, int l) {
             const double2* src = reinterpret_cast<const double2*>(cfg + l);
-            double2* dst = reinterpret_cast<double2*>(slice + slot * 8);
-            const double2 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
-            dst[0] = q0; dst[1] = q1; dst[2] = q2; dst[3] = q3;
+            double2* dst = reinterpret_cast<double2*>(slice + slot * 6);
+            const double2 q0 = src[0], q1 = src[1], q2 = src[2];
+            dst[0] = q0; dst[1] = q1; dst[2] = q2;
         };
         put(lane, min(lA + lane, L));
         if (lane < 2) put(64 + lane, min(lA + 64 + lane, L));
@@ -656,7 +671,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
         }
     }
     __syncthreads();            // every wave still running reaches it (ended waves do not count)
-    const LegCoef* cfs = reinterpret_cast<const LegCoef*>(slice);
+    const AnaCoef* cfs = reinterpret_cast<const AnaCoef*>(slice);
     const double2* as = reinterpret_cast<const double2*>(slice + 66 * 8);
     auto cf = [&](int l) { return cfs[l - lA]; };
     auto aT = [&](int l) { return as[l - lA]; };
@@ -672,17 +687,16 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
                 kk = D.stk[(long long)m * npair + pr];
             }
             if (!__any(kk < 0)) break;
-            const LegCoef c = cf(l);
+            const AnaCoef c = cf(l);
             const double2 t = NC != 2 ? aT(l) : z2;
             const double2 e = NC != 1 ? aE(l) : z2;
             const double2 b = NC != 1 ? aB(l) : z2;
-            const LegCoef cn = cf(min(l + 1, L));
             const double w0 = kk == 0 ? v0 : 0.0, w1 = kk == 0 ? v1 : 0.0;
             const double xw0 = mul_nc(x, w0), xw1 = mul_nc(x, w1);
             if (((l - m) & 1) == 0) syn_accumulate<NC, true>(A, c, w0, w1, xw0, xw1, s2, t, e, b);
             else syn_accumulate<NC, false>(A, c, w0, w1, xw0, xw1, s2, t, e, b);
             if (l < L) {
-                rec_step(cn, x, v0, v1);
+                rec_ana(c, mul_nc(x, v0), v0, v1);
                 if (kk < 0 && fabs(v0) > SC_HI) { v0 *= SC_DN; v1 *= SC_DN; ++kk; }
             }
             ++l;
@@ -690,29 +704,28 @@ __global__ __launch_bounds__(1024) void k_sht_synth_leg_seg(ShtDev D, const LegC
         // fast path (onset state loaded above when the onset is the first l)
         double xv1 = mul_nc(x, v1);
         if (l <= lend && ((l - m) & 1)) {
-            const LegCoef c = cf(l);
-            const LegCoef cn = cf(min(l + 1, L));
+            const AnaCoef c = cf(l);
             const double2 t = NC != 2 ? aT(l) : z2, e = NC != 1 ? aE(l) : z2, b = NC != 1 ? aB(l) : z2;
             const double xv0 = mul_nc(x, v0);
             syn_accumulate<NC, false>(A, c, v0, v1, xv0, xv1, s2, t, e, b);
-            rec_from(cn, xv0, v0, v1);               // past L: unused
+            rec_ana(c, xv0, v0, v1);                 // past L: unused
             xv1 = xv0;
             ++l;
         }
         for (; l + 1 <= lend; l += 2) {
-            const LegCoef c0 = cf(l), c1 = cf(l + 1), c2 = cf(min(l + 2, L));
+            const AnaCoef c0 = cf(l), c1 = cf(l + 1);
             const double2 t0 = NC != 2 ? aT(l) : z2, e0 = NC != 1 ? aE(l) : z2, b0 = NC != 1 ? aB(l) : z2;
             const double2 t1 = NC != 2 ? aT(l + 1) : z2, e1 = NC != 1 ? aE(l + 1) : z2, b1 = NC != 1 ? aB(l + 1) : z2;
             const double xa = mul_nc(x, v0);
             syn_accumulate<NC, true>(A, c0, v0, v1, xa, xv1, s2, t0, e0, b0);
-            rec_from(c1, xa, v0, v1);
+            rec_ana(c0, xa, v0, v1);
             const double xb = mul_nc(x, v0);
             syn_accumulate<NC, false>(A, c1, v0, v1, xb, xa, s2, t1, e1, b1);
-            rec_from(c2, xb, v0, v1);
+            rec_ana(c1, xb, v0, v1);
             xv1 = xb;
         }
         if (l <= lend) {
-            const LegCoef c = cf(l);
+            const AnaCoef c = cf(l);
             const double2 t = NC != 2 ? aT(l) : z2, e = NC != 1 ? aE(l) : z2, b = NC != 1 ? aB(l) : z2;
             syn_accumulate<NC, true>(A, c, v0, v1, mul_nc(x, v0), xv1, s2, t, e, b);
         }
@@ -2074,13 +2087,6 @@ __device__ __forceinline__ void ana_term(double* a, const AnaCoef& c, double v0,
         a[o + 2] = fma(F1, U1.x, fma(F2, Q2.y, a[o + 2]));
         a[o + 3] = fma(F1, U1.y, fma(-F2, Q2.x, a[o + 3]));
     }
-}
-
-// the analysis' recurrence step (the same arithmetic as rec_from)
-__device__ __forceinline__ void rec_ana(const AnaCoef& c, double xv0, double& v0, double& v1) {
-    const double vn = c.a1 * fma(-c.b1, v1, xv0);
-    v1 = v0;
-    v0 = vn;
 }
 
 template <int NC, int ASR, bool SEGL>
@@ -4234,8 +4240,9 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
     }
     const long long nin = (long long)nmap * ncomp * p->nlm;
     // the batch's comps are contiguous: the input pass sees B * ncomp comps
+    // (the on-the-fly synthesis takes the spin-2 a_lm scaled by Q_l: AnaCoef)
     hipLaunchKernelGGL(k_sht_alm_in, dim3(nblocks(nin, 256)), dim3(256), 0, S(stream), p->L, p->nlm, nmap * ncomp, alm,
-                       layout, p->ain, bl);
+                       layout, p->ain, bl, ncomp, p->mf ? nullptr : p->acq);
     GS_LAUNCH_CHECK("k_sht_alm_in");
     if (p->mf) {
         if (sht_synth_mfma(p, nmap, ncomp, S(stream))) return -1;
@@ -4247,7 +4254,7 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
         // wave's LDS slice stages 64 l of coefficients and a_lm)
         const dim3 g2(p->L + 1, p->ngroup, nmap), b2(64 * syn_nseg);
         const size_t lds = (size_t)syn_nseg * (66 * 8 + 3 * 64 * 2) * sizeof(double);
-#define GS_SS(NC) hipLaunchKernelGGL((k_sht_synth_leg_seg<NC>), g2, b2, lds, S(stream), p->devseg(p->syn_seg), p->coef, \
+#define GS_SS(NC) hipLaunchKernelGGL((k_sht_synth_leg_seg<NC>), g2, b2, lds, S(stream), p->devseg(p->syn_seg), p->acoef, \
                                      p->ain, p->phi)
         if (ncomp == 1) GS_SS(1); else if (ncomp == 2) GS_SS(2); else GS_SS(3);
 #undef GS_SS
@@ -4256,7 +4263,7 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
     }
     const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr), nmap);
 #define GS_SL(NC, SR) hipLaunchKernelGGL((k_sht_synth_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
-                                         p->coef, p->ain, p->phi, p->syn_paired)
+                                         p->acoef, p->ain, p->phi, p->syn_paired)
 #define GS_SL2(NC) do { if (p->syn_sr == 2) GS_SL(NC, 2); else GS_SL(NC, 1); } while (0)
     if (ncomp == 1) GS_SL2(1); else if (ncomp == 2) GS_SL2(2); else GS_SL2(3);
 #undef GS_SL2
