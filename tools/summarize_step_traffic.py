@@ -31,7 +31,7 @@ def window(path, counter):
         raise SystemExit(f"{path}: markers not found ({len(marks)})")
     per = collections.defaultdict(float)
     for r in rows[marks[-2] + 1:marks[-1]]:
-        per[r["Kernel_Name"].replace("void ", "").split("(")[0]] += float(r["Counter_Value"])
+        per[r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]] += float(r["Counter_Value"])
     return per
 
 
