@@ -81,6 +81,9 @@ def parse():
                          "measured while the GPU's clocks still ramp up (clock_ramp); reported in the line "
                          "(default 200; 0 turns it off)")
     ap.add_argument("--profile-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--opt", action="append", default=[],
+                    help="NAME=VALUE library option (gs_option_set, include/gibbs_capi.h) set before any plan is made "
+                         "(A/B of a plan choice; the line's config records it)")
     a = ap.parse_args()
     one = a.workload == "masked" or a.workload in MASKED_HEAD
     a.nchains = a.nchains or (1 if one else 32)
@@ -340,6 +343,11 @@ def main():
     if ctx.rank == 0:
         build()
     ctx.barrier()
+    if args.opt:
+        from gibbssampler_amd import _capi
+        for o in args.opt:
+            k, v = o.split("=", 1)
+            _capi.set_option(k, v)
     try:
         if args.workload in HARMONIC:
             line = run_harmonic(args, ctx, cpu)
@@ -350,6 +358,8 @@ def main():
         else:
             line = run_masked_head(args, ctx, cpu)
         if ctx.rank == 0:
+            if args.opt:
+                line["config"]["library_options"] = dict(o.split("=", 1) for o in args.opt)
             print(json.dumps(line))
     finally:
         ctx.close()
