@@ -2601,6 +2601,13 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 #ifndef GS_MF_SPIPE
 #define GS_MF_SPIPE 1
 #endif
+// wave priority while a wave issues its MFMA burst (s_setprio; 0 = off): a
+// wave with matrix work ready is picked before the staging waves of the SIMD
+#ifndef GS_MF_PRIO
+#define GS_MF_PRIO 0
+#endif
+__device__ __forceinline__ void mf_prio_hi() { if (GS_MF_PRIO) __builtin_amdgcn_s_setprio(GS_MF_PRIO); }
+__device__ __forceinline__ void mf_prio_lo() { if (GS_MF_PRIO) __builtin_amdgcn_s_setprio(0); }
 constexpr int MF_CH = 32;                          // l staged per chunk (two blocks)
 constexpr int MF_TL_MAX = 256;                     // tiles of a support-skipping analysis (N_side <= 2048)
 // RIN: the input is the caller's real-layout a_lm (areal, comp stride
@@ -2859,6 +2866,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
             __builtin_amdgcn_sched_barrier(0);
             if (!GS_MF_SPIPE) opnd(q, apc, amc);
             if (on) {
+                mf_prio_hi();
 #pragma unroll
                 for (int c = 0; c < CPW; ++c) {
                     if (c < ncl) {                  // (a column group without maps: no MFMAs)
@@ -2866,6 +2874,7 @@ __global__ __launch_bounds__(256 * (CGW / CPW)) GS_MF_SYN_ATTR void k_sht_synth_
                         Cm[c] = mfma64(amc, bq[q & 1][2 * c + 1], Cm[c]);
                     }
                 }
+                mf_prio_lo();
             }
             __builtin_amdgcn_sched_barrier(0);
             // the next quad's operands while these MFMAs run (their fp64 chain
@@ -3359,6 +3368,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
             if (s + 1 < 4) ldsA(s + 1, aq[(s + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
             if (cur.any) {
+                mf_prio_hi();
 #pragma unroll
                 for (int p = 0; p < 2; ++p) {
                     double gz[NF];
@@ -3387,6 +3397,7 @@ __global__ __launch_bounds__(NT) GS_MF_ANA_ATTR void k_sht_anal_mfma(ShtDev D, M
                         }
                     }
                 }
+                mf_prio_lo();
             }
             __builtin_amdgcn_sched_barrier(0);
             tload(nxt, tn, s, gv);                  // (the last tile reloads its own: harmless)
@@ -3760,9 +3771,14 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     if (gscr_need && sht_alloc(p, &p->gscr, (size_t)gscr_need)) { sht_free(p); return -1; }
     {
         // one merged ring launch when every length fits a small LDS buffer
-        // (GS_SHT_MERGE_RINGS=0/1 forces it off/on where legal)
+        // (GS_SHT_MERGE_RINGS=0/1 forces it off/on where legal).  Up to M = 4096
+        // (N_side 512: two components of the longest Bluestein FFT fill the
+        // 160-KB LDS): measured at N_side 512, 32 spin-2 maps, alm2map 9.95 ->
+        // 9.11 ms, map2alm 10.66 -> 9.64 ms, and the f2 block maps take the
+        // constant-ring (Parseval) route only here: masked ASIS 2702 -> 1613 ms
+        // per 32-chain step (profiles/r06o_*)
         const int mmax = Ms.empty() ? 0 : Ms.back();
-        bool merge = mmax <= 2048 && mmax <= p->lds_fft_max && p->nsplit == 0;
+        bool merge = mmax <= 4096 && mmax <= p->lds_fft_max && p->nsplit == 0;
         if (const char* e = gs_detail::option("GS_SHT_MERGE_RINGS")) merge = std::atoi(e) != 0 && mmax <= p->lds_fft_max && p->nsplit == 0;
         if (merge && Ms.size() > 1) {
             std::vector<int> all(p->npair);

@@ -306,6 +306,34 @@ def test_ring_stage_merged_and_per_class_vs_oracle(gsopt, merge, N, L):
     np.testing.assert_allclose(ga, wa, rtol=0, atol=1e-11 * np.abs(wa).max())
 
 
+@pytest.mark.parametrize("mfma", [False, True])
+def test_ring_stage_merged_equals_per_class_n512(gsopt, mfma):
+    """N_side 512 (FFT lengths up to M = 4096: the polar Bluestein rings) runs
+    the merged ring stage by default since r06; it equals the per-class
+    launches (GS_SHT_MERGE_RINGS=0) to rounding -- batched spin-2 maps on both
+    Legendre stages, both directions, and the N^-1-weighted operator whose
+    constant rings skip the DFTs only in the merged stage."""
+    torch = _torch()
+    from gibbssampler_amd.sht import HealpixSHT
+    from gibbssampler_amd.data import band_mask
+    N, L, B = 512, 1024, 3
+    g = torch.Generator(device="cuda").manual_seed(5)
+    alm = torch.randn((B, 2, (L + 1) ** 2), generator=g, device="cuda", dtype=torch.float64)
+    maps = torch.randn((B, 2, 12 * N * N), generator=g, device="cuda", dtype=torch.float64)
+    w = torch.from_numpy(np.stack([band_mask(N)] * 2) * 25.0).cuda()
+    out = {}
+    for mg in ("1", "0"):
+        gsopt.setenv("GS_SHT_MERGE_RINGS", mg)
+        sht = HealpixSHT(N, L)
+        if mfma:
+            sht.set_mfma(True)
+        out[mg] = [sht.alm2map_batch(alm, 2).cpu().numpy(), sht.map2alm_batch(maps, 2).cpu().numpy(),
+                   sht.apply_weighted_batch(alm, 2, w).cpu().numpy()]
+        del sht
+    for a, b in zip(out["0"], out["1"]):
+        np.testing.assert_allclose(b, a, rtol=0, atol=1e-12 * np.abs(a).max())
+
+
 @pytest.mark.parametrize("N,L,comps", [(256, 512, 2), (512, 1024, 3)])
 def test_cpu_baseline_sht_equals_device(N, L, comps):
     """The CPU baseline's transforms (oracle/sht_cpu.cpp: own FFTs and scaled
