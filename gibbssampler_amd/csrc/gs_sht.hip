@@ -3596,7 +3596,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
         };
         pick({{2, 1}, {1, 1}, {1, 0}}, "GS_SHT_SYN", p->syn_sr, p->syn_paired);
         pick({{4, 1}, {2, 1}, {1, 1}, {1, 0}}, "GS_SHT_ANA", p->ana_sr, p->ana_paired);
-        if ((p->syn_sr != 1 && p->syn_sr != 2) || (p->ana_sr != 1 && p->ana_sr != 2 && p->ana_sr != 4)) {
+        if ((p->syn_sr != 1 && p->syn_sr != 2 && p->syn_sr != 4) || (p->ana_sr != 1 && p->ana_sr != 2 && p->ana_sr != 4)) {
             delete p;
             return set_error("gs_sht_create: bad GS_SHT_SYN / GS_SHT_ANA override");
         }
@@ -4280,7 +4280,7 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
     const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr), nmap);
 #define GS_SL(NC, SR) hipLaunchKernelGGL((k_sht_synth_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
                                          p->acoef, p->ain, p->phi, p->syn_paired)
-#define GS_SL2(NC) do { if (p->syn_sr == 2) GS_SL(NC, 2); else GS_SL(NC, 1); } while (0)
+#define GS_SL2(NC) do { if (p->syn_sr == 4) GS_SL(NC, 4); else if (p->syn_sr == 2) GS_SL(NC, 2); else GS_SL(NC, 1); } while (0)
     if (ncomp == 1) GS_SL2(1); else if (ncomp == 2) GS_SL2(2); else GS_SL2(3);
 #undef GS_SL2
 #undef GS_SL
@@ -4375,7 +4375,8 @@ int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real,
     // each 64-B run completed by the workgroups of its four m, which one chain's
     // launch keeps co-resident (all chains in one grid measured 24.4 against 19.1
     // ms for 16 chains at N_side 256: the runs' pieces then reach L2 too far apart)
-    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr), 1);
+    const int bsr = p->syn_sr >= 2 ? 2 : 1;           // ring groups per lane (the block kernels: 1 or 2)
+    const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * bsr - 1) / (4 * bsr), 1);
     // staged variant when m = 0's coefficients, a_lm and block indices fit 64 KB
     // of LDS (GS_SHT_BLK_STAGE=0 turns it off: tests)
     const size_t stg = (size_t)(p->L + 1) * (4 * sizeof(double2) + nfield * (sizeof(double2) + sizeof(int)));
@@ -4388,8 +4389,8 @@ int gs_sht_synth_blocks(gs_sht* p, int nmap, int nfield, const double* alm_real,
     else hipLaunchKernelGGL((k_sht_synth_blocks<NF, SR, false>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
                             p->coef, p->ain + b * nfield * p->nlm, blk, ph + b * cst, p->syn_paired, cst); } while (0)
     for (long long b = 0; b < nmap; ++b) {
-        if (nfield == 1) { if (p->syn_sr == 2) GS_SB(1, 2); else GS_SB(1, 1); }
-        else { if (p->syn_sr == 2) GS_SB(2, 2); else GS_SB(2, 1); }
+        if (nfield == 1) { if (bsr == 2) GS_SB(1, 2); else GS_SB(1, 1); }
+        else { if (bsr == 2) GS_SB(2, 2); else GS_SB(2, 1); }
     }
 #undef GS_SB
     GS_LAUNCH_CHECK("k_sht_synth_blocks");

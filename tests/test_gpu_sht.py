@@ -207,14 +207,14 @@ def test_adjointness_nside2048():
     test_adjointness_fullsize(2048, 4096, 1)
 
 
-SHAPES = [("2,1", "4,1"), ("2,0", "2,1"), ("1,1", "2,0"), ("1,0", "1,1"), ("2,1", "1,0")]
+SHAPES = [("2,1", "4,1"), ("2,0", "2,1"), ("1,1", "2,0"), ("1,0", "1,1"), ("2,1", "1,0"), ("4,1", "4,0")]
 
 
 @pytest.mark.parametrize("syn,ana", SHAPES)
 @pytest.mark.parametrize("N,L", [(16, 32), (64, 100)])
 def test_legendre_launch_shapes_vs_oracle(gsopt, syn, ana, N, L):
-    """Every Legendre launch shape the plan may pick (ring groups per lane 1/2
-    for synthesis, 1/2/4 for analysis; m paired or not) -- chosen by map size
+    """Every Legendre launch shape the plan may pick (ring groups per lane
+    1/2/4 for synthesis and analysis; m paired or not) -- chosen by map size
     for occupancy, forced here with GS_SHT_SYN / GS_SHT_ANA -- against the
     dense oracle (TEB, both directions; 64/100 with several ring groups)."""
     torch = _torch()
