@@ -69,3 +69,20 @@ def test_attach_cpu_assembly():
     assert "100.0" in out["cpu_baseline"]["sample"]
     ready = {"value": 3.0, "unit": "chain-iterations/s", "cores": 16, "kind": "port", "sample": "s"}
     assert bench.attach_cpu(dict(line), ready)["cpu_baseline"] == ready
+
+
+def test_bench_parse_defaults(monkeypatch):
+    """bench.py's defaults: the driver's 20-step command samples 5 sweeps for the
+    roofline timing (every 4th), long runs every 10th; --opt pairs are kept for
+    the line's config (library options set before any plan is made)."""
+    import bench
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "20", "--warmup", "5"])
+    a = bench.parse()
+    assert (a.steps, a.warmup, a.time_every, a.nchains) == (20, 5, 4, 32)
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.steps, a.time_every) == (500, 10)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "masked_asis", "--opt", "GS_SHT_MERGE_RINGS=0"])
+    a = bench.parse()
+    assert (a.nchains, a.lmax, a.nside, a.steps) == (1, 512, 256, 5)
+    assert a.opt == ["GS_SHT_MERGE_RINGS=0"]
