@@ -1212,7 +1212,26 @@ __device__ __forceinline__ const double2* ring_twiddles_lds(double2* twl, int M,
 // (mod J); J > 1 only for short rings, reduced in LDS in a fixed order.
 struct Fold4 { double2 nk, nmk, sk, smk; };
 
-template <int NB>
+// the pixel operations a ring stage applies before its pixels leave it: y ->
+// the value stored for comp c at the ring pair's pixels iN (north) / iS (south)
+struct PixNone {
+    static constexpr bool kConst = false;
+    __device__ __forceinline__ double2 operator()(int, long long, long long, bool, double2 y) const { return y; }
+};
+struct PixAux {                     // the aux-variable v | s update (gs_aux.h), comps (chain, field)
+    gs::GsAuxPix a;
+    static constexpr bool kConst = false;
+    __device__ __forceinline__ double2 operator()(int c, long long iN, long long iS, bool eq, double2 y) const {
+        const int b = c / a.F, k = c - b * a.F;
+        const double yn = gs::mc_aux_pixel(a, b, k, iN, y.x);
+        return make_double2(yn, eq ? 0.0 : gs::mc_aux_pixel(a, b, k, iS, y.y));
+    }
+};
+
+// Op (PixAux): the aux-variable step applied to the synthesised pixels A b s
+// on their way out -- the map stored is y = v + N^-1 d (and v), the pixel
+// kernel k_mc_v's arithmetic on the same values (bit-identical)
+template <int NB, class Op = PixNone>
 __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long long npix,
                                                          const int* __restrict__ pairs,
                                                          const PairGeom* __restrict__ geom,
@@ -1221,7 +1240,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
                                                          const double2* __restrict__ bsk,
                                                          double2* __restrict__ gscratch, double* __restrict__ maps,
                                                          double2* __restrict__ sscr, int nsplit, int sstride,
-                                                         const int* __restrict__ comp_lmax, int comp_div, int twoff) {
+                                                         const int* __restrict__ comp_lmax, int comp_div, int twoff,
+                                                         Op op = Op{}) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -1339,7 +1359,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         for (int k = threadIdx.x; k < h; k += BD) {
             const double2 b = cmul(buf[k], expi_pi_u32(2u * k, n));
             const double2 a = A[k];
-            const double2 y0 = make_double2(a.x + b.x, a.y + b.y), y1 = make_double2(a.x - b.x, a.y - b.y);
+            const double2 y0 = op(comp, g.startN + k, g.startS + k, eq, make_double2(a.x + b.x, a.y + b.y));
+            const double2 y1 = op(comp, g.startN + k + h, g.startS + k + h, eq, make_double2(a.x - b.x, a.y - b.y));
             mc[g.startN + k] = y0.x;
             mc[g.startN + k + h] = y1.x;
             if (!eq) { mc[g.startS + k] = y0.y; mc[g.startS + k + h] = y1.y; }
@@ -1348,7 +1369,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     }
     dft_inverse<NB>(buf, g, twx, twM, bsk);
     for (int j = threadIdx.x; j < n; j += BD) {
-        const double2 y = buf[j];
+        const double2 y = op(comp, g.startN + j, g.startS + j, eq, buf[j]);
         mc[g.startN + j] = y.x;
         if (!eq) mc[g.startS + j] = y.y;
     }
@@ -1893,15 +1914,7 @@ struct PixWeights {                 // the masked PCG's N^-1 (weights [wnc][Npix
         return make_double2(wc[iN] * y.x, eq ? 0.0 : wc[iS] * y.y);
     }
 };
-struct PixAux {                     // the aux-variable v | s update (gs_aux.h), comps (chain, field)
-    gs::GsAuxPix a;
-    static constexpr bool kConst = false;
-    __device__ __forceinline__ double2 operator()(int c, long long iN, long long iS, bool eq, double2 y) const {
-        const int b = c / a.F, k = c - b * a.F;
-        const double yn = gs::mc_aux_pixel(a, b, k, iN, y.x);
-        return make_double2(yn, eq ? 0.0 : gs::mc_aux_pixel(a, b, k, iS, y.y));
-    }
-};
+// (PixAux: above, with k_sht_synth_ring)
 
 // fused ring stage: per ring pair the synthesis ring work (fold, inverse DFT),
 // a pixel operation (the masked PCG's N^-1 weights: the operator A^T N^-1 A; or
@@ -3819,6 +3832,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     }
     {
         const void* fns[] = {(const void*)k_sht_synth_ring<4>, (const void*)k_sht_synth_ring<8>,
+                             (const void*)k_sht_synth_ring<4, PixAux>, (const void*)k_sht_synth_ring<8, PixAux>,
                              (const void*)k_sht_anal_ring<4>, (const void*)k_sht_anal_ring<8>};
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3897,7 +3911,8 @@ static void ring_lds(int M, int bd, bool glob, bool short_red, size_t& lds, int&
 
 static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const double* maps_in, double* maps_out,
                           hipStream_t st, const double2* phi = nullptr, const int* comp_lmax = nullptr,
-                          int comp_div = 1, const double* wts = nullptr, int wnc = 3) {
+                          int comp_div = 1, const double* wts = nullptr, int wnc = 3,
+                          const gs::GsAuxPix* aux = nullptr) {
     if (!phi) phi = p->phi;
     const int M = p->cls_M[c];
     const bool glob = M > p->lds_fft_max;
@@ -3908,15 +3923,26 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
     ring_lds(M, bd, glob, M < 8 * bd, lds, twoff);
     const dim3 grid(p->cls_n[c], ncomp);
     double2* scr = glob ? p->gscr : nullptr;
-    if (synth) {
+    if (synth && aux) {
+        // the aux-variable step on the pixels as they leave (PixAux)
+        const PixAux op{*aux};
+        if (nb8)
+            hipLaunchKernelGGL((k_sht_synth_ring<8, PixAux>), grid, dim3(bd), lds, st, p->L, p->npair, p->npix,
+                               p->cls_pairs[c], p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit,
+                               p->split_n, comp_lmax, comp_div, twoff, op);
+        else
+            hipLaunchKernelGGL((k_sht_synth_ring<4, PixAux>), grid, dim3(bd), lds, st, p->L, p->npair, p->npix,
+                               p->cls_pairs[c], p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit,
+                               p->split_n, comp_lmax, comp_div, twoff, op);
+    } else if (synth) {
         if (nb8)
             hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
                                p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
-                               comp_lmax, comp_div, twoff);
+                               comp_lmax, comp_div, twoff, PixNone{});
         else
             hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
                                p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
-                               comp_lmax, comp_div, twoff);
+                               comp_lmax, comp_div, twoff, PixNone{});
     } else {
         if (nb8)
             hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
@@ -3952,7 +3978,9 @@ static int ring_mc_ncb(int M, int ncomp) {
 
 static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, double* maps_out, void* stream,
                      const double2* phi = nullptr, const int* comp_lmax = nullptr, int comp_div = 1, const double* wts = nullptr,
-                     int wnc = 3, const int* pflag = nullptr, const int* pconst = nullptr) {
+                     int wnc = 3, const int* pflag = nullptr, const int* pconst = nullptr,
+                     const gs::GsAuxPix* aux = nullptr) {
+    if (aux && p->merged_n > 0) return set_error("sht_rings: the aux store runs on the per-class ring stage");
     if (p->merged_n > 0) {
         // all ring pairs in one launch: the block size and LDS of the longest FFT
         // (shorter rings leave threads idle; their fold reduction uses the
@@ -3989,11 +4017,11 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
             if (nb8)
                 hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
-                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff);
+                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff, PixNone{});
             else
                 hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
-                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff);
+                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff, PixNone{});
         } else {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
@@ -4020,7 +4048,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
     for (size_t c = 0; c < ncls; ++c) {
         const bool on_side = fork && c != big && p->cls_M[c] <= p->lds_fft_max;
         if (sht_ring_class(p, c, synth, ncomp, maps_in, maps_out, on_side ? p->side : S(stream), phi, comp_lmax,
-                           comp_div, wts, wnc))
+                           comp_div, wts, wnc, aux))
             return -1;
     }
     if (fork) {
@@ -4235,7 +4263,7 @@ static int sht_set_mfma(gs_sht* p, int on) {
 // synthesis of B maps (alm [B][ncomp][n], maps [B][ncomp][Npix]); bl (real layout
 // only): the per-l beam applied on the input load
 static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double* alm, const double* bl, double* maps,
-                       void* stream) {
+                       void* stream, const gs::GsAuxPix* aux = nullptr) {
     if (check_sht(p)) return -1;
     if (ncomp < 1 || ncomp > 3) return set_error("gs_sht_alm2map: ncomp must be 1 (T), 2 (E,B) or 3 (T,E,B)");
     if (layout != GS_ALM_REAL && layout != GS_ALM_COMPLEX) return set_error("gs_sht_alm2map: bad layout");
@@ -4249,6 +4277,8 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
         return 0;
     }
     if (sht_reserve(p, nmap, S(stream))) return -1;
+    if (aux && (p->mf || p->merged_n > 0 || nmap > 1))
+        return set_error("gs_sht_alm2map: the aux store is for one map on the per-class ring stage");
     if (p->mf && layout == GS_ALM_REAL) {
         // the table kernel reads the real layout (and the beam) itself
         if (sht_synth_mfma(p, nmap, ncomp, S(stream), nullptr, alm, bl)) return -1;
@@ -4275,7 +4305,8 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
         if (ncomp == 1) GS_SS(1); else if (ncomp == 2) GS_SS(2); else GS_SS(3);
 #undef GS_SS
         GS_LAUNCH_CHECK("k_sht_synth_leg_seg");
-        return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp);
+        return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp, nullptr,
+                         nullptr, aux);
     }
     const dim3 grid(p->syn_paired ? p->L / 2 + 1 : p->L + 1, (p->ngroup + 4 * p->syn_sr - 1) / (4 * p->syn_sr), nmap);
 #define GS_SL(NC, SR) hipLaunchKernelGGL((k_sht_synth_leg<NC, SR>), grid, dim3(LEG_BLOCK), 0, S(stream), p->dev(), \
@@ -4285,7 +4316,8 @@ static int sht_alm2map(gs_sht* p, int nmap, int ncomp, int layout, const double*
 #undef GS_SL2
 #undef GS_SL
     GS_LAUNCH_CHECK("k_sht_synth_leg");
-    return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp);
+    return sht_rings(p, true, nmap * ncomp, nullptr, maps, stream, nullptr, nullptr, 1, nullptr, ncomp, nullptr,
+                     nullptr, aux);
 }
 
 int gs_sht_alm2map(gs_sht* p, int ncomp, int layout, const double* alm, double* maps, void* stream) {
@@ -4591,9 +4623,21 @@ int gs_sht_aux_pass_batch(gs_sht* p, int nmap, int ncomp, const double* alm_in, 
     if (ncomp < 1 || ncomp > 3 || nmap < 1 || !alm_in || !aux || !alm_out)
         return set_error("gs_sht_aux_pass_batch: bad argument");
     const char* fe = gs_detail::option("GS_SHT_FUSED_AUX");
+    if (fe && std::atoi(fe) == 0) return 1;
+    if (!p->mf && p->merged_n == 0 && nmap == 1) {
+        // large maps (per-class ring stage, the on-the-fly Legendre kernels): the
+        // v | s step runs on the synthesised pixels as the ring stage stores them,
+        // so A b s is never written and read back; y = v + N^-1 d goes to the
+        // plan's map workspace and the analysis reads it from there (the same
+        // bits as the synthesis, k_mc_v and the analysis in turn)
+        if (sht_reserve(p, nmap, S(stream))) return -1;
+        const gs::GsAuxPix* a = reinterpret_cast<const gs::GsAuxPix*>(aux);
+        if (sht_alm2map(p, nmap, ncomp, GS_ALM_REAL, alm_in, bl, p->mapw, stream, a)) return -1;
+        return sht_analysis(p, nmap, ncomp, GS_ALM_REAL, p->mapw, alm_out, 0, stream);
+    }
     const int M = p->merged_M;
     const int ncb = (p->mf && p->merged_n > 0) ? ring_mc_ncb(M, nmap * ncomp) : 1;
-    if (ncb < 2 || (fe && std::atoi(fe) == 0)) return 1;
+    if (ncb < 2) return 1;
     if (sht_reserve(p, nmap, S(stream))) return -1;
     if (sht_synth_mfma(p, nmap, ncomp, S(stream), nullptr, alm_in, bl)) return -1;
     {

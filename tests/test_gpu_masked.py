@@ -760,6 +760,45 @@ def test_f2_large_vs_oracle_tables(f2_large, gsopt, blocks_mfma):
 
 @pytest.mark.parametrize("F", [2, 3])
 @pytest.mark.parametrize("over", [False, True])
+@pytest.mark.parametrize("N,L", [(8, 16), (64, 128)])
+def test_aux_store_per_class_bit_identical(gsopt, F, over, N, L):
+    """large single maps (per-class ring stage, the on-the-fly Legendre kernels:
+    configs[4]'s path, forced here at small N with GS_SHT_MERGE_RINGS=0): the v | s
+    step applied as the synthesis ring stage stores its pixels gives the bits of
+    the synthesis, k_mc_v and the analysis in turn (GS_SHT_FUSED_AUX=0)."""
+    import torch
+    from gibbssampler_amd import _capi
+    from gibbssampler_amd.masked import MaskedCR
+    _, _, _, _, _, _, _, dl, _ = _teb_problem(N, L)
+    rng = np.random.default_rng(N + F)
+    npix = 12 * N * N
+    th, _ = O.pixel_angles(N)
+    mask = (np.abs(np.cos(th)) > 0.2).astype(float)
+    maps = rng.standard_normal((3, npix)) * np.array([[30.0], [0.3], [0.3]])
+    ntemp = np.full(npix, 40.0 ** 2) * np.linspace(0.9, 1.1, npix)
+    npol = np.full(npix, 0.2 ** 2) * np.linspace(1.2, 0.8, npix)
+    ell = np.arange(L + 1)
+    bl = np.exp(-0.5 * ell * (ell + 1) * (0.07 / np.sqrt(8 * np.log(2))) ** 2)
+    s0 = rng.standard_normal((3, (L + 1) ** 2)) * np.array([[3.0], [0.05], [0.005]])
+    pix = {"T": maps[0], "Q": maps[1], "U": maps[2]}
+    rows = (1, 2) if F == 2 else (0, 1, 2)
+    spec = ("EE", "BB") if F == 2 else ("TT", "EE", "BB", "TE")
+    gsopt.setenv("GS_SHT_MERGE_RINGS", "0")
+    out = []
+    for fused in ("1", "0"):
+        gsopt.setenv("GS_SHT_FUSED_AUX", fused)
+        cr = MaskedCR(pix, ntemp, npol, bl, L, N, mask=mask, nfields=F, n_gibbs=3, overrelaxation=over, rng="native",
+                      seed=8, chain=2, sht_mode="recurrence")
+        s = torch.from_numpy(np.ascontiguousarray(np.stack([s0[r] for r in rows])[None])).cuda()
+        d = torch.from_numpy(np.ascontiguousarray(np.stack([dl[k] for k in spec])[None])).cuda()
+        cr.step(_capi.GS_MCR_OVERRELAX if over else _capi.GS_MCR_AUX, d, s, iteration=5)
+        out.append((s.cpu().numpy(), cr.v.cpu().numpy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("F", [2, 3])
+@pytest.mark.parametrize("over", [False, True])
 def test_aux_fused_pass_bit_identical(gsopt, F, over):
     """the table path's fused v | s + s | v-analysis pass (gs_sht_aux_pass_batch:
     synthesis, the k_mc_v update in the ring workgroup, analysis) and the reuse of
