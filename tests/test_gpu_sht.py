@@ -260,6 +260,30 @@ def test_segmented_analysis_vs_oracle(gsopt, seg, ana, N, L):
         np.testing.assert_allclose(ga, wa, rtol=0, atol=1e-11 * np.abs(wa).max())
 
 
+@pytest.mark.parametrize("seg", [0, 200])
+def test_analysis_launch_shapes_agree_long_l(gsopt, seg):
+    """The large-map analysis shapes (4 ring groups per lane, m paired or not;
+    unsegmented, or segments over 64 l on the unsegmented kernel) against the
+    2-group shape at l_max 512 -- several hundred l per m, onsets spread over
+    the range -- for T, EB and TEB: only the partial-sum grouping differs."""
+    torch = _torch()
+    from gibbssampler_amd.sht import HealpixSHT
+    N, L = 128, 512
+    rng = np.random.default_rng(512 + seg)
+    for ncomp in (1, 2, 3):
+        maps = torch.from_numpy(rng.standard_normal((ncomp, 12 * N * N))).cuda()
+        res = {}
+        for ana in ("4,1", "4,0", "2,1"):
+            gsopt.setenv("GS_SHT_SEG", str(seg))
+            gsopt.setenv("GS_SHT_ANA", ana)
+            sht = HealpixSHT(N, L)
+            res[ana] = sht.map2alm(maps, iter=0, layout="complex", ncomp=ncomp).cpu().numpy()
+            del sht
+        ref = res["2,1"]
+        for ana in ("4,1", "4,0"):
+            np.testing.assert_allclose(res[ana], ref, rtol=0, atol=1e-12 * np.abs(ref).max())
+
+
 @pytest.mark.parametrize("N,L,seg", [(256, 512, 64), (256, 512, 16), (512, 1024, 64)])
 def test_segmented_analysis_matches_single_walk(gsopt, N, L, seg):
     """At the HEAD masked modes' size (and N_side 512): segmented and
