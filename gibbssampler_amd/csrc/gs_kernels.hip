@@ -2081,7 +2081,8 @@ __global__ void k_record_trace(long long n, const double* __restrict__ dl, doubl
 static const char* const k_options[] = {
     "GS_SWEEP_TW", "GS_SWEEP_THROUGHPUT", "GS_MH_SPLIT", "GS_CLS_PRE", "GS_CLS_PRE_MANY", "GS_F2_GROUP_BYTES",
     "GS_F2_BATCH_BYTES", "GS_SHT_LDS_FFT_MAX", "GS_SHT_SEG", "GS_SHT_SYN", "GS_SHT_ANA", "GS_SHT_MERGE_RINGS",
-    "GS_SHT_CONST_RINGS", "GS_SHT_BLOCKS_MFMA", "GS_SHT_BLK_STAGE", "GS_SHT_FUSED_AUX", "GS_SHT_MFMA_MAX_GB"};
+    "GS_SHT_CONST_RINGS", "GS_SHT_BLOCKS_MFMA", "GS_SHT_BLK_STAGE", "GS_SHT_FUSED_AUX", "GS_SHT_MFMA_MAX_GB",
+    "GS_SHT_RING_TW2"};
 static bool opt_known(const char* name) {
     for (const char* k : k_options)
         if (std::strcmp(k, name) == 0) return true;

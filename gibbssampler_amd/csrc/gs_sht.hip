@@ -980,6 +980,23 @@ __global__ __launch_bounds__(LEG_BLOCK) void k_sht_synth_blocks(ShtDev D, const 
 // forward (dir = -1): X_k = sum_j x_j e^{-2 pi i jk/M};  dir = +1: conjugate
 // twiddles; tw[k] = e^{-2 pi i k / Mmax}, k < Mmax/2.  Each thread owns at most
 // NB butterflies per stage (M / 2 <= NB * blockDim).
+// e^{dir 2 pi i t / Mmax} for 0 <= t < Mmax from the half-circle table, or
+// (Mmax < 0: a ring workgroup whose full table does not fit its LDS) from the
+// two-level LDS tables hi[a] = e^{-2 pi i 64 a / |Mmax|}, lo[b] = e^{-2 pi i b /
+// |Mmax|} (b < 64) at tw, tw + |Mmax| / 64: one complex product, no global load
+__device__ __forceinline__ double2 twid(int t, int dir, const double2* __restrict__ tw, int Mmax) {
+    if (Mmax < 0) {
+        double2 w = cmul(tw[t >> 6], tw[(-Mmax >> 6) + (t & 63)]);
+        if (dir > 0) w.y = -w.y;
+        return w;
+    }
+    const int h = Mmax >> 1;
+    double2 w = tw[t < h ? t : t - h];
+    if (t >= h) { w.x = -w.x; w.y = -w.y; }
+    if (dir > 0) w.y = -w.y;
+    return w;
+}
+
 #if defined(GS_FFT_RADIX2)
 template <int NB>
 __device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
@@ -987,14 +1004,13 @@ __device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const dou
     for (int Ns = 1; Ns < M; Ns <<= 1) {
         double2 o0[NB], o1[NB];
         int id[NB];
-        const int tstride = Mmax / (2 * Ns);
+        const int tstride = (Mmax < 0 ? -Mmax : Mmax) / (2 * Ns);
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
             const int j = threadIdx.x + t * blockDim.x;
             if (j < half) {
                 const double2 a = buf[j];
-                double2 w = tw[(j & (Ns - 1)) * tstride];
-                if (dir > 0) w.y = -w.y;
+                const double2 w = twid((j & (Ns - 1)) * tstride, dir, tw, Mmax);
                 const double2 b = cmul(buf[j + half], w);
                 o0[t] = make_double2(a.x + b.x, a.y + b.y);
                 o1[t] = make_double2(a.x - b.x, a.y - b.y);
@@ -1011,15 +1027,6 @@ __device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const dou
     }
 }
 #else
-// e^{dir 2 pi i t / Mmax} for 0 <= t < Mmax from the half-circle table
-__device__ __forceinline__ double2 twid(int t, int dir, const double2* __restrict__ tw, int Mmax) {
-    const int h = Mmax >> 1;
-    double2 w = tw[t < h ? t : t - h];
-    if (t >= h) { w.x = -w.x; w.y = -w.y; }
-    if (dir > 0) w.y = -w.y;
-    return w;
-}
-
 // v <- DFT_R(v) in registers, natural order: v_k = sum_n v_n e^{dir 2 pi i nk/R}
 // (R = 8: three radix-2 decimation-in-frequency levels, then the bit reversal)
 template <int R>
@@ -1063,7 +1070,7 @@ __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int 
                                                int Mmax) {
     constexpr int NBF = NV / R;
     const int nb = M / R;
-    const int step = Mmax / (Ns * R);
+    const int step = (Mmax < 0 ? -Mmax : Mmax) / (Ns * R);
     double2 v[NBF][R];
 #pragma unroll
     for (int b = 0; b < NBF; ++b) {
@@ -1107,6 +1114,31 @@ __device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const dou
 }
 #endif
 
+// an elementwise pass over j < n, j = threadIdx.x + u blockDim (u < U; the
+// ring kernels have n <= U blockDim, a rest loop covers more): every load of
+// the thread is issued before its first use -- one memory round trip instead
+// of U (a large ring workgroup has its CU to itself, nothing else hides the
+// latency); the uses run in the same order on the same values
+// (U capped at 8: the 16-per-thread passes of the global-scratch classes
+// would spill)
+constexpr int ew_u(int u) { return u > 8 ? 8 : u; }
+template <int U, class Ld, class Use>
+__device__ __forceinline__ void ew_pass(int n, Ld ld, Use use) {
+    using T = decltype(ld(0));
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int j = threadIdx.x + u * blockDim.x;
+        if (j < n) v[u] = ld(j);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int j = threadIdx.x + u * blockDim.x;
+        if (j < n) use(j, v[u]);
+    }
+    for (int j = threadIdx.x + U * blockDim.x; j < n; j += blockDim.x) use(j, ld(j));
+}
+
 // forward DFT of length n held in buf[0..n) (Bluestein when n is not a power
 // of two: M = g.M, kernel V = FFT of the chirp, followed in the plan's table by
 // the chirp c_j = e^{-i pi j^2 / n}, j < n, itself -- tabulated at plan time
@@ -1116,20 +1148,20 @@ template <int NB>
 __device__ __forceinline__ void bluestein_forward(double2* buf, int n, int M, const double2* __restrict__ V,
                                   const double2* __restrict__ tw, int Mmax) {
     const double2* __restrict__ C = V + M;
-    for (int j = threadIdx.x; j < M; j += blockDim.x) {
-        if (j < n) buf[j] = cmul(buf[j], C[j]);   // c_j = e^{-i pi j^2/n}
-        else buf[j] = make_double2(0.0, 0.0);
-    }
+    const double2 z = make_double2(0.0, 0.0);
+    // c_j = e^{-i pi j^2/n}; M <= 2 NB blockDim
+    ew_pass<ew_u(2 * NB)>(M, [&](int j) { return j < n ? C[j] : z; },
+                    [&](int j, double2 c) { buf[j] = j < n ? cmul(buf[j], c) : z; });
     __syncthreads();
     fft_pow2<NB>(buf, M, -1, tw, Mmax);
-    for (int j = threadIdx.x; j < M; j += blockDim.x) buf[j] = cmul(buf[j], V[j]);
+    ew_pass<ew_u(2 * NB)>(M, [&](int j) { return V[j]; }, [&](int j, double2 v) { buf[j] = cmul(buf[j], v); });
     __syncthreads();
     fft_pow2<NB>(buf, M, +1, tw, Mmax);
     const double inv = 1.0 / M;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        const double2 v = cmul(buf[j], C[j]);
+    ew_pass<ew_u(2 * NB)>(n, [&](int j) { return C[j]; }, [&](int j, double2 c) {
+        const double2 v = cmul(buf[j], c);
         buf[j] = make_double2(v.x * inv, v.y * inv);
-    }
+    });
     __syncthreads();
 }
 
@@ -1201,6 +1233,25 @@ __device__ __forceinline__ const double2* ring_twiddles_lds(double2* twl, int M,
     twM = M;
     return twl;
 }
+// the two-level tables of twid (Mmax < 0) at twl: Mmax / 64 + 64 entries, read
+// from the half-circle table (twM = -Mmax)
+__device__ __forceinline__ const double2* ring_twiddles_two(double2* twl, const double2* __restrict__ tw, int Mmax,
+                                                            int& twM) {
+    const int nh = Mmax >> 6;
+    for (int t = threadIdx.x; t < nh + 64; t += blockDim.x)
+        twl[t] = twid(t < nh ? 64 * t : t - nh, -1, tw, Mmax);
+    twM = -Mmax;
+    return twl;
+}
+// the same with the loads of a thread issued together (M / 2 <= U blockDim)
+template <int U>
+__device__ __forceinline__ const double2* ring_twiddles_lds_u(double2* twl, int M, const double2* __restrict__ tw,
+                                                              int Mmax, int& twM) {
+    const int st = Mmax / M;
+    ew_pass<U>(M / 2, [&](int t) { return tw[t * st]; }, [&](int t, double2 v) { twl[t] = v; });
+    twM = M;
+    return twl;
+}
 
 // ---------------------------------------------------------------------------
 // synthesis: ring stage.  grid (pairs of this M class, ncomp)
@@ -1257,7 +1308,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     const int n = g.nphi;
     const double2* twx = tw;
     int twM = Mmax;
-    if (twoff >= 0) twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
+    if (twoff >= 0) twx = ring_twiddles_lds_u<ew_u(NB)>(lbuf + twoff, g.M, tw, Mmax, twM);
+    else if (twoff <= -2) twx = ring_twiddles_two(lbuf + (-2 - twoff), tw, Mmax, twM);
     const long long plane = phi_plane(L, npair);
     const double2* PN = phi + (2LL * comp + 0) * plane;
     const double2* PS = phi + (2LL * comp + 1) * plane;
@@ -1353,18 +1405,17 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         bluestein_inverse<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += BD) A[k] = buf[k];
         __syncthreads();
-        for (int k = threadIdx.x; k < h; k += BD) buf[k] = Zo[k];
+        ew_pass<ew_u(NB)>(h, [&](int k) { return Zo[k]; }, [&](int k, double2 v) { buf[k] = v; });
         __syncthreads();
         bluestein_inverse<NB>(buf, h, g.M, V, twx, twM);
-        for (int k = threadIdx.x; k < h; k += BD) {
+        ew_pass<ew_u(NB)>(h, [&](int k) { return A[k]; }, [&](int k, double2 a) {
             const double2 b = cmul(buf[k], expi_pi_u32(2u * k, n));
-            const double2 a = A[k];
             const double2 y0 = op(comp, g.startN + k, g.startS + k, eq, make_double2(a.x + b.x, a.y + b.y));
             const double2 y1 = op(comp, g.startN + k + h, g.startS + k + h, eq, make_double2(a.x - b.x, a.y - b.y));
             mc[g.startN + k] = y0.x;
             mc[g.startN + k + h] = y1.x;
             if (!eq) { mc[g.startS + k] = y0.y; mc[g.startS + k + h] = y1.y; }
-        }
+        });
         return;
     }
     dft_inverse<NB>(buf, g, twx, twM, bsk);
@@ -1395,7 +1446,8 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
     double2* buf = gscratch ? gscratch + ((long long)comp * gridDim.x + blockIdx.x) * Mmax : lbuf;
     const double2* twx = tw;
     int twM = Mmax;
-    if (twoff >= 0) twx = ring_twiddles_lds(lbuf + twoff, g.M, tw, Mmax, twM);
+    if (twoff >= 0) twx = ring_twiddles_lds_u<ew_u(NB)>(lbuf + twoff, g.M, tw, Mmax, twM);
+    else if (twoff <= -2) twx = ring_twiddles_two(lbuf + (-2 - twoff), tw, Mmax, twM);
     const int n = g.nphi;
     const bool eq = g.startS < 0;
     const double* mc = maps + (long long)comp * npix;
@@ -1410,26 +1462,28 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         const int h = n / 2;
         double2* O = sscr + ((long long)comp * nsplit + g.sslot) * sstride;
         const double2* V = bsk + g.bs_off;
-        for (int k = threadIdx.x; k < h; k += blockDim.x)
-            buf[k] = make_double2(mv(g.startN + 2 * k + 1), eq ? 0.0 : mv(g.startS + 2 * k + 1));
+        // (h <= M / 2 <= NB blockDim)
+        ew_pass<ew_u(NB)>(h, [&](int k) { return make_double2(mv(g.startN + 2 * k + 1), eq ? 0.0 : mv(g.startS + 2 * k + 1)); },
+                    [&](int k, double2 v) { buf[k] = v; });
         __syncthreads();
         bluestein_forward<NB>(buf, h, g.M, V, twx, twM);
         for (int k = threadIdx.x; k < h; k += blockDim.x) O[k] = buf[k];
         __syncthreads();
-        for (int k = threadIdx.x; k < h; k += blockDim.x)
-            buf[k] = make_double2(mv(g.startN + 2 * k), eq ? 0.0 : mv(g.startS + 2 * k));
+        ew_pass<ew_u(NB)>(h, [&](int k) { return make_double2(mv(g.startN + 2 * k), eq ? 0.0 : mv(g.startS + 2 * k)); },
+                    [&](int k, double2 v) { buf[k] = v; });
         __syncthreads();
         bluestein_forward<NB>(buf, h, g.M, V, twx, twM);
-        for (int k = threadIdx.x; k < h; k += blockDim.x) {
+        ew_pass<ew_u(NB)>(h, [&](int k) { return O[k]; }, [&](int k, double2 ok) {
             const double2 e = buf[k];
-            const double2 o = cmul(O[k], expi_pi_neg_u32(2u * k, n));
+            const double2 o = cmul(ok, expi_pi_neg_u32(2u * k, n));
             buf[k] = make_double2(e.x + o.x, e.y + o.y);
             buf[k + h] = make_double2(e.x - o.x, e.y - o.y);
-        }
+        });
         __syncthreads();
     } else {
-        for (int j = threadIdx.x; j < n; j += blockDim.x)
-            buf[j] = make_double2(mv(g.startN + j), eq ? 0.0 : mv(g.startS + j));
+        // (n <= M <= 2 NB blockDim)
+        ew_pass<ew_u(2 * NB)>(n, [&](int j) { return make_double2(mv(g.startN + j), eq ? 0.0 : mv(g.startS + j)); },
+                        [&](int j, double2 v) { buf[j] = v; });
         __syncthreads();
         dft_forward<NB>(buf, g, twx, twM, bsk);
     }
@@ -3493,6 +3547,7 @@ struct gs_sht {
     double2* sscr = nullptr;     // split rings: [comp][slot][split_n] half-transform scratch
     int nsplit = 0, split_n = 0;
     int lds_fft_max = LDS_FFT_MAX;   // FFT lengths held in LDS (GS_SHT_LDS_FFT_MAX lowers it: tests)
+    int ring_tw2 = 0;                // GS_SHT_RING_TW2=1: the two-level twiddle tables for every LDS ring class (tests)
     double* mapw = nullptr;      // [cap][3][npix] Jacobi residual maps
     double2* ain = nullptr;      // [cap][3][nlm] a_lm in healpy complex order
     int cap = 1;                 // maps of a batch the per-map workspace (phi, part, ain, mapw) holds
@@ -3583,6 +3638,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
     if (nside < 1 || nside > 8192 || (nside & (nside - 1))) return set_error("gs_sht_create: nside must be a power of two <= 8192");
     if (lmax < 0 || lmax > 4 * nside) return set_error("gs_sht_create: lmax out of range (0..4 nside)");
     gs_sht* p = new gs_sht();
+    if (const char* e = gs_detail::option("GS_SHT_RING_TW2")) p->ring_tw2 = std::atoi(e) != 0;
     if (const char* e = gs_detail::option("GS_SHT_LDS_FFT_MAX")) {
         const int v = std::atoi(e);
         if (v >= 16 && v <= LDS_FFT_MAX && (v & (v - 1)) == 0) p->lds_fft_max = v;
@@ -3836,7 +3892,7 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
                              (const void*)k_sht_anal_ring<4>, (const void*)k_sht_anal_ring<8>};
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      LDS_FFT_MAX * (int)sizeof(double2) + 64 * 4 * (int)sizeof(double2));
+                                      std::max(LDS_FFT_MAX + 64 * 4, LDS_FFT_MAX + Mmax / 64 + 64) * (int)sizeof(double2));
         const void* mc[] = {(const void*)k_sht_synth_ring_mc<8>, (const void*)k_sht_anal_ring_mc<8>,
                             (const void*)k_sht_apply_ring_mc<8, PixWeights>, (const void*)k_sht_apply_ring_mc<8, PixAux>,
                             (const void*)k_sht_parseval_ring_mc<8>};
@@ -3894,15 +3950,20 @@ int gs_sht_info(const gs_sht* p, int* nside, int* lmax, long long* npix, long lo
 // LDS of a ring launch (double2 entries): the FFT buffer (M; global scratch
 // instead when glob), the fold reduction of short rings (4 per thread) aliasing
 // it, then the twiddle table (M / 2) when the total stays within RING_LDS_TW_MAX
-// (else the FFT reads the plan's global table; twoff = -1)
+// (twoff >= 0); else, for an LDS buffer, the two-level tables of twid (Mmax / 64
+// + 64 entries at -2 - twoff: M = 8192 rings no longer wait on a global
+// twiddle load in every FFT pass); glob: the plan's global table (twoff = -1)
 constexpr size_t RING_LDS_TW_MAX = 96 * 1024;
-static void ring_lds(int M, int bd, bool glob, bool short_red, size_t& lds, int& twoff) {
+static void ring_lds(int M, int bd, bool glob, bool short_red, int Mmax, size_t& lds, int& twoff, bool tw2 = false) {
     const long long red = short_red ? 4LL * bd : 0;
     const long long r0 = glob ? red : std::max<long long>(M, red);
     const long long with_tw = r0 + M / 2;
-    if (!glob && (size_t)with_tw * sizeof(double2) <= RING_LDS_TW_MAX) {
+    if (!glob && !tw2 && (size_t)with_tw * sizeof(double2) <= RING_LDS_TW_MAX) {
         twoff = (int)r0;
         lds = (size_t)with_tw * sizeof(double2);
+    } else if (!glob) {
+        twoff = -2 - (int)r0;
+        lds = (size_t)(r0 + Mmax / 64 + 64) * sizeof(double2);
     } else {
         twoff = -1;
         lds = (size_t)r0 * sizeof(double2);
@@ -3920,7 +3981,7 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
     const bool nb8 = M / 2 > 4 * bd;
     size_t lds = 0;
     int twoff = -1;
-    ring_lds(M, bd, glob, M < 8 * bd, lds, twoff);
+    ring_lds(M, bd, glob, M < 8 * bd, p->Mmax, lds, twoff, p->ring_tw2);
     const dim3 grid(p->cls_n[c], ncomp);
     double2* scr = glob ? p->gscr : nullptr;
     if (synth && aux) {
@@ -4011,7 +4072,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
         const bool nb8 = M / 2 > 4 * bd;
         size_t lds = 0;
         int twoff = -1;
-        ring_lds(M, bd, false, true, lds, twoff);
+        ring_lds(M, bd, false, true, p->Mmax, lds, twoff, p->ring_tw2);
         const dim3 grid(p->merged_n, ncomp);
         if (synth) {
             if (nb8)

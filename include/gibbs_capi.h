@@ -104,7 +104,8 @@ const char* gs_last_error(void);
  *   GS_F2_GROUP_BYTES, GS_F2_BATCH_BYTES  f2 workspace budgets (bytes)
  *   GS_SHT_LDS_FFT_MAX, GS_SHT_SEG, GS_SHT_SYN, GS_SHT_ANA, GS_SHT_MERGE_RINGS,
  *   GS_SHT_CONST_RINGS, GS_SHT_BLOCKS_MFMA, GS_SHT_BLK_STAGE, GS_SHT_FUSED_AUX,
- *   GS_SHT_MFMA_MAX_GB   SHT launch shapes / paths (gs_sht.hip documents each)
+ *   GS_SHT_MFMA_MAX_GB, GS_SHT_RING_TW2  SHT launch shapes / paths (gs_sht.hip
+ *                        documents each)
  * gs_option_set(name, NULL) unsets; an unknown name is an error. */
 int gs_option_set(const char* name, const char* value);
 const char* gs_option_get(const char* name);   /* NULL when unset or unknown */

@@ -260,6 +260,28 @@ def test_segmented_analysis_vs_oracle(gsopt, seg, ana, N, L):
         np.testing.assert_allclose(ga, wa, rtol=0, atol=1e-11 * np.abs(wa).max())
 
 
+@pytest.mark.parametrize("N,L", [(16, 40), (64, 100)])
+def test_ring_two_level_twiddles_vs_oracle(gsopt, N, L):
+    """The per-class ring FFTs with the two-level LDS twiddle tables (the
+    M = 8192 classes of N_side >= 2048 take them: the full table does not fit
+    beside the buffer), forced at small sizes with GS_SHT_RING_TW2 on the
+    per-class stage: TEB both directions against the dense oracle."""
+    torch = _torch()
+    from gibbssampler_amd.sht import HealpixSHT
+    gsopt.setenv("GS_SHT_RING_TW2", "1")
+    gsopt.setenv("GS_SHT_MERGE_RINGS", "0")
+    sht = HealpixSHT(N, L)
+    rng = np.random.default_rng(N * L + 2)
+    a = _rand_alm(L, 3, rng)
+    want = _oracle_maps(a, N, L, 3)
+    got = sht.alm2map(torch.from_numpy(a).cuda(), ncomp=3, layout="complex").cpu().numpy().reshape(3, -1)
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-11 * np.abs(want).max())
+    maps = rng.standard_normal((3, O.npix(N)))
+    wa = _oracle_alm(maps, N, L, 3, 0)
+    ga = sht.map2alm(torch.from_numpy(maps).cuda(), iter=0, layout="complex", ncomp=3).cpu().numpy().reshape(3, -1)
+    np.testing.assert_allclose(ga, wa, rtol=0, atol=1e-11 * np.abs(wa).max())
+
+
 @pytest.mark.parametrize("seg", [0, 200])
 def test_analysis_launch_shapes_agree_long_l(gsopt, seg):
     """The large-map analysis shapes (4 ring groups per lane, m paired or not;

@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/shtpmc_$TAG
 rm -rf $O; mkdir -p $O
 B="tools/sht_bench.py --nside $NS --lmax $LM --reps 2"
-K="k_sht_(anal|synth)_leg"
+K=${KRE:-"k_sht_(anal|synth)_leg"}   # KRE: another kernel regex (the ring stage)
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY \
     SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex "$K" -d $O/stall -o run \
     --output-format csv -- python3 $B > $O/stall.log 2>&1
