@@ -1114,29 +1114,30 @@ __device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const dou
 }
 #endif
 
-// an elementwise pass over j < n, j = threadIdx.x + u blockDim (u < U; the
-// ring kernels have n <= U blockDim, a rest loop covers more): every load of
-// the thread is issued before its first use -- one memory round trip instead
-// of U (a large ring workgroup has its CU to itself, nothing else hides the
-// latency); the uses run in the same order on the same values
+// an elementwise pass over j < n in batches of U per thread (j = j0 + u
+// blockDim): every load of a batch is issued before its first use -- one
+// memory round trip per batch instead of one per element (a large ring
+// workgroup has its CU to itself, nothing else hides the latency); the uses
+// run in the same order on the same values
 // (U capped at 8: the 16-per-thread passes of the global-scratch classes
 // would spill)
 constexpr int ew_u(int u) { return u > 8 ? 8 : u; }
 template <int U, class Ld, class Use>
 __device__ __forceinline__ void ew_pass(int n, Ld ld, Use use) {
     using T = decltype(ld(0));
-    T v[U];
+    for (int j0 = threadIdx.x; j0 < n; j0 += U * blockDim.x) {
+        T v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int j = threadIdx.x + u * blockDim.x;
-        if (j < n) v[u] = ld(j);
-    }
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u * blockDim.x;
+            if (j < n) v[u] = ld(j);
+        }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int j = threadIdx.x + u * blockDim.x;
-        if (j < n) use(j, v[u]);
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u * blockDim.x;
+            if (j < n) use(j, v[u]);
+        }
     }
-    for (int j = threadIdx.x + U * blockDim.x; j < n; j += blockDim.x) use(j, ld(j));
 }
 
 // forward DFT of length n held in buf[0..n) (Bluestein when n is not a power
@@ -1265,13 +1266,31 @@ struct Fold4 { double2 nk, nmk, sk, smk; };
 
 // the pixel operations a ring stage applies before its pixels leave it: y ->
 // the value stored for comp c at the ring pair's pixels iN (north) / iS (south)
+// pre / fin: the same operation with the pixel's loads issued first (fin(pre(..),
+// y) == operator()(.., y)), so the per-class ring stage batches them
 struct PixNone {
     static constexpr bool kConst = false;
+    struct Pre {};
     __device__ __forceinline__ double2 operator()(int, long long, long long, bool, double2 y) const { return y; }
+    __device__ __forceinline__ Pre pre(int, long long, long long, bool) const { return Pre{}; }
+    __device__ __forceinline__ double2 fin(int, long long, long long, bool, const Pre&, double2 y) const { return y; }
 };
 struct PixAux {                     // the aux-variable v | s update (gs_aux.h), comps (chain, field)
     gs::GsAuxPix a;
     static constexpr bool kConst = false;
+    struct Pre { gs::GsAuxPre n, s; };
+    __device__ __forceinline__ Pre pre(int c, long long iN, long long iS, bool eq) const {
+        const int b = c / a.F, k = c - b * a.F;
+        Pre q;
+        q.n = gs::mc_aux_load(a, b, k, iN);
+        q.s = eq ? gs::GsAuxPre{0.0, 0.0, 0.0, 0.0} : gs::mc_aux_load(a, b, k, iS);
+        return q;
+    }
+    __device__ __forceinline__ double2 fin(int c, long long iN, long long iS, bool eq, const Pre& q, double2 y) const {
+        const int b = c / a.F, k = c - b * a.F;
+        const double yn = gs::mc_aux_apply(a, b, k, iN, q.n, y.x);
+        return make_double2(yn, eq ? 0.0 : gs::mc_aux_apply(a, b, k, iS, q.s, y.y));
+    }
     __device__ __forceinline__ double2 operator()(int c, long long iN, long long iS, bool eq, double2 y) const {
         const int b = c / a.F, k = c - b * a.F;
         const double yn = gs::mc_aux_pixel(a, b, k, iN, y.x);
@@ -1408,10 +1427,14 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         ew_pass<ew_u(NB)>(h, [&](int k) { return Zo[k]; }, [&](int k, double2 v) { buf[k] = v; });
         __syncthreads();
         bluestein_inverse<NB>(buf, h, g.M, V, twx, twM);
-        ew_pass<ew_u(NB)>(h, [&](int k) { return A[k]; }, [&](int k, double2 a) {
+        struct Ld { double2 a; typename Op::Pre q0, q1; };
+        ew_pass<1>(h, [&](int k) {
+            return Ld{A[k], op.pre(comp, g.startN + k, g.startS + k, eq), op.pre(comp, g.startN + k + h, g.startS + k + h, eq)};
+        }, [&](int k, const Ld& ld) {
+            const double2 a = ld.a;
             const double2 b = cmul(buf[k], expi_pi_u32(2u * k, n));
-            const double2 y0 = op(comp, g.startN + k, g.startS + k, eq, make_double2(a.x + b.x, a.y + b.y));
-            const double2 y1 = op(comp, g.startN + k + h, g.startS + k + h, eq, make_double2(a.x - b.x, a.y - b.y));
+            const double2 y0 = op.fin(comp, g.startN + k, g.startS + k, eq, ld.q0, make_double2(a.x + b.x, a.y + b.y));
+            const double2 y1 = op.fin(comp, g.startN + k + h, g.startS + k + h, eq, ld.q1, make_double2(a.x - b.x, a.y - b.y));
             mc[g.startN + k] = y0.x;
             mc[g.startN + k + h] = y1.x;
             if (!eq) { mc[g.startS + k] = y0.y; mc[g.startS + k + h] = y1.y; }
@@ -1419,10 +1442,24 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         return;
     }
     dft_inverse<NB>(buf, g, twx, twM, bsk);
-    for (int j = threadIdx.x; j < n; j += BD) {
-        const double2 y = op(comp, g.startN + j, g.startS + j, eq, buf[j]);
-        mc[g.startN + j] = y.x;
-        if (!eq) mc[g.startS + j] = y.y;
+    // the pixel operation's loads of UO pixels issued before the first use (more spill)
+    constexpr int UO = 2;
+    for (int j0 = threadIdx.x; j0 < n; j0 += UO * BD) {
+        typename Op::Pre q[UO];
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int j = j0 + u * BD;
+            if (j < n) q[u] = op.pre(comp, g.startN + j, g.startS + j, eq);
+        }
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            const int j = j0 + u * BD;
+            if (j < n) {
+                const double2 y = op.fin(comp, g.startN + j, g.startS + j, eq, q[u], buf[j]);
+                mc[g.startN + j] = y.x;
+                if (!eq) mc[g.startS + j] = y.y;
+            }
+        }
     }
 }
 
