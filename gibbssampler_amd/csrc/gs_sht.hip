@@ -1080,8 +1080,19 @@ __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int 
             for (int k = 0; k < R; ++k) v[b][k] = buf[j + k * nb];
             if (Ns > 1) {
                 const int jm = j & (Ns - 1);
+                if (R == 8 && Mmax < 0) {
+                    // two-level tables: w^k from one lookup of w (depth <= 3
+                    // products) -- 2 LDS reads per butterfly instead of 14
+                    const double2 w1 = twid(jm * step, dir, tw, Mmax);
+                    const double2 w2 = cmul(w1, w1), w4 = cmul(w2, w2);
+                    const double2 w[8] = {w1, w1, w2, cmul(w1, w2), w4, cmul(w1, w4), cmul(w2, w4),
+                                          cmul(cmul(w1, w2), w4)};
 #pragma unroll
-                for (int k = 1; k < R; ++k) v[b][k] = cmul(v[b][k], twid(jm * k * step, dir, tw, Mmax));
+                    for (int k = 1; k < R; ++k) v[b][k] = cmul(v[b][k], w[k]);
+                } else {
+#pragma unroll
+                    for (int k = 1; k < R; ++k) v[b][k] = cmul(v[b][k], twid(jm * k * step, dir, tw, Mmax));
+                }
             }
             dft_reg<R>(v[b], dir);
         }
