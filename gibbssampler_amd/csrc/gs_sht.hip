@@ -997,36 +997,6 @@ __device__ __forceinline__ double2 twid(int t, int dir, const double2* __restric
     return w;
 }
 
-#if defined(GS_FFT_RADIX2)
-template <int NB>
-__device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
-    const int half = M >> 1;
-    for (int Ns = 1; Ns < M; Ns <<= 1) {
-        double2 o0[NB], o1[NB];
-        int id[NB];
-        const int tstride = (Mmax < 0 ? -Mmax : Mmax) / (2 * Ns);
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-            const int j = threadIdx.x + t * blockDim.x;
-            if (j < half) {
-                const double2 a = buf[j];
-                const double2 w = twid((j & (Ns - 1)) * tstride, dir, tw, Mmax);
-                const double2 b = cmul(buf[j + half], w);
-                o0[t] = make_double2(a.x + b.x, a.y + b.y);
-                o1[t] = make_double2(a.x - b.x, a.y - b.y);
-                id[t] = ((j / Ns) * 2 * Ns) + (j & (Ns - 1));
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-            const int j = threadIdx.x + t * blockDim.x;
-            if (j < half) { buf[id[t]] = o0[t]; buf[id[t] + Ns] = o1[t]; }
-        }
-        __syncthreads();
-    }
-}
-#else
 // v <- DFT_R(v) in registers, natural order: v_k = sum_n v_n e^{dir 2 pi i nk/R}
 // (R = 8: three radix-2 decimation-in-frequency levels, then the bit reversal)
 template <int R>
@@ -1061,13 +1031,21 @@ __device__ __forceinline__ void dft_reg(double2* v, int dir) {
     }
 }
 
+// elementwise operations an FFT applies to its input as the first pass reads it
+// and to its output before the last pass writes it (index in natural order)
+struct FftId {
+    __device__ __forceinline__ double2 operator()(int, double2 v) const { return v; }
+};
+
 // one Stockham stage of radix R at span Ns (Ns = product of the earlier
 // radices): butterfly j reads x[j + k M/R], twiddles by e^{dir 2 pi i (j mod Ns) k
 // / (Ns R)}, and writes y[(j - j mod Ns) R + j mod Ns + k Ns] (in place: all
-// reads, barrier, all writes).  NV complex values per thread at most.
-template <int R, int NV>
+// reads, barrier, all writes).  NV complex values per thread at most.  The first
+// stage (Ns = 1) applies in to what it reads, the last (Ns R = M) out to what
+// it writes -- the Bluestein chirp / kernel products without passes of their own
+template <int R, int NV, class In = FftId, class Out = FftId>
 __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int dir, const double2* __restrict__ tw,
-                                               int Mmax) {
+                                               int Mmax, const In& in = In{}, const Out& out = Out{}) {
     constexpr int NBF = NV / R;
     const int nb = M / R;
     const int step = (Mmax < 0 ? -Mmax : Mmax) / (Ns * R);
@@ -1078,6 +1056,10 @@ __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int 
         if (j < nb) {
 #pragma unroll
             for (int k = 0; k < R; ++k) v[b][k] = buf[j + k * nb];
+            if (Ns == 1) {
+#pragma unroll
+                for (int k = 0; k < R; ++k) v[b][k] = in(j + k * nb, v[b][k]);
+            }
             if (Ns > 1) {
                 const int jm = j & (Ns - 1);
                 if (R == 8 && Mmax < 0) {
@@ -1095,6 +1077,12 @@ __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int 
                 }
             }
             dft_reg<R>(v[b], dir);
+            if (Ns * R == M) {
+                const int jm = j & (Ns - 1);
+                const int base = (j - jm) * R + jm;
+#pragma unroll
+                for (int k = 0; k < R; ++k) v[b][k] = out(base + k * Ns, v[b][k]);
+            }
         }
     }
     __syncthreads();
@@ -1114,16 +1102,16 @@ __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int 
 // in-place power-of-two FFT in buf (LDS or global scratch), M <= 2 NB blockDim:
 // mixed-radix Stockham, one radix-2 or radix-4 stage first (M = 2^(3q+1) or
 // 2^(3q+2)), then radix-8 stages -- 5 block-wide passes at M = 8192 instead of 13
-template <int NB>
-__device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax) {
+template <int NB, class In = FftId, class Out = FftId>
+__device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax,
+                                         const In& in = In{}, const Out& out = Out{}) {
     constexpr int NV = 2 * NB;
     const int p = 31 - __clz(M);
     int Ns = 1;
-    if (p % 3 == 1) { stockham_stage<2, NV>(buf, M, 1, dir, tw, Mmax); Ns = 2; }
-    else if (p % 3 == 2) { stockham_stage<4, NV>(buf, M, 1, dir, tw, Mmax); Ns = 4; }
-    for (; Ns < M; Ns *= 8) stockham_stage<8, NV>(buf, M, Ns, dir, tw, Mmax);
+    if (p % 3 == 1) { stockham_stage<2, NV>(buf, M, 1, dir, tw, Mmax, in, out); Ns = 2; }
+    else if (p % 3 == 2) { stockham_stage<4, NV>(buf, M, 1, dir, tw, Mmax, in, out); Ns = 4; }
+    for (; Ns < M; Ns *= 8) stockham_stage<8, NV>(buf, M, Ns, dir, tw, Mmax, in, out);
 }
-#endif
 
 // an elementwise pass over j < n in batches of U per thread (j = j0 + u
 // blockDim): every load of a batch is issued before its first use -- one
@@ -1156,36 +1144,40 @@ __device__ __forceinline__ void ew_pass(int n, Ld ld, Use use) {
 // the chirp c_j = e^{-i pi j^2 / n}, j < n, itself -- tabulated at plan time
 // with the same function, so the ring kernels load it instead of two fp64
 // sincospi per element); result in buf[0..n)
+// (cj: conj(DFT(conj x)) -- the conjugations ride in the first and last products)
+// The products with the chirp (x_j c_j, j < n; 0 past n), the kernel V and the
+// chirp again (with 1 / M) are applied by the FFTs' first / last passes as they
+// read / write (FftId hooks): the same operations as separate passes, 3 LDS
+// round trips and 3 barriers fewer
 template <int NB>
 __device__ __forceinline__ void bluestein_forward(double2* buf, int n, int M, const double2* __restrict__ V,
-                                  const double2* __restrict__ tw, int Mmax) {
+                                  const double2* __restrict__ tw, int Mmax, bool cj = false) {
     const double2* __restrict__ C = V + M;
     const double2 z = make_double2(0.0, 0.0);
-    // c_j = e^{-i pi j^2/n}; M <= 2 NB blockDim
-    ew_pass<ew_u(2 * NB)>(M, [&](int j) { return j < n ? C[j] : z; },
-                    [&](int j, double2 c) { buf[j] = j < n ? cmul(buf[j], c) : z; });
-    __syncthreads();
-    fft_pow2<NB>(buf, M, -1, tw, Mmax);
-    ew_pass<ew_u(2 * NB)>(M, [&](int j) { return V[j]; }, [&](int j, double2 v) { buf[j] = cmul(buf[j], v); });
-    __syncthreads();
-    fft_pow2<NB>(buf, M, +1, tw, Mmax);
     const double inv = 1.0 / M;
-    ew_pass<ew_u(2 * NB)>(n, [&](int j) { return C[j]; }, [&](int j, double2 c) {
-        const double2 v = cmul(buf[j], c);
-        buf[j] = make_double2(v.x * inv, v.y * inv);
-    });
-    __syncthreads();
+    // c_j = e^{-i pi j^2/n}
+    auto chirp_in = [&](int j, double2 x) {
+        if (j >= n) return z;
+        if (cj) x.y = -x.y;
+        return cmul(x, C[j]);
+    };
+    auto kern = [&](int j, double2 y) { return cmul(y, V[j]); };
+    auto chirp_out = [&](int j, double2 y) {
+        if (j >= n) return y;
+        const double2 v = cmul(y, C[j]);
+        double2 r = make_double2(v.x * inv, v.y * inv);
+        if (cj) r.y = -r.y;
+        return r;
+    };
+    fft_pow2<NB>(buf, M, -1, tw, Mmax, chirp_in, kern);
+    fft_pow2<NB>(buf, M, +1, tw, Mmax, FftId{}, chirp_out);
 }
 
 // conj(DFT(conj x)) = unnormalised inverse DFT, Bluestein of length n
 template <int NB>
 __device__ __forceinline__ void bluestein_inverse(double2* buf, int n, int M, const double2* __restrict__ V,
                                   const double2* __restrict__ tw, int Mmax) {
-    for (int j = threadIdx.x; j < n; j += blockDim.x) buf[j].y = -buf[j].y;
-    __syncthreads();
-    bluestein_forward<NB>(buf, n, M, V, tw, Mmax);
-    for (int j = threadIdx.x; j < n; j += blockDim.x) buf[j].y = -buf[j].y;
-    __syncthreads();
+    bluestein_forward<NB>(buf, n, M, V, tw, Mmax, true);
 }
 
 template <int NB>
