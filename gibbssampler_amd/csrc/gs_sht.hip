@@ -1347,6 +1347,46 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
         const double cm = (m == 0 ? 1.0 : 2.0) * (neg ? -1.0 : 1.0);
         return make_double2(cm * v.x, cm * v.y);
     };
+    // a folded bin pair (k, n - k) -> the FFT input
+    auto emit = [&](int k, int nk, Fold4 f) {
+        if (g.phi_half) {
+            // e^{i pi k / n}; for nk = n - k: e^{i pi (n - k) / n} = -conj(e^{i pi k / n})
+            const double2 ek = expi_pi_u32(k, n);
+            const double2 enk = make_double2(-ek.x, ek.y);
+            f.nk = cmul(f.nk, ek);
+            f.sk = cmul(f.sk, ek);
+            f.nmk = cmul(f.nmk, enk);
+            f.smk = cmul(f.smk, enk);
+        }
+        if (nk == k) { f.nmk = f.nk; f.smk = f.sk; }
+        // Z_k = hN_k + i hS_k, hX_k = (G_k + conj G_-k)/2
+        const double2 hn = make_double2(0.5 * (f.nk.x + f.nmk.x), 0.5 * (f.nk.y - f.nmk.y));
+        const double2 hs = make_double2(0.5 * (f.sk.x + f.smk.x), 0.5 * (f.sk.y - f.smk.y));
+        buf[k] = make_double2(hn.x - hs.y, hn.y + hs.x);
+        if (nk != k) {
+            const double2 hn2 = make_double2(hn.x, -hn.y), hs2 = make_double2(hs.x, -hs.y);
+            buf[nk] = make_double2(hn2.x - hs2.y, hn2.y + hs2.x);
+        }
+    };
+    const double2 z2 = make_double2(0.0, 0.0);
+    if (J == 1 && n > Lc) {
+        // long rings: each side of a bin pair holds at most one m (k or n - k,
+        // both below n), so the fold is a gather -- the loads of a batch of
+        // bin pairs issued together (ew_pass); the same sums as the loop below
+        struct G4 { double2 nk, sk, nmk, smk; };
+        ew_pass<2>(K, [&](int k) {
+            const int nk = (n - k) % n;
+            G4 r = {z2, z2, z2, z2};
+            if (k <= Lc) { r.nk = H(PN, k, false); if (!eq) r.sk = H(PS, k, false); }
+            if (nk != k && nk <= Lc) { r.nmk = H(PN, nk, false); if (!eq) r.smk = H(PS, nk, false); }
+            return r;
+        }, [&](int k, const G4& r) {
+            Fold4 f = {z2, z2, z2, z2};
+            f.nk.x += r.nk.x; f.nk.y += r.nk.y; f.sk.x += r.sk.x; f.sk.y += r.sk.y;
+            f.nmk.x += r.nmk.x; f.nmk.y += r.nmk.y; f.smk.x += r.smk.x; f.smk.y += r.smk.y;
+            emit(k, (n - k) % n, f);
+        });
+    } else
     for (int s0 = 0; s0 < K * J; s0 += BD) {
         const int sl = s0 + threadIdx.x;
         Fold4 f = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
@@ -1379,26 +1419,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
             }
             __syncthreads();
         }
-        if (sl < K * J && j0 == 0) {
-            if (g.phi_half) {
-                // e^{i pi k / n}; for nk = n - k: e^{i pi (n - k) / n} = -conj(e^{i pi k / n})
-                const double2 ek = expi_pi_u32(k, n);
-                const double2 enk = make_double2(-ek.x, ek.y);
-                f.nk = cmul(f.nk, ek);
-                f.sk = cmul(f.sk, ek);
-                f.nmk = cmul(f.nmk, enk);
-                f.smk = cmul(f.smk, enk);
-            }
-            if (nk == k) { f.nmk = f.nk; f.smk = f.sk; }
-            // Z_k = hN_k + i hS_k, hX_k = (G_k + conj G_-k)/2
-            const double2 hn = make_double2(0.5 * (f.nk.x + f.nmk.x), 0.5 * (f.nk.y - f.nmk.y));
-            const double2 hs = make_double2(0.5 * (f.sk.x + f.smk.x), 0.5 * (f.sk.y - f.smk.y));
-            buf[k] = make_double2(hn.x - hs.y, hn.y + hs.x);
-            if (nk != k) {
-                const double2 hn2 = make_double2(hn.x, -hn.y), hs2 = make_double2(hs.x, -hs.y);
-                buf[nk] = make_double2(hn2.x - hs2.y, hn2.y + hs2.x);
-            }
-        }
+        if (sl < K * J && j0 == 0) emit(k, nk, f);
     }
     __syncthreads();
     double* mc = maps + (long long)comp * npix;
