@@ -1247,6 +1247,25 @@ __device__ __forceinline__ const double2* ring_twiddles_two(double2* twl, const 
     twM = -Mmax;
     return twl;
 }
+// a ring's phase factors e^{i pi t / n}, t < 2n, from two LDS tables (a per-ring
+// two-level table built at the kernel start: 2n / 64 + 64 sincospi instead of
+// one per use -- the fold's, the split combine's and the phase stores'
+// half-pixel and odd-sample factors); tables at tab, visible after a barrier
+struct RingPh {
+    const double2* A;
+    const double2* B;
+    __device__ __forceinline__ double2 pos(unsigned t) const { return cmul(A[t >> 6], B[t & 63]); }
+    __device__ __forceinline__ double2 neg(unsigned t) const { const double2 e = pos(t); return make_double2(e.x, -e.y); }
+};
+__device__ __forceinline__ RingPh ring_phases(double2* tab, unsigned n) {
+    const int na = (int)((2 * n + 63) / 64);
+    for (int i = threadIdx.x; i < na + 64; i += blockDim.x)
+        tab[i] = i < na ? expi_pi_u32(64u * (unsigned)i, n) : expi_pi_u32((unsigned)(i - na), n);
+    return RingPh{tab, tab + na};
+}
+// LDS entries of ring_phases for rings of a class of length M (n <= M + 1)
+inline int ring_ph_entries(int M) { return (2 * M + 2 + 63) / 64 + 64; }
+
 // the same with the loads of a thread issued together (M / 2 <= U blockDim)
 template <int U>
 __device__ __forceinline__ const double2* ring_twiddles_lds_u(double2* twl, int M, const double2* __restrict__ tw,
@@ -1314,7 +1333,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
                                                          double2* __restrict__ gscratch, double* __restrict__ maps,
                                                          double2* __restrict__ sscr, int nsplit, int sstride,
                                                          const int* __restrict__ comp_lmax, int comp_div, int twoff,
-                                                         Op op = Op{}) {
+                                                         int phoff, Op op = Op{}) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -1332,6 +1351,8 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     int twM = Mmax;
     if (twoff >= 0) twx = ring_twiddles_lds_u<ew_u(NB)>(lbuf + twoff, g.M, tw, Mmax, twM);
     else if (twoff <= -2) twx = ring_twiddles_two(lbuf + (-2 - twoff), tw, Mmax, twM);
+    const RingPh ph = ring_phases(lbuf + phoff, (unsigned)g.nphi);
+    __syncthreads();                                // the phase tables before the fold
     const long long plane = phi_plane(L, npair);
     const double2* PN = phi + (2LL * comp + 0) * plane;
     const double2* PS = phi + (2LL * comp + 1) * plane;
@@ -1351,7 +1372,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     auto emit = [&](int k, int nk, Fold4 f) {
         if (g.phi_half) {
             // e^{i pi k / n}; for nk = n - k: e^{i pi (n - k) / n} = -conj(e^{i pi k / n})
-            const double2 ek = expi_pi_u32(k, n);
+            const double2 ek = ph.pos((unsigned)k);
             const double2 enk = make_double2(-ek.x, ek.y);
             f.nk = cmul(f.nk, ek);
             f.sk = cmul(f.sk, ek);
@@ -1456,7 +1477,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
             return Ld{A[k], op.pre(comp, g.startN + k, g.startS + k, eq), op.pre(comp, g.startN + k + h, g.startS + k + h, eq)};
         }, [&](int k, const Ld& ld) {
             const double2 a = ld.a;
-            const double2 b = cmul(buf[k], expi_pi_u32(2u * k, n));
+            const double2 b = cmul(buf[k], ph.pos(2u * k));
             const double2 y0 = op.fin(comp, g.startN + k, g.startS + k, eq, ld.q0, make_double2(a.x + b.x, a.y + b.y));
             const double2 y1 = op.fin(comp, g.startN + k + h, g.startS + k + h, eq, ld.q1, make_double2(a.x - b.x, a.y - b.y));
             mc[g.startN + k] = y0.x;
@@ -1499,7 +1520,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
                                                         const double2* __restrict__ bsk,
                                                         double2* __restrict__ gscratch, double2* __restrict__ phi,
                                                         double2* __restrict__ sscr, int nsplit, int sstride, int twoff,
-                                                        const double* __restrict__ wts, int wnc) {
+                                                        int phoff, const double* __restrict__ wts, int wnc) {
     extern __shared__ double2 lbuf[];
     const int p = pairs[blockIdx.x];
     const int comp = blockIdx.y;
@@ -1509,6 +1530,8 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
     int twM = Mmax;
     if (twoff >= 0) twx = ring_twiddles_lds_u<ew_u(NB)>(lbuf + twoff, g.M, tw, Mmax, twM);
     else if (twoff <= -2) twx = ring_twiddles_two(lbuf + (-2 - twoff), tw, Mmax, twM);
+    // (visible to the combine and the stores below: the FFTs' barriers come first)
+    const RingPh ph = ring_phases(lbuf + phoff, (unsigned)g.nphi);
     const int n = g.nphi;
     const bool eq = g.startS < 0;
     const double* mc = maps + (long long)comp * npix;
@@ -1536,7 +1559,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         bluestein_forward<NB>(buf, h, g.M, V, twx, twM);
         ew_pass<ew_u(NB)>(h, [&](int k) { return O[k]; }, [&](int k, double2 ok) {
             const double2 e = buf[k];
-            const double2 o = cmul(ok, expi_pi_neg_u32(2u * k, n));
+            const double2 o = cmul(ok, ph.neg(2u * k));
             buf[k] = make_double2(e.x + o.x, e.y + o.y);
             buf[k + h] = make_double2(e.x - o.x, e.y - o.y);
         });
@@ -1559,7 +1582,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
         double2 xn = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
         double2 xs = make_double2(0.5 * (a.y + b.y), -0.5 * (a.x - b.x));
         if (g.phi_half) {
-            const double2 e = expi_pi_neg_u32(m, n);
+            const double2 e = ph.neg((unsigned)m % (2u * (unsigned)n));
             xn = cmul(xn, e);
             xs = cmul(xs, e);
         }
@@ -3953,7 +3976,8 @@ int gs_sht_create(int nside, int lmax, gs_sht** out) {
                              (const void*)k_sht_anal_ring<4>, (const void*)k_sht_anal_ring<8>};
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      std::max(LDS_FFT_MAX + 64 * 4, LDS_FFT_MAX + Mmax / 64 + 64) * (int)sizeof(double2));
+                                      (std::max(LDS_FFT_MAX + 64 * 4, LDS_FFT_MAX + Mmax / 64 + 64) +
+                                       ring_ph_entries(LDS_FFT_MAX)) * (int)sizeof(double2));
         const void* mc[] = {(const void*)k_sht_synth_ring_mc<8>, (const void*)k_sht_anal_ring_mc<8>,
                             (const void*)k_sht_apply_ring_mc<8, PixWeights>, (const void*)k_sht_apply_ring_mc<8, PixAux>,
                             (const void*)k_sht_parseval_ring_mc<8>};
@@ -4015,7 +4039,8 @@ int gs_sht_info(const gs_sht* p, int* nside, int* lmax, long long* npix, long lo
 // + 64 entries at -2 - twoff: M = 8192 rings no longer wait on a global
 // twiddle load in every FFT pass); glob: the plan's global table (twoff = -1)
 constexpr size_t RING_LDS_TW_MAX = 96 * 1024;
-static void ring_lds(int M, int bd, bool glob, bool short_red, int Mmax, size_t& lds, int& twoff, bool tw2 = false) {
+static void ring_lds(int M, int bd, bool glob, bool short_red, int Mmax, size_t& lds, int& twoff, int& phoff,
+                     bool tw2 = false) {
     const long long red = short_red ? 4LL * bd : 0;
     const long long r0 = glob ? red : std::max<long long>(M, red);
     const long long with_tw = r0 + M / 2;
@@ -4029,6 +4054,9 @@ static void ring_lds(int M, int bd, bool glob, bool short_red, int Mmax, size_t&
         twoff = -1;
         lds = (size_t)r0 * sizeof(double2);
     }
+    // then the ring's phase tables (ring_phases)
+    phoff = (int)(lds / sizeof(double2));
+    lds += (size_t)ring_ph_entries(M) * sizeof(double2);
 }
 
 static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const double* maps_in, double* maps_out,
@@ -4042,7 +4070,8 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
     const bool nb8 = M / 2 > 4 * bd;
     size_t lds = 0;
     int twoff = -1;
-    ring_lds(M, bd, glob, M < 8 * bd, p->Mmax, lds, twoff, p->ring_tw2);
+    int phoff = 0;
+    ring_lds(M, bd, glob, M < 8 * bd, p->Mmax, lds, twoff, phoff, p->ring_tw2);
     const dim3 grid(p->cls_n[c], ncomp);
     double2* scr = glob ? p->gscr : nullptr;
     if (synth && aux) {
@@ -4051,27 +4080,27 @@ static int sht_ring_class(gs_sht* p, size_t c, bool synth, int ncomp, const doub
         if (nb8)
             hipLaunchKernelGGL((k_sht_synth_ring<8, PixAux>), grid, dim3(bd), lds, st, p->L, p->npair, p->npix,
                                p->cls_pairs[c], p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit,
-                               p->split_n, comp_lmax, comp_div, twoff, op);
+                               p->split_n, comp_lmax, comp_div, twoff, phoff, op);
         else
             hipLaunchKernelGGL((k_sht_synth_ring<4, PixAux>), grid, dim3(bd), lds, st, p->L, p->npair, p->npix,
                                p->cls_pairs[c], p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit,
-                               p->split_n, comp_lmax, comp_div, twoff, op);
+                               p->split_n, comp_lmax, comp_div, twoff, phoff, op);
     } else if (synth) {
         if (nb8)
             hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
                                p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
-                               comp_lmax, comp_div, twoff, PixNone{});
+                               comp_lmax, comp_div, twoff, phoff, PixNone{});
         else
             hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
                                p->geom, phi, p->tw, p->Mmax, p->bsk, scr, maps_out, p->sscr, p->nsplit, p->split_n,
-                               comp_lmax, comp_div, twoff, PixNone{});
+                               comp_lmax, comp_div, twoff, phoff, PixNone{});
     } else {
         if (nb8)
             hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts, wnc);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, phoff, wts, wnc);
         else
             hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, st, p->L, p->npair, p->npix, p->cls_pairs[c],
-                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, wts, wnc);
+                               p->geom, maps_in, p->tw, p->Mmax, p->bsk, scr, p->phi, p->sscr, p->nsplit, p->split_n, twoff, phoff, wts, wnc);
     }
     GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring" : "k_sht_anal_ring");
     return 0;
@@ -4133,26 +4162,27 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
         const bool nb8 = M / 2 > 4 * bd;
         size_t lds = 0;
         int twoff = -1;
-        ring_lds(M, bd, false, true, p->Mmax, lds, twoff, p->ring_tw2);
+        int phoff = 0;
+        ring_lds(M, bd, false, true, p->Mmax, lds, twoff, phoff, p->ring_tw2);
         const dim3 grid(p->merged_n, ncomp);
         if (synth) {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_synth_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
-                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff, PixNone{});
+                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff, phoff, PixNone{});
             else
                 hipLaunchKernelGGL(k_sht_synth_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, ph, p->tw, p->Mmax, p->bsk, nullptr, maps_out, p->sscr,
-                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff, PixNone{});
+                                   p->nsplit, p->split_n, comp_lmax, comp_div, twoff, phoff, PixNone{});
         } else {
             if (nb8)
                 hipLaunchKernelGGL(k_sht_anal_ring<8>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n, twoff, wts, wnc);
+                                   p->nsplit, p->split_n, twoff, phoff, wts, wnc);
             else
                 hipLaunchKernelGGL(k_sht_anal_ring<4>, grid, dim3(bd), lds, S(stream), p->L, p->npair, p->npix,
                                    p->merged_pairs, p->geom, maps_in, p->tw, p->Mmax, p->bsk, nullptr, p->phi, p->sscr,
-                                   p->nsplit, p->split_n, twoff, wts, wnc);
+                                   p->nsplit, p->split_n, twoff, phoff, wts, wnc);
         }
         GS_LAUNCH_CHECK(synth ? "k_sht_synth_ring (merged)" : "k_sht_anal_ring (merged)");
         return 0;
