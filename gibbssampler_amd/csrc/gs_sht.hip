@@ -1250,18 +1250,28 @@ __device__ __forceinline__ const double2* ring_twiddles_two(double2* twl, const 
 // a ring's phase factors e^{i pi t / n}, t < 2n, from two LDS tables (a per-ring
 // two-level table built at the kernel start: 2n / 64 + 64 sincospi instead of
 // one per use -- the fold's, the split combine's and the phase stores'
-// half-pixel and odd-sample factors); tables at tab, visible after a barrier
+// half-pixel and odd-sample factors); tables at tab, visible after a barrier.
+// tab == nullptr (the merged one-component launch, whose results the
+// multi-component kernels reproduce bit for bit): the direct sincospi
 struct RingPh {
     const double2* A;
     const double2* B;
-    __device__ __forceinline__ double2 pos(unsigned t) const { return cmul(A[t >> 6], B[t & 63]); }
-    __device__ __forceinline__ double2 neg(unsigned t) const { const double2 e = pos(t); return make_double2(e.x, -e.y); }
+    unsigned n;
+    __device__ __forceinline__ double2 pos(unsigned t) const {
+        return A ? cmul(A[t >> 6], B[t & 63]) : expi_pi_u32(t, n);
+    }
+    __device__ __forceinline__ double2 neg(unsigned t) const {
+        if (!A) return expi_pi_neg_u32(t, n);
+        const double2 e = pos(t);
+        return make_double2(e.x, -e.y);
+    }
 };
 __device__ __forceinline__ RingPh ring_phases(double2* tab, unsigned n) {
+    if (!tab) return RingPh{nullptr, nullptr, n};
     const int na = (int)((2 * n + 63) / 64);
     for (int i = threadIdx.x; i < na + 64; i += blockDim.x)
         tab[i] = i < na ? expi_pi_u32(64u * (unsigned)i, n) : expi_pi_u32((unsigned)(i - na), n);
-    return RingPh{tab, tab + na};
+    return RingPh{tab, tab + na, n};
 }
 // LDS entries of ring_phases for rings of a class of length M (n <= M + 1)
 inline int ring_ph_entries(int M) { return (2 * M + 2 + 63) / 64 + 64; }
@@ -1351,7 +1361,7 @@ __global__ __launch_bounds__(1024) void k_sht_synth_ring(int L, int npair, long 
     int twM = Mmax;
     if (twoff >= 0) twx = ring_twiddles_lds_u<ew_u(NB)>(lbuf + twoff, g.M, tw, Mmax, twM);
     else if (twoff <= -2) twx = ring_twiddles_two(lbuf + (-2 - twoff), tw, Mmax, twM);
-    const RingPh ph = ring_phases(lbuf + phoff, (unsigned)g.nphi);
+    const RingPh ph = ring_phases(phoff >= 0 ? lbuf + phoff : nullptr, (unsigned)g.nphi);
     __syncthreads();                                // the phase tables before the fold
     const long long plane = phi_plane(L, npair);
     const double2* PN = phi + (2LL * comp + 0) * plane;
@@ -1531,7 +1541,7 @@ __global__ __launch_bounds__(1024) void k_sht_anal_ring(int L, int npair, long l
     if (twoff >= 0) twx = ring_twiddles_lds_u<ew_u(NB)>(lbuf + twoff, g.M, tw, Mmax, twM);
     else if (twoff <= -2) twx = ring_twiddles_two(lbuf + (-2 - twoff), tw, Mmax, twM);
     // (visible to the combine and the stores below: the FFTs' barriers come first)
-    const RingPh ph = ring_phases(lbuf + phoff, (unsigned)g.nphi);
+    const RingPh ph = ring_phases(phoff >= 0 ? lbuf + phoff : nullptr, (unsigned)g.nphi);
     const int n = g.nphi;
     const bool eq = g.startS < 0;
     const double* mc = maps + (long long)comp * npix;
@@ -4164,6 +4174,7 @@ static int sht_rings(gs_sht* p, bool synth, int ncomp, const double* maps_in, do
         int twoff = -1;
         int phoff = 0;
         ring_lds(M, bd, false, true, p->Mmax, lds, twoff, phoff, p->ring_tw2);
+        phoff = -1;                                 // as the multi-component kernels: direct sincospi
         const dim3 grid(p->merged_n, ncomp);
         if (synth) {
             if (nb8)
