@@ -96,7 +96,7 @@ def _real_dot(a, b):
     return float((a * b).sum())
 
 
-@pytest.mark.parametrize("N,L", [(256, 512), (512, 1024)])
+@pytest.mark.parametrize("N,L", [(256, 512), (512, 1024), (1024, 2048)])
 @pytest.mark.parametrize("ncomp", [1, 3])
 def test_adjointness_fullsize(N, L, ncomp):
     """<A a, m> = <a, A^T m> in the real layout, A^T = map2alm(iter=0)/w (exact)."""
@@ -153,6 +153,9 @@ def _lambda_mp(l, m, x):
 @pytest.mark.parametrize("N,L,modes", [
     (256, 512, [(512, 0), (512, 500), (400, 390), (300, 150), (511, 511)]),
     (512, 1024, [(1024, 1000), (1000, 990), (900, 30), (1024, 1024)]),
+    # per-class ring stage with M = 8192 Bluestein rings: the two-level twiddle
+    # and phase tables, the Bluestein products inside the FFT passes
+    (1024, 2048, [(2048, 0), (2000, 1990), (1500, 700), (700, 3)]),
 ])
 def test_single_modes_vs_scipy(N, L, modes):
     """a single a_lm (l, m) -> 2 Re(a Y_lm) at every pixel of sampled rings,
