@@ -1016,6 +1016,38 @@ __device__ __forceinline__ void dft_reg(double2* v, int dir) {
         v[3] = rot4(v[3]);
         bfly(v[0], v[1]); bfly(v[2], v[3]);
         const double2 t = v[1]; v[1] = v[2]; v[2] = t;          // bit reversal
+    } else if constexpr (R == 16) {
+        // 16 = 4 x 4: DFT_4 over a of v[4a + b], the twiddles e^{dir 2 pi i b k1 / 16},
+        // DFT_4 over b; X[k1 + 4 k2]
+        constexpr double W[10][2] = {{1.0, 0.0},
+                                     {0.92387953251128675613, 0.38268343236508977173},
+                                     {0.70710678118654752440, 0.70710678118654752440},
+                                     {0.38268343236508977173, 0.92387953251128675613},
+                                     {0.0, 1.0},
+                                     {-0.38268343236508977173, 0.92387953251128675613},
+                                     {-0.70710678118654752440, 0.70710678118654752440},
+                                     {-0.92387953251128675613, 0.38268343236508977173},
+                                     {-1.0, 0.0},
+                                     {-0.92387953251128675613, -0.38268343236508977173}};
+        double2 t[4][4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            double2 q[4] = {v[b], v[4 + b], v[8 + b], v[12 + b]};
+            dft_reg<4>(q, dir);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) t[b][k] = q[k];
+        }
+#pragma unroll
+        for (int b = 1; b < 4; ++b)
+#pragma unroll
+            for (int k = 1; k < 4; ++k) t[b][k] = cmul(t[b][k], make_double2(W[b * k][0], sg * W[b * k][1]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double2 q[4] = {t[0][k], t[1][k], t[2][k], t[3][k]};
+            dft_reg<4>(q, dir);
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) v[k + 4 * k2] = q[k2];
+        }
     } else {
         constexpr double C = 0.70710678118654752440;
         bfly(v[0], v[4]); bfly(v[1], v[5]); bfly(v[2], v[6]); bfly(v[3], v[7]);
@@ -1046,7 +1078,7 @@ struct FftId {
 template <int R, int NV, class In = FftId, class Out = FftId>
 __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int dir, const double2* __restrict__ tw,
                                                int Mmax, const In& in = In{}, const Out& out = Out{}) {
-    constexpr int NBF = NV / R;
+    constexpr int NBF = NV / R > 0 ? NV / R : 1;   // radix 16 at 8 values per thread: half the threads
     const int nb = M / R;
     const int step = (Mmax < 0 ? -Mmax : Mmax) / (Ns * R);
     double2 v[NBF][R];
@@ -1100,15 +1132,17 @@ __device__ __forceinline__ void stockham_stage(double2* buf, int M, int Ns, int 
 }
 
 // in-place power-of-two FFT in buf (LDS or global scratch), M <= 2 NB blockDim:
-// mixed-radix Stockham, one radix-2 or radix-4 stage first (M = 2^(3q+1) or
-// 2^(3q+2)), then radix-8 stages -- 5 block-wide passes at M = 8192 instead of 13
+// mixed-radix Stockham, one radix-16 or radix-4 stage first (M = 2^(3q+1), or
+// 2^(3q+2); radix 2 at M = 2), then radix-8 stages -- 4 block-wide passes at M =
+// 8192 instead of 13
 template <int NB, class In = FftId, class Out = FftId>
 __device__ __forceinline__ void fft_pow2(double2* buf, int M, int dir, const double2* __restrict__ tw, int Mmax,
                                          const In& in = In{}, const Out& out = Out{}) {
     constexpr int NV = 2 * NB;
     const int p = 31 - __clz(M);
     int Ns = 1;
-    if (p % 3 == 1) { stockham_stage<2, NV>(buf, M, 1, dir, tw, Mmax, in, out); Ns = 2; }
+    if (p % 3 == 1 && p >= 4) { stockham_stage<16, NV>(buf, M, 1, dir, tw, Mmax, in, out); Ns = 16; }
+    else if (p % 3 == 1) { stockham_stage<2, NV>(buf, M, 1, dir, tw, Mmax, in, out); Ns = 2; }
     else if (p % 3 == 2) { stockham_stage<4, NV>(buf, M, 1, dir, tw, Mmax, in, out); Ns = 4; }
     for (; Ns < M; Ns *= 8) stockham_stage<8, NV>(buf, M, Ns, dir, tw, Mmax, in, out);
 }
@@ -1615,8 +1649,8 @@ __device__ __forceinline__ int ilog2d(int x) { return 31 - __clz(x); }
 template <int R, int NV>
 __device__ __forceinline__ void stockham_stage_mc(double2* buf, int SB, int nc, int lgM, int Ns, int dir,
                                                   const double2* __restrict__ tw, int Mmax) {
-    constexpr int NBF = NV / R;
-    constexpr int LGR = R == 2 ? 1 : (R == 4 ? 2 : 3);
+    constexpr int NBF = NV / R > 0 ? NV / R : 1;
+    constexpr int LGR = R == 2 ? 1 : (R == 4 ? 2 : (R == 8 ? 3 : 4));
     const int lgnb = lgM - LGR;
     const int nb = 1 << lgnb;
     const int nbt = nb * nc;
@@ -1659,7 +1693,8 @@ __device__ __forceinline__ void fft_pow2_mc(double2* buf, int SB, int nc, int M,
                                             const double2* __restrict__ tw, int Mmax) {
     const int p = ilog2d(M);
     int Ns = 1;
-    if (p % 3 == 1) { stockham_stage_mc<2, NV>(buf, SB, nc, p, 1, dir, tw, Mmax); Ns = 2; }
+    if (p % 3 == 1 && p >= 4) { stockham_stage_mc<16, NV>(buf, SB, nc, p, 1, dir, tw, Mmax); Ns = 16; }
+    else if (p % 3 == 1) { stockham_stage_mc<2, NV>(buf, SB, nc, p, 1, dir, tw, Mmax); Ns = 2; }
     else if (p % 3 == 2) { stockham_stage_mc<4, NV>(buf, SB, nc, p, 1, dir, tw, Mmax); Ns = 4; }
     for (; Ns < M; Ns *= 8) stockham_stage_mc<8, NV>(buf, SB, nc, p, Ns, dir, tw, Mmax);
 }
